@@ -1,0 +1,136 @@
+/*
+ * streamoptima.h — C-ABI of libstreamoptima_hip.so, the MI355X (gfx950) per-block
+ * encode path of a StreamOptima-compatible block video encoder.
+ *
+ * The reference (Suyashagarw/StreamOptima) is pure Python and has no FFI: its drop-in
+ * boundary is the Y_Video_codec / decoder Python API.  Each entry point below replaces
+ * the reference functions cited next to it; the Python facade in streamoptima_amd/
+ * (Encoder.py, decoder.py) keeps the reference's method names and calls these through
+ * ctypes (see INTEGRATION.md for the binding).
+ *
+ * Conventions
+ *  - Frames are uint8, row-major, pitch == width, resident in device (HBM) memory; every
+ *    frame buffer must be readable for 16 bytes past its last pixel.
+ *  - H and W are the encoded frame size and must be multiples of bs (the reference's
+ *    pad_hw, Encoder.py:140-155, is applied by the caller; see DESIGN.md for 1080p).
+ *  - Blocks are numbered in raster order, nb = (H/bs) * (W/bs).
+ *  - All pointers except `refs` (a HOST array of device pointers) are device pointers
+ *    allocated by the caller (PyTorch tensors in the facade).  The library never
+ *    allocates device memory; all calls are asynchronous on `stream` (a hipStream_t).
+ *  - Return 0 (SO_OK) on success, SO_E_* (< 0) for bad arguments, or a positive
+ *    hipError_t.  so_last_error() returns a thread-local message for the last failure.
+ *  - No C++ exception crosses this boundary.
+ *
+ * Canonical output layout (shared with tests/golden and the CPU oracle):
+ *   split[nb]            uint8   1 = variable-block-size split (4 sub-blocks, Z order)
+ *   inter mv[nb][4][3]   int16   (dx, dy, ref) per sub-block; unsplit => entry 0 only
+ *   intra mv[nb][4]      int16   dx per sub-block (-1 for blocks at x == 0)
+ *   qtc[nb][bs*bs]       int16   quantised coefficients; split => 4 x (bs/2)^2 Z order
+ *   tokens[nb]           int32   len(entropy_encoder_block(...)) summed over sub-blocks
+ *   mae_num[nb]          int32   block MAE * bs*bs (an integer SAD), -1 = inf
+ */
+#ifndef STREAMOPTIMA_H
+#define STREAMOPTIMA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SO_OK 0
+#define SO_E_INVALID (-1)      /* bad argument (message in so_last_error) */
+#define SO_E_UNSUPPORTED (-2)  /* valid in the reference but not built for gfx950 yet */
+#define SO_MAX_REF 4           /* nRefFrames supported by the kernels */
+#define SO_ABI_VERSION 1
+
+/* library identification / diagnostics */
+int so_abi_version(void);
+const char* so_last_error(void);
+
+/*
+ * Full-search integer-pel motion estimation for every bs x bs block of `cur`.
+ * Replaces find_best_match + compute_mae + is_better_mv (Encoder.py:678-717, 314-315,
+ * 771-773) as called from inter_prediction (Encoder.py:505-562).
+ *   refs[nref]   host array of device pointers to H x W reference frames
+ *   sr           search range (dx, dy in [-sr, sr]); candidate valid iff
+ *                0 <= x+dx < W-bs and 0 <= y+dy < H-bs (strict, like the reference)
+ *   out_best     int32 [nb][4]: (dx, dy, ref, sad); sad = -1 if no candidate is valid
+ *   out_sub      optional int32 [nb][4][4]: the same for the four (bs/2) sub-blocks of
+ *                every block (VBSEnable, Encoder.py:512-544); NULL to skip
+ */
+int so_me_full_search(const uint8_t* cur, const uint8_t* const* refs, int nref, int H,
+                      int W, int bs, int sr, int32_t* out_best, int32_t* out_sub,
+                      void* stream);
+
+/*
+ * Residual, DCT, quantisation, token count, VBS rate-distortion split decision,
+ * dequantisation, IDCT and reconstruction for every block of a P-frame.
+ * Replaces calculate_inter_frame_residual (Encoder.py:432-460), apply_2d_dct (:779),
+ * quantize_TC (:787), entropy_encoder_block's length (:1086), calculate_RD_cost (:1133)
+ * and the split decision (:564-578), the per-block loop of complete_inter_flow
+ * (:1665-1697) and reconstruct_frame / reconstruct_block (:824-932).
+ *   best/sub     outputs of so_me_full_search (sub may be NULL when vbs == 0)
+ *   qp_rd        QP in effect during inter_prediction (used for the RD decision)
+ *   qp_row       device int32 [H/bs] per-row QP (rate control), or NULL => qp_rd
+ *   lam          lambda of calculate_RD_cost
+ *   out_recon    H x W uint8 reconstruction (may not alias any ref)
+ */
+int so_inter_tq_recon(const uint8_t* cur, const uint8_t* const* refs, int nref, int H,
+                      int W, int bs, const int32_t* best, const int32_t* sub, int qp_rd,
+                      const int32_t* qp_row, int vbs, double lam, uint8_t* out_split,
+                      int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
+                      int32_t* out_mae_num, uint8_t* out_recon, void* stream);
+
+/* int32 elements of scratch so_encode_p_frame needs: nb*4 (+ nb*16 with vbs) */
+size_t so_p_frame_scratch_elems(int H, int W, int bs, int vbs);
+
+/*
+ * One P-frame of complete_inter_flow (Encoder.py:1644-1709): so_me_full_search then
+ * so_inter_tq_recon, with `scratch` (device int32, so_p_frame_scratch_elems) between.
+ */
+int so_encode_p_frame(const uint8_t* cur, const uint8_t* const* refs, int nref, int H,
+                      int W, int bs, int sr, int qp_rd, const int32_t* qp_row, int vbs,
+                      double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc,
+                      int32_t* out_tokens, int32_t* out_mae_num, uint8_t* out_recon,
+                      int32_t* scratch, void* stream);
+
+/* int32 elements of scratch so_encode_i_frame / so_intra_recon need: nb*(bs*bs) + nb*8 */
+size_t so_i_frame_scratch_elems(int H, int W, int bs);
+
+/*
+ * One I-frame of complete_intra_flow, intra_mode 0 (Encoder.py:1582-1642):
+ * intra_prediction (:1238-1347, horizontal search intra_find_best_match_horizontal
+ * :1010-1045, canvas generalised from the hard-coded 288x352 to H x W), per-block
+ * DCT/quant/tokens/VBS-RD, and reconstruct_frame_intra (:1350-1417; unclipped canvas,
+ * final astype(uint8) == mod-256 wrap).  out_mv is int16 [nb][4].
+ */
+int so_encode_i_frame(const uint8_t* cur, int H, int W, int bs, int sr, int qp_rd,
+                      const int32_t* qp_row, int vbs, double lam, uint8_t* out_split,
+                      int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
+                      int32_t* out_mae_num, uint8_t* out_recon, int32_t* scratch,
+                      void* stream);
+
+/* Decoder: P-frame reconstruction from symbols (decoder.py:97-211). */
+int so_inter_recon(const uint8_t* const* refs, int nref, int H, int W, int bs, int qp,
+                   const int32_t* qp_row, const uint8_t* split, const int16_t* mv,
+                   const int16_t* qtc, uint8_t* out_recon, void* stream);
+
+/* Decoder: I-frame reconstruction from symbols (decoder.py:330-432, mode 0). */
+int so_intra_recon(int H, int W, int bs, int qp, const int32_t* qp_row,
+                   const uint8_t* split, const int16_t* mv, const int16_t* qtc,
+                   uint8_t* out_recon, int32_t* scratch, void* stream);
+
+/*
+ * Sum of squared differences of two uint8 planes of n pixels, ADDED into *out_sse
+ * (device uint64; zero it first).  PSNR per frame (calculate_metrics, Encoder.py:934)
+ * is 10*log10(255^2 / (sse / n)) on the host.
+ */
+int so_sse_u8(const uint8_t* a, const uint8_t* b, int64_t n, uint64_t* out_sse,
+              void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STREAMOPTIMA_H */

@@ -1,0 +1,58 @@
+"""Oracle GOP driver: the reference's encode() loop (Encoder.py:1790-1898) over the C
+oracle's frame functions.  TEST INFRASTRUCTURE ONLY (checker for tests/ and bench).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import oracle as O
+
+
+def row_qp_schedule(bitrate_per_row, tables, n_rows):
+    qps, budget, spent = [], bitrate_per_row, 0
+    for r in range(n_rows):
+        budget = bitrate_per_row if r == 0 else bitrate_per_row + (budget - spent)
+        got = next(((q, b) for q, b in enumerate(tables[0]) if b < budget), None)
+        if got is None:
+            raise TypeError("no QP fits the row budget")
+        q, spent = got
+        qps.append(q)
+    return qps
+
+
+def bitrate_per_row(target, frame_rate, h, bs):
+    num, unit = target.split(" ")
+    num = int(num)
+    tb = num * 1024 if unit == "kbps" else num * 1048576 if unit == "mbps" else num
+    return (tb // frame_rate) / (h / bs)
+
+
+def encode_gop(frames, qp, intra_dur, bs=16, sr=16, vbs=False, lam=0.015, nref=1, rc=None,
+               target=None, tables=None, intra_thresh=None, frame_rate=30):
+    f, h, w = frames.shape
+    ref_frames = [np.full((h, w), 128, np.uint8)]
+    qp_sched = None
+    if rc is not None and rc > 0:
+        qp_sched = row_qp_schedule(bitrate_per_row(target, frame_rate, h, bs), tables, h // bs)
+    out = []
+    for i in range(f):
+        cur = frames[i]
+        if i % intra_dur == 0:
+            r = O.intra_frame(cur, bs, sr, qp, qp_sched, vbs, lam)
+            ft = 0
+        else:
+            r = O.inter_frame(cur, ref_frames, bs, sr, qp, qp_sched, vbs, lam)
+            ft = 1
+            if rc is not None and rc > 1 and int(r["tokens"].sum()) > intra_thresh:
+                r = O.intra_frame(cur, bs, sr, qp_sched[-1], qp_sched, vbs, lam)
+                ft = 0
+        r["frame_type"] = ft
+        r["qp_row"] = list(qp_sched) if qp_sched else []
+        sse = O.sse(cur, r["recon"])
+        r["psnr"] = float("inf") if sse == 0 else float(10 * np.log10((255 ** 2) / (sse / (h * w))))
+        out.append(r)
+        if i < f - 1:
+            if len(ref_frames) >= nref:
+                ref_frames.pop(0)
+            ref_frames.append(r["recon"])
+    return out

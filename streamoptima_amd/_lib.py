@@ -1,0 +1,95 @@
+"""ctypes binding of libstreamoptima_hip.so (include/streamoptima.h).
+
+`import torch` happens first so that the library's libamdhip64.so.7 dependency resolves
+to the HIP runtime PyTorch already loaded (one runtime per process).  There is no CPU
+fallback: if the library is missing or was built for another target, every call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the CDLL load)
+
+from .build import LIB_PATH
+
+_lock = threading.Lock()
+_lib = None
+
+SO_OK = 0
+SO_E_INVALID = -1
+SO_E_UNSUPPORTED = -2
+MAX_REF = 4
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_d = ctypes.c_double
+_sz = ctypes.c_size_t
+
+_SIGS = {
+    "so_abi_version": ([], _i),
+    "so_last_error": ([], ctypes.c_char_p),
+    "so_me_full_search": ([_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp], _i),
+    "so_inter_tq_recon": ([_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _d, _vp, _vp, _vp, _vp,
+                           _vp, _vp, _vp], _i),
+    "so_p_frame_scratch_elems": ([_i, _i, _i, _i], _sz),
+    "so_encode_p_frame": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _d, _vp, _vp, _vp, _vp, _vp,
+                           _vp, _vp, _vp], _i),
+    "so_i_frame_scratch_elems": ([_i, _i, _i], _sz),
+    "so_encode_i_frame": ([_vp, _i, _i, _i, _i, _i, _vp, _i, _d, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                           _vp], _i),
+    "so_inter_recon": ([_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp], _i),
+    "so_intra_recon": ([_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
+    "so_sse_u8": ([_vp, _vp, ctypes.c_int64, _vp, _vp], _i),
+}
+
+EXPORTED = tuple(_SIGS)
+
+
+class HipPathError(RuntimeError):
+    """Raised when the gfx950 library is unavailable or a kernel call fails."""
+
+
+def load(path: str | None = None):
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise HipPathError(
+                f"{p} is missing: build it with `python -m streamoptima_amd.build` (hipcc, gfx950). "
+                "There is no CPU fallback for the encode path.")
+        lib = ctypes.CDLL(p)
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = res
+        if lib.so_abi_version() != 1:
+            raise HipPathError("libstreamoptima_hip.so ABI mismatch")
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != SO_OK:
+        msg = load().so_last_error().decode(errors="replace")
+        if rc == SO_E_INVALID:
+            raise ValueError(f"{what}: {msg}")
+        if rc == SO_E_UNSUPPORTED:
+            raise NotImplementedError(f"{what}: {msg}")
+        raise HipPathError(f"{what}: HIP error {rc}: {msg}")
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def ref_array(refs) -> ctypes.Array:
+    arr = (ctypes.c_void_p * len(refs))(*[r.data_ptr() for r in refs])
+    return arr
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,131 @@
+"""Text bitstream of the reference (host-side formatting of the GPU symbols).
+
+  * entropy_encoder_block   — Encoder.py:1086-1131: anti-diagonal scan, RLE tokens
+                              (-count, values... for non-zero runs, count for zero runs,
+                              a trailing zero run as a single 0).  Values keep the input's
+                              element type (np.int64 for the package arrays), so str()
+                              of the list matches the reference byte for byte.
+  * differential_encoder_frame — Encoder.py:1419-1520 (MV / QP differential line,
+                              including the reference's split-under-RC intra quirk).
+  * entropy_encoder_frame   — Encoder.py:1522-1542.
+"""
+from __future__ import annotations
+
+from functools import lru_cache
+
+import numpy as np
+
+
+@lru_cache(maxsize=8)
+def scan_order(n: int) -> np.ndarray:
+    """flat indices i*n+j in the order entropy_encoder_block visits them."""
+    order = []
+    for k in range(2 * n - 1):
+        i, j = (0, k) if k < n else (k - n + 1, n - 1)
+        while i < n and j >= 0:
+            order.append(i * n + j)
+            i += 1
+            j -= 1
+    return np.array(order, dtype=np.int64)
+
+
+def entropy_encoder_block(residual_block, block_size) -> list:
+    arr = np.asarray(residual_block)
+    vals = arr.reshape(-1)[scan_order(block_size)] if arr.ndim == 2 else arr.reshape(-1)
+    nz = vals != 0
+    out = []
+    n = len(vals)
+    if n == 0:
+        return out
+    # boundaries of maximal runs
+    change = np.flatnonzero(nz[1:] != nz[:-1]) + 1
+    starts = np.concatenate(([0], change))
+    ends = np.concatenate((change, [n]))
+    for s, e in zip(starts.tolist(), ends.tolist()):
+        if nz[s]:
+            out.append(-(e - s))
+            out.extend(vals[s:e])      # numpy scalars, like residual_block[i][j]
+        elif e == n:
+            out.append(0)
+        else:
+            out.append(e - s)
+    return out
+
+
+def token_count(residual_block, block_size) -> int:
+    vals = np.asarray(residual_block).reshape(-1)
+    nz = vals != 0
+    return int(nz.sum() + 1 + (nz[1:] != nz[:-1]).sum()) if vals.size else 0
+
+
+def differential_encoder_frame(frame_type, mv_for_frame, Qp_for_frame, rc_flag, num_blocks_per_row) -> str:
+    rc = rc_flag is not None and rc_flag > 0
+    parts = []
+    ref_qp = 0
+    diff_qp = None
+    if frame_type == 0:
+        ref = 0
+        for j, mv in enumerate(mv_for_frame):
+            rc_row = rc and j % num_blocks_per_row == 0
+            if rc_row:
+                diff_qp = Qp_for_frame[int(j // num_blocks_per_row)] - ref_qp
+            if mv[0] == 0:
+                d = mv[1] - ref
+                s = (f"{diff_qp}@0'({d})" if rc_row else f"0'({d})")
+                parts.append(s if j == 0 else ";" + s)
+                ref = mv[1]
+            else:
+                for k, sb in enumerate(mv[1]):
+                    d = sb - ref
+                    if k == 0:
+                        parts.append(f";{d}@1'({d}," if rc_row else f";1'({d},")
+                    elif k == 3:
+                        parts.append(f"{d})")
+                    else:
+                        parts.append(f"{d},")
+                    ref = sb
+            if rc_row:
+                ref_qp = Qp_for_frame[int(j // num_blocks_per_row)]
+    else:
+        ref = (0, 0, 0)
+        for j, mv in enumerate(mv_for_frame):
+            rc_row = rc and j % num_blocks_per_row == 0
+            if rc_row:
+                diff_qp = Qp_for_frame[int(j // num_blocks_per_row)] - ref_qp
+            if mv[0] == 0:
+                m = mv[1]
+                d = (m[0] - ref[0], m[1] - ref[1], m[2] - ref[2])
+                s = (f"{diff_qp}@0'{d}" if rc_row else f"0'{d}")
+                parts.append(s if j == 0 else ";" + s)
+                ref = m
+            else:
+                for k, sb in enumerate(mv[1]):
+                    d = (sb[0] - ref[0], sb[1] - ref[1], sb[2] - ref[2])
+                    if k == 0:
+                        parts.append(f";{diff_qp}@1'({d}," if rc_row else f";1'({d},")
+                    elif k == 3:
+                        parts.append(f"{d})")
+                    else:
+                        parts.append(f"{d},")
+                    ref = sb
+            if rc_row:
+                ref_qp = Qp_for_frame[int(j // num_blocks_per_row)]
+    return "".join(parts)
+
+
+def entropy_encoder_frame(frame_residuals, block_size) -> str:
+    parts = []
+    for i, residual in enumerate(frame_residuals):
+        if residual[0] == 0:
+            s = "0'(" + str(entropy_encoder_block(residual[1], block_size)) + ")"
+            parts.append(s if i == 0 else ";" + s)
+        else:
+            for k, sb in enumerate(residual[1]):
+                t = str(entropy_encoder_block(sb, block_size // 2))
+                if k == 0:
+                    parts.append(";1'(" + t + ",")
+                elif k == 3:
+                    parts.append(t + ")")
+                else:
+                    parts.append(t + ",")
+    return "".join(parts)

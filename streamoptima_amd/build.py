@@ -1,0 +1,72 @@
+"""Build libstreamoptima_hip.so (gfx950) in-tree with hipcc.
+
+The library links against the HIP runtime that PyTorch ships (torch/lib/libamdhip64.so,
+soname libamdhip64.so.7) so a process that imported torch first uses ONE HIP runtime.
+Device code is compiled with -ffp-contract=off: the FP64 DCT must keep pocketfft's
+separate multiply/add roundings to stay bit-exact with the reference (so_dct.h).
+"""
+from __future__ import annotations
+
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+LIB_NAME = "libstreamoptima_hip.so"
+LIB_PATH = os.path.join(PKG, LIB_NAME)
+ARCH = os.environ.get("SO_OFFLOAD_ARCH", "gfx950")
+
+
+def _torch_lib_dir() -> str:
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        raise RuntimeError("PyTorch (ROCm) is required to build against its HIP runtime")
+    return os.path.join(os.path.dirname(spec.origin), "lib")
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found")
+
+
+def sources() -> list[str]:
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    deps = sources() + glob.glob(os.path.join(CSRC, "*.h")) + [
+        os.path.join(os.path.dirname(PKG), "include", "streamoptima.h"), __file__]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB_PATH
+    tlib = _torch_lib_dir()
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
+           "-I", os.path.join(os.path.dirname(PKG), "include"),
+           "-o", LIB_PATH + ".tmp", *sources(),
+           f"-L{tlib}", "-lamdhip64", f"-Wl,-rpath,{tlib}"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-6000:]}")
+    if verbose and r.stderr:
+        print(r.stderr[-4000:], file=sys.stderr)
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

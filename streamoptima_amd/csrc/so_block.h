@@ -1,0 +1,255 @@
+// so_block.h — per-block transform pipeline shared by the P-frame, I-frame and decoder
+// kernels.  One block is owned by a group of G lanes inside one wavefront (G = 16 for
+// 16x16 blocks, 8 for 8x8), so all cross-lane exchange stays inside the wave: LDS
+// transposes ordered by wavefront-scope fences, reductions by __shfl_xor.
+//
+// Lane l of a 16x16 group owns block row l:   residual row -> LDS -> column l -> DCT-II
+// -> LDS -> row l -> DCT-II -> rint (apply_2d_dct, Encoder.py:779-784) -> quantise
+// (quantize_TC :787) -> token count (entropy_encoder_block :1086 length) ...
+// For VBS the same 16 lanes run the four 8x8 sub-blocks: lane l owns sub-block
+// j = l >> 2, rows/cols (l & 3) and (l & 3) + 4.
+#pragma once
+#include "so_common.h"
+#include "so_dct.h"
+
+namespace so {
+
+SO_DEV void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// scan position of (i, j) in the anti-diagonal order of entropy_encoder_block
+SO_DEV int scan_index(int n, int i, int j) {
+    const int k = i + j;
+    const int before = (k < n) ? (k * (k + 1)) / 2 : n * n - ((2 * n - 1 - k) * (2 * n - k)) / 2;
+    const int first_i = (k < n) ? 0 : k - n + 1;
+    return before + (i - first_i);
+}
+
+template <int G>
+SO_DEV int group_sum(int v) {
+#pragma unroll
+    for (int m = G / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+
+// ---- byte row fetch ----------------------------------------------------------------------
+// NB bytes of frame row `py` starting at column px.  `fast` == the reference's strict
+// in-bounds test held (0 <= px < W-bs, 0 <= py0 < H-bs), so the 4-byte-aligned words
+// read below stay inside the frame buffer; otherwise handle_boundary_conditions
+// (Encoder.py:750-768): zero-filled partial copy.
+template <int NB>
+SO_DEV void fetch_row(const uint8_t* __restrict__ f, int W, int H, int px, int py, bool fast, int* out) {
+    if (fast) {
+        const uint8_t* p = f + (size_t)py * W + px;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(a & 3);
+        uint32_t w[NB / 4 + 1];
+#pragma unroll
+        for (int k = 0; k <= NB / 4; ++k) w[k] = q[k];
+#pragma unroll
+        for (int k = 0; k < NB / 4; ++k) {
+            uint32_t v = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+            out[4 * k + 0] = v & 255;
+            out[4 * k + 1] = (v >> 8) & 255;
+            out[4 * k + 2] = (v >> 16) & 255;
+            out[4 * k + 3] = v >> 24;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            const int xx = px + k;
+            out[k] = (py >= 0 && py < H && xx >= 0 && xx < W) ? f[(size_t)py * W + xx] : 0;
+        }
+    }
+}
+
+// aligned row of the current frame (x multiple of NB, W multiple of NB)
+template <int NB>
+SO_DEV void load_cur_row(const uint8_t* __restrict__ f, int W, int x, int y, int* out) {
+    const uint8_t* p = f + (size_t)y * W + x;
+    if constexpr (NB == 16) {
+        uint4 v = *reinterpret_cast<const uint4*>(p);
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) out[k] = (w[k >> 2] >> (8 * (k & 3))) & 255;
+    } else {
+        uint2 v = *reinterpret_cast<const uint2*>(p);
+        uint32_t w[2] = {v.x, v.y};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) out[k] = (w[k >> 2] >> (8 * (k & 3))) & 255;
+    }
+}
+
+template <int NB>
+SO_DEV void store_row_u8(uint8_t* __restrict__ f, int W, int x, int y, const int* v) {
+    uint32_t w[NB / 4];
+#pragma unroll
+    for (int k = 0; k < NB / 4; ++k)
+        w[k] = (uint32_t)(v[4 * k] & 255) | ((uint32_t)(v[4 * k + 1] & 255) << 8) |
+               ((uint32_t)(v[4 * k + 2] & 255) << 16) | ((uint32_t)(v[4 * k + 3] & 255) << 24);
+    uint8_t* p = f + (size_t)y * W + x;
+    if constexpr (NB == 16) *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+    else *reinterpret_cast<uint2*>(p) = make_uint2(w[0], w[1]);
+}
+
+template <int NB>
+SO_DEV void store_row_i16(int16_t* __restrict__ p, const int* v) {
+    uint32_t w[NB / 2];
+#pragma unroll
+    for (int k = 0; k < NB / 2; ++k) w[k] = (uint32_t)(uint16_t)v[2 * k] | ((uint32_t)(uint16_t)v[2 * k + 1] << 16);
+    if constexpr (NB == 16) {
+        reinterpret_cast<uint4*>(p)[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        reinterpret_cast<uint4*>(p)[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    } else {
+        reinterpret_cast<uint4*>(p)[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+template <int NB>
+SO_DEV void load_row_i16(const int16_t* __restrict__ p, int* v) {
+    uint32_t w[NB / 2];
+    if constexpr (NB == 16) {
+        uint4 a = reinterpret_cast<const uint4*>(p)[0], b = reinterpret_cast<const uint4*>(p)[1];
+        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+    } else {
+        uint4 a = reinterpret_cast<const uint4*>(p)[0];
+        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+    }
+#pragma unroll
+    for (int k = 0; k < NB / 2; ++k) {
+        v[2 * k] = (int)(int16_t)(w[k] & 0xFFFF);
+        v[2 * k + 1] = (int)(int16_t)(w[k] >> 16);
+    }
+}
+
+// ---- 2-D transforms through LDS --------------------------------------------------------------
+// N x N transform of one block by N lanes (lane l owns row l on input and output).
+// lds: N rows of pitch N+1 doubles owned by this lane group.
+template <int N, bool INVERSE>
+SO_DEV void xform2d_rows(double* lds, int l, const int* in_row, double* out_row) {
+    constexpr int P = N + 1;
+#pragma unroll
+    for (int c = 0; c < N; ++c) lds[l * P + c] = (double)in_row[c];
+    wave_sync();
+    double v[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) v[r] = lds[r * P + l];
+    if constexpr (INVERSE) dct::dct3<N>(v); else dct::dct2<N>(v);   // axis 0 (columns)
+#pragma unroll
+    for (int r = 0; r < N; ++r) lds[r * P + l] = v[r];
+    wave_sync();
+#pragma unroll
+    for (int c = 0; c < N; ++c) v[c] = lds[l * P + c];
+    if constexpr (INVERSE) dct::dct3<N>(v); else dct::dct2<N>(v);   // axis 1 (rows)
+#pragma unroll
+    for (int c = 0; c < N; ++c) out_row[c] = v[c];
+    wave_sync();   // lds free for reuse
+}
+
+// Four 8x8 sub-blocks by 16 lanes: lane l owns sub-block j = l >> 2 and rows
+// (l & 3), (l & 3) + 4 on input and output.  lds: 4 x 8 x 9 doubles.
+template <bool INVERSE>
+SO_DEV void xform2d_sub(double* lds, int l, const int (&in)[2][8], double (&out)[2][8]) {
+    const int j = l >> 2, r0 = l & 3;
+    double* s = lds + j * 72;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) s[(r0 + 4 * h) * 9 + c] = (double)in[h][c];
+    wave_sync();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        double v[8];
+        const int col = r0 + 4 * h;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] = s[r * 9 + col];
+        if constexpr (INVERSE) dct::dct3<8>(v); else dct::dct2<8>(v);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) s[r * 9 + col] = v[r];
+    }
+    wave_sync();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        double v[8];
+        const int row = r0 + 4 * h;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = s[row * 9 + c];
+        if constexpr (INVERSE) dct::dct3<8>(v); else dct::dct2<8>(v);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) out[h][c] = v[c];
+    }
+    wave_sync();
+}
+
+// ---- quantisation + tokens ------------------------------------------------------------------
+// quantise row `row` of an n x n block: q = round_half_even(tc / 2^q_exp)
+template <int N>
+SO_DEV void quant_row(const int* tc, int row, int qp, int* q) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) q[c] = quant_rne(tc[c], q_exp(row, c, N, qp));
+}
+
+template <int N>
+SO_DEV void dequant_row(const int* q, int row, int qp, int* d) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) d[c] = q[c] * (1 << q_exp(row, c, N, qp));
+}
+
+// Token count of an N x N block (N lanes, lane l owns row l) = nnz + number of maximal
+// runs in anti-diagonal scan order (entropy_encoder_block emits one token per zero run,
+// one count token per non-zero run, and one token per non-zero value).
+// flags: N*N bytes of LDS owned by the group.
+template <int N>
+SO_DEV int block_tokens(uint8_t* flags, int l, const int* q) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) flags[scan_index(N, l, c)] = q[c] != 0;
+    wave_sync();
+    int nnz = 0, tr = 0;
+    int prev = flags[l == 0 ? 0 : l * N - 1];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const int f = flags[l * N + k];
+        nnz += f;
+        tr += (f != prev);
+        prev = f;
+    }
+    wave_sync();
+    return group_sum<N>(nnz + tr) + 1;
+}
+
+// Token counts of the four 8x8 sub-blocks (16 lanes, lane l owns sub j = l>>2, rows
+// (l&3), (l&3)+4).  Returns the sum over the 4 sub-blocks (RD bits and residual_size).
+SO_DEV int sub_tokens(uint8_t* flags, int l, const int (&q)[2][8]) {
+    const int j = l >> 2, r0 = l & 3;
+    uint8_t* s = flags + j * 64;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) s[scan_index(8, r0 + 4 * h, c)] = q[h][c] != 0;
+    wave_sync();
+    int nnz = 0, tr = 0;
+    const int base = r0 * 16;
+    int prev = s[base == 0 ? 0 : base - 1];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int f = s[base + k];
+        nnz += f;
+        tr += (f != prev);
+        prev = f;
+    }
+    wave_sync();
+    return group_sum<16>(nnz + tr) + 4;
+}
+
+// calculate_RD_cost (Encoder.py:1133-1158): lam * bits + mae, two roundings (no FMA:
+// this translation unit is compiled with -ffp-contract=off).
+SO_DEV double rd_cost(double lam, int bits, double mae) {
+    const double lb = lam * (double)bits;
+    return lb + mae;
+}
+
+}  // namespace so

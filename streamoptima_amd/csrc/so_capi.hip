@@ -1,0 +1,259 @@
+// so_capi.hip — the extern "C" boundary of libstreamoptima_hip.so (include/streamoptima.h).
+// Argument validation, thread-local error text, launches; no device allocation, no host
+// synchronisation (every entry point is capturable into a hipGraph).
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "so_common.h"
+
+namespace so {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, int bs, int sr,
+              int32_t* out_best, int32_t* out_sub, hipStream_t st);
+int inter_tq_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int bs, const int32_t* best,
+                    const int32_t* sub, int qp_rd, const int32_t* qp_row, int vbs, double lam,
+                    uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
+                    int32_t* out_mae, uint8_t* out_recon, hipStream_t st);
+int inter_recon_launch(const RefSet& refs, int H, int W, int bs, int qp, const int32_t* qp_row,
+                       const uint8_t* split, const int16_t* mv, const int16_t* qtc, uint8_t* out_recon,
+                       hipStream_t st);
+int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int qp_rd, const int32_t* qp_row,
+                        int vbs, double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc,
+                        int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon, int32_t* idres,
+                        hipStream_t st);
+int intra_recon_launch(int H, int W, int bs, int sr, int qp, const int32_t* qp_row, const uint8_t* split,
+                       const int16_t* mv, const int16_t* qtc, uint8_t* out_recon, int32_t* idres,
+                       hipStream_t st);
+
+// ---- validation ------------------------------------------------------------------------------
+static int check_geom(const char* fn, int H, int W, int bs, int vbs) {
+    if (bs != 16 && bs != 8) {
+        set_error("%s: block_size %d not built (gfx950 kernels exist for 16 and 8)", fn, bs);
+        return SO_E_UNSUPPORTED;
+    }
+    if (vbs && bs != 16) {
+        set_error("%s: VBSEnable needs block_size 16 (8x8 sub-blocks)", fn);
+        return SO_E_UNSUPPORTED;
+    }
+    if (H <= 0 || W <= 0 || H % bs || W % bs) {
+        set_error("%s: frame %dx%d must be a positive multiple of block_size %d (pad with pad_hw)", fn, W, H, bs);
+        return SO_E_INVALID;
+    }
+    if ((long long)H * W > (1ll << 31)) {
+        set_error("%s: frame too large", fn);
+        return SO_E_INVALID;
+    }
+    return SO_OK;
+}
+
+static int check_sr(const char* fn, int sr) {
+    if (sr < 0 || sr > 64) {
+        set_error("%s: search_range %d outside [0, 64]", fn, sr);
+        return SO_E_UNSUPPORTED;
+    }
+    return SO_OK;
+}
+
+static int check_qp(const char* fn, int qp) {
+    if (qp < 0 || qp > 20) {
+        set_error("%s: Qp %d outside [0, 20]", fn, qp);
+        return SO_E_INVALID;
+    }
+    return SO_OK;
+}
+
+static int make_refs(const char* fn, const uint8_t* const* refs, int nref, RefSet* rs) {
+    if (refs == nullptr || nref < 1 || nref > kMaxRef) {
+        set_error("%s: nref %d outside [1, %d]", fn, nref, kMaxRef);
+        return SO_E_INVALID;
+    }
+    for (int i = 0; i < kMaxRef; ++i) rs->p[i] = i < nref ? refs[i] : refs[0];
+    for (int i = 0; i < nref; ++i)
+        if (!refs[i]) {
+            set_error("%s: refs[%d] is NULL", fn, i);
+            return SO_E_INVALID;
+        }
+    return SO_OK;
+}
+
+#define SO_TRY(x)                 \
+    do {                          \
+        int _rc = (x);            \
+        if (_rc != SO_OK) return _rc; \
+    } while (0)
+
+#define SO_NEED(p, fn)                                  \
+    do {                                                \
+        if (!(p)) {                                     \
+            set_error("%s: %s is NULL", fn, #p);        \
+            return SO_E_INVALID;                        \
+        }                                               \
+    } while (0)
+
+// ---- SSE (PSNR) -------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) sse_kernel(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b,
+                                                  int64_t n, unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long part[4];
+    unsigned long long acc = 0;
+    const int64_t n16 = n / 16;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+        const uint4 va = reinterpret_cast<const uint4*>(a)[i];
+        const uint4 vb = reinterpret_cast<const uint4*>(b)[i];
+        const uint32_t wa[4] = {va.x, va.y, va.z, va.w}, wb[4] = {vb.x, vb.y, vb.z, vb.w};
+        uint32_t s = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int d = (int)((wa[k] >> (8 * e)) & 255) - (int)((wb[k] >> (8 * e)) & 255);
+                s += (uint32_t)(d * d);
+            }
+        acc += s;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (int64_t i = n16 * 16; i < n; ++i) {
+            const int d = (int)a[i] - (int)b[i];
+            acc += (unsigned long long)(d * d);
+        }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(out, part[0] + part[1] + part[2] + part[3]);
+}
+
+}  // namespace so
+
+using namespace so;
+
+extern "C" {
+
+int so_abi_version(void) { return SO_ABI_VERSION; }
+
+const char* so_last_error(void) { return g_err; }
+
+int so_me_full_search(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W, int bs,
+                      int sr, int32_t* out_best, int32_t* out_sub, void* stream) {
+    const char* fn = "so_me_full_search";
+    SO_TRY(check_geom(fn, H, W, bs, out_sub != nullptr));
+    SO_TRY(check_sr(fn, sr));
+    SO_NEED(cur, fn);
+    SO_NEED(out_best, fn);
+    RefSet rs;
+    SO_TRY(make_refs(fn, refs, nref, &rs));
+    return me_launch(cur, rs, nref, H, W, bs, sr, out_best, out_sub, (hipStream_t)stream);
+}
+
+int so_inter_tq_recon(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W, int bs,
+                      const int32_t* best, const int32_t* sub, int qp_rd, const int32_t* qp_row, int vbs,
+                      double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
+                      int32_t* out_mae_num, uint8_t* out_recon, void* stream) {
+    const char* fn = "so_inter_tq_recon";
+    SO_TRY(check_geom(fn, H, W, bs, vbs));
+    SO_TRY(check_qp(fn, qp_rd));
+    SO_NEED(cur, fn); SO_NEED(best, fn); SO_NEED(out_split, fn); SO_NEED(out_mv, fn);
+    SO_NEED(out_qtc, fn); SO_NEED(out_tokens, fn); SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn);
+    if (vbs) SO_NEED(sub, fn);
+    RefSet rs;
+    SO_TRY(make_refs(fn, refs, nref, &rs));
+    for (int i = 0; i < nref; ++i)
+        if (refs[i] == out_recon) {
+            set_error("%s: out_recon aliases refs[%d]", fn, i);
+            return SO_E_INVALID;
+        }
+    return inter_tq_launch(cur, rs, H, W, bs, best, vbs ? sub : nullptr, qp_rd, qp_row, vbs, lam, out_split,
+                           out_mv, out_qtc, out_tokens, out_mae_num, out_recon, (hipStream_t)stream);
+}
+
+size_t so_p_frame_scratch_elems(int H, int W, int bs, int vbs) {
+    if (bs <= 0) return 0;
+    const size_t nb = (size_t)(W / bs) * (size_t)(H / bs);
+    return nb * 4 + (vbs ? nb * 16 : 0);
+}
+
+int so_encode_p_frame(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W, int bs, int sr,
+                      int qp_rd, const int32_t* qp_row, int vbs, double lam, uint8_t* out_split,
+                      int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae_num,
+                      uint8_t* out_recon, int32_t* scratch, void* stream) {
+    const char* fn = "so_encode_p_frame";
+    SO_TRY(check_geom(fn, H, W, bs, vbs));
+    SO_NEED(scratch, fn);
+    const size_t nb = (size_t)(W / bs) * (size_t)(H / bs);
+    int32_t* best = scratch;
+    int32_t* sub = vbs ? scratch + nb * 4 : nullptr;
+    SO_TRY(so_me_full_search(cur, refs, nref, H, W, bs, sr, best, sub, stream));
+    return so_inter_tq_recon(cur, refs, nref, H, W, bs, best, sub, qp_rd, qp_row, vbs, lam, out_split, out_mv,
+                             out_qtc, out_tokens, out_mae_num, out_recon, stream);
+}
+
+size_t so_i_frame_scratch_elems(int H, int W, int bs) {
+    if (bs <= 0) return 0;
+    const size_t nb = (size_t)(W / bs) * (size_t)(H / bs);
+    return nb * (size_t)bs * bs + nb * 8;
+}
+
+int so_encode_i_frame(const uint8_t* cur, int H, int W, int bs, int sr, int qp_rd, const int32_t* qp_row,
+                      int vbs, double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc,
+                      int32_t* out_tokens, int32_t* out_mae_num, uint8_t* out_recon, int32_t* scratch,
+                      void* stream) {
+    const char* fn = "so_encode_i_frame";
+    SO_TRY(check_geom(fn, H, W, bs, vbs));
+    SO_TRY(check_sr(fn, sr));
+    SO_TRY(check_qp(fn, qp_rd));
+    SO_NEED(cur, fn); SO_NEED(out_split, fn); SO_NEED(out_mv, fn); SO_NEED(out_qtc, fn);
+    SO_NEED(out_tokens, fn); SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn); SO_NEED(scratch, fn);
+    return intra_encode_launch(cur, H, W, bs, sr, qp_rd, qp_row, vbs, lam, out_split, out_mv, out_qtc, out_tokens,
+                               out_mae_num, out_recon, scratch, (hipStream_t)stream);
+}
+
+int so_inter_recon(const uint8_t* const* refs, int nref, int H, int W, int bs, int qp, const int32_t* qp_row,
+                   const uint8_t* split, const int16_t* mv, const int16_t* qtc, uint8_t* out_recon, void* stream) {
+    const char* fn = "so_inter_recon";
+    SO_TRY(check_geom(fn, H, W, bs, 0));
+    SO_TRY(check_qp(fn, qp));
+    SO_NEED(split, fn); SO_NEED(mv, fn); SO_NEED(qtc, fn); SO_NEED(out_recon, fn);
+    RefSet rs;
+    SO_TRY(make_refs(fn, refs, nref, &rs));
+    return inter_recon_launch(rs, H, W, bs, qp, qp_row, split, mv, qtc, out_recon, (hipStream_t)stream);
+}
+
+int so_intra_recon(int H, int W, int bs, int qp, const int32_t* qp_row, const uint8_t* split, const int16_t* mv,
+                   const int16_t* qtc, uint8_t* out_recon, int32_t* scratch, void* stream) {
+    const char* fn = "so_intra_recon";
+    SO_TRY(check_geom(fn, H, W, bs, 0));
+    SO_TRY(check_qp(fn, qp));
+    SO_NEED(split, fn); SO_NEED(mv, fn); SO_NEED(qtc, fn); SO_NEED(out_recon, fn); SO_NEED(scratch, fn);
+    // the recon kernel only needs sr to size its ring: the largest reachable offset is 64
+    return intra_recon_launch(H, W, bs, 64, qp, qp_row, split, mv, qtc, out_recon, scratch, (hipStream_t)stream);
+}
+
+int so_sse_u8(const uint8_t* a, const uint8_t* b, int64_t n, uint64_t* out_sse, void* stream) {
+    const char* fn = "so_sse_u8";
+    SO_NEED(a, fn); SO_NEED(b, fn); SO_NEED(out_sse, fn);
+    if (n < 0) {
+        set_error("%s: n < 0", fn);
+        return SO_E_INVALID;
+    }
+    if ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) {
+        set_error("%s: planes must be 16-byte aligned", fn);
+        return SO_E_INVALID;
+    }
+    int64_t blocks = (n / 16 + 255) / 256;
+    if (blocks < 1) blocks = 1;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(sse_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a, b, n,
+                       reinterpret_cast<unsigned long long*>(out_sse));
+    return check_launch("sse_kernel");
+}
+
+}  // extern "C"

@@ -1,0 +1,306 @@
+// so_dct.h — FP64 DCT-II / DCT-III for gfx950 that is BITWISE identical to
+// scipy.fftpack.dct/idct(norm='ortho') (the reference's apply_2d_dct / apply_2d_idct,
+// Encoder.py:779-817, decoder.py:455-462).
+//
+// scipy.fftpack reaches pocketfft (C++, inside SciPy 1.15.3): T_dcst23 folds the DCT into
+// a length-N real FFT (rfftp) made of radix-4 / radix-2 passes.  A DCT coefficient that
+// is mathematically an exact .5 (e.g. the DC term when the block sum == 8 mod 16) is
+// rounded by np.round on whichever side pocketfft's own float64 error lands, so matching
+// the reference bit-for-bit requires the same operations in the same order with the same
+// (not correctly rounded) twiddles.  Everything below is straight-line code after
+// unrolling; the kernels are compiled with -ffp-contract=off so no FMA contraction can
+// change a rounding.
+//
+// N = 16: rfftp factors [4, 4];  N = 8: [2, 4].  One lane transforms one length-N vector
+// held in registers.
+#pragma once
+#include "so_common.h"
+
+namespace so {
+namespace dct {
+
+// pocketfft T_dcst23 twiddle[i] ~= cos(pi (i+1) / (2N)) (4N-point sincos table values)
+struct TW16 {
+    static SO_DEV double dct(int i) {
+        constexpr double t[15] = {
+            0x1.fd88da3d12526p-1, 0x1.f6297cff75cb0p-1, 0x1.e9f4156c62ddap-1, 0x1.d906bcf328d46p-1,
+            0x1.c38b2f180bdb1p-1, 0x1.a9b66290ea1a3p-1, 0x1.8bc806b151741p-1, 0x1.6a09e667f3bccp-1,
+            0x1.44cf325091dd6p-1, 0x1.1c73b39ae68c8p-1, 0x1.e2b5d3806f639p-2, 0x1.87de2a6aea961p-2,
+            0x1.294062ed59f04p-2, 0x1.8f8b83c69a60ap-3, 0x1.917a6bc29b424p-4};
+        return t[i];
+    }
+    // rfftp first-factor twiddles, pocketfft layout wa[i + x*(ido-1)], ido = 4
+    static SO_DEV double rf(int i) {
+        constexpr double t[9] = {
+            0x1.d906bcf328d46p-1, 0x1.87de2a6aea963p-2, 0.0,
+            0x1.6a09e667f3bccp-1, 0x1.6a09e667f3bcdp-1, 0.0,
+            0x1.87de2a6aea963p-2, 0x1.d906bcf328d46p-1, 0.0};
+        return t[i];
+    }
+    static constexpr double fct = 0x1.6a09e667f3bcdp-3;  // T(1/sqrt(32))
+};
+struct TW8 {
+    static SO_DEV double dct(int i) {
+        constexpr double t[7] = {
+            0x1.f6297cff75cb0p-1, 0x1.d906bcf328d46p-1, 0x1.a9b66290ea1a3p-1, 0x1.6a09e667f3bccp-1,
+            0x1.1c73b39ae68c8p-1, 0x1.87de2a6aea963p-2, 0x1.8f8b83c69a60ap-3};
+        return t[i];
+    }
+    static SO_DEV double rf(int i) {
+        constexpr double t[2] = {0x1.6a09e667f3bccp-1, 0x1.6a09e667f3bcdp-1};
+        return t[i];
+    }
+    static constexpr double fct = 0x1.0p-2;  // T(1/sqrt(16))
+};
+
+constexpr double kSqrt2 = 0x1.6a09e667f3bcdp+0;
+constexpr double kHsqt2 = 0x1.6a09e667f3bcdp-1;
+
+#define SO_PM(a, b, c, d) { a = (c) + (d); b = (c) - (d); }
+#define SO_MULPM(a, b, c, d, e, f) { a = (c) * (e) + (d) * (f); b = (c) * (f) - (d) * (e); }
+
+// ---- real-FFT passes (radix 2 / radix 4), compile-time ido / l1 ----------------------
+template <int IDO, int L1, class TW>
+SO_DEV void radf2(const double* cc, double* ch) {
+#define CC(a, b, c) cc[(a) + IDO * ((b) + L1 * (c))]
+#define CH(a, b, c) ch[(a) + IDO * ((b) + 2 * (c))]
+#define WA(x, i) TW::rf((i) + (x) * (IDO - 1))
+#pragma unroll
+    for (int k = 0; k < L1; k++) SO_PM(CH(0, 0, k), CH(IDO - 1, 1, k), CC(0, k, 0), CC(0, k, 1));
+    if constexpr ((IDO & 1) == 0) {
+#pragma unroll
+        for (int k = 0; k < L1; k++) {
+            CH(0, 1, k) = -CC(IDO - 1, k, 1);
+            CH(IDO - 1, 0, k) = CC(IDO - 1, k, 0);
+        }
+    }
+    if constexpr (IDO > 2) {
+#pragma unroll
+        for (int k = 0; k < L1; k++)
+#pragma unroll
+            for (int i = 2; i < IDO; i += 2) {
+                const int ic = IDO - i;
+                double tr2, ti2;
+                SO_MULPM(tr2, ti2, WA(0, i - 2), WA(0, i - 1), CC(i - 1, k, 1), CC(i, k, 1));
+                SO_PM(CH(i - 1, 0, k), CH(ic - 1, 1, k), CC(i - 1, k, 0), tr2);
+                SO_PM(CH(i, 0, k), CH(ic, 1, k), ti2, CC(i, k, 0));
+            }
+    }
+#undef CC
+#undef CH
+}
+
+template <int IDO, int L1, class TW>
+SO_DEV void radf4(const double* cc, double* ch) {
+#define CC(a, b, c) cc[(a) + IDO * ((b) + L1 * (c))]
+#define CH(a, b, c) ch[(a) + IDO * ((b) + 4 * (c))]
+#pragma unroll
+    for (int k = 0; k < L1; k++) {
+        double tr1, tr2;
+        SO_PM(tr1, CH(0, 2, k), CC(0, k, 3), CC(0, k, 1));
+        SO_PM(tr2, CH(IDO - 1, 1, k), CC(0, k, 0), CC(0, k, 2));
+        SO_PM(CH(0, 0, k), CH(IDO - 1, 3, k), tr2, tr1);
+    }
+    if constexpr ((IDO & 1) == 0) {
+#pragma unroll
+        for (int k = 0; k < L1; k++) {
+            double ti1 = -kHsqt2 * (CC(IDO - 1, k, 1) + CC(IDO - 1, k, 3));
+            double tr1 = kHsqt2 * (CC(IDO - 1, k, 1) - CC(IDO - 1, k, 3));
+            SO_PM(CH(IDO - 1, 0, k), CH(IDO - 1, 2, k), CC(IDO - 1, k, 0), tr1);
+            SO_PM(CH(0, 3, k), CH(0, 1, k), ti1, CC(IDO - 1, k, 2));
+        }
+    }
+    if constexpr (IDO > 2) {
+#pragma unroll
+        for (int k = 0; k < L1; k++)
+#pragma unroll
+            for (int i = 2; i < IDO; i += 2) {
+                const int ic = IDO - i;
+                double ci2, ci3, ci4, cr2, cr3, cr4, ti1, ti2, ti3, ti4, tr1, tr2, tr3, tr4;
+                SO_MULPM(cr2, ci2, WA(0, i - 2), WA(0, i - 1), CC(i - 1, k, 1), CC(i, k, 1));
+                SO_MULPM(cr3, ci3, WA(1, i - 2), WA(1, i - 1), CC(i - 1, k, 2), CC(i, k, 2));
+                SO_MULPM(cr4, ci4, WA(2, i - 2), WA(2, i - 1), CC(i - 1, k, 3), CC(i, k, 3));
+                SO_PM(tr1, tr4, cr4, cr2);
+                SO_PM(ti1, ti4, ci2, ci4);
+                SO_PM(tr2, tr3, CC(i - 1, k, 0), cr3);
+                SO_PM(ti2, ti3, CC(i, k, 0), ci3);
+                SO_PM(CH(i - 1, 0, k), CH(ic - 1, 3, k), tr2, tr1);
+                SO_PM(CH(i, 0, k), CH(ic, 3, k), ti1, ti2);
+                SO_PM(CH(i - 1, 2, k), CH(ic - 1, 1, k), tr3, ti4);
+                SO_PM(CH(i, 2, k), CH(ic, 1, k), tr4, ti3);
+            }
+    }
+#undef CC
+#undef CH
+}
+
+template <int IDO, int L1, class TW>
+SO_DEV void radb2(const double* cc, double* ch) {
+#define CC(a, b, c) cc[(a) + IDO * ((b) + 2 * (c))]
+#define CH(a, b, c) ch[(a) + IDO * ((b) + L1 * (c))]
+#pragma unroll
+    for (int k = 0; k < L1; k++) SO_PM(CH(0, k, 0), CH(0, k, 1), CC(0, 0, k), CC(IDO - 1, 1, k));
+    if constexpr ((IDO & 1) == 0) {
+#pragma unroll
+        for (int k = 0; k < L1; k++) {
+            CH(IDO - 1, k, 0) = 2.0 * CC(IDO - 1, 0, k);
+            CH(IDO - 1, k, 1) = -2.0 * CC(0, 1, k);
+        }
+    }
+    if constexpr (IDO > 2) {
+#pragma unroll
+        for (int k = 0; k < L1; ++k)
+#pragma unroll
+            for (int i = 2; i < IDO; i += 2) {
+                const int ic = IDO - i;
+                double ti2, tr2;
+                SO_PM(CH(i - 1, k, 0), tr2, CC(i - 1, 0, k), CC(ic - 1, 1, k));
+                SO_PM(ti2, CH(i, k, 0), CC(i, 0, k), CC(ic, 1, k));
+                SO_MULPM(CH(i, k, 1), CH(i - 1, k, 1), WA(0, i - 2), WA(0, i - 1), ti2, tr2);
+            }
+    }
+#undef CC
+#undef CH
+}
+
+template <int IDO, int L1, class TW>
+SO_DEV void radb4(const double* cc, double* ch) {
+#define CC(a, b, c) cc[(a) + IDO * ((b) + 4 * (c))]
+#define CH(a, b, c) ch[(a) + IDO * ((b) + L1 * (c))]
+#pragma unroll
+    for (int k = 0; k < L1; k++) {
+        double tr1, tr2;
+        SO_PM(tr2, tr1, CC(0, 0, k), CC(IDO - 1, 3, k));
+        double tr3 = 2.0 * CC(IDO - 1, 1, k);
+        double tr4 = 2.0 * CC(0, 2, k);
+        SO_PM(CH(0, k, 0), CH(0, k, 2), tr2, tr3);
+        SO_PM(CH(0, k, 3), CH(0, k, 1), tr1, tr4);
+    }
+    if constexpr ((IDO & 1) == 0) {
+#pragma unroll
+        for (int k = 0; k < L1; k++) {
+            double tr1, tr2, ti1, ti2;
+            SO_PM(ti1, ti2, CC(0, 3, k), CC(0, 1, k));
+            SO_PM(tr2, tr1, CC(IDO - 1, 0, k), CC(IDO - 1, 2, k));
+            CH(IDO - 1, k, 0) = tr2 + tr2;
+            CH(IDO - 1, k, 1) = kSqrt2 * (tr1 - ti1);
+            CH(IDO - 1, k, 2) = ti2 + ti2;
+            CH(IDO - 1, k, 3) = -kSqrt2 * (tr1 + ti1);
+        }
+    }
+    if constexpr (IDO > 2) {
+#pragma unroll
+        for (int k = 0; k < L1; ++k)
+#pragma unroll
+            for (int i = 2; i < IDO; i += 2) {
+                double ci2, ci3, ci4, cr2, cr3, cr4, ti1, ti2, ti3, ti4, tr1, tr2, tr3, tr4;
+                const int ic = IDO - i;
+                SO_PM(tr2, tr1, CC(i - 1, 0, k), CC(ic - 1, 3, k));
+                SO_PM(ti1, ti2, CC(i, 0, k), CC(ic, 3, k));
+                SO_PM(tr4, ti3, CC(i, 2, k), CC(ic, 1, k));
+                SO_PM(tr3, ti4, CC(i - 1, 2, k), CC(ic - 1, 1, k));
+                SO_PM(CH(i - 1, k, 0), cr3, tr2, tr3);
+                SO_PM(CH(i, k, 0), ci3, ti2, ti3);
+                SO_PM(cr4, cr2, tr1, tr4);
+                SO_PM(ci2, ci4, ti1, ti4);
+                SO_MULPM(CH(i, k, 1), CH(i - 1, k, 1), WA(0, i - 2), WA(0, i - 1), ci2, cr2);
+                SO_MULPM(CH(i, k, 2), CH(i - 1, k, 2), WA(1, i - 2), WA(1, i - 1), ci3, cr3);
+                SO_MULPM(CH(i, k, 3), CH(i - 1, k, 3), WA(2, i - 2), WA(2, i - 1), ci4, cr4);
+            }
+    }
+#undef CC
+#undef CH
+#undef WA
+}
+
+// halfcomplex -> real (unscaled), then copy_and_norm(fct)
+template <int N> struct Rfft;
+template <> struct Rfft<16> {
+    using TW = TW16;
+    static SO_DEV void backward(double* c) {
+        double ch[16];
+        radb4<4, 1, TW16>(c, ch);
+        radb4<1, 4, TW16>(ch, c);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) c[i] *= TW16::fct;
+    }
+    static SO_DEV void forward(double* c) {
+        double ch[16];
+        radf4<1, 4, TW16>(c, ch);
+        radf4<4, 1, TW16>(ch, c);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) c[i] *= TW16::fct;
+    }
+};
+template <> struct Rfft<8> {
+    using TW = TW8;
+    static SO_DEV void backward(double* c) {
+        double ch[8];
+        radb2<4, 1, TW8>(c, ch);
+        radb4<1, 2, TW8>(ch, c);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) c[i] *= TW8::fct;
+    }
+    static SO_DEV void forward(double* c) {
+        double ch[8];
+        radf4<1, 2, TW8>(c, ch);
+        radf2<4, 1, TW8>(ch, c);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) c[i] *= TW8::fct;
+    }
+};
+
+// DCT-II, ortho (pocketfft T_dcst23::exec type 2, cosine)
+template <int N>
+SO_DEV void dct2(double* c) {
+    using TW = typename Rfft<N>::TW;
+    constexpr int NS2 = (N + 1) / 2;
+    c[0] *= 2;
+    c[N - 1] *= 2;
+#pragma unroll
+    for (int k = 1; k < N - 1; k += 2) {
+        double t = c[k + 1];
+        c[k + 1] -= c[k];
+        c[k] += t;
+    }
+    Rfft<N>::backward(c);
+#pragma unroll
+    for (int k = 1; k < NS2; ++k) {
+        const int kc = N - k;
+        double t1 = TW::dct(k - 1) * c[kc] + TW::dct(kc - 1) * c[k];
+        double t2 = TW::dct(k - 1) * c[k] - TW::dct(kc - 1) * c[kc];
+        c[k] = 0.5 * (t1 + t2);
+        c[kc] = 0.5 * (t1 - t2);
+    }
+    c[NS2] *= TW::dct(NS2 - 1);
+    c[0] *= kSqrt2 * 0.5;
+}
+
+// DCT-III, ortho (pocketfft T_dcst23::exec type 3, cosine)
+template <int N>
+SO_DEV void dct3(double* c) {
+    using TW = typename Rfft<N>::TW;
+    constexpr int NS2 = (N + 1) / 2;
+    c[0] *= kSqrt2;
+#pragma unroll
+    for (int k = 1; k < NS2; ++k) {
+        const int kc = N - k;
+        double t1 = c[k] + c[kc], t2 = c[k] - c[kc];
+        c[k] = TW::dct(k - 1) * t2 + TW::dct(kc - 1) * t1;
+        c[kc] = TW::dct(k - 1) * t1 - TW::dct(kc - 1) * t2;
+    }
+    c[NS2] *= 2 * TW::dct(NS2 - 1);
+    Rfft<N>::forward(c);
+#pragma unroll
+    for (int k = 1; k < N - 1; k += 2) {
+        double t = c[k];
+        c[k] -= c[k + 1];
+        c[k + 1] += t;
+    }
+}
+
+#undef SO_PM
+#undef SO_MULPM
+
+}  // namespace dct
+}  // namespace so

@@ -1,0 +1,282 @@
+// so_me.hip — full-search integer-pel motion estimation for gfx950.
+//
+// Replaces find_best_match / compute_mae / is_better_mv (Encoder.py:678-717, 314-315,
+// 771-773).  Semantics reproduced exactly:
+//   * candidates dx, dy in [-sr, sr] for each reference frame; valid iff
+//       0 <= x+dx < W-bs  and  0 <= y+dy < H-bs          (strict, Encoder.py:695)
+//   * MAE = SAD / bs^2 exactly (power-of-two divisor), so integer SAD compares the same;
+//   * keep if mae < best or (mae == best and (|dx|+|dy|, ref) strictly smaller), scanning
+//     ref (outer), dx (middle), dy (inner) => the result is the lexicographic minimum of
+//       key = (SAD, |dx|+|dy|, ref, scan),  scan = (dx+sr)*(2sr+1) + (dy+sr)
+//     which is packed into one uint64 so the argmin is a plain min (LDS atomicMin).
+//   * no valid candidate => mv (0,0,0), MAE inf (SAD reported as -1).
+//
+// Fast path (sr == 16, bs in {16, 8}): a workgroup owns a TB x TB tile of blocks and
+// stages the reference window (tile + 2*sr halo) in LDS once per reference.  A task is
+// (block, dx): the lane keeps the current block in VGPRs, slides down the 2*sr+bs window
+// rows once, and for every (cur row r, window row j) pair adds one 16-px row SAD into
+// acc[j - r] with v_sad_u8 (4 byte-|diffs| + accumulate per instruction) after aligning
+// the window bytes with v_alignbyte.  All 2*sr+1 dy candidates of the lane's dx share
+// each window-row load, so LDS traffic is (bs+2sr)*(bs/4+1) dwords per 33 candidates.
+// With VBS the same workgroup also runs the 8x8 sub-block searches on the same window.
+//
+// Generic path (any sr <= 64): one thread per (block, candidate) with a global atomicMin.
+#include "so_common.h"
+
+namespace so {
+
+SO_DEV uint64_t me_key(uint32_t sad, uint32_t l1, uint32_t ref, uint32_t scan) {
+    return ((uint64_t)sad << 32) | ((uint64_t)l1 << 24) | ((uint64_t)ref << 16) | (uint64_t)scan;
+}
+constexpr uint64_t kNoKey = ~0ull;
+
+SO_DEV void decode_key(uint64_t k, int sr, int32_t* out) {
+    if (k == kNoKey) {
+        out[0] = 0; out[1] = 0; out[2] = 0; out[3] = -1;
+        return;
+    }
+    const int d = 2 * sr + 1;
+    const int scan = (int)(k & 0xFFFF);
+    out[0] = scan / d - sr;
+    out[1] = scan % d - sr;
+    out[2] = (int)((k >> 16) & 0xFF);
+    out[3] = (int)(k >> 32);
+}
+
+// ---------------------------------------------------------------------------------------
+// Fast path
+// ---------------------------------------------------------------------------------------
+template <int BS>
+struct MeTile {
+    static constexpr int SR = 16;
+    static constexpr int D = 2 * SR + 1;                 // 33 candidates per axis
+    static constexpr int TB = (BS == 16) ? 8 : 16;       // blocks per tile side
+    static constexpr int TPX = TB * BS;                  // 128 px
+    static constexpr int WR = TPX + 2 * SR;              // window rows
+    static constexpr int WC = TPX + 2 * SR;              // window cols
+    static constexpr int WPD = (WC + 16) / 4 + 1;        // pitch in dwords (+1 breaks bank stride)
+    static constexpr int NBLK = TB * TB;
+    static constexpr int NWAVES = 11;                    // 704 threads; 33*64 = 3*704
+    static constexpr int NTHREADS = NWAVES * 64;
+};
+
+// One task: block (or sub-block) of size TBS at frame (x, y), window coordinates of its
+// top-left (wrow0, wcol0) = position - (tile origin - SR), candidate column dxi.
+// Returns the lane's best key over the 33 dy candidates.
+template <int TBS, int SR>
+SO_DEV uint64_t me_task(const uint32_t* __restrict__ win, int wpd, const uint8_t* __restrict__ cur,
+                        int W, int H, int x, int y, int wrow0, int wcol0, int dxi, int ref) {
+    constexpr int D = 2 * SR + 1;
+    constexpr int NDW = TBS / 4;  // dwords per block row
+    uint32_t cr[TBS][NDW];
+#pragma unroll
+    for (int r = 0; r < TBS; ++r) {
+        const uint8_t* p = cur + (size_t)(y + r) * W + x;
+        if constexpr (TBS == 16) {
+            uint4 v = *reinterpret_cast<const uint4*>(p);
+            cr[r][0] = v.x; cr[r][1] = v.y; cr[r][2] = v.z; cr[r][3] = v.w;
+        } else {
+            uint2 v = *reinterpret_cast<const uint2*>(p);
+            cr[r][0] = v.x; cr[r][1] = v.y;
+        }
+    }
+    uint32_t acc[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) acc[i] = 0;
+
+    const int c = wcol0 + dxi;
+    const uint32_t sh = (uint32_t)(c & 3);
+    const uint32_t* rowp = win + wrow0 * wpd + (c >> 2);
+#pragma unroll
+    for (int j = 0; j < TBS + 2 * SR; ++j) {
+        uint32_t w[NDW + 1];
+#pragma unroll
+        for (int k = 0; k <= NDW; ++k) w[k] = rowp[j * wpd + k];
+        uint32_t rr[NDW];
+#pragma unroll
+        for (int k = 0; k < NDW; ++k) rr[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+#pragma unroll
+        for (int r = 0; r < TBS; ++r) {
+            const int di = j - r;
+            if (di >= 0 && di < D) {
+#pragma unroll
+                for (int k = 0; k < NDW; ++k) acc[di] = __builtin_amdgcn_sad_u8(cr[r][k], rr[k], acc[di]);
+            }
+        }
+    }
+    const int dx = dxi - SR;
+    const bool xok = (x + dx >= 0) && (x + dx < W - TBS);
+    uint64_t best = kNoKey;
+    if (xok) {
+        const uint32_t adx = (uint32_t)(dx < 0 ? -dx : dx);
+#pragma unroll
+        for (int di = 0; di < D; ++di) {
+            const int dy = di - SR;
+            const bool ok = (y + dy >= 0) && (y + dy < H - TBS);
+            const uint64_t k = me_key(acc[di], adx + (uint32_t)(dy < 0 ? -dy : dy), (uint32_t)ref,
+                                      (uint32_t)(dxi * D + di));
+            best = (ok && k < best) ? k : best;
+        }
+    }
+    return best;
+}
+
+template <int BS, bool SUB>
+__global__ void __launch_bounds__(MeTile<BS>::NTHREADS)
+me_fast_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W,
+               int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub) {
+    using T = MeTile<BS>;
+    constexpr int SR = T::SR, D = T::D, TB = T::TB, SB = BS / 2;
+    __shared__ uint32_t win[T::WR * T::WPD];
+    __shared__ unsigned long long keys[T::NBLK * (SUB ? 5 : 1)];
+
+    const int nbx = W / BS, nby = H / BS;
+    const int tiles_x = (nbx + TB - 1) / TB;
+    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    const int x0 = tx * T::TPX, y0 = ty * T::TPX;
+    const int tid = threadIdx.x;
+
+    for (int i = tid; i < T::NBLK * (SUB ? 5 : 1); i += T::NTHREADS) keys[i] = kNoKey;
+
+    constexpr int NFULL = T::NBLK * D;               // 2112 (bs16) / 8448 (bs8)
+    constexpr int NSUBT = SUB ? 4 * T::NBLK * D : 0;
+    constexpr int NTASK = NFULL + NSUBT;
+
+    for (int r = 0; r < nref; ++r) {
+        const uint8_t* ref = refs.p[r];
+        __syncthreads();  // previous reference's tasks done with the window
+        // stage the window: rows y0-SR .., cols x0-SR .. (dwords; zero outside the frame)
+        constexpr int WCD = T::WC / 4;
+        for (int i = tid; i < T::WR * T::WPD; i += T::NTHREADS) {
+            const int wr = i / T::WPD, wc = i % T::WPD;
+            const int gy = y0 - SR + wr, gx = x0 - SR + wc * 4;
+            uint32_t v = 0;
+            if (wc < WCD && gy >= 0 && gy < H && gx >= 0 && gx + 4 <= W)
+                v = *reinterpret_cast<const uint32_t*>(ref + (size_t)gy * W + gx);
+            win[i] = v;
+        }
+        __syncthreads();
+        for (int t0 = 0; t0 < NTASK; t0 += T::NTHREADS) {
+            const int t = t0 + tid;
+            if (t >= NTASK) break;
+            if (t < NFULL) {
+                const int blk = t / D, dxi = t % D;
+                const int bxl = blk % TB, byl = blk / TB;
+                const int gbx = tx * TB + bxl, gby = ty * TB + byl;
+                if (gbx < nbx && gby < nby) {
+                    const uint64_t k = me_task<BS, SR>(win, T::WPD, cur, W, H, gbx * BS, gby * BS,
+                                                      byl * BS, bxl * BS, dxi, r);
+                    if (k != kNoKey) atomicMin(&keys[blk], (unsigned long long)k);
+                }
+            } else if constexpr (SUB) {
+                const int s = (t - NFULL) / D, dxi = (t - NFULL) % D;
+                const int blk = s >> 2, j = s & 3;
+                const int bxl = blk % TB, byl = blk / TB;
+                const int gbx = tx * TB + bxl, gby = ty * TB + byl;
+                if (gbx < nbx && gby < nby) {
+                    const int ox = (j & 1) * SB, oy = (j >> 1) * SB;
+                    const uint64_t k = me_task<SB, SR>(win, T::WPD, cur, W, H, gbx * BS + ox,
+                                                      gby * BS + oy, byl * BS + oy, bxl * BS + ox, dxi, r);
+                    if (k != kNoKey) atomicMin(&keys[T::NBLK + s], (unsigned long long)k);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < T::NBLK * (SUB ? 5 : 1); i += T::NTHREADS) {
+        const int blk = i < T::NBLK ? i : (i - T::NBLK) >> 2;
+        const int gbx = tx * TB + blk % TB, gby = ty * TB + blk / TB;
+        if (gbx >= nbx || gby >= nby) continue;
+        const int b = gby * nbx + gbx;
+        if (i < T::NBLK) decode_key(keys[i], SR, out_best + (size_t)b * 4);
+        else decode_key(keys[i], SR, out_sub + ((size_t)b * 4 + ((i - T::NBLK) & 3)) * 4);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Generic path: one thread per (block, ref, candidate); keys in global memory.
+// ---------------------------------------------------------------------------------------
+// The generic path keeps each unit's key in the first 8 bytes of its own 16-byte output
+// record (stride 2 in uint64 units) and decodes it in place at the end.
+__global__ void me_generic_init(unsigned long long* keys, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) keys[2 * (size_t)i] = kNoKey;
+}
+
+__global__ void me_generic_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H,
+                                  int W, int bs, int sb_mode, int sr,
+                                  unsigned long long* __restrict__ keys) {
+    // sb_mode 0: full blocks (size bs); 1: sub-blocks (size bs/2, 4 per block)
+    const int d = 2 * sr + 1;
+    const int nbx = W / bs, nby = H / bs;
+    const int nunit = nbx * nby * (sb_mode ? 4 : 1);
+    const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long ntot = (long long)nunit * nref * d * d;
+    if (t >= ntot) return;
+    const int cand = (int)(t % (d * d));
+    const int r = (int)((t / (d * d)) % nref);
+    const int u = (int)(t / ((long long)d * d * nref));
+    int b = sb_mode ? u >> 2 : u;
+    const int tbs = sb_mode ? bs / 2 : bs;
+    int x = (b % nbx) * bs, y = (b / nbx) * bs;
+    if (sb_mode) { x += (u & 1) * tbs; y += ((u >> 1) & 1) * tbs; }
+    const int dxi = cand / d, di = cand % d;
+    const int dx = dxi - sr, dy = di - sr;
+    if (!(x + dx >= 0 && x + dx < W - tbs && y + dy >= 0 && y + dy < H - tbs)) return;
+    const uint8_t* ref = refs.p[r];
+    uint32_t sad = 0;
+    for (int i = 0; i < tbs; ++i)
+        for (int j = 0; j < tbs; ++j) {
+            int a = cur[(size_t)(y + i) * W + x + j], c = ref[(size_t)(y + dy + i) * W + x + dx + j];
+            sad += (uint32_t)(a > c ? a - c : c - a);
+        }
+    const uint32_t l1 = (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy));
+    atomicMin(&keys[2 * (size_t)u], (unsigned long long)me_key(sad, l1, (uint32_t)r, (uint32_t)cand));
+}
+
+__global__ void me_generic_finalize(int n, int sr, int32_t* __restrict__ out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const unsigned long long k = *reinterpret_cast<const unsigned long long*>(out + (size_t)i * 4);
+        decode_key(k, sr, out + (size_t)i * 4);
+    }
+}
+
+int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, int bs, int sr,
+              int32_t* out_best, int32_t* out_sub, hipStream_t st) {
+    const int nbx = W / bs, nby = H / bs;
+    if (sr == 16 && (bs == 16 || bs == 8) && (out_sub == nullptr || bs == 16)) {
+        if (bs == 16) {
+            using T = MeTile<16>;
+            const int tiles = ((nbx + T::TB - 1) / T::TB) * ((nby + T::TB - 1) / T::TB);
+            if (out_sub)
+                hipLaunchKernelGGL((me_fast_kernel<16, true>), dim3(tiles), dim3(T::NTHREADS), 0, st,
+                                   cur, refs, nref, H, W, out_best, out_sub);
+            else
+                hipLaunchKernelGGL((me_fast_kernel<16, false>), dim3(tiles), dim3(T::NTHREADS), 0, st,
+                                   cur, refs, nref, H, W, out_best, out_sub);
+        } else {
+            using T = MeTile<8>;
+            const int tiles = ((nbx + T::TB - 1) / T::TB) * ((nby + T::TB - 1) / T::TB);
+            hipLaunchKernelGGL((me_fast_kernel<8, false>), dim3(tiles), dim3(T::NTHREADS), 0, st,
+                               cur, refs, nref, H, W, out_best, nullptr);
+        }
+        return check_launch("me_fast_kernel");
+    }
+    // generic
+    const int d = 2 * sr + 1;
+    for (int mode = 0; mode < (out_sub ? 2 : 1); ++mode) {
+        const int nunit = nbx * nby * (mode ? 4 : 1);
+        int32_t* out = mode ? out_sub : out_best;
+        unsigned long long* keys = reinterpret_cast<unsigned long long*>(out);
+        hipLaunchKernelGGL(me_generic_init, dim3((nunit + 255) / 256), dim3(256), 0, st, keys, nunit);
+        const long long ntot = (long long)nunit * nref * d * d;
+        hipLaunchKernelGGL(me_generic_kernel, dim3((unsigned)((ntot + 255) / 256)), dim3(256), 0, st,
+                           cur, refs, nref, H, W, bs, mode, sr, keys);
+        hipLaunchKernelGGL(me_generic_finalize, dim3((nunit + 255) / 256), dim3(256), 0, st, nunit,
+                           sr, out);
+    }
+    return check_launch("me_generic_kernel");
+}
+
+}  // namespace so

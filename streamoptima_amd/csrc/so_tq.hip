@@ -1,0 +1,241 @@
+// so_tq.hip — P-frame transform / quantisation / RD / reconstruction, and the decoder's
+// inter reconstruction, for gfx950.
+//
+// inter_tq_kernel replaces, for every block of a P-frame at once:
+//   calculate_inter_frame_residual (Encoder.py:432-460, handle_boundary_conditions :750),
+//   apply_2d_dct (:779) -> quantize_TC (:787) -> len(entropy_encoder_block) (:1086),
+//   the VBS decision calculate_RD_cost(1,1,..) vs (1,0,..) (:564-578, :1133-1158),
+//   the per-row-QP requantisation of complete_inter_flow (:1665-1697) and
+//   reconstruct_frame / reconstruct_block (:824-932): rescale, IDCT, + pred, uint8 wrap.
+// 16 lanes of one wavefront own one 16x16 block (8 lanes for 8x8 blocks); a 256-thread
+// workgroup carries 16 blocks.  Everything between the HBM reads (cur, pred, ME result)
+// and the HBM writes (QTC, recon, symbols) stays in VGPRs / LDS.
+#include "so_block.h"
+
+namespace so {
+
+template <int BS, bool VBS>
+__global__ void __launch_bounds__(256)
+inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W,
+                const int32_t* __restrict__ best, const int32_t* __restrict__ sub, int qp_rd,
+                const int32_t* __restrict__ qp_row, double lam, uint8_t* __restrict__ out_split,
+                int16_t* __restrict__ out_mv, int16_t* __restrict__ out_qtc,
+                int32_t* __restrict__ out_tokens, int32_t* __restrict__ out_mae,
+                uint8_t* __restrict__ out_recon) {
+    constexpr int G = BS, BPW = 256 / G, SB = BS / 2;
+    constexpr int LDS_D = VBS ? 288 : BS * (BS + 1);
+    __shared__ double ldsd[BPW * LDS_D];
+    __shared__ uint8_t ldsf[BPW * BS * BS];
+    const int tid = threadIdx.x, g = tid / G, l = tid % G;
+    const int nbx = W / BS, nb = nbx * (H / BS);
+    const int b = blockIdx.x * BPW + g;
+    if (b >= nb) return;  // whole lane group leaves; only wave-scope exchange below
+    double* dl = ldsd + g * LDS_D;
+    uint8_t* fl = ldsf + g * BS * BS;
+    const int bx = b % nbx, by = b / nbx, x = bx * BS, y = by * BS;
+    const int qpr = qp_row ? qp_row[by] : qp_rd;
+
+    const int32_t* bb = best + (size_t)b * 4;
+    const int dx = bb[0], dy = bb[1], rf = bb[2], sad = bb[3];
+    const bool fast = (0 <= x + dx) && (x + dx < W - BS) && (0 <= y + dy) && (y + dy < H - BS);
+    int pred[BS], crow[BS], res[BS];
+    fetch_row<BS>(refs.p[rf], W, H, x + dx, y + dy + l, fast, pred);
+    load_cur_row<BS>(cur, W, x, y + l, crow);
+#pragma unroll
+    for (int c = 0; c < BS; ++c) res[c] = crow[c] - pred[c];
+    double tcd[BS];
+    xform2d_rows<BS, false>(dl, l, res, tcd);
+    int tc[BS], q[BS];
+#pragma unroll
+    for (int c = 0; c < BS; ++c) tc[c] = (int)__builtin_rint(tcd[c]);
+    quant_row<BS>(tc, l, qp_rd, q);
+
+    bool split = false;
+    int mae_num = sad;
+    // sub-block state (VBS)
+    const int j = l >> 2, r0 = l & 3;
+    int sdx = 0, sdy = 0, sref = 0, xs = 0, ys = 0;
+    int spred[2][8], stc[2][8], qs[2][8];
+    if constexpr (VBS) {
+        if (x != 0 && y != 0) {
+            const int32_t* sj = sub + ((size_t)b * 4 + j) * 4;
+            sdx = sj[0]; sdy = sj[1]; sref = sj[2];
+            xs = x + (j & 1) * SB; ys = y + (j >> 1) * SB;
+            const bool sfast = (0 <= xs + sdx) && (xs + sdx < W - SB) && (0 <= ys + sdy) && (ys + sdy < H - SB);
+            int sres[2][8];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int row = r0 + 4 * h;
+                int scur[8];
+                fetch_row<8>(refs.p[sref], W, H, xs + sdx, ys + sdy + row, sfast, spred[h]);
+                load_cur_row<8>(cur, W, xs, ys + row, scur);
+#pragma unroll
+                for (int c = 0; c < 8; ++c) sres[h][c] = scur[c] - spred[h][c];
+            }
+            double std_[2][8];
+            xform2d_sub<false>(dl, l, sres, std_);
+            const int qpm1_rd = qp_rd > 0 ? qp_rd - 1 : qp_rd;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+#pragma unroll
+                for (int c = 0; c < 8; ++c) stc[h][c] = (int)__builtin_rint(std_[h][c]);
+                quant_row<8>(stc[h], r0 + 4 * h, qpm1_rd, qs[h]);
+            }
+            const int tok_b = block_tokens<BS>(fl, l, q);
+            const int tok_v = sub_tokens(fl, l, qs);
+            int ssum = 0;
+            bool vinf = false;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int s = sub[((size_t)b * 4 + k) * 4 + 3];
+                vinf |= s < 0;
+                ssum += s;
+            }
+            const double mae_b = sad < 0 ? __builtin_inf() : (double)sad / 256.0;
+            const double mae_v = vinf ? __builtin_inf() : (double)ssum / 256.0;
+            const double c_v = rd_cost(lam, 64 + 8 * tok_v, mae_v);
+            const double c_b = rd_cost(lam, 16 + 8 * tok_b, mae_b);
+            split = !(c_b < c_v);
+            mae_num = vinf ? -1 : ssum;
+        }
+    }
+
+    int tok;
+    if (!split) {
+        if (qpr != qp_rd) quant_row<BS>(tc, l, qpr, q);
+        tok = block_tokens<BS>(fl, l, q);
+        store_row_i16<BS>(out_qtc + (size_t)b * BS * BS + l * BS, q);
+        int dq[BS], rec[BS];
+        dequant_row<BS>(q, l, qpr, dq);
+        double rd[BS];
+        xform2d_rows<BS, true>(dl, l, dq, rd);
+#pragma unroll
+        for (int c = 0; c < BS; ++c) rec[c] = pred[c] + (int)__builtin_rint(rd[c]);
+        store_row_u8<BS>(out_recon, W, x, y + l, rec);
+        if (l < 12) out_mv[(size_t)b * 12 + l] = (int16_t)(l == 0 ? dx : l == 1 ? dy : l == 2 ? rf : 0);
+    } else {
+        if constexpr (VBS) {
+            const int qpm1 = qpr > 0 ? qpr - 1 : qpr;
+            const int qpm1_rd = qp_rd > 0 ? qp_rd - 1 : qp_rd;
+            if (qpm1 != qpm1_rd)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) quant_row<8>(stc[h], r0 + 4 * h, qpm1, qs[h]);
+            tok = sub_tokens(fl, l, qs);
+            int sdq[2][8];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                store_row_i16<8>(out_qtc + (size_t)b * BS * BS + j * 64 + (r0 + 4 * h) * 8, qs[h]);
+                dequant_row<8>(qs[h], r0 + 4 * h, qpm1, sdq[h]);
+            }
+            double srd[2][8];
+            xform2d_sub<true>(dl, l, sdq, srd);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                int rec[8];
+#pragma unroll
+                for (int c = 0; c < 8; ++c) rec[c] = spred[h][c] + (int)__builtin_rint(srd[h][c]);
+                store_row_u8<8>(out_recon, W, xs, ys + r0 + 4 * h, rec);
+            }
+            if (r0 < 3) out_mv[(size_t)b * 12 + 3 * j + r0] = (int16_t)(r0 == 0 ? sdx : r0 == 1 ? sdy : sref);
+        } else {
+            tok = 0;
+        }
+    }
+    if (l == 0) {
+        out_split[b] = (uint8_t)split;
+        out_tokens[b] = tok;
+        out_mae[b] = mae_num;
+    }
+}
+
+// Decoder: reconstruct a P-frame from (split, mv, qtc) — decoder.py:97-211, which is the
+// same arithmetic as reconstruct_frame (Encoder.py:831-932).
+template <int BS, bool VBS>
+__global__ void __launch_bounds__(256)
+inter_recon_kernel(RefSet refs, int H, int W, int qp, const int32_t* __restrict__ qp_row,
+                   const uint8_t* __restrict__ split, const int16_t* __restrict__ mv,
+                   const int16_t* __restrict__ qtc, uint8_t* __restrict__ out_recon) {
+    constexpr int G = BS, BPW = 256 / G, SB = BS / 2;
+    constexpr int LDS_D = VBS ? 288 : BS * (BS + 1);
+    __shared__ double ldsd[BPW * LDS_D];
+    const int tid = threadIdx.x, g = tid / G, l = tid % G;
+    const int nbx = W / BS, nb = nbx * (H / BS);
+    const int b = blockIdx.x * BPW + g;
+    if (b >= nb) return;
+    double* dl = ldsd + g * LDS_D;
+    const int bx = b % nbx, by = b / nbx, x = bx * BS, y = by * BS;
+    const int qpr = qp_row ? qp_row[by] : qp;
+    const int16_t* m = mv + (size_t)b * 12;
+    if (!VBS || !split[b]) {
+        const int dx = m[0], dy = m[1], rf = m[2];
+        const bool fast = (0 <= x + dx) && (x + dx < W - BS) && (0 <= y + dy) && (y + dy < H - BS);
+        int pred[BS], q[BS], dq[BS], rec[BS];
+        fetch_row<BS>(refs.p[rf], W, H, x + dx, y + dy + l, fast, pred);
+        load_row_i16<BS>(qtc + (size_t)b * BS * BS + l * BS, q);
+        dequant_row<BS>(q, l, qpr, dq);
+        double rd[BS];
+        xform2d_rows<BS, true>(dl, l, dq, rd);
+#pragma unroll
+        for (int c = 0; c < BS; ++c) rec[c] = pred[c] + (int)__builtin_rint(rd[c]);
+        store_row_u8<BS>(out_recon, W, x, y + l, rec);
+    } else if constexpr (VBS) {
+        const int j = l >> 2, r0 = l & 3;
+        const int qpm1 = qpr > 0 ? qpr - 1 : qpr;
+        const int sdx = m[3 * j], sdy = m[3 * j + 1], sref = m[3 * j + 2];
+        const int xs = x + (j & 1) * SB, ys = y + (j >> 1) * SB;
+        const bool sfast = (0 <= xs + sdx) && (xs + sdx < W - SB) && (0 <= ys + sdy) && (ys + sdy < H - SB);
+        int spred[2][8], sdq[2][8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            int qv[8];
+            fetch_row<8>(refs.p[sref], W, H, xs + sdx, ys + sdy + r0 + 4 * h, sfast, spred[h]);
+            load_row_i16<8>(qtc + (size_t)b * BS * BS + j * 64 + (r0 + 4 * h) * 8, qv);
+            dequant_row<8>(qv, r0 + 4 * h, qpm1, sdq[h]);
+        }
+        double srd[2][8];
+        xform2d_sub<true>(dl, l, sdq, srd);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            int rec[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) rec[c] = spred[h][c] + (int)__builtin_rint(srd[h][c]);
+            store_row_u8<8>(out_recon, W, xs, ys + r0 + 4 * h, rec);
+        }
+    }
+}
+
+int inter_tq_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int bs, const int32_t* best,
+                    const int32_t* sub, int qp_rd, const int32_t* qp_row, int vbs, double lam,
+                    uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
+                    int32_t* out_mae, uint8_t* out_recon, hipStream_t st) {
+    const int nb = (W / bs) * (H / bs);
+    const int bpw = 256 / bs;
+    dim3 grid((nb + bpw - 1) / bpw), blk(256);
+    if (bs == 16 && vbs)
+        hipLaunchKernelGGL((inter_tq_kernel<16, true>), grid, blk, 0, st, cur, refs, H, W, best, sub, qp_rd,
+                           qp_row, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon);
+    else if (bs == 16)
+        hipLaunchKernelGGL((inter_tq_kernel<16, false>), grid, blk, 0, st, cur, refs, H, W, best, sub, qp_rd,
+                           qp_row, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon);
+    else
+        hipLaunchKernelGGL((inter_tq_kernel<8, false>), grid, blk, 0, st, cur, refs, H, W, best, sub, qp_rd,
+                           qp_row, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon);
+    return check_launch("inter_tq_kernel");
+}
+
+int inter_recon_launch(const RefSet& refs, int H, int W, int bs, int qp, const int32_t* qp_row,
+                       const uint8_t* split, const int16_t* mv, const int16_t* qtc, uint8_t* out_recon,
+                       hipStream_t st) {
+    const int nb = (W / bs) * (H / bs);
+    const int bpw = 256 / bs;
+    dim3 grid((nb + bpw - 1) / bpw), blk(256);
+    if (bs == 16)
+        hipLaunchKernelGGL((inter_recon_kernel<16, true>), grid, blk, 0, st, refs, H, W, qp, qp_row, split, mv,
+                           qtc, out_recon);
+    else
+        hipLaunchKernelGGL((inter_recon_kernel<8, false>), grid, blk, 0, st, refs, H, W, qp, qp_row, split, mv,
+                           qtc, out_recon);
+    return check_launch("inter_recon_kernel");
+}
+
+}  // namespace so

@@ -1,0 +1,154 @@
+"""Device-resident frame engine: HBM buffers + launches of the gfx950 kernels.
+
+Everything here stays on the GPU: frames, reconstructions, symbols (split / mv / qtc /
+tokens / mae) and scratch are torch uint8/int16/int32 tensors allocated once and reused;
+each frame is one or two C-ABI calls on the current stream with no host synchronisation.
+The Python facade (Encoder.py / decoder.py) builds the reference's data structures from
+these tensors only when asked.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _lib
+
+SLACK = 64  # bytes readable past every plane (kernels read aligned words at row ends)
+
+
+def alloc_planes(n: int, h: int, w: int, device, fill: int | None = None) -> torch.Tensor:
+    """[n, h, w] uint8 planes laid out back to back with SLACK bytes after the last one."""
+    flat = torch.empty(n * h * w + SLACK, dtype=torch.uint8, device=device)
+    if fill is not None:
+        flat.fill_(fill)
+    else:
+        flat[n * h * w:].zero_()
+    return flat[: n * h * w].view(n, h, w)
+
+
+@dataclass
+class FrameSymbols:
+    """Per-frame output of the encode path (canonical layout, include/streamoptima.h)."""
+    frame_type: int            # 0 = intra, 1 = inter
+    split: torch.Tensor        # uint8 [nb]
+    mv: torch.Tensor           # int16 [nb, 4, 3] (inter) or [nb, 4] (intra)
+    qtc: torch.Tensor          # int16 [nb, bs*bs]
+    tokens: torch.Tensor       # int32 [nb]
+    mae_num: torch.Tensor      # int32 [nb]  (block MAE * bs^2, -1 = inf)
+    recon: torch.Tensor        # uint8 [h, w]
+    qp_rd: int = 0
+    qp_row: list | None = None
+    extra: dict = field(default_factory=dict)
+
+
+class Engine:
+    """Kernels for one frame geometry on one device."""
+
+    def __init__(self, height: int, width: int, block_size: int = 16, search_range: int = 16,
+                 vbs: bool = False, lam: float | None = None, device=None):
+        if height % block_size or width % block_size:
+            raise ValueError(f"frame {width}x{height} is not a multiple of block_size {block_size}")
+        self.h, self.w, self.bs, self.sr = height, width, block_size, search_range
+        self.vbs = bool(vbs)
+        self.lam = float(lam) if lam is not None else 0.0
+        if self.vbs and lam is None:
+            raise ValueError("VBSEnable needs lam (calculate_RD_cost multiplies by it)")
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise _lib.HipPathError("the encode path runs on a ROCm GPU only (no CPU fallback)")
+        self.lib = _lib.load()
+        self.nbx, self.nby = width // block_size, height // block_size
+        self.nb = self.nbx * self.nby
+        ps = self.lib.so_p_frame_scratch_elems(height, width, block_size, int(self.vbs))
+        is_ = self.lib.so_i_frame_scratch_elems(height, width, block_size)
+        self.scratch = torch.empty(max(ps, is_), dtype=torch.int32, device=self.device)
+
+    # ---- allocation ----------------------------------------------------------------------
+    def new_symbols(self, frame_type: int) -> FrameSymbols:
+        d, nb, bs = self.device, self.nb, self.bs
+        mv_shape = (nb, 4, 3) if frame_type == 1 else (nb, 4)
+        return FrameSymbols(frame_type=frame_type,
+                            split=torch.empty(nb, dtype=torch.uint8, device=d),
+                            mv=torch.empty(mv_shape, dtype=torch.int16, device=d),
+                            qtc=torch.empty((nb, bs * bs), dtype=torch.int16, device=d),
+                            tokens=torch.empty(nb, dtype=torch.int32, device=d),
+                            mae_num=torch.empty(nb, dtype=torch.int32, device=d),
+                            recon=alloc_planes(1, self.h, self.w, d)[0])
+
+    def qp_row_tensor(self, qp_row) -> torch.Tensor | None:
+        if qp_row is None:
+            return None
+        t = torch.as_tensor(list(qp_row), dtype=torch.int32)
+        if t.numel() != self.nby:
+            raise ValueError(f"qp_row needs {self.nby} entries, got {t.numel()}")
+        return t.to(self.device, non_blocking=True)
+
+    def _check_plane(self, t: torch.Tensor, name: str):
+        if t.dtype != torch.uint8 or t.device != self.device or tuple(t.shape) != (self.h, self.w):
+            raise ValueError(f"{name} must be a uint8 {self.h}x{self.w} tensor on {self.device}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+
+    # ---- encode -------------------------------------------------------------------------
+    def encode_p(self, cur: torch.Tensor, refs: list, qp_rd: int, qp_row=None,
+                 out: FrameSymbols | None = None, qp_row_dev: torch.Tensor | None = None) -> FrameSymbols:
+        """complete_inter_flow (Encoder.py:1644) for one frame; asynchronous."""
+        self._check_plane(cur, "cur")
+        for k, r in enumerate(refs):
+            self._check_plane(r, f"refs[{k}]")
+        if not 1 <= len(refs) <= _lib.MAX_REF:
+            raise ValueError(f"nRefFrames must be in [1, {_lib.MAX_REF}]")
+        out = out or self.new_symbols(1)
+        qr = qp_row_dev if qp_row_dev is not None else self.qp_row_tensor(qp_row)
+        rc = self.lib.so_encode_p_frame(
+            cur.data_ptr(), _lib.ref_array(refs), len(refs), self.h, self.w, self.bs, self.sr,
+            int(qp_rd), _lib.ptr(qr), int(self.vbs), self.lam, out.split.data_ptr(),
+            out.mv.data_ptr(), out.qtc.data_ptr(), out.tokens.data_ptr(), out.mae_num.data_ptr(),
+            out.recon.data_ptr(), self.scratch.data_ptr(), _lib.stream_handle(self.device))
+        _lib.check(rc, "so_encode_p_frame")
+        out.frame_type, out.qp_rd = 1, int(qp_rd)
+        out.qp_row = None if qp_row is None else list(qp_row)
+        return out
+
+    def encode_i(self, cur: torch.Tensor, qp_rd: int, qp_row=None, out: FrameSymbols | None = None,
+                 qp_row_dev: torch.Tensor | None = None) -> FrameSymbols:
+        """complete_intra_flow (Encoder.py:1582), intra_mode 0, for one frame; asynchronous."""
+        self._check_plane(cur, "cur")
+        out = out or self.new_symbols(0)
+        qr = qp_row_dev if qp_row_dev is not None else self.qp_row_tensor(qp_row)
+        rc = self.lib.so_encode_i_frame(
+            cur.data_ptr(), self.h, self.w, self.bs, self.sr, int(qp_rd), _lib.ptr(qr), int(self.vbs),
+            self.lam, out.split.data_ptr(), out.mv.data_ptr(), out.qtc.data_ptr(), out.tokens.data_ptr(),
+            out.mae_num.data_ptr(), out.recon.data_ptr(), self.scratch.data_ptr(),
+            _lib.stream_handle(self.device))
+        _lib.check(rc, "so_encode_i_frame")
+        out.frame_type, out.qp_rd = 0, int(qp_rd)
+        out.qp_row = None if qp_row is None else list(qp_row)
+        return out
+
+    # ---- decode ---------------------------------------------------------------------------
+    def recon_inter(self, refs: list, split, mv, qtc, qp: int, qp_row=None, out=None) -> torch.Tensor:
+        out = out if out is not None else alloc_planes(1, self.h, self.w, self.device)[0]
+        qr = self.qp_row_tensor(qp_row)
+        rc = self.lib.so_inter_recon(_lib.ref_array(refs), len(refs), self.h, self.w, self.bs, int(qp),
+                                     _lib.ptr(qr), split.data_ptr(), mv.data_ptr(), qtc.data_ptr(),
+                                     out.data_ptr(), _lib.stream_handle(self.device))
+        _lib.check(rc, "so_inter_recon")
+        return out
+
+    def recon_intra(self, split, mv, qtc, qp: int, qp_row=None, out=None) -> torch.Tensor:
+        out = out if out is not None else alloc_planes(1, self.h, self.w, self.device)[0]
+        qr = self.qp_row_tensor(qp_row)
+        rc = self.lib.so_intra_recon(self.h, self.w, self.bs, int(qp), _lib.ptr(qr), split.data_ptr(),
+                                     mv.data_ptr(), qtc.data_ptr(), out.data_ptr(), self.scratch.data_ptr(),
+                                     _lib.stream_handle(self.device))
+        _lib.check(rc, "so_intra_recon")
+        return out
+
+    # ---- metrics ---------------------------------------------------------------------------
+    def sse_into(self, a: torch.Tensor, b: torch.Tensor, acc: torch.Tensor) -> None:
+        """acc (uint64 view of an int64 device scalar) += sum((a-b)^2)."""
+        rc = self.lib.so_sse_u8(a.data_ptr(), b.data_ptr(), a.numel(), acc.data_ptr(),
+                                _lib.stream_handle(self.device))
+        _lib.check(rc, "so_sse_u8")
