@@ -161,3 +161,12 @@ def sse(a: np.ndarray, b: np.ndarray) -> int:
     a = np.ascontiguousarray(a, np.uint8)
     b = np.ascontiguousarray(b, np.uint8)
     return int(lib().oc_sse_u8(_p(a), _p(b), ctypes.c_int64(a.size)))
+
+
+def me_block(cur: np.ndarray, refs, x: int, y: int, bs: int, sr: int) -> tuple:
+    cur = np.ascontiguousarray(cur, dtype=np.uint8)
+    h, w = refs[0].shape
+    arrs, ptrs = _refs_array(refs)
+    out = np.zeros(4, np.int32)
+    lib().oc_me_block(_p(cur), cur.shape[1], ptrs, len(refs), h, w, x, y, bs, sr, _p(out))
+    return tuple(int(v) for v in out)

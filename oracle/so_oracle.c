@@ -716,3 +716,10 @@ EXPORT int64_t oc_sse_u8(const uint8_t *a, const uint8_t *b, int64_t n) {
     for (int64_t i = 0; i < n; ++i) { int64_t d = (int64_t)a[i] - b[i]; s += d * d; }
     return s;
 }
+
+/* find_best_match for one block (Encoder.py:678-717); out = (dx, dy, ref, sad or -1) */
+EXPORT void oc_me_block(const uint8_t *cur, int cstride, const uint8_t *const *refs, int nref, int H,
+                        int W, int x, int y, int bs, int sr, int32_t *out) {
+    om_mv m = find_best_match(cur + (size_t)y * cstride + x, cstride, refs, nref, H, W, x, y, bs, sr);
+    out[0] = m.dx; out[1] = m.dy; out[2] = m.ref; out[3] = (int32_t)m.sad;
+}

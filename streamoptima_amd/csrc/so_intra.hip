@@ -163,7 +163,7 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int sr, int qp_rd
         xform2d_rows<BS, true>(dl, l, dq, rd);
 #pragma unroll
         for (int c = 0; c < BS; ++c) rb[l * BS + c] = (int)__builtin_rint(rd[c]);
-        if (l < 4) out_mv[(size_t)b * 4 + l] = (int16_t)(l == 0 ? mv : 0);
+        for (int k = l; k < 4; k += G) out_mv[(size_t)b * 4 + k] = (int16_t)(k == 0 ? mv : 0);
     } else {
         if constexpr (VBS) {
             const int qpm1 = qpr > 0 ? qpr - 1 : qpr;

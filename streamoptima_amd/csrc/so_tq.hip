@@ -112,7 +112,7 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W,
 #pragma unroll
         for (int c = 0; c < BS; ++c) rec[c] = pred[c] + (int)__builtin_rint(rd[c]);
         store_row_u8<BS>(out_recon, W, x, y + l, rec);
-        if (l < 12) out_mv[(size_t)b * 12 + l] = (int16_t)(l == 0 ? dx : l == 1 ? dy : l == 2 ? rf : 0);
+        for (int k = l; k < 12; k += G) out_mv[(size_t)b * 12 + k] = (int16_t)(k == 0 ? dx : k == 1 ? dy : k == 2 ? rf : 0);
     } else {
         if constexpr (VBS) {
             const int qpm1 = qpr > 0 ? qpr - 1 : qpr;

@@ -1,0 +1,65 @@
+"""The C-ABI library: builds for gfx950, loads, exports every declared symbol, and rejects
+bad arguments on the host side (no GPU needed for any of this)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "streamoptima.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\*]+\s+)+\*?(so_\w+)\(", src, re.M)))
+
+
+def test_header_declares_entry_points():
+    names = _declared()
+    for n in ("so_me_full_search", "so_inter_tq_recon", "so_encode_p_frame", "so_encode_i_frame",
+              "so_inter_recon", "so_intra_recon", "so_sse_u8", "so_last_error", "so_abi_version"):
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    from streamoptima_amd import _lib, build
+    build.build()
+    lib = _lib.load()
+    missing = [n for n in _declared() if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(_lib.EXPORTED) == set(_declared())
+    out = subprocess.run(["nm", "-D", "--defined-only", build.LIB_PATH], capture_output=True, text=True).stdout
+    for n in _declared():
+        assert re.search(rf"\bT {n}\b", out), n
+
+
+def test_code_object_is_gfx950():
+    from streamoptima_amd import build
+    blob = open(build.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_host_side_validation_without_gpu():
+    from streamoptima_amd import _lib
+    lib = _lib.load()
+    bad = lib.so_encode_p_frame(None, None, 1, 64, 64, 12, 16, 4, None, 0, 0.0, None, None, None, None, None,
+                                None, None, None)
+    assert bad == _lib.SO_E_UNSUPPORTED
+    assert b"block_size 12" in lib.so_last_error()
+    bad = lib.so_encode_i_frame(None, 60, 64, 16, 16, 4, None, 0, 0.0, None, None, None, None, None, None, None,
+                                None)
+    assert bad == _lib.SO_E_INVALID
+    assert lib.so_p_frame_scratch_elems(2160, 3840, 16, 1) == 32400 * 20
+    assert lib.so_i_frame_scratch_elems(64, 64, 16) == 16 * 256 + 16 * 8
+    with pytest.raises(NotImplementedError):
+        _lib.check(lib.so_me_full_search(None, None, 1, 64, 64, 16, 99, None, None, None), "me")
+
+
+def test_product_never_imports_the_oracle():
+    pkg = os.path.join(ROOT, "streamoptima_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".h", ".cpp")):
+                text = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in re.sub(r"#.*|//.*", "", text).replace("oracles", ""), f

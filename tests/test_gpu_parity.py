@@ -225,21 +225,21 @@ def test_intra_vs_oracle(gpu, h, w, bs, sr, vbs, nref, qp, kind):
 
 
 def test_decoder_matches_encoder_recon(gpu, tmp_path, monkeypatch):
-    """decoder.decode over the package lists == the encoder's reconstruction (closed loop)."""
+    """decoder.decode over the package lists == the encoder's reconstruction (closed loop).
+    nRefFrames=1: with more references the reference's own decoder disagrees with its
+    encoder (it clears the list on I-frames, decoder.py:520 vs Encoder.py:1864)."""
     from streamoptima_amd.Encoder import Y_Video_codec
     from streamoptima_amd.synth import synth_sequence
     seq = synth_sequence(5, 96, 160, seed=4)
     monkeypatch.chdir(tmp_path)
-    enc = Y_Video_codec(96, 160, 5, 16, 16, 3, 3, 0, 0.015, True, nRefFrames=2, y_only_frame_arr=seq, device=gpu)
+    enc = Y_Video_codec(96, 160, 5, 16, 16, 3, 3, 0, 0.015, True, nRefFrames=1, y_only_frame_arr=seq, device=gpu)
     enc.encode(block_size=16)
     pkg = enc.encoded_package
     dec = enc.decoder.decode(pkg["frame_type_seq"], pkg["approx residual"], pkg["Qp_per_row_per_frame"],
                              pkg["MVS per Frame"], 0, 3, 16, 5, 160, 96)
-    # the decoder clears its reference list on I-frames while the encoder keeps it
-    # (decoder.py:520 vs Encoder.py:1864); with nRefFrames=2 frame 4 (after the I-frame
-    # at 3) may legitimately differ, frames 0-3 must match
-    for i in range(4):
+    for i in range(5):
         assert (dec[i] == enc._symbols[i].recon.cpu().numpy()).all()
+        assert torch.equal(enc.decoded_device[i], enc._symbols[i].recon)
 
 
 def test_gop_vs_oracle_multiref(gpu, tmp_path, monkeypatch):
