@@ -21,6 +21,9 @@
 // With VBS the same workgroup also runs the 8x8 sub-block searches on the same window.
 //
 // Generic path (any sr <= 64): one thread per (block, candidate) with a global atomicMin.
+#include <stdlib.h>
+#include <string.h>
+
 #include "so_common.h"
 
 namespace so {
@@ -194,6 +197,162 @@ me_fast_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
 }
 
 // ---------------------------------------------------------------------------------------
+// QSAD path (default): one wavefront per (sub-)block, current block in SGPRs.
+//
+// v_qsad_pk_u16_u8 D, S0(8 ref bytes), S1(4 cur bytes), S2 computes four SADs of S1
+// against S0 at byte offsets 0..3 and accumulates them into four packed u16 (16 |diffs|
+// per instruction, and the 4-byte-aligned window words need no byte alignment).  A
+// 16x16 SAD is at most 65280, so u16 accumulators are exact.
+// Lane (s, g), s < 7, g < 9: dx = 4g + i - 16 (i = 0..3), dy = 5s + t - 16 (t = 0..4):
+// 63 lanes x 20 candidates >= 33 x 33; invalid slots are masked at the argmin.  The
+// lane slides over its 5 + bs - 1 window rows; for every (row, cur row r) pair with
+// t = row - r in range it issues bs/4 QSADs.  The current block is wave-uniform, so it
+// lives in SGPRs (scalar loads) and feeds S1 directly.
+// ---------------------------------------------------------------------------------------
+template <int TBS>
+SO_DEV uint64_t me_qsad_task(const uint32_t* __restrict__ win, int wpd, const uint32_t (&cr)[TBS][TBS / 4],
+                             int lane, int W, int H, int x, int y, int wrow0, int wcol0, int ref) {
+    constexpr int SR = 16, D = 33, NDW = TBS / 4, DYS = 5, NG = 9, NROW = DYS + TBS - 1;
+    const int s = lane / NG, g = lane - s * NG;
+    uint64_t acc[DYS];
+#pragma unroll
+    for (int t = 0; t < DYS; ++t) acc[t] = 0;
+    const uint32_t* rowp = win + (wrow0 + DYS * s) * wpd + (wcol0 >> 2) + g;
+    // one window row in flight ahead of the one being consumed; the scheduling barrier
+    // keeps the compiler from hoisting every row's loads (register pressure -> spills)
+    uint32_t wc[NDW + 1], wn[NDW + 1];
+#pragma unroll
+    for (int k = 0; k <= NDW; ++k) wc[k] = rowp[k];
+#pragma unroll
+    for (int jj = 0; jj < NROW; ++jj) {
+        if (jj + 1 < NROW) {
+#pragma unroll
+            for (int k = 0; k <= NDW; ++k) wn[k] = rowp[(jj + 1) * wpd + k];
+        }
+#pragma unroll
+        for (int t = 0; t < DYS; ++t) {
+            const int r = jj - t;
+            if (r >= 0 && r < TBS) {
+#pragma unroll
+                for (int k = 0; k < NDW; ++k)
+                    acc[t] = __builtin_amdgcn_qsad_pk_u16_u8(((uint64_t)wc[k + 1] << 32) | wc[k], cr[r][k], acc[t]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k <= NDW; ++k) wc[k] = wn[k];
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    uint64_t best = kNoKey;
+    if (s < 7) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int dxi = 4 * g + i, dx = dxi - SR;
+            const bool xok = dxi < D && (x + dx >= 0) && (x + dx < W - TBS);
+            const uint32_t adx = (uint32_t)(dx < 0 ? -dx : dx);
+#pragma unroll
+            for (int t = 0; t < DYS; ++t) {
+                const int di = DYS * s + t, dy = di - SR;
+                const bool ok = xok && di < D && (y + dy >= 0) && (y + dy < H - TBS);
+                const uint32_t sad = (uint32_t)((acc[t] >> (16 * i)) & 0xFFFF);
+                const uint64_t k = me_key(sad, adx + (uint32_t)(dy < 0 ? -dy : dy), (uint32_t)ref,
+                                          (uint32_t)(dxi * D + di));
+                best = (ok && k < best) ? k : best;
+            }
+        }
+    }
+    return best;
+}
+
+SO_DEV uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint32_t lo = __shfl_xor((uint32_t)v, m, 64), hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
+        const uint64_t o = ((uint64_t)hi << 32) | lo;
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+// The current (sub-)block is wave-uniform: read it through the constant address space so
+// the compiler issues scalar loads and keeps the pixels in SGPRs (QSAD operand S1).
+typedef const __attribute__((address_space(4))) uint32_t* const_u32p;
+template <int TBS>
+SO_DEV void load_cur_sgpr(const uint8_t* __restrict__ cur, int W, int x, int y, uint32_t (&cr)[TBS][TBS / 4]) {
+#pragma unroll
+    for (int r = 0; r < TBS; ++r) {
+        const_u32p p = (const_u32p)(cur + (size_t)(y + r) * W + x);
+#pragma unroll
+        for (int k = 0; k < TBS / 4; ++k) cr[r][k] = p[k];
+    }
+}
+
+template <int BS, bool SUB>
+__global__ void __launch_bounds__(1024)
+me_qsad_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W,
+               int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub) {
+    using T = MeTile<BS>;
+    constexpr int SR = T::SR, TB = T::TB, SB = BS / 2, NW = 16;
+    __shared__ uint32_t win[T::WR * T::WPD];
+    __shared__ unsigned long long keys[T::NBLK * (SUB ? 5 : 1)];
+    const int nbx = W / BS, nby = H / BS;
+    const int tiles_x = (nbx + TB - 1) / TB;
+    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    const int x0 = tx * T::TPX, y0 = ty * T::TPX;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int i = tid; i < T::NBLK * (SUB ? 5 : 1); i += NW * 64) keys[i] = kNoKey;
+    constexpr int NUNIT = T::NBLK * (SUB ? 5 : 1);
+    for (int r = 0; r < nref; ++r) {
+        const uint8_t* ref = refs.p[r];
+        __syncthreads();
+        constexpr int WCD = T::WC / 4;
+        for (int i = tid; i < T::WR * T::WPD; i += NW * 64) {
+            const int wr = i / T::WPD, wc = i % T::WPD;
+            const int gy = y0 - SR + wr, gx = x0 - SR + wc * 4;
+            uint32_t v = 0;
+            if (wc < WCD && gy >= 0 && gy < H && gx >= 0 && gx + 4 <= W)
+                v = *reinterpret_cast<const uint32_t*>(ref + (size_t)gy * W + gx);
+            win[i] = v;
+        }
+        __syncthreads();
+        for (int u = wave; u < NUNIT; u += NW) {          // wave-uniform unit index
+            if (u < T::NBLK) {
+                const int bxl = u % TB, byl = u / TB;
+                const int gbx = tx * TB + bxl, gby = ty * TB + byl;
+                if (gbx >= nbx || gby >= nby) continue;
+                uint32_t cr[BS][BS / 4];
+                load_cur_sgpr<BS>(cur, W, gbx * BS, gby * BS, cr);
+                uint64_t k = me_qsad_task<BS>(win, T::WPD, cr, lane, W, H, gbx * BS, gby * BS, byl * BS,
+                                              bxl * BS, r);
+                k = wave_min_u64(k);
+                if (lane == 0 && k != kNoKey) atomicMin(&keys[u], (unsigned long long)k);
+            } else if constexpr (SUB) {
+                const int sidx = u - T::NBLK, blk = sidx >> 2, j = sidx & 3;
+                const int bxl = blk % TB, byl = blk / TB;
+                const int gbx = tx * TB + bxl, gby = ty * TB + byl;
+                if (gbx >= nbx || gby >= nby) continue;
+                const int ox = (j & 1) * SB, oy = (j >> 1) * SB;
+                uint32_t cr[SB][SB / 4];
+                load_cur_sgpr<SB>(cur, W, gbx * BS + ox, gby * BS + oy, cr);
+                uint64_t k = me_qsad_task<SB>(win, T::WPD, cr, lane, W, H, gbx * BS + ox, gby * BS + oy,
+                                              byl * BS + oy, bxl * BS + ox, r);
+                k = wave_min_u64(k);
+                if (lane == 0 && k != kNoKey) atomicMin(&keys[u], (unsigned long long)k);
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < NUNIT; i += NW * 64) {
+        const int blk = i < T::NBLK ? i : (i - T::NBLK) >> 2;
+        const int gbx = tx * TB + blk % TB, gby = ty * TB + blk / TB;
+        if (gbx >= nbx || gby >= nby) continue;
+        const int b = gby * nbx + gbx;
+        if (i < T::NBLK) decode_key(keys[i], SR, out_best + (size_t)b * 4);
+        else decode_key(keys[i], SR, out_sub + ((size_t)b * 4 + ((i - T::NBLK) & 3)) * 4);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // Generic path: one thread per (block, ref, candidate); keys in global memory.
 // ---------------------------------------------------------------------------------------
 // The generic path keeps each unit's key in the first 8 bytes of its own 16-byte output
@@ -246,6 +405,25 @@ int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, in
               int32_t* out_best, int32_t* out_sub, hipStream_t st) {
     const int nbx = W / bs, nby = H / bs;
     if (sr == 16 && (bs == 16 || bs == 8) && (out_sub == nullptr || bs == 16)) {
+        static const bool use_sad = getenv("SO_ME_IMPL") && strcmp(getenv("SO_ME_IMPL"), "sad") == 0;
+        if (!use_sad) {
+            if (bs == 16) {
+                using T = MeTile<16>;
+                const int tiles = ((nbx + T::TB - 1) / T::TB) * ((nby + T::TB - 1) / T::TB);
+                if (out_sub)
+                    hipLaunchKernelGGL((me_qsad_kernel<16, true>), dim3(tiles), dim3(1024), 0, st, cur, refs, nref,
+                                       H, W, out_best, out_sub);
+                else
+                    hipLaunchKernelGGL((me_qsad_kernel<16, false>), dim3(tiles), dim3(1024), 0, st, cur, refs, nref,
+                                       H, W, out_best, out_sub);
+            } else {
+                using T = MeTile<8>;
+                const int tiles = ((nbx + T::TB - 1) / T::TB) * ((nby + T::TB - 1) / T::TB);
+                hipLaunchKernelGGL((me_qsad_kernel<8, false>), dim3(tiles), dim3(1024), 0, st, cur, refs, nref, H,
+                                   W, out_best, nullptr);
+            }
+            return check_launch("me_qsad_kernel");
+        }
         if (bs == 16) {
             using T = MeTile<16>;
             const int tiles = ((nbx + T::TB - 1) / T::TB) * ((nby + T::TB - 1) / T::TB);
