@@ -105,7 +105,7 @@ def kernel_roofline(codec, frames_dev, reps: int) -> dict:
         _lib.check(lib.so_inter_tq_recon(cur.data_ptr(), refs, 1, h, w, bs, best.data_ptr(), _lib.ptr(sub),
                                          4, None, int(eng.vbs), eng.lam, sym.split.data_ptr(), sym.mv.data_ptr(),
                                          sym.qtc.data_ptr(), sym.tokens.data_ptr(), sym.mae_num.data_ptr(),
-                                         sym.recon.data_ptr(), st), "tq")
+                                         sym.recon.data_ptr(), sym.sse.data_ptr(), st), "tq")
 
     out = {}
     for name, fn in (("me", me), ("tq", tq)):

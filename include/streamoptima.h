@@ -76,12 +76,14 @@ int so_me_full_search(const uint8_t* cur, const uint8_t* const* refs, int nref, 
  *   qp_row       device int32 [H/bs] per-row QP (rate control), or NULL => qp_rd
  *   lam          lambda of calculate_RD_cost
  *   out_recon    H x W uint8 reconstruction (may not alias any ref)
+ *   out_sse      optional int32 [nb]: per-block sum of (cur - recon)^2, for the PSNR of
+ *                calculate_metrics (Encoder.py:934) without a separate frame pass; NULL to skip
  */
 int so_inter_tq_recon(const uint8_t* cur, const uint8_t* const* refs, int nref, int H,
                       int W, int bs, const int32_t* best, const int32_t* sub, int qp_rd,
                       const int32_t* qp_row, int vbs, double lam, uint8_t* out_split,
                       int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
-                      int32_t* out_mae_num, uint8_t* out_recon, void* stream);
+                      int32_t* out_mae_num, uint8_t* out_recon, int32_t* out_sse, void* stream);
 
 /* int32 elements of scratch so_encode_p_frame needs: nb*4 (+ nb*16 with vbs) */
 size_t so_p_frame_scratch_elems(int H, int W, int bs, int vbs);
@@ -94,7 +96,7 @@ int so_encode_p_frame(const uint8_t* cur, const uint8_t* const* refs, int nref, 
                       int W, int bs, int sr, int qp_rd, const int32_t* qp_row, int vbs,
                       double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc,
                       int32_t* out_tokens, int32_t* out_mae_num, uint8_t* out_recon,
-                      int32_t* scratch, void* stream);
+                      int32_t* out_sse, int32_t* scratch, void* stream);
 
 /* int32 elements of scratch so_encode_i_frame / so_intra_recon need: nb*(bs*bs) + nb*8 */
 size_t so_i_frame_scratch_elems(int H, int W, int bs);
@@ -104,13 +106,14 @@ size_t so_i_frame_scratch_elems(int H, int W, int bs);
  * intra_prediction (:1238-1347, horizontal search intra_find_best_match_horizontal
  * :1010-1045, canvas generalised from the hard-coded 288x352 to H x W), per-block
  * DCT/quant/tokens/VBS-RD, and reconstruct_frame_intra (:1350-1417; unclipped canvas,
- * final astype(uint8) == mod-256 wrap).  out_mv is int16 [nb][4].
+ * final astype(uint8) == mod-256 wrap).  out_mv is int16 [nb][4].  out_sse: optional
+ * int32 [H] per PIXEL ROW sum of (cur - recon)^2 (the recon is produced row-parallel).
  */
 int so_encode_i_frame(const uint8_t* cur, int H, int W, int bs, int sr, int qp_rd,
                       const int32_t* qp_row, int vbs, double lam, uint8_t* out_split,
                       int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
-                      int32_t* out_mae_num, uint8_t* out_recon, int32_t* scratch,
-                      void* stream);
+                      int32_t* out_mae_num, uint8_t* out_recon, int32_t* out_sse,
+                      int32_t* scratch, void* stream);
 
 /* Decoder: P-frame reconstruction from symbols (decoder.py:97-211). */
 int so_inter_recon(const uint8_t* const* refs, int nref, int H, int W, int bs, int qp,

@@ -317,7 +317,6 @@ class Y_Video_codec:
         RCFlag > 1 needs residual_size.  Returns symbols per frame and a device SSE array."""
         eng = self.engine()
         nframes = frames_dev.shape[0]
-        sse = torch.zeros(nframes, dtype=torch.int64, device=self.device)
         ref_frames = [alloc_planes(1, eng.h, eng.w, self.device, fill=128)[0]]
         out_syms, ftypes, qp_rows = [], [], []
         rc_on = self._rc_on()
@@ -351,7 +350,8 @@ class Y_Video_codec:
                 if len(ref_frames) >= self.nRefFrames:
                     ref_frames.pop(0)
                 ref_frames.append(sym.recon)
-            eng.sse_into(cur, sym.recon, sse[i:i + 1])
+        # per-block / per-row SSE came out of the encode kernels; one reduction per GOP
+        sse = torch.stack([s.sse for s in out_syms]).sum(dim=1, dtype=torch.int64)
         return {"symbols": out_syms, "sse": sse, "frame_type": ftypes, "qp_rows": qp_rows}
 
     def _save_recon(self, syms):

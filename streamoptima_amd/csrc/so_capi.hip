@@ -22,14 +22,14 @@ int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, in
 int inter_tq_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int bs, const int32_t* best,
                     const int32_t* sub, int qp_rd, const int32_t* qp_row, int vbs, double lam,
                     uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
-                    int32_t* out_mae, uint8_t* out_recon, hipStream_t st);
+                    int32_t* out_mae, uint8_t* out_recon, int32_t* out_sse, hipStream_t st);
 int inter_recon_launch(const RefSet& refs, int H, int W, int bs, int qp, const int32_t* qp_row,
                        const uint8_t* split, const int16_t* mv, const int16_t* qtc, uint8_t* out_recon,
                        hipStream_t st);
 int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int qp_rd, const int32_t* qp_row,
                         int vbs, double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc,
-                        int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon, int32_t* idres,
-                        hipStream_t st);
+                        int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon, int32_t* out_sse,
+                        int32_t* idres, hipStream_t st);
 int intra_recon_launch(int H, int W, int bs, int sr, int qp, const int32_t* qp_row, const uint8_t* split,
                        const int16_t* mv, const int16_t* qtc, uint8_t* out_recon, int32_t* idres,
                        hipStream_t st);
@@ -58,6 +58,14 @@ static int check_geom(const char* fn, int H, int W, int bs, int vbs) {
 static int check_sr(const char* fn, int sr) {
     if (sr < 0 || sr > 64) {
         set_error("%s: search_range %d outside [0, 64]", fn, sr);
+        return SO_E_UNSUPPORTED;
+    }
+    return SO_OK;
+}
+
+static int check_intra_width(const char* fn, int W) {
+    if (W > 8192) {   // intra_recon_kernel keeps one pixel row (12 B/px) in LDS
+        set_error("%s: intra frames wider than 8192 px are not built", fn);
         return SO_E_UNSUPPORTED;
     }
     return SO_OK;
@@ -157,7 +165,7 @@ int so_me_full_search(const uint8_t* cur, const uint8_t* const* refs, int nref, 
 int so_inter_tq_recon(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W, int bs,
                       const int32_t* best, const int32_t* sub, int qp_rd, const int32_t* qp_row, int vbs,
                       double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
-                      int32_t* out_mae_num, uint8_t* out_recon, void* stream) {
+                      int32_t* out_mae_num, uint8_t* out_recon, int32_t* out_sse, void* stream) {
     const char* fn = "so_inter_tq_recon";
     SO_TRY(check_geom(fn, H, W, bs, vbs));
     SO_TRY(check_qp(fn, qp_rd));
@@ -172,7 +180,7 @@ int so_inter_tq_recon(const uint8_t* cur, const uint8_t* const* refs, int nref, 
             return SO_E_INVALID;
         }
     return inter_tq_launch(cur, rs, H, W, bs, best, vbs ? sub : nullptr, qp_rd, qp_row, vbs, lam, out_split,
-                           out_mv, out_qtc, out_tokens, out_mae_num, out_recon, (hipStream_t)stream);
+                           out_mv, out_qtc, out_tokens, out_mae_num, out_recon, out_sse, (hipStream_t)stream);
 }
 
 size_t so_p_frame_scratch_elems(int H, int W, int bs, int vbs) {
@@ -184,7 +192,7 @@ size_t so_p_frame_scratch_elems(int H, int W, int bs, int vbs) {
 int so_encode_p_frame(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W, int bs, int sr,
                       int qp_rd, const int32_t* qp_row, int vbs, double lam, uint8_t* out_split,
                       int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae_num,
-                      uint8_t* out_recon, int32_t* scratch, void* stream) {
+                      uint8_t* out_recon, int32_t* out_sse, int32_t* scratch, void* stream) {
     const char* fn = "so_encode_p_frame";
     SO_TRY(check_geom(fn, H, W, bs, vbs));
     SO_NEED(scratch, fn);
@@ -193,7 +201,7 @@ int so_encode_p_frame(const uint8_t* cur, const uint8_t* const* refs, int nref, 
     int32_t* sub = vbs ? scratch + nb * 4 : nullptr;
     SO_TRY(so_me_full_search(cur, refs, nref, H, W, bs, sr, best, sub, stream));
     return so_inter_tq_recon(cur, refs, nref, H, W, bs, best, sub, qp_rd, qp_row, vbs, lam, out_split, out_mv,
-                             out_qtc, out_tokens, out_mae_num, out_recon, stream);
+                             out_qtc, out_tokens, out_mae_num, out_recon, out_sse, stream);
 }
 
 size_t so_i_frame_scratch_elems(int H, int W, int bs) {
@@ -204,16 +212,17 @@ size_t so_i_frame_scratch_elems(int H, int W, int bs) {
 
 int so_encode_i_frame(const uint8_t* cur, int H, int W, int bs, int sr, int qp_rd, const int32_t* qp_row,
                       int vbs, double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc,
-                      int32_t* out_tokens, int32_t* out_mae_num, uint8_t* out_recon, int32_t* scratch,
-                      void* stream) {
+                      int32_t* out_tokens, int32_t* out_mae_num, uint8_t* out_recon, int32_t* out_sse,
+                      int32_t* scratch, void* stream) {
     const char* fn = "so_encode_i_frame";
     SO_TRY(check_geom(fn, H, W, bs, vbs));
+    SO_TRY(check_intra_width(fn, W));
     SO_TRY(check_sr(fn, sr));
     SO_TRY(check_qp(fn, qp_rd));
     SO_NEED(cur, fn); SO_NEED(out_split, fn); SO_NEED(out_mv, fn); SO_NEED(out_qtc, fn);
     SO_NEED(out_tokens, fn); SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn); SO_NEED(scratch, fn);
     return intra_encode_launch(cur, H, W, bs, sr, qp_rd, qp_row, vbs, lam, out_split, out_mv, out_qtc, out_tokens,
-                               out_mae_num, out_recon, scratch, (hipStream_t)stream);
+                               out_mae_num, out_recon, out_sse, scratch, (hipStream_t)stream);
 }
 
 int so_inter_recon(const uint8_t* const* refs, int nref, int H, int W, int bs, int qp, const int32_t* qp_row,
@@ -231,6 +240,7 @@ int so_intra_recon(int H, int W, int bs, int qp, const int32_t* qp_row, const ui
                    const int16_t* qtc, uint8_t* out_recon, int32_t* scratch, void* stream) {
     const char* fn = "so_intra_recon";
     SO_TRY(check_geom(fn, H, W, bs, 0));
+    SO_TRY(check_intra_width(fn, W));
     SO_TRY(check_qp(fn, qp));
     SO_NEED(split, fn); SO_NEED(mv, fn); SO_NEED(qtc, fn); SO_NEED(out_recon, fn); SO_NEED(scratch, fn);
     // the recon kernel only needs sr to size its ring: the largest reachable offset is 64

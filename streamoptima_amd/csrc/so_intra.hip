@@ -10,9 +10,9 @@
 // mv -1.  The hard-coded 288x352 canvas (:1248) is generalised to the frame size.
 //
 // reconstruct_frame_intra (:1350-1417) is sequential along each block row (a block copies
-// from the reconstructed canvas left of it, unclipped float, final astype(uint8) wrap) but
-// the rows are independent: intra_recon_rows runs one wavefront per block row over
-// int32 values, the dequant/IDCT having been done for all blocks in parallel.
+// from the reconstructed canvas left of it, unclipped float, final astype(uint8) wrap);
+// intra_recon_kernel resolves those copy chains in parallel (pointer jumping), the
+// dequant/IDCT having been done for all blocks in parallel.
 #include "so_block.h"
 
 namespace so {
@@ -68,6 +68,31 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int sr, int qp_rd
         for (int c = 0; c < BS; ++c) s += abs(crow[c] - 128);
         sad = group_sum<G>(s);
         mv = -1;
+    } else if (BS == 16 && sr == 16) {
+        // Fast path.  A candidate dx > 0 reads only 128s (the canvas from x on), so its
+        // SAD equals dx = 0's and the |dx| tie rule always prefers dx = 0: only
+        // dx in [-16, 0] can win, and there (SAD, |dx|) is unique.  Canvas row bytes
+        // [x-16, x+16) = 4 original words + 4 words of 0x80; candidate words are funnel
+        // shifts of that array at compile-time offsets; v_sad_u8 per word.
+        const uint8_t* rp = cur + (size_t)(y + l) * W + x;
+        const uint4 lv = *reinterpret_cast<const uint4*>(rp - 16), cv = *reinterpret_cast<const uint4*>(rp);
+        const uint32_t Z[9] = {lv.x, lv.y, lv.z, lv.w, 0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u,
+                               0x80808080u};
+        const uint32_t C[4] = {cv.x, cv.y, cv.z, cv.w};
+        uint32_t bestk = 0xFFFFFFFFu;
+#pragma unroll
+        for (int dx = -16; dx <= 0; ++dx) {
+            const int off = 16 + dx, d = off >> 2, sh = off & 3;
+            uint32_t srow = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                srow = __builtin_amdgcn_sad_u8(C[k], __builtin_amdgcn_alignbyte(Z[d + k + 1], Z[d + k], sh), srow);
+            const int sfull = group_sum<G>((int)srow);
+            const uint32_t key = ((uint32_t)sfull << 8) | (uint32_t)(-dx);
+            bestk = key < bestk ? key : bestk;
+        }
+        sad = (int)(bestk >> 8);
+        mv = -(int)(bestk & 0xFF);
     } else {
         uint32_t bestk = 0xFFFFFFFFu;
         for (int dxi = 0; dxi <= 2 * sr; ++dxi) {
@@ -103,24 +128,64 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int sr, int qp_rd
             int scur[2][8];
 #pragma unroll
             for (int h = 0; h < 2; ++h) load_cur_row<8>(cur, W, xs, y + oy + r0 + 4 * h, scur[h]);
-            uint32_t bestk = 0xFFFFFFFFu;
-            for (int dxi = 0; dxi <= 2 * sr; ++dxi) {
-                const int dx = dxi - sr;
-                if (!(xs + dx >= 0 && xs + dx + SB <= W)) continue;
-                int s = 0;
+            int ssad;
+            if (sr == 16) {
+                // fast path, as for the full block: only dx in [-16, 0] can win
+                uint32_t Zs[2][9], Cs[2][2];
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const uint8_t* lr = left + (oy + r0 + 4 * h) * kIntraMaxSr;
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) s += abs(scur[h][c] - canvas_at(lr, sr, xs + dx + c, x));
+                    const uint8_t* rp = cur + (size_t)(y + oy + r0 + 4 * h) * W + x;
+                    const uint4 lv = *reinterpret_cast<const uint4*>(rp - 16);
+                    const uint2 cv = *reinterpret_cast<const uint2*>(rp + (j & 1) * 8);
+                    Zs[h][0] = lv.x; Zs[h][1] = lv.y; Zs[h][2] = lv.z; Zs[h][3] = lv.w;
+                    Zs[h][4] = Zs[h][5] = Zs[h][6] = Zs[h][7] = Zs[h][8] = 0x80808080u;
+                    Cs[h][0] = cv.x; Cs[h][1] = cv.y;
                 }
-                s += __shfl_xor(s, 1, 64);
-                s += __shfl_xor(s, 2, 64);
-                const uint32_t k = intra_key(s, dx, 2 * sr - dxi);
-                bestk = k < bestk ? k : bestk;
+                const int base = 16 + (j & 1) * 8;   // canvas byte of column xs relative to x-16
+                uint32_t bestk = 0xFFFFFFFFu;
+#pragma unroll
+                for (int dx = -16; dx <= 0; ++dx) {
+                    const int off = base + dx;        // 0 .. 24, depends on j (wave-divergent)
+                    const int d = off >> 2, sh = off & 3;
+                    uint32_t srow = 0;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        // runtime word index (j differs across lanes): select from registers
+                        uint32_t w0 = Zs[h][0], w1 = Zs[h][1], w2 = Zs[h][2];
+#pragma unroll
+                        for (int q = 1; q <= 6; ++q)
+                            if (d == q) { w0 = Zs[h][q]; w1 = Zs[h][q + 1]; w2 = Zs[h][q + 2]; }
+                        srow = __builtin_amdgcn_sad_u8(Cs[h][0], __builtin_amdgcn_alignbyte(w1, w0, sh), srow);
+                        srow = __builtin_amdgcn_sad_u8(Cs[h][1], __builtin_amdgcn_alignbyte(w2, w1, sh), srow);
+                    }
+                    int s4 = (int)srow;
+                    s4 += __shfl_xor(s4, 1, 64);
+                    s4 += __shfl_xor(s4, 2, 64);
+                    const uint32_t key = ((uint32_t)s4 << 8) | (uint32_t)(-dx);
+                    bestk = key < bestk ? key : bestk;
+                }
+                ssad = (int)(bestk >> 8);
+                smv = -(int)(bestk & 0xFF);
+            } else {
+                uint32_t bestk = 0xFFFFFFFFu;
+                for (int dxi = 0; dxi <= 2 * sr; ++dxi) {
+                    const int dx = dxi - sr;
+                    if (!(xs + dx >= 0 && xs + dx + SB <= W)) continue;
+                    int s = 0;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const uint8_t* lr = left + (oy + r0 + 4 * h) * kIntraMaxSr;
+#pragma unroll
+                        for (int c = 0; c < 8; ++c) s += abs(scur[h][c] - canvas_at(lr, sr, xs + dx + c, x));
+                    }
+                    s += __shfl_xor(s, 1, 64);
+                    s += __shfl_xor(s, 2, 64);
+                    const uint32_t k = intra_key(s, dx, 2 * sr - dxi);
+                    bestk = k < bestk ? k : bestk;
+                }
+                ssad = (int)(bestk >> 15);
+                smv = 2 * sr - (int)(bestk & 0xFF) - sr;
             }
-            const int ssad = (int)(bestk >> 15);
-            smv = 2 * sr - (int)(bestk & 0xFF) - sr;
             int sres[2][8];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -180,7 +245,7 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int sr, int qp_rd
             }
             double srd[2][8];
             xform2d_sub<true>(dl, l, sdq, srd);
-            // idres is row-major bs x bs for every block (intra_recon_rows indexes pixels)
+            // idres is row-major bs x bs for every block (intra_recon_kernel indexes pixels)
 #pragma unroll
             for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -243,77 +308,77 @@ dequant_idct_kernel(int H, int W, int qp, const int32_t* __restrict__ qp_row,
     }
 }
 
-// Row-sequential intra reconstruction: one wavefront per block row.  Lane t owns
-// PPL = bs*bs/64 pixels of the current block.  The canvas left of the block is kept as
-// int32 (unclipped, like the reference's float canvas) in an LDS ring of the previous
-// NR blocks; columns at or right of the block read 128.
+// Intra reconstruction (reconstruct_frame_intra, Encoder.py:1350-1417 / decoder.py:367-432):
+// every pixel of a block copies the canvas at column src = x + c + mv (same pixel row)
+// and adds its IDCT residual; the canvas is the reconstruction where src < x and 128
+// where src >= x; blocks at x == 0 use 128.  So pixel p's value is
+//     128 + res[p] + res[src(p)] + res[src(src(p))] + ...   (until a source is >= its x)
+// a chain that only moves left inside one pixel row.  One workgroup per pixel row
+// resolves all chains by pointer jumping (log2(#blocks) rounds) in LDS: the sequential
+// block-by-block dependency of the reference costs no serial latency here.
 template <int BS>
-__global__ void __launch_bounds__(64)
-intra_recon_rows_kernel(int H, int W, int sr, const uint8_t* __restrict__ split,
-                        const int16_t* __restrict__ mv, const int32_t* __restrict__ idres,
-                        uint8_t* __restrict__ out_recon) {
-    constexpr int PPL = BS * BS / 64, SB = BS / 2;
-    constexpr int NR = kIntraMaxSr / BS + 1;
-    __shared__ int ring[NR][BS * BS];
-    const int t = threadIdx.x;
-    const int nbx = W / BS;
-    const int by = blockIdx.x;
-    const int y = by * BS;
-    const int nring = (sr + BS - 1) / BS + 1;
-    int res_next[PPL];
-    {
-        const int32_t* rb = idres + (size_t)(by * nbx) * BS * BS;
-#pragma unroll
-        for (int p = 0; p < PPL; ++p) res_next[p] = rb[t * PPL + p];
+__global__ void __launch_bounds__(256)
+intra_recon_kernel(int H, int W, const uint8_t* __restrict__ split, const int16_t* __restrict__ mv,
+                   const int32_t* __restrict__ idres, const uint8_t* __restrict__ cur,
+                   uint8_t* __restrict__ out_recon, int32_t* __restrict__ out_sse) {
+    constexpr int SB = BS / 2, NT = 256;
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];   // 12 * W bytes
+    int* sval[2] = {reinterpret_cast<int*>(dyn), reinterpret_cast<int*>(dyn) + W};
+    short* snxt[2] = {reinterpret_cast<short*>(dyn + 8 * (size_t)W), reinterpret_cast<short*>(dyn + 8 * (size_t)W) + W};
+    __shared__ int ssum[NT / 64];
+    const int yy = blockIdx.x, tid = threadIdx.x;
+    const int by = yy / BS, i = yy - by * BS, nbx = W / BS;
+    for (int p = tid; p < W; p += NT) {
+        const int bx = p / BS, c = p - bx * BS, x = bx * BS, b = by * nbx + bx;
+        const int res = idres[(size_t)b * BS * BS + i * BS + c];
+        int nx = -1;
+        if (x != 0) {
+            const int jj = split[b] ? ((i >= SB) * 2 + (c >= SB)) : 0;
+            const int src = x + c + mv[(size_t)b * 4 + jj];
+            nx = src < x ? src : -1;
+        }
+        sval[0][p] = res;
+        snxt[0][p] = (short)nx;
     }
-    for (int bx = 0; bx < nbx; ++bx) {
-        const int b = by * nbx + bx, x = bx * BS;
-        int res[PPL];
-#pragma unroll
-        for (int p = 0; p < PPL; ++p) res[p] = res_next[p];
-        if (bx + 1 < nbx) {
-            const int32_t* rb = idres + (size_t)(b + 1) * BS * BS;
-#pragma unroll
-            for (int p = 0; p < PPL; ++p) res_next[p] = rb[t * PPL + p];
-        }
-        const bool sp = split[b] != 0;
-        int v[PPL];
-#pragma unroll
-        for (int p = 0; p < PPL; ++p) {
-            const int pix = t * PPL + p, i = pix / BS, c = pix % BS;
-            if (x == 0) {
-                v[p] = 128 + res[p];
-            } else {
-                const int jj = sp ? ((i >= SB) * 2 + (c >= SB)) : 0;
-                const int src = x + c + mv[(size_t)b * 4 + jj];
-                int base = 128;
-                if (src < x) {
-                    const int sbx = src / BS;
-                    base = ring[sbx % nring][i * BS + (src - sbx * BS)];
-                }
-                v[p] = base + res[p];
+    __syncthreads();
+    int cb = 0;
+    // chain length <= number of blocks in the row; every hop moves >= 1 block left
+    for (int span = 1; span < nbx; span <<= 1) {
+        for (int p = tid; p < W; p += NT) {
+            const int nx = snxt[cb][p];
+            int v = sval[cb][p], n2 = nx;
+            if (nx >= 0) {
+                v += sval[cb][nx];
+                n2 = snxt[cb][nx];
             }
+            sval[cb ^ 1][p] = v;
+            snxt[cb ^ 1][p] = (short)n2;
         }
-        wave_sync();
+        __syncthreads();
+        cb ^= 1;
+    }
+    int sse = 0;
+    for (int p = tid; p < W; p += NT) {
+        const int v = (128 + sval[cb][p]) & 255;
+        out_recon[(size_t)yy * W + p] = (uint8_t)v;
+        if (out_sse) {
+            const int d = (int)cur[(size_t)yy * W + p] - v;
+            sse += d * d;
+        }
+    }
+    if (out_sse) {
 #pragma unroll
-        for (int p = 0; p < PPL; ++p) ring[bx % nring][t * PPL + p] = v[p];
-        wave_sync();
-        if constexpr (PPL == 4) {
-            const int pix = t * 4, i = pix / BS, c = pix % BS;
-            const uint32_t w = (uint32_t)(v[0] & 255) | ((uint32_t)(v[1] & 255) << 8) |
-                               ((uint32_t)(v[2] & 255) << 16) | ((uint32_t)(v[3] & 255) << 24);
-            *reinterpret_cast<uint32_t*>(out_recon + (size_t)(y + i) * W + x + c) = w;
-        } else {
-            const int pix = t, i = pix / BS, c = pix % BS;
-            out_recon[(size_t)(y + i) * W + x + c] = (uint8_t)(v[0] & 255);
-        }
+        for (int m = 32; m >= 1; m >>= 1) sse += __shfl_xor(sse, m, 64);
+        if ((tid & 63) == 0) ssum[tid >> 6] = sse;
+        __syncthreads();
+        if (tid == 0) out_sse[yy] = ssum[0] + ssum[1] + ssum[2] + ssum[3];
     }
 }
 
 int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int qp_rd, const int32_t* qp_row,
                         int vbs, double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc,
-                        int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon, int32_t* idres,
-                        hipStream_t st) {
+                        int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon, int32_t* out_sse,
+                        int32_t* idres, hipStream_t st) {
     const int nb = (W / bs) * (H / bs);
     const int bpw = 256 / bs;
     dim3 grid((nb + bpw - 1) / bpw), blk(256);
@@ -329,12 +394,12 @@ int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int qp
     int rc = check_launch("intra_tq_kernel");
     if (rc) return rc;
     if (bs == 16)
-        hipLaunchKernelGGL((intra_recon_rows_kernel<16>), dim3(H / bs), dim3(64), 0, st, H, W, sr, out_split,
-                           out_mv, idres, out_recon);
+        hipLaunchKernelGGL((intra_recon_kernel<16>), dim3(H), dim3(256), 12 * (size_t)W, st, H, W, out_split, out_mv, idres, cur,
+                           out_recon, out_sse);
     else
-        hipLaunchKernelGGL((intra_recon_rows_kernel<8>), dim3(H / bs), dim3(64), 0, st, H, W, sr, out_split,
-                           out_mv, idres, out_recon);
-    return check_launch("intra_recon_rows_kernel");
+        hipLaunchKernelGGL((intra_recon_kernel<8>), dim3(H), dim3(256), 12 * (size_t)W, st, H, W, out_split, out_mv, idres, cur,
+                           out_recon, out_sse);
+    return check_launch("intra_recon_kernel");
 }
 
 int intra_recon_launch(int H, int W, int bs, int sr, int qp, const int32_t* qp_row, const uint8_t* split,
@@ -350,12 +415,12 @@ int intra_recon_launch(int H, int W, int bs, int sr, int qp, const int32_t* qp_r
     int rc = check_launch("dequant_idct_kernel");
     if (rc) return rc;
     if (bs == 16)
-        hipLaunchKernelGGL((intra_recon_rows_kernel<16>), dim3(H / bs), dim3(64), 0, st, H, W, sr, split, mv,
-                           idres, out_recon);
+        hipLaunchKernelGGL((intra_recon_kernel<16>), dim3(H), dim3(256), 12 * (size_t)W, st, H, W, split, mv, idres, nullptr,
+                           out_recon, nullptr);
     else
-        hipLaunchKernelGGL((intra_recon_rows_kernel<8>), dim3(H / bs), dim3(64), 0, st, H, W, sr, split, mv,
-                           idres, out_recon);
-    return check_launch("intra_recon_rows_kernel");
+        hipLaunchKernelGGL((intra_recon_kernel<8>), dim3(H), dim3(256), 12 * (size_t)W, st, H, W, split, mv, idres, nullptr,
+                           out_recon, nullptr);
+    return check_launch("intra_recon_kernel");
 }
 
 }  // namespace so

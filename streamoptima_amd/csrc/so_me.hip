@@ -209,55 +209,81 @@ me_fast_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
 // t = row - r in range it issues bs/4 QSADs.  The current block is wave-uniform, so it
 // lives in SGPRs (scalar loads) and feeds S1 directly.
 // ---------------------------------------------------------------------------------------
+// The current (sub-)block is wave-uniform: read it through the constant address space so
+// the compiler issues scalar loads and keeps the pixels in SGPRs (QSAD operand S1).
+typedef const __attribute__((address_space(4))) uint32_t* const_u32p;
+template <int NR, int NDW>
+SO_DEV void load_cur_sgpr(const uint8_t* __restrict__ cur, int W, int x, int y, uint32_t (&cr)[NR][NDW]) {
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const_u32p p = (const_u32p)(cur + (size_t)(y + r) * W + x);
+#pragma unroll
+        for (int k = 0; k < NDW; ++k) cr[r][k] = p[k];
+    }
+}
+
 template <int TBS>
-SO_DEV uint64_t me_qsad_task(const uint32_t* __restrict__ win, int wpd, const uint32_t (&cr)[TBS][TBS / 4],
+SO_DEV uint64_t me_qsad_task(const uint32_t* __restrict__ win, int wpd, const uint8_t* __restrict__ cur,
                              int lane, int W, int H, int x, int y, int wrow0, int wcol0, int ref) {
-    constexpr int SR = 16, D = 33, NDW = TBS / 4, DYS = 5, NG = 9, NROW = DYS + TBS - 1;
+    constexpr int SR = 16, D = 33, NDW = TBS / 4, DYS = 5, NG = 9;
+    constexpr int HALF = 8, NPASS = TBS / HALF, NROW = DYS + HALF - 1;
+    // opaque per call: stops LICM from hoisting 20 per-lane key constants out of the
+    // caller's block loop (they were kept live across it and spilled)
+    asm volatile("" : "+v"(lane));
     const int s = lane / NG, g = lane - s * NG;
     uint64_t acc[DYS];
 #pragma unroll
     for (int t = 0; t < DYS; ++t) acc[t] = 0;
-    const uint32_t* rowp = win + (wrow0 + DYS * s) * wpd + (wcol0 >> 2) + g;
-    // one window row in flight ahead of the one being consumed; the scheduling barrier
-    // keeps the compiler from hoisting every row's loads (register pressure -> spills)
-    uint32_t wc[NDW + 1], wn[NDW + 1];
+    // the current rows are consumed in passes of 8 (<= 32 SGPRs live)
 #pragma unroll
-    for (int k = 0; k <= NDW; ++k) wc[k] = rowp[k];
+    for (int pass = 0; pass < NPASS; ++pass) {
+        uint32_t cr[HALF][NDW];
+        load_cur_sgpr<HALF, NDW>(cur, W, x, y + pass * HALF, cr);
+        const uint32_t* rowp = win + (wrow0 + DYS * s + pass * HALF) * wpd + (wcol0 >> 2) + g;
+        // one window row in flight ahead of the one being consumed; the scheduling barrier
+        // keeps the compiler from hoisting every row's loads (register pressure -> spills)
+        uint32_t wc[NDW + 1], wn[NDW + 1];
 #pragma unroll
-    for (int jj = 0; jj < NROW; ++jj) {
-        if (jj + 1 < NROW) {
+        for (int k = 0; k <= NDW; ++k) wc[k] = rowp[k];
 #pragma unroll
-            for (int k = 0; k <= NDW; ++k) wn[k] = rowp[(jj + 1) * wpd + k];
-        }
+        for (int jj = 0; jj < NROW; ++jj) {
+            if (jj + 1 < NROW) {
 #pragma unroll
-        for (int t = 0; t < DYS; ++t) {
-            const int r = jj - t;
-            if (r >= 0 && r < TBS) {
-#pragma unroll
-                for (int k = 0; k < NDW; ++k)
-                    acc[t] = __builtin_amdgcn_qsad_pk_u16_u8(((uint64_t)wc[k + 1] << 32) | wc[k], cr[r][k], acc[t]);
+                for (int k = 0; k <= NDW; ++k) wn[k] = rowp[(jj + 1) * wpd + k];
             }
-        }
-#pragma unroll
-        for (int k = 0; k <= NDW; ++k) wc[k] = wn[k];
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    uint64_t best = kNoKey;
-    if (s < 7) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int dxi = 4 * g + i, dx = dxi - SR;
-            const bool xok = dxi < D && (x + dx >= 0) && (x + dx < W - TBS);
-            const uint32_t adx = (uint32_t)(dx < 0 ? -dx : dx);
 #pragma unroll
             for (int t = 0; t < DYS; ++t) {
-                const int di = DYS * s + t, dy = di - SR;
-                const bool ok = xok && di < D && (y + dy >= 0) && (y + dy < H - TBS);
-                const uint32_t sad = (uint32_t)((acc[t] >> (16 * i)) & 0xFFFF);
-                const uint64_t k = me_key(sad, adx + (uint32_t)(dy < 0 ? -dy : dy), (uint32_t)ref,
-                                          (uint32_t)(dxi * D + di));
-                best = (ok && k < best) ? k : best;
+                const int r = jj - t;
+                if (r >= 0 && r < HALF) {
+#pragma unroll
+                    for (int k = 0; k < NDW; ++k)
+                        acc[t] = __builtin_amdgcn_qsad_pk_u16_u8(((uint64_t)wc[k + 1] << 32) | wc[k], cr[r][k], acc[t]);
+                }
             }
+#pragma unroll
+            for (int k = 0; k <= NDW; ++k) wc[k] = wn[k];
+            // row fence: this row's QSADs are complete and the next-next row's loads have not
+            // been hoisted above it (an IR-level barrier; sched_barrier alone is not)
+            asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]) : : "memory");
+        }
+    }
+    // no branch here: a branch around the epilogue lets the compiler sink every QSAD
+    // into it and issue all window loads first (register pressure -> spills)
+    const bool lane_ok = s < 7;
+    uint64_t best = kNoKey;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int dxi = 4 * g + i, dx = dxi - SR;
+        const bool xok = lane_ok && dxi < D && (x + dx >= 0) && (x + dx < W - TBS);
+        const uint32_t adx = (uint32_t)(dx < 0 ? -dx : dx);
+#pragma unroll
+        for (int t = 0; t < DYS; ++t) {
+            const int di = DYS * s + t, dy = di - SR;
+            const bool ok = xok && di < D && (y + dy >= 0) && (y + dy < H - TBS);
+            const uint32_t sad = (uint32_t)((acc[t] >> (16 * i)) & 0xFFFF);
+            const uint64_t k = me_key(sad, adx + (uint32_t)(dy < 0 ? -dy : dy), (uint32_t)ref,
+                                      (uint32_t)(dxi * D + di));
+            best = (ok && k < best) ? k : best;
         }
     }
     return best;
@@ -275,17 +301,6 @@ SO_DEV uint64_t wave_min_u64(uint64_t v) {
 
 // The current (sub-)block is wave-uniform: read it through the constant address space so
 // the compiler issues scalar loads and keeps the pixels in SGPRs (QSAD operand S1).
-typedef const __attribute__((address_space(4))) uint32_t* const_u32p;
-template <int TBS>
-SO_DEV void load_cur_sgpr(const uint8_t* __restrict__ cur, int W, int x, int y, uint32_t (&cr)[TBS][TBS / 4]) {
-#pragma unroll
-    for (int r = 0; r < TBS; ++r) {
-        const_u32p p = (const_u32p)(cur + (size_t)(y + r) * W + x);
-#pragma unroll
-        for (int k = 0; k < TBS / 4; ++k) cr[r][k] = p[k];
-    }
-}
-
 template <int BS, bool SUB>
 __global__ void __launch_bounds__(1024)
 me_qsad_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W,
@@ -320,9 +335,7 @@ me_qsad_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
                 const int bxl = u % TB, byl = u / TB;
                 const int gbx = tx * TB + bxl, gby = ty * TB + byl;
                 if (gbx >= nbx || gby >= nby) continue;
-                uint32_t cr[BS][BS / 4];
-                load_cur_sgpr<BS>(cur, W, gbx * BS, gby * BS, cr);
-                uint64_t k = me_qsad_task<BS>(win, T::WPD, cr, lane, W, H, gbx * BS, gby * BS, byl * BS,
+                uint64_t k = me_qsad_task<BS>(win, T::WPD, cur, lane, W, H, gbx * BS, gby * BS, byl * BS,
                                               bxl * BS, r);
                 k = wave_min_u64(k);
                 if (lane == 0 && k != kNoKey) atomicMin(&keys[u], (unsigned long long)k);
@@ -332,9 +345,7 @@ me_qsad_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
                 const int gbx = tx * TB + bxl, gby = ty * TB + byl;
                 if (gbx >= nbx || gby >= nby) continue;
                 const int ox = (j & 1) * SB, oy = (j >> 1) * SB;
-                uint32_t cr[SB][SB / 4];
-                load_cur_sgpr<SB>(cur, W, gbx * BS + ox, gby * BS + oy, cr);
-                uint64_t k = me_qsad_task<SB>(win, T::WPD, cr, lane, W, H, gbx * BS + ox, gby * BS + oy,
+                uint64_t k = me_qsad_task<SB>(win, T::WPD, cur, lane, W, H, gbx * BS + ox, gby * BS + oy,
                                               byl * BS + oy, bxl * BS + ox, r);
                 k = wave_min_u64(k);
                 if (lane == 0 && k != kNoKey) atomicMin(&keys[u], (unsigned long long)k);
@@ -349,6 +360,171 @@ me_qsad_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
         const int b = gby * nbx + gbx;
         if (i < T::NBLK) decode_key(keys[i], SR, out_best + (size_t)b * 4);
         else decode_key(keys[i], SR, out_sub + ((size_t)b * 4 + ((i - T::NBLK) & 3)) * 4);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Wave path (default): one wavefront per (sub-)block, current block in SGPRs, v_sad_u8.
+//
+// Measured on gfx950 (tools/ubench_sad.cpp): v_sad_u8 ~4.4 cycles per wave64 instruction
+// (256 |diffs|) vs ~20.8 for v_qsad_pk_u16_u8 (1024 |diffs|), so plain v_sad_u8 it is.
+// Phase 1: lane = hh*32 + xi: dx = xi - 16 (xi < 32), dy = 16*hh + t - 16 (t < 17), i.e.
+// the two lane halves cover dy in [-16, 0] and [0, 16] (dy 0 twice).  The lane slides
+// over its 17 + bs - 1 window rows and adds each aligned 4-byte group into acc[t] for
+// every current row r = row - t (current pixels are wave-uniform SGPR operands).
+// Phase 2: the dx = +16 column, lanes 0..32 one dy each, full SAD.
+// VGPRs: 17 accumulators + one window row; PMC showed the per-lane-block kernel above
+// waiting 47% of its time at 2.75 waves/SIMD, this one runs at up to 8 waves/SIMD.
+// ---------------------------------------------------------------------------------------
+template <int TBS>
+SO_DEV uint64_t me_wave_task(const uint32_t* __restrict__ win, int wpd, const uint8_t* __restrict__ cur,
+                             int lane, int W, int H, int x, int y, int wrow0, int wcol0, int ref) {
+    constexpr int SR = 16, D = 33, NDW = TBS / 4, NT = 17;
+    constexpr int HALF = 8, NPASS = TBS / HALF, NROW = NT + HALF - 1;   // <= 32 SGPRs of pixels live
+    asm volatile("" : "+v"(lane));   // keep per-lane constants inside the caller's loop
+    const int xi = lane & 31, hh = lane >> 5;
+    uint32_t acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = 0;
+    const int c = wcol0 + xi;
+    const uint32_t sh = (uint32_t)(c & 3);
+#pragma unroll
+    for (int pass = 0; pass < NPASS; ++pass) {
+        uint32_t cr[HALF][NDW];
+        load_cur_sgpr<HALF, NDW>(cur, W, x, y + pass * HALF, cr);
+        const uint32_t* rowp = win + (wrow0 + 16 * hh + pass * HALF) * wpd + (c >> 2);
+        uint32_t wc[NDW + 1], wn[NDW + 1];
+#pragma unroll
+        for (int k = 0; k <= NDW; ++k) wc[k] = rowp[k];
+#pragma unroll
+        for (int jj = 0; jj < NROW; ++jj) {
+            if (jj + 1 < NROW) {   // one row in flight ahead of the row being consumed
+#pragma unroll
+                for (int k = 0; k <= NDW; ++k) wn[k] = rowp[(jj + 1) * wpd + k];
+            }
+            uint32_t rr[NDW];
+#pragma unroll
+            for (int k = 0; k < NDW; ++k) rr[k] = __builtin_amdgcn_alignbyte(wc[k + 1], wc[k], sh);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int r = jj - t;
+                if (r >= 0 && r < HALF) {
+#pragma unroll
+                    for (int k = 0; k < NDW; ++k) acc[t] = __builtin_amdgcn_sad_u8(cr[r][k], rr[k], acc[t]);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k <= NDW; ++k) wc[k] = wn[k];
+            // row fence (IR level): this row's SADs complete here and no later row's loads or
+            // alignments are hoisted above it -- keeps VGPRs ~ 17 acc + 2 rows
+            asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]),
+                         "+v"(acc[6]), "+v"(acc[7]), "+v"(acc[8]), "+v"(acc[9]), "+v"(acc[10]), "+v"(acc[11]),
+                         "+v"(acc[12]), "+v"(acc[13]), "+v"(acc[14]), "+v"(acc[15]), "+v"(acc[16]) : : "memory");
+        }
+    }
+    uint64_t best = kNoKey;
+    {
+        const int dx = xi - SR;
+        const bool xok = (x + dx >= 0) && (x + dx < W - TBS);
+        const uint32_t adx = (uint32_t)(dx < 0 ? -dx : dx);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int di = 16 * hh + t, dy = di - SR;
+            const bool ok = xok && (y + dy >= 0) && (y + dy < H - TBS);
+            const uint64_t k = me_key(acc[t], adx + (uint32_t)(dy < 0 ? -dy : dy), (uint32_t)ref,
+                                      (uint32_t)(xi * D + di));
+            best = (ok && k < best) ? k : best;
+        }
+    }
+    // phase 2: dx = +16, lane = di
+    {
+        const int di = lane < D ? lane : D - 1;
+        const int c2 = wcol0 + 32;
+        const uint32_t sh2 = (uint32_t)(c2 & 3);
+        const uint32_t* rowp = win + (wrow0 + di) * wpd + (c2 >> 2);
+        uint32_t a2 = 0;
+#pragma unroll
+        for (int pass = 0; pass < NPASS; ++pass) {
+            uint32_t cr[HALF][NDW];
+            load_cur_sgpr<HALF, NDW>(cur, W, x, y + pass * HALF, cr);
+#pragma unroll
+            for (int r = 0; r < HALF; ++r) {
+                uint32_t w[NDW + 1];
+#pragma unroll
+                for (int k = 0; k <= NDW; ++k) w[k] = rowp[(pass * HALF + r) * wpd + k];
+#pragma unroll
+                for (int k = 0; k < NDW; ++k)
+                    a2 = __builtin_amdgcn_sad_u8(cr[r][k], __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh2), a2);
+            }
+            asm volatile("" : "+v"(a2) : : "memory");
+        }
+        const int dx = SR, dy = di - SR;
+        const bool ok = lane < D && (x + dx < W - TBS) && (y + dy >= 0) && (y + dy < H - TBS);
+        const uint64_t k = me_key(a2, (uint32_t)(dx + (dy < 0 ? -dy : dy)), (uint32_t)ref, (uint32_t)(32 * D + di));
+        best = (ok && k < best) ? k : best;
+    }
+    return best;
+}
+
+template <int BS, bool SUB>
+__global__ void __launch_bounds__(512)
+me_wave_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W,
+               int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub) {
+    constexpr int SR = 16, SB = BS / 2, NW = 8;
+    constexpr int TBX = (BS == 16) ? 8 : 16, TBY = (BS == 16) ? 4 : 8;   // 128 x 64 px tile
+    constexpr int WR = TBY * BS + 2 * SR, WC = TBX * BS + 2 * SR;
+    constexpr int WPD = (WC + 16) / 4 + 1, WCD = WC / 4;
+    constexpr int NBLK = TBX * TBY, NUNIT = NBLK * (SUB ? 5 : 1);
+    __shared__ uint32_t win[WR * WPD];
+    __shared__ unsigned long long keys[NUNIT];
+    const int nbx = W / BS, nby = H / BS;
+    const int tiles_x = (nbx + TBX - 1) / TBX;
+    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    const int x0 = tx * TBX * BS, y0 = ty * TBY * BS;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int i = tid; i < NUNIT; i += NW * 64) keys[i] = kNoKey;
+    for (int r = 0; r < nref; ++r) {
+        const uint8_t* ref = refs.p[r];
+        __syncthreads();
+        for (int i = tid; i < WR * WPD; i += NW * 64) {
+            const int wr = i / WPD, wc = i % WPD;
+            const int gy = y0 - SR + wr, gx = x0 - SR + wc * 4;
+            uint32_t v = 0;
+            if (wc < WCD && gy >= 0 && gy < H && gx >= 0 && gx + 4 <= W)
+                v = *reinterpret_cast<const uint32_t*>(ref + (size_t)gy * W + gx);
+            win[i] = v;
+        }
+        __syncthreads();
+        for (int u = wave; u < NUNIT; u += NW) {
+            if (u < NBLK) {
+                const int bxl = u % TBX, byl = u / TBX;
+                const int gbx = tx * TBX + bxl, gby = ty * TBY + byl;
+                if (gbx >= nbx || gby >= nby) continue;
+                uint64_t k = me_wave_task<BS>(win, WPD, cur, lane, W, H, gbx * BS, gby * BS, byl * BS, bxl * BS, r);
+                k = wave_min_u64(k);
+                if (lane == 0 && k != kNoKey) atomicMin(&keys[u], (unsigned long long)k);
+            } else if constexpr (SUB) {
+                const int sidx = u - NBLK, blk = sidx >> 2, j = sidx & 3;
+                const int bxl = blk % TBX, byl = blk / TBX;
+                const int gbx = tx * TBX + bxl, gby = ty * TBY + byl;
+                if (gbx >= nbx || gby >= nby) continue;
+                const int ox = (j & 1) * SB, oy = (j >> 1) * SB;
+                uint64_t k = me_wave_task<SB>(win, WPD, cur, lane, W, H, gbx * BS + ox, gby * BS + oy, byl * BS + oy,
+                                              bxl * BS + ox, r);
+                k = wave_min_u64(k);
+                if (lane == 0 && k != kNoKey) atomicMin(&keys[u], (unsigned long long)k);
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < NUNIT; i += NW * 64) {
+        const int blk = i < NBLK ? i : (i - NBLK) >> 2;
+        const int gbx = tx * TBX + blk % TBX, gby = ty * TBY + blk / TBX;
+        if (gbx >= nbx || gby >= nby) continue;
+        const int b = gby * nbx + gbx;
+        if (i < NBLK) decode_key(keys[i], SR, out_best + (size_t)b * 4);
+        else decode_key(keys[i], SR, out_sub + ((size_t)b * 4 + ((i - NBLK) & 3)) * 4);
     }
 }
 
@@ -405,8 +581,26 @@ int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, in
               int32_t* out_best, int32_t* out_sub, hipStream_t st) {
     const int nbx = W / bs, nby = H / bs;
     if (sr == 16 && (bs == 16 || bs == 8) && (out_sub == nullptr || bs == 16)) {
-        static const bool use_sad = getenv("SO_ME_IMPL") && strcmp(getenv("SO_ME_IMPL"), "sad") == 0;
-        if (!use_sad) {
+        // SO_ME_IMPL (A/B only): "wave" / "qsad" select the alternative kernels; default: v_sad_u8
+        // per (block, dx) lane (fastest measured, tools/me_ab.py)
+        const char* impl = getenv("SO_ME_IMPL");
+        const bool use_wave = impl && strcmp(impl, "wave") == 0;
+        const bool use_qsad = impl && strcmp(impl, "qsad") == 0;
+        if (use_wave) {
+            const int tbx = bs == 16 ? 8 : 16, tby = bs == 16 ? 4 : 8;
+            const int tiles = ((nbx + tbx - 1) / tbx) * ((nby + tby - 1) / tby);
+            if (bs == 16 && out_sub)
+                hipLaunchKernelGGL((me_wave_kernel<16, true>), dim3(tiles), dim3(512), 0, st, cur, refs, nref, H, W,
+                                   out_best, out_sub);
+            else if (bs == 16)
+                hipLaunchKernelGGL((me_wave_kernel<16, false>), dim3(tiles), dim3(512), 0, st, cur, refs, nref, H, W,
+                                   out_best, out_sub);
+            else
+                hipLaunchKernelGGL((me_wave_kernel<8, false>), dim3(tiles), dim3(512), 0, st, cur, refs, nref, H, W,
+                                   out_best, nullptr);
+            return check_launch("me_wave_kernel");
+        }
+        if (use_qsad) {
             if (bs == 16) {
                 using T = MeTile<16>;
                 const int tiles = ((nbx + T::TB - 1) / T::TB) * ((nby + T::TB - 1) / T::TB);

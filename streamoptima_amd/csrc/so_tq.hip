@@ -21,7 +21,7 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W,
                 const int32_t* __restrict__ qp_row, double lam, uint8_t* __restrict__ out_split,
                 int16_t* __restrict__ out_mv, int16_t* __restrict__ out_qtc,
                 int32_t* __restrict__ out_tokens, int32_t* __restrict__ out_mae,
-                uint8_t* __restrict__ out_recon) {
+                uint8_t* __restrict__ out_recon, int32_t* __restrict__ out_sse) {
     constexpr int G = BS, BPW = 256 / G, SB = BS / 2;
     constexpr int LDS_D = VBS ? 288 : BS * (BS + 1);
     __shared__ double ldsd[BPW * LDS_D];
@@ -100,7 +100,7 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W,
         }
     }
 
-    int tok;
+    int tok, sse = 0;
     if (!split) {
         if (qpr != qp_rd) quant_row<BS>(tc, l, qpr, q);
         tok = block_tokens<BS>(fl, l, q);
@@ -112,6 +112,12 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W,
 #pragma unroll
         for (int c = 0; c < BS; ++c) rec[c] = pred[c] + (int)__builtin_rint(rd[c]);
         store_row_u8<BS>(out_recon, W, x, y + l, rec);
+        sse = 0;
+#pragma unroll
+        for (int c = 0; c < BS; ++c) {
+            const int d = crow[c] - (rec[c] & 255);
+            sse += d * d;
+        }
         for (int k = l; k < 12; k += G) out_mv[(size_t)b * 12 + k] = (int16_t)(k == 0 ? dx : k == 1 ? dy : k == 2 ? rf : 0);
     } else {
         if constexpr (VBS) {
@@ -129,22 +135,31 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W,
             }
             double srd[2][8];
             xform2d_sub<true>(dl, l, sdq, srd);
+            sse = 0;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                int rec[8];
+                int rec[8], scur[8];
 #pragma unroll
                 for (int c = 0; c < 8; ++c) rec[c] = spred[h][c] + (int)__builtin_rint(srd[h][c]);
                 store_row_u8<8>(out_recon, W, xs, ys + r0 + 4 * h, rec);
+                load_cur_row<8>(cur, W, xs, ys + r0 + 4 * h, scur);
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const int d = scur[c] - (rec[c] & 255);
+                    sse += d * d;
+                }
             }
             if (r0 < 3) out_mv[(size_t)b * 12 + 3 * j + r0] = (int16_t)(r0 == 0 ? sdx : r0 == 1 ? sdy : sref);
         } else {
             tok = 0;
         }
     }
+    if (out_sse) sse = group_sum<G>(sse);
     if (l == 0) {
         out_split[b] = (uint8_t)split;
         out_tokens[b] = tok;
         out_mae[b] = mae_num;
+        if (out_sse) out_sse[b] = sse;
     }
 }
 
@@ -207,19 +222,19 @@ inter_recon_kernel(RefSet refs, int H, int W, int qp, const int32_t* __restrict_
 int inter_tq_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int bs, const int32_t* best,
                     const int32_t* sub, int qp_rd, const int32_t* qp_row, int vbs, double lam,
                     uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
-                    int32_t* out_mae, uint8_t* out_recon, hipStream_t st) {
+                    int32_t* out_mae, uint8_t* out_recon, int32_t* out_sse, hipStream_t st) {
     const int nb = (W / bs) * (H / bs);
     const int bpw = 256 / bs;
     dim3 grid((nb + bpw - 1) / bpw), blk(256);
     if (bs == 16 && vbs)
         hipLaunchKernelGGL((inter_tq_kernel<16, true>), grid, blk, 0, st, cur, refs, H, W, best, sub, qp_rd,
-                           qp_row, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon);
+                           qp_row, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon, out_sse);
     else if (bs == 16)
         hipLaunchKernelGGL((inter_tq_kernel<16, false>), grid, blk, 0, st, cur, refs, H, W, best, sub, qp_rd,
-                           qp_row, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon);
+                           qp_row, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon, out_sse);
     else
         hipLaunchKernelGGL((inter_tq_kernel<8, false>), grid, blk, 0, st, cur, refs, H, W, best, sub, qp_rd,
-                           qp_row, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon);
+                           qp_row, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon, out_sse);
     return check_launch("inter_tq_kernel");
 }
 

@@ -37,6 +37,7 @@ class FrameSymbols:
     tokens: torch.Tensor       # int32 [nb]
     mae_num: torch.Tensor      # int32 [nb]  (block MAE * bs^2, -1 = inf)
     recon: torch.Tensor        # uint8 [h, w]
+    sse: torch.Tensor | None = None   # int32 [max(nb, h)]: per-block (P) / per-row (I) SSE, zero-padded
     qp_rd: int = 0
     qp_row: list | None = None
     extra: dict = field(default_factory=dict)
@@ -74,7 +75,8 @@ class Engine:
                             qtc=torch.empty((nb, bs * bs), dtype=torch.int16, device=d),
                             tokens=torch.empty(nb, dtype=torch.int32, device=d),
                             mae_num=torch.empty(nb, dtype=torch.int32, device=d),
-                            recon=alloc_planes(1, self.h, self.w, d)[0])
+                            recon=alloc_planes(1, self.h, self.w, d)[0],
+                            sse=torch.zeros(max(nb, self.h), dtype=torch.int32, device=d))
 
     def qp_row_tensor(self, qp_row) -> torch.Tensor | None:
         if qp_row is None:
@@ -105,7 +107,7 @@ class Engine:
             cur.data_ptr(), _lib.ref_array(refs), len(refs), self.h, self.w, self.bs, self.sr,
             int(qp_rd), _lib.ptr(qr), int(self.vbs), self.lam, out.split.data_ptr(),
             out.mv.data_ptr(), out.qtc.data_ptr(), out.tokens.data_ptr(), out.mae_num.data_ptr(),
-            out.recon.data_ptr(), self.scratch.data_ptr(), _lib.stream_handle(self.device))
+            out.recon.data_ptr(), _lib.ptr(out.sse), self.scratch.data_ptr(), _lib.stream_handle(self.device))
         _lib.check(rc, "so_encode_p_frame")
         out.frame_type, out.qp_rd = 1, int(qp_rd)
         out.qp_row = None if qp_row is None else list(qp_row)
@@ -120,7 +122,7 @@ class Engine:
         rc = self.lib.so_encode_i_frame(
             cur.data_ptr(), self.h, self.w, self.bs, self.sr, int(qp_rd), _lib.ptr(qr), int(self.vbs),
             self.lam, out.split.data_ptr(), out.mv.data_ptr(), out.qtc.data_ptr(), out.tokens.data_ptr(),
-            out.mae_num.data_ptr(), out.recon.data_ptr(), self.scratch.data_ptr(),
+            out.mae_num.data_ptr(), out.recon.data_ptr(), _lib.ptr(out.sse), self.scratch.data_ptr(),
             _lib.stream_handle(self.device))
         _lib.check(rc, "so_encode_i_frame")
         out.frame_type, out.qp_rd = 0, int(qp_rd)

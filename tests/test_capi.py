@@ -44,11 +44,11 @@ def test_host_side_validation_without_gpu():
     from streamoptima_amd import _lib
     lib = _lib.load()
     bad = lib.so_encode_p_frame(None, None, 1, 64, 64, 12, 16, 4, None, 0, 0.0, None, None, None, None, None,
-                                None, None, None)
+                                None, None, None, None)
     assert bad == _lib.SO_E_UNSUPPORTED
     assert b"block_size 12" in lib.so_last_error()
     bad = lib.so_encode_i_frame(None, 60, 64, 16, 16, 4, None, 0, 0.0, None, None, None, None, None, None, None,
-                                None)
+                                None, None)
     assert bad == _lib.SO_E_INVALID
     assert lib.so_p_frame_scratch_elems(2160, 3840, 16, 1) == 32400 * 20
     assert lib.so_i_frame_scratch_elems(64, 64, 16) == 16 * 256 + 16 * 8

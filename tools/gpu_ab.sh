@@ -1,0 +1,9 @@
+#!/bin/bash
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 120 ./tools/ubench_sad > gpurun_out/ubench_sad.log 2>&1; rc=$?; echo "ubench rc=$rc"; cat gpurun_out/ubench_sad.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python tools/me_ab.py > gpurun_out/me_ab.log 2>&1; rc=$?; echo "ab rc=$rc"; cat gpurun_out/me_ab.log | grep -v amdgpu.ids
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 python -m pytest tests -q -m gpu -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+echo "pytest rc=$rc"; grep -E "passed|failed|FAILED" gpurun_out/pytest_gpu.log | tail
