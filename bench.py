@@ -8,9 +8,14 @@ variant), synthetic frames (streamoptima_amd/synth.py) already resident in HBM.
 One step = one whole GOP encode (ME, residual, DCT/Q/IDCT, tokens, reconstruction and
 PSNR SSE per frame), exactly the work Y_Video_codec.encode() launches per GOP.
 
-Multi-GPU (torchrun): one process per GPU, each rank encodes its own independent GOP
-(seed = rank) — GOPs are independent units, so there is no data-path collective and the
-scaling is weak.  Timing: barrier + synchronize on both sides, max over ranks.
+Multi-GPU (torchrun), two modes:
+  --shard gop (default): one process per GPU, each rank encodes its own independent GOP
+      (seed = rank).  GOPs are independent units, so there is no data-path collective:
+      weak scaling.
+  --shard stripe (configs[3] semantics): all ranks encode ONE GOP, each its own block-row
+      stripe of every frame, with one in-place all_gather of the reconstruction per frame
+      over RCCL/xGMI (streamoptima_amd/dist.py): strong scaling.
+Timing: barrier + synchronize on both sides, max over ranks.
 
 Prints ONE JSON line on rank 0 (driver contract), including:
   roofline     — the dominant kernel (ME) timed live with HIP events on its stream
@@ -32,12 +37,18 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-SAD_PEAK_OPS = 256 * 4 * 32 * 2.4e9 * 4   # CUs x SIMD32 lanes x 2.4 GHz x 4 |diffs| per v_sad_u8
+# v_sad_u8 issue limit: one wave64 instruction (64 lanes x 4 byte-|diffs|) per 4 cycles per
+# SIMD, 1024 SIMDs, 2.4 GHz.  tools/ubench_sad.cpp measured 5.60e11 wave-instr/s on the box
+# (4.39 cycles) = 1.434e14 |diffs|/s = 91% of this.
+SAD_PEAK_OPS = 1024 * 2.4e9 / 4 * 64 * 4
+SAD_MEASURED_OPS = 5.603e11 * 256
+METRIC = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "BASELINE.json")))["metric"]
 
 CONFIGS = {
     "4k": dict(workload="4K 30-frame I+P GOP (configs[2])", h=2160, w=3840, frames=30, qp=4),
     "1080p": dict(workload="1080p 30-frame I+P GOP (configs[1], 1920x1088 internal)", h=1080, w=1920,
                   frames=30, qp=4),
+    "4k120": dict(workload="4K 120-frame I+P GOP (configs[3])", h=2160, w=3840, frames=120, qp=4),
 }
 
 
@@ -52,6 +63,10 @@ def parse():
     ap.add_argument("--cpu-rows", type=int, default=4, help="block rows per frame type for the CPU sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=20)
+    ap.add_argument("--shard", choices=("gop", "stripe"), default="gop",
+                    help="multi-GPU: independent GOP per rank (weak) or block-row stripes of one GOP (strong)")
+    ap.add_argument("--pcie", action="store_true",
+                    help="also time the PCIe-inclusive path (pinned host frames in, symbols out)")
     return ap.parse_args()
 
 
@@ -81,6 +96,10 @@ def max_over_ranks(x: float, world: int) -> float:
     t = torch.tensor([x], dtype=torch.float64, device="cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def me_kernel_name() -> str:
+    return "me_fast_kernel" if os.environ.get("SO_ME_IMPL") == "fast" else "me_tile_kernel"
 
 
 def kernel_roofline(codec, frames_dev, reps: int) -> dict:
@@ -165,6 +184,49 @@ def cpu_baseline(cfg, rows: int) -> dict:
             "host": platform.processor() or platform.machine(), "os_cpu_count": os.cpu_count()}
 
 
+def psnr_delta_vs_reference(dev) -> dict:
+    """Encode the reference's own 4-frame CIF GOP fixture (tests/golden/gop_cif_vbs0.npz,
+    produced by the reference encoder, tests/golden/make_golden.py) on this GPU and compare
+    PSNR per frame and the reconstructions with the reference's."""
+    from streamoptima_amd.Encoder import Y_Video_codec
+    g = np.load(os.path.join(ROOT, "tests", "golden", "gop_cif_vbs0.npz"))
+    frames = g["frames"]
+    f, h, w = frames.shape
+    codec = Y_Video_codec(h, w, f, 16, 16, 4, 4, 0, 0.015, False, y_only_frame_arr=frames, device=dev)
+    res = codec.encode_device(codec._upload_padded(frames), 4)
+    torch.cuda.synchronize()
+    sse = res["sse"].cpu().numpy()
+    psnr = [10 * np.log10(255 ** 2 / (float(s) / (h * w))) for s in sse]
+    same = all(np.array_equal(s.recon.cpu().numpy(), g["recon"][i]) for i, s in enumerate(res["symbols"]))
+    return {"psnr_delta_db_max": float(np.max(np.abs(np.array(psnr) - g["psnr"]))), "bit_exact_recon": bool(same),
+            "fixture": "reference encoder, CIF 4-frame GOP QP4 (tests/golden/gop_cif_vbs0.npz)"}
+
+
+def pcie_inclusive(codec, cfg, frames_dev, reps: int = 2) -> dict:
+    """GOP time including the upload of pinned host source planes and the download of every
+    frame's symbol arrays (split, mv, qtc, tokens): the rate a host-memory caller sees."""
+    f = frames_dev.shape[0]
+    host = frames_dev.cpu().pin_memory()
+    eng = codec.engine()
+    pre = [eng.new_symbols(0 if i % f == 0 else 1) for i in range(f)]
+    outs = [{k: torch.empty(getattr(p, k).shape, dtype=getattr(p, k).dtype).pin_memory()
+             for k in ("split", "mv", "qtc", "tokens")} for p in pre]
+    best = None
+    for _ in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        frames_dev.copy_(host, non_blocking=True)
+        res = codec.encode_device(frames_dev, f, symbols=pre)
+        for s, o in zip(res["symbols"], outs):
+            for k, t in o.items():
+                t.copy_(getattr(s, k), non_blocking=True)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    return {"pcie_inclusive_mpx_s": round(f * cfg["h"] * cfg["w"] / best / 1e6, 2),
+            "pcie_inclusive_ms_per_gop": round(best * 1e3, 3)}
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup()
@@ -179,12 +241,19 @@ def main():
     hp = -(-h // 16) * 16
     codec = Y_Video_codec(h, w, f, 16, 16, cfg["qp"], f, 0, 0.015, args.vbs, y_only_frame_arr=None, device=dev)
     eng = codec.engine()
+    stripe = args.shard == "stripe"
     frames = alloc_planes(f, hp, w, dev, fill=128)
-    frames[:, :h, :].copy_(synth_sequence_torch(f, h, w, seed=rank, device=dev))
+    frames[:, :h, :].copy_(synth_sequence_torch(f, h, w, seed=0 if stripe else rank, device=dev))
     pre = [eng.new_symbols(0 if i % f == 0 else 1) for i in range(f)]
+    if stripe:
+        from streamoptima_amd.dist import StripeGOPEncoder
+        senc = StripeGOPEncoder(eng)
 
-    def step():
-        return codec.encode_device(frames, f, symbols=pre)
+        def step():
+            return senc.encode(frames, f, cfg["qp"])
+    else:
+        def step():
+            return codec.encode_device(frames, f, symbols=pre)
 
     for _ in range(args.warmup):
         step()
@@ -203,6 +272,8 @@ def main():
     psnr_mean = float(np.mean([10 * np.log10(255 ** 2 / (s / (hp * w))) for s in sse if s > 0]))
 
     rl = kernel_roofline(codec, frames, args.kernel_reps) if rank == 0 else None
+    delta = psnr_delta_vs_reference(dev) if rank == 0 else None
+    pcie = pcie_inclusive(codec, cfg, frames) if rank == 0 and args.pcie and not stripe else None
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, args.cpu_rows)
@@ -210,7 +281,8 @@ def main():
         barrier(world)
         return
     ms_per_step = elapsed / args.steps * 1e3
-    mpx = world * args.steps * f * h * w / elapsed / 1e6
+    units = 1 if stripe else world          # GOPs encoded per step across the job
+    mpx = units * args.steps * f * h * w / elapsed / 1e6
     me_gbs = rl["me_bytes"] / rl["me_s"] / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_me_traffic.json")
@@ -220,26 +292,30 @@ def main():
         except Exception:
             traffic = None
     line = {
-        "metric": "encoded Mpixels/sec (4K 30-frame I+P GOP, full-search ME +-16, QP 4)"
-        if args.config == "4k" else "encoded Mpixels/sec (1080p 30-frame I+P GOP, full-search ME +-16, QP 4)",
+        "metric": METRIC,
         "value": round(mpx, 2), "unit": "Mpx/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "strong" if stripe else "weak",
         "vs_baseline": None, "dtype": "u8", "data": "synthetic (splitmix64 texture, +2/+1 px/frame motion)",
         "config": {"workload": cfg["workload"], "width": w, "height": h, "frames": f, "block_size": 16,
                    "search_range": 16, "qp": cfg["qp"], "vbs": bool(args.vbs), "nRefFrames": 1,
-                   "transform": "fp64 pocketfft-exact DCT", "parallelism": f"gop-per-rank x{world}"},
-        "roofline": {"bound": "hbm", "kernel": "me_fast_kernel", "achieved": round(me_gbs, 2),
+                   "transform": "fp64 pocketfft-exact DCT",
+                   "parallelism": f"stripe x{world} (all_gather recon per frame)" if stripe else f"gop-per-rank x{world}"},
+        "roofline": {"bound": "hbm", "kernel": me_kernel_name(), "achieved": round(me_gbs, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(me_gbs / HBM_PEAK_GBS, 5),
                      "traffic": traffic, "algorithmic_bytes": rl["me_bytes"],
                      "launch_us": round(rl["me_s"] * 1e6, 2),
                      "valu_sad": {"achieved_ops": rl["sad_ops"] / rl["me_s"], "peak_ops": SAD_PEAK_OPS,
                                   "frac": round(rl["sad_ops"] / rl["me_s"] / SAD_PEAK_OPS, 4),
+                                  "measured_peak_ops": SAD_MEASURED_OPS,
                                   "candidates": rl["cands"]},
                      "tq_kernel": {"launch_us": round(rl["tq_s"] * 1e6, 2),
                                    "achieved_gbs": round(rl["tq_bytes"] / rl["tq_s"] / 1e9, 2)}},
         "cpu_baseline": cpu,
         "psnr_mean_db": round(psnr_mean, 4),
+        "psnr_delta_vs_reference": delta,
     }
+    if pcie:
+        line.update(pcie)
     if cpu:
         line["gpu_over_cpu"] = round(mpx / cpu["value"], 1)
     print(json.dumps(line), flush=True)

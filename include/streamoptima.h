@@ -98,6 +98,21 @@ int so_encode_p_frame(const uint8_t* cur, const uint8_t* const* refs, int nref, 
                       int32_t* out_tokens, int32_t* out_mae_num, uint8_t* out_recon,
                       int32_t* out_sse, int32_t* scratch, void* stream);
 
+/*
+ * Stripe variant of so_encode_p_frame for multi-GPU sharding: encodes only
+ * the block rows [by0, by1) of the frame.  cur, refs and out_recon are still the FULL
+ * H x W planes (the search reads the whole reference; only the stripe's pixel rows of
+ * out_recon are written).  Symbol outputs (split, mv, qtc, tokens, mae_num, sse) and the
+ * scratch are STRIPE-LOCAL: block (bx, by) is record (by - by0) * (W/bs) + bx.  qp_row is
+ * the full-frame [H/bs] array.  Concatenating the stripes of by0 = 0 .. H/bs in order
+ * reproduces so_encode_p_frame exactly.  so_p_frame_scratch_elems(H, W, ...) suffices.
+ */
+int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W,
+                     int bs, int sr, int by0, int by1, int qp_rd, const int32_t* qp_row,
+                     int vbs, double lam, uint8_t* out_split, int16_t* out_mv,
+                     int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae_num,
+                     uint8_t* out_recon, int32_t* out_sse, int32_t* scratch, void* stream);
+
 /* int32 elements of scratch so_encode_i_frame / so_intra_recon need: nb*(bs*bs) + nb*8 */
 size_t so_i_frame_scratch_elems(int H, int W, int bs);
 
@@ -114,6 +129,18 @@ int so_encode_i_frame(const uint8_t* cur, int H, int W, int bs, int sr, int qp_r
                       int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
                       int32_t* out_mae_num, uint8_t* out_recon, int32_t* out_sse,
                       int32_t* scratch, void* stream);
+
+/*
+ * Stripe variant of so_encode_i_frame: block rows [by0, by1), same conventions as
+ * so_encode_p_rows; out_sse is [(by1 - by0) * bs] per pixel row of the stripe.  Intra
+ * mode 0 reads only original pixels and its reconstruction is row-local, so stripes need
+ * no halo.
+ */
+int so_encode_i_rows(const uint8_t* cur, int H, int W, int bs, int sr, int by0, int by1,
+                     int qp_rd, const int32_t* qp_row, int vbs, double lam, uint8_t* out_split,
+                     int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
+                     int32_t* out_mae_num, uint8_t* out_recon, int32_t* out_sse,
+                     int32_t* scratch, void* stream);
 
 /* Decoder: P-frame reconstruction from symbols (decoder.py:97-211). */
 int so_inter_recon(const uint8_t* const* refs, int nref, int H, int W, int bs, int qp,

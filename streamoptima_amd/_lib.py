@@ -36,9 +36,13 @@ _SIGS = {
     "so_p_frame_scratch_elems": ([_i, _i, _i, _i], _sz),
     "so_encode_p_frame": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _d, _vp, _vp, _vp, _vp, _vp,
                            _vp, _vp, _vp, _vp], _i),
+    "so_encode_p_rows": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _d, _vp, _vp, _vp, _vp,
+                          _vp, _vp, _vp, _vp, _vp], _i),
     "so_i_frame_scratch_elems": ([_i, _i, _i], _sz),
     "so_encode_i_frame": ([_vp, _i, _i, _i, _i, _i, _vp, _i, _d, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                            _vp, _vp], _i),
+    "so_encode_i_rows": ([_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _d, _vp, _vp, _vp, _vp, _vp, _vp,
+                          _vp, _vp, _vp], _i),
     "so_inter_recon": ([_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "so_intra_recon": ([_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "so_sse_u8": ([_vp, _vp, ctypes.c_int64, _vp, _vp], _i),

@@ -17,19 +17,19 @@ void set_error(const char* fmt, ...) {
     va_end(ap);
 }
 
-int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, int bs, int sr,
+int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, int bs, int sr, int by0, int by1,
               int32_t* out_best, int32_t* out_sub, hipStream_t st);
-int inter_tq_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int bs, const int32_t* best,
-                    const int32_t* sub, int qp_rd, const int32_t* qp_row, int vbs, double lam,
-                    uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
+int inter_tq_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int bs, int by0, int by1,
+                    const int32_t* best, const int32_t* sub, int qp_rd, const int32_t* qp_row, int vbs,
+                    double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
                     int32_t* out_mae, uint8_t* out_recon, int32_t* out_sse, hipStream_t st);
 int inter_recon_launch(const RefSet& refs, int H, int W, int bs, int qp, const int32_t* qp_row,
                        const uint8_t* split, const int16_t* mv, const int16_t* qtc, uint8_t* out_recon,
                        hipStream_t st);
-int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int qp_rd, const int32_t* qp_row,
-                        int vbs, double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc,
-                        int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon, int32_t* out_sse,
-                        int32_t* idres, hipStream_t st);
+int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int by0, int by1, int qp_rd,
+                        const int32_t* qp_row, int vbs, double lam, uint8_t* out_split, int16_t* out_mv,
+                        int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon,
+                        int32_t* out_sse, int32_t* idres, hipStream_t st);
 int intra_recon_launch(int H, int W, int bs, int sr, int qp, const int32_t* qp_row, const uint8_t* split,
                        const int16_t* mv, const int16_t* qtc, uint8_t* out_recon, int32_t* idres,
                        hipStream_t st);
@@ -67,6 +67,14 @@ static int check_intra_width(const char* fn, int W) {
     if (W > 8192) {   // intra_recon_kernel keeps one pixel row (12 B/px) in LDS
         set_error("%s: intra frames wider than 8192 px are not built", fn);
         return SO_E_UNSUPPORTED;
+    }
+    return SO_OK;
+}
+
+static int check_rows(const char* fn, int H, int bs, int by0, int by1) {
+    if (by0 < 0 || by1 < by0 || by1 > H / bs) {
+        set_error("%s: block-row range [%d, %d) outside [0, %d]", fn, by0, by1, H / bs);
+        return SO_E_INVALID;
     }
     return SO_OK;
 }
@@ -159,7 +167,7 @@ int so_me_full_search(const uint8_t* cur, const uint8_t* const* refs, int nref, 
     SO_NEED(out_best, fn);
     RefSet rs;
     SO_TRY(make_refs(fn, refs, nref, &rs));
-    return me_launch(cur, rs, nref, H, W, bs, sr, out_best, out_sub, (hipStream_t)stream);
+    return me_launch(cur, rs, nref, H, W, bs, sr, 0, H / bs, out_best, out_sub, (hipStream_t)stream);
 }
 
 int so_inter_tq_recon(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W, int bs,
@@ -179,8 +187,9 @@ int so_inter_tq_recon(const uint8_t* cur, const uint8_t* const* refs, int nref, 
             set_error("%s: out_recon aliases refs[%d]", fn, i);
             return SO_E_INVALID;
         }
-    return inter_tq_launch(cur, rs, H, W, bs, best, vbs ? sub : nullptr, qp_rd, qp_row, vbs, lam, out_split,
-                           out_mv, out_qtc, out_tokens, out_mae_num, out_recon, out_sse, (hipStream_t)stream);
+    return inter_tq_launch(cur, rs, H, W, bs, 0, H / bs, best, vbs ? sub : nullptr, qp_rd, qp_row, vbs, lam,
+                           out_split, out_mv, out_qtc, out_tokens, out_mae_num, out_recon, out_sse,
+                           (hipStream_t)stream);
 }
 
 size_t so_p_frame_scratch_elems(int H, int W, int bs, int vbs) {
@@ -189,19 +198,43 @@ size_t so_p_frame_scratch_elems(int H, int W, int bs, int vbs) {
     return nb * 4 + (vbs ? nb * 16 : 0);
 }
 
+int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W, int bs, int sr,
+                     int by0, int by1, int qp_rd, const int32_t* qp_row, int vbs, double lam, uint8_t* out_split,
+                     int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae_num,
+                     uint8_t* out_recon, int32_t* out_sse, int32_t* scratch, void* stream) {
+    const char* fn = "so_encode_p_rows";
+    SO_TRY(check_geom(fn, H, W, bs, vbs));
+    SO_TRY(check_sr(fn, sr));
+    SO_TRY(check_qp(fn, qp_rd));
+    SO_TRY(check_rows(fn, H, bs, by0, by1));
+    SO_NEED(cur, fn); SO_NEED(scratch, fn); SO_NEED(out_split, fn); SO_NEED(out_mv, fn);
+    SO_NEED(out_qtc, fn); SO_NEED(out_tokens, fn); SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn);
+    RefSet rs;
+    SO_TRY(make_refs(fn, refs, nref, &rs));
+    for (int i = 0; i < nref; ++i)
+        if (refs[i] == out_recon) {
+            set_error("%s: out_recon aliases refs[%d]", fn, i);
+            return SO_E_INVALID;
+        }
+    const size_t nbs = (size_t)(W / bs) * (size_t)(by1 - by0);
+    int32_t* best = scratch;
+    int32_t* sub = vbs ? scratch + nbs * 4 : nullptr;
+    hipStream_t st = (hipStream_t)stream;
+    SO_TRY(me_launch(cur, rs, nref, H, W, bs, sr, by0, by1, best, sub, st));
+    return inter_tq_launch(cur, rs, H, W, bs, by0, by1, best, sub, qp_rd, qp_row, vbs, lam, out_split, out_mv,
+                           out_qtc, out_tokens, out_mae_num, out_recon, out_sse, st);
+}
+
 int so_encode_p_frame(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W, int bs, int sr,
                       int qp_rd, const int32_t* qp_row, int vbs, double lam, uint8_t* out_split,
                       int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae_num,
                       uint8_t* out_recon, int32_t* out_sse, int32_t* scratch, void* stream) {
-    const char* fn = "so_encode_p_frame";
-    SO_TRY(check_geom(fn, H, W, bs, vbs));
-    SO_NEED(scratch, fn);
-    const size_t nb = (size_t)(W / bs) * (size_t)(H / bs);
-    int32_t* best = scratch;
-    int32_t* sub = vbs ? scratch + nb * 4 : nullptr;
-    SO_TRY(so_me_full_search(cur, refs, nref, H, W, bs, sr, best, sub, stream));
-    return so_inter_tq_recon(cur, refs, nref, H, W, bs, best, sub, qp_rd, qp_row, vbs, lam, out_split, out_mv,
-                             out_qtc, out_tokens, out_mae_num, out_recon, out_sse, stream);
+    if (bs <= 0) {
+        set_error("so_encode_p_frame: block_size %d", bs);
+        return SO_E_UNSUPPORTED;
+    }
+    return so_encode_p_rows(cur, refs, nref, H, W, bs, sr, 0, H / bs, qp_rd, qp_row, vbs, lam, out_split, out_mv,
+                            out_qtc, out_tokens, out_mae_num, out_recon, out_sse, scratch, stream);
 }
 
 size_t so_i_frame_scratch_elems(int H, int W, int bs) {
@@ -210,19 +243,32 @@ size_t so_i_frame_scratch_elems(int H, int W, int bs) {
     return nb * (size_t)bs * bs + nb * 8;
 }
 
-int so_encode_i_frame(const uint8_t* cur, int H, int W, int bs, int sr, int qp_rd, const int32_t* qp_row,
-                      int vbs, double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc,
-                      int32_t* out_tokens, int32_t* out_mae_num, uint8_t* out_recon, int32_t* out_sse,
-                      int32_t* scratch, void* stream) {
-    const char* fn = "so_encode_i_frame";
+int so_encode_i_rows(const uint8_t* cur, int H, int W, int bs, int sr, int by0, int by1, int qp_rd,
+                     const int32_t* qp_row, int vbs, double lam, uint8_t* out_split, int16_t* out_mv,
+                     int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae_num, uint8_t* out_recon,
+                     int32_t* out_sse, int32_t* scratch, void* stream) {
+    const char* fn = "so_encode_i_rows";
     SO_TRY(check_geom(fn, H, W, bs, vbs));
     SO_TRY(check_intra_width(fn, W));
     SO_TRY(check_sr(fn, sr));
     SO_TRY(check_qp(fn, qp_rd));
+    SO_TRY(check_rows(fn, H, bs, by0, by1));
     SO_NEED(cur, fn); SO_NEED(out_split, fn); SO_NEED(out_mv, fn); SO_NEED(out_qtc, fn);
     SO_NEED(out_tokens, fn); SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn); SO_NEED(scratch, fn);
-    return intra_encode_launch(cur, H, W, bs, sr, qp_rd, qp_row, vbs, lam, out_split, out_mv, out_qtc, out_tokens,
-                               out_mae_num, out_recon, out_sse, scratch, (hipStream_t)stream);
+    return intra_encode_launch(cur, H, W, bs, sr, by0, by1, qp_rd, qp_row, vbs, lam, out_split, out_mv, out_qtc,
+                               out_tokens, out_mae_num, out_recon, out_sse, scratch, (hipStream_t)stream);
+}
+
+int so_encode_i_frame(const uint8_t* cur, int H, int W, int bs, int sr, int qp_rd, const int32_t* qp_row,
+                      int vbs, double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc,
+                      int32_t* out_tokens, int32_t* out_mae_num, uint8_t* out_recon, int32_t* out_sse,
+                      int32_t* scratch, void* stream) {
+    if (bs <= 0) {
+        set_error("so_encode_i_frame: block_size %d", bs);
+        return SO_E_UNSUPPORTED;
+    }
+    return so_encode_i_rows(cur, H, W, bs, sr, 0, H / bs, qp_rd, qp_row, vbs, lam, out_split, out_mv, out_qtc,
+                            out_tokens, out_mae_num, out_recon, out_sse, scratch, stream);
 }
 
 int so_inter_recon(const uint8_t* const* refs, int nref, int H, int W, int bs, int qp, const int32_t* qp_row,

@@ -30,7 +30,7 @@ SO_DEV int canvas_at(const uint8_t* left /* LDS row: cols x0-sr .. x0-1 */, int 
 
 template <int BS, bool VBS>
 __global__ void __launch_bounds__(256)
-intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int sr, int qp_rd,
+intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int by0, int nrows, int sr, int qp_rd,
                 const int32_t* __restrict__ qp_row, double lam, uint8_t* __restrict__ out_split,
                 int16_t* __restrict__ out_mv, int16_t* __restrict__ out_qtc,
                 int32_t* __restrict__ out_tokens, int32_t* __restrict__ out_mae,
@@ -41,13 +41,13 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int sr, int qp_rd
     __shared__ uint8_t ldsf[BPW * BS * BS];
     __shared__ uint8_t ldsl[BPW * BS * kIntraMaxSr];
     const int tid = threadIdx.x, g = tid / G, l = tid % G;
-    const int nbx = W / BS, nb = nbx * (H / BS);
-    const int b = blockIdx.x * BPW + g;
+    const int nbx = W / BS, nb = nbx * nrows;
+    const int b = blockIdx.x * BPW + g;   // block index inside the stripe [by0, by0 + nrows)
     if (b >= nb) return;
     double* dl = ldsd + g * LDS_D;
     uint8_t* fl = ldsf + g * BS * BS;
     uint8_t* left = ldsl + g * BS * kIntraMaxSr;
-    const int bx = b % nbx, by = b / nbx, x = bx * BS, y = by * BS;
+    const int bx = b % nbx, by = by0 + b / nbx, x = bx * BS, y = by * BS;
     const int qpr = qp_row ? qp_row[by] : qp_rd;
 
     // stage the original pixels left of the block (cols x-sr .. x-1, 0 where < 0)
@@ -318,7 +318,7 @@ dequant_idct_kernel(int H, int W, int qp, const int32_t* __restrict__ qp_row,
 // block-by-block dependency of the reference costs no serial latency here.
 template <int BS>
 __global__ void __launch_bounds__(256)
-intra_recon_kernel(int H, int W, const uint8_t* __restrict__ split, const int16_t* __restrict__ mv,
+intra_recon_kernel(int H, int W, int by0, const uint8_t* __restrict__ split, const int16_t* __restrict__ mv,
                    const int32_t* __restrict__ idres, const uint8_t* __restrict__ cur,
                    uint8_t* __restrict__ out_recon, int32_t* __restrict__ out_sse) {
     constexpr int SB = BS / 2, NT = 256;
@@ -326,10 +326,11 @@ intra_recon_kernel(int H, int W, const uint8_t* __restrict__ split, const int16_
     int* sval[2] = {reinterpret_cast<int*>(dyn), reinterpret_cast<int*>(dyn) + W};
     short* snxt[2] = {reinterpret_cast<short*>(dyn + 8 * (size_t)W), reinterpret_cast<short*>(dyn + 8 * (size_t)W) + W};
     __shared__ int ssum[NT / 64];
-    const int yy = blockIdx.x, tid = threadIdx.x;
-    const int by = yy / BS, i = yy - by * BS, nbx = W / BS;
+    // pixel row yl of the stripe starting at block row by0; symbols are stripe-local
+    const int yl = blockIdx.x, yy = by0 * BS + yl, tid = threadIdx.x;
+    const int byl = yl / BS, i = yl - byl * BS, nbx = W / BS;
     for (int p = tid; p < W; p += NT) {
-        const int bx = p / BS, c = p - bx * BS, x = bx * BS, b = by * nbx + bx;
+        const int bx = p / BS, c = p - bx * BS, x = bx * BS, b = byl * nbx + bx;
         const int res = idres[(size_t)b * BS * BS + i * BS + c];
         int nx = -1;
         if (x != 0) {
@@ -371,34 +372,36 @@ intra_recon_kernel(int H, int W, const uint8_t* __restrict__ split, const int16_
         for (int m = 32; m >= 1; m >>= 1) sse += __shfl_xor(sse, m, 64);
         if ((tid & 63) == 0) ssum[tid >> 6] = sse;
         __syncthreads();
-        if (tid == 0) out_sse[yy] = ssum[0] + ssum[1] + ssum[2] + ssum[3];
+        if (tid == 0) out_sse[yl] = ssum[0] + ssum[1] + ssum[2] + ssum[3];
     }
 }
 
-int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int qp_rd, const int32_t* qp_row,
-                        int vbs, double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc,
-                        int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon, int32_t* out_sse,
-                        int32_t* idres, hipStream_t st) {
-    const int nb = (W / bs) * (H / bs);
+int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int by0, int by1, int qp_rd,
+                        const int32_t* qp_row, int vbs, double lam, uint8_t* out_split, int16_t* out_mv,
+                        int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon,
+                        int32_t* out_sse, int32_t* idres, hipStream_t st) {
+    const int nrows = by1 - by0;
+    if (nrows <= 0) return SO_OK;
+    const int nb = (W / bs) * nrows;
     const int bpw = 256 / bs;
     dim3 grid((nb + bpw - 1) / bpw), blk(256);
     if (bs == 16 && vbs)
-        hipLaunchKernelGGL((intra_tq_kernel<16, true>), grid, blk, 0, st, cur, H, W, sr, qp_rd, qp_row, lam,
+        hipLaunchKernelGGL((intra_tq_kernel<16, true>), grid, blk, 0, st, cur, H, W, by0, nrows, sr, qp_rd, qp_row, lam,
                            out_split, out_mv, out_qtc, out_tokens, out_mae, idres);
     else if (bs == 16)
-        hipLaunchKernelGGL((intra_tq_kernel<16, false>), grid, blk, 0, st, cur, H, W, sr, qp_rd, qp_row, lam,
+        hipLaunchKernelGGL((intra_tq_kernel<16, false>), grid, blk, 0, st, cur, H, W, by0, nrows, sr, qp_rd, qp_row, lam,
                            out_split, out_mv, out_qtc, out_tokens, out_mae, idres);
     else
-        hipLaunchKernelGGL((intra_tq_kernel<8, false>), grid, blk, 0, st, cur, H, W, sr, qp_rd, qp_row, lam,
+        hipLaunchKernelGGL((intra_tq_kernel<8, false>), grid, blk, 0, st, cur, H, W, by0, nrows, sr, qp_rd, qp_row, lam,
                            out_split, out_mv, out_qtc, out_tokens, out_mae, idres);
     int rc = check_launch("intra_tq_kernel");
     if (rc) return rc;
     if (bs == 16)
-        hipLaunchKernelGGL((intra_recon_kernel<16>), dim3(H), dim3(256), 12 * (size_t)W, st, H, W, out_split, out_mv, idres, cur,
-                           out_recon, out_sse);
+        hipLaunchKernelGGL((intra_recon_kernel<16>), dim3(nrows * bs), dim3(256), 12 * (size_t)W, st, H, W, by0, out_split,
+                           out_mv, idres, cur, out_recon, out_sse);
     else
-        hipLaunchKernelGGL((intra_recon_kernel<8>), dim3(H), dim3(256), 12 * (size_t)W, st, H, W, out_split, out_mv, idres, cur,
-                           out_recon, out_sse);
+        hipLaunchKernelGGL((intra_recon_kernel<8>), dim3(nrows * bs), dim3(256), 12 * (size_t)W, st, H, W, by0, out_split,
+                           out_mv, idres, cur, out_recon, out_sse);
     return check_launch("intra_recon_kernel");
 }
 
@@ -415,11 +418,11 @@ int intra_recon_launch(int H, int W, int bs, int sr, int qp, const int32_t* qp_r
     int rc = check_launch("dequant_idct_kernel");
     if (rc) return rc;
     if (bs == 16)
-        hipLaunchKernelGGL((intra_recon_kernel<16>), dim3(H), dim3(256), 12 * (size_t)W, st, H, W, split, mv, idres, nullptr,
-                           out_recon, nullptr);
+        hipLaunchKernelGGL((intra_recon_kernel<16>), dim3(H), dim3(256), 12 * (size_t)W, st, H, W, 0, split, mv, idres,
+                           nullptr, out_recon, nullptr);
     else
-        hipLaunchKernelGGL((intra_recon_kernel<8>), dim3(H), dim3(256), 12 * (size_t)W, st, H, W, split, mv, idres, nullptr,
-                           out_recon, nullptr);
+        hipLaunchKernelGGL((intra_recon_kernel<8>), dim3(H), dim3(256), 12 * (size_t)W, st, H, W, 0, split, mv, idres,
+                           nullptr, out_recon, nullptr);
     return check_launch("intra_recon_kernel");
 }
 

@@ -16,7 +16,7 @@ namespace so {
 
 template <int BS, bool VBS>
 __global__ void __launch_bounds__(256)
-inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W,
+inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W, int by0, int nrows,
                 const int32_t* __restrict__ best, const int32_t* __restrict__ sub, int qp_rd,
                 const int32_t* __restrict__ qp_row, double lam, uint8_t* __restrict__ out_split,
                 int16_t* __restrict__ out_mv, int16_t* __restrict__ out_qtc,
@@ -27,12 +27,12 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W,
     __shared__ double ldsd[BPW * LDS_D];
     __shared__ uint8_t ldsf[BPW * BS * BS];
     const int tid = threadIdx.x, g = tid / G, l = tid % G;
-    const int nbx = W / BS, nb = nbx * (H / BS);
-    const int b = blockIdx.x * BPW + g;
+    const int nbx = W / BS, nb = nbx * nrows;
+    const int b = blockIdx.x * BPW + g;   // block index inside the stripe [by0, by0 + nrows)
     if (b >= nb) return;  // whole lane group leaves; only wave-scope exchange below
     double* dl = ldsd + g * LDS_D;
     uint8_t* fl = ldsf + g * BS * BS;
-    const int bx = b % nbx, by = b / nbx, x = bx * BS, y = by * BS;
+    const int bx = b % nbx, by = by0 + b / nbx, x = bx * BS, y = by * BS;
     const int qpr = qp_row ? qp_row[by] : qp_rd;
 
     const int32_t* bb = best + (size_t)b * 4;
@@ -219,21 +219,23 @@ inter_recon_kernel(RefSet refs, int H, int W, int qp, const int32_t* __restrict_
     }
 }
 
-int inter_tq_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int bs, const int32_t* best,
-                    const int32_t* sub, int qp_rd, const int32_t* qp_row, int vbs, double lam,
-                    uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
+int inter_tq_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int bs, int by0, int by1,
+                    const int32_t* best, const int32_t* sub, int qp_rd, const int32_t* qp_row, int vbs,
+                    double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
                     int32_t* out_mae, uint8_t* out_recon, int32_t* out_sse, hipStream_t st) {
-    const int nb = (W / bs) * (H / bs);
+    const int nrows = by1 - by0;
+    if (nrows <= 0) return SO_OK;
+    const int nb = (W / bs) * nrows;
     const int bpw = 256 / bs;
     dim3 grid((nb + bpw - 1) / bpw), blk(256);
     if (bs == 16 && vbs)
-        hipLaunchKernelGGL((inter_tq_kernel<16, true>), grid, blk, 0, st, cur, refs, H, W, best, sub, qp_rd,
+        hipLaunchKernelGGL((inter_tq_kernel<16, true>), grid, blk, 0, st, cur, refs, H, W, by0, nrows, best, sub, qp_rd,
                            qp_row, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon, out_sse);
     else if (bs == 16)
-        hipLaunchKernelGGL((inter_tq_kernel<16, false>), grid, blk, 0, st, cur, refs, H, W, best, sub, qp_rd,
+        hipLaunchKernelGGL((inter_tq_kernel<16, false>), grid, blk, 0, st, cur, refs, H, W, by0, nrows, best, sub, qp_rd,
                            qp_row, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon, out_sse);
     else
-        hipLaunchKernelGGL((inter_tq_kernel<8, false>), grid, blk, 0, st, cur, refs, H, W, best, sub, qp_rd,
+        hipLaunchKernelGGL((inter_tq_kernel<8, false>), grid, blk, 0, st, cur, refs, H, W, by0, nrows, best, sub, qp_rd,
                            qp_row, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon, out_sse);
     return check_launch("inter_tq_kernel");
 }

@@ -129,6 +129,51 @@ class Engine:
         out.qp_row = None if qp_row is None else list(qp_row)
         return out
 
+    # ---- stripes (multi-GPU sharding) --------------------------------------
+    def new_stripe_symbols(self, frame_type: int, by0: int, by1: int, recon: torch.Tensor) -> FrameSymbols:
+        """Stripe-local symbol buffers for block rows [by0, by1); `recon` is the full plane
+        the stripe's rows are written into."""
+        d, bs = self.device, self.bs
+        nbs = self.nbx * (by1 - by0)
+        mv_shape = (nbs, 4, 3) if frame_type == 1 else (nbs, 4)
+        return FrameSymbols(frame_type=frame_type,
+                            split=torch.empty(nbs, dtype=torch.uint8, device=d),
+                            mv=torch.empty(mv_shape, dtype=torch.int16, device=d),
+                            qtc=torch.empty((nbs, bs * bs), dtype=torch.int16, device=d),
+                            tokens=torch.empty(nbs, dtype=torch.int32, device=d),
+                            mae_num=torch.empty(nbs, dtype=torch.int32, device=d),
+                            recon=recon,
+                            sse=torch.zeros(max(nbs, (by1 - by0) * bs), dtype=torch.int32, device=d),
+                            extra={"by0": by0, "by1": by1})
+
+    def encode_p_rows(self, cur, refs, by0: int, by1: int, qp_rd: int, out: FrameSymbols,
+                      qp_row_dev: torch.Tensor | None = None) -> FrameSymbols:
+        """so_encode_p_rows: block rows [by0, by1) of a P-frame; asynchronous."""
+        self._check_plane(cur, "cur")
+        for k, r in enumerate(refs):
+            self._check_plane(r, f"refs[{k}]")
+        rc = self.lib.so_encode_p_rows(
+            cur.data_ptr(), _lib.ref_array(refs), len(refs), self.h, self.w, self.bs, self.sr, int(by0), int(by1),
+            int(qp_rd), _lib.ptr(qp_row_dev), int(self.vbs), self.lam, out.split.data_ptr(), out.mv.data_ptr(),
+            out.qtc.data_ptr(), out.tokens.data_ptr(), out.mae_num.data_ptr(), out.recon.data_ptr(),
+            _lib.ptr(out.sse), self.scratch.data_ptr(), _lib.stream_handle(self.device))
+        _lib.check(rc, "so_encode_p_rows")
+        out.frame_type, out.qp_rd = 1, int(qp_rd)
+        return out
+
+    def encode_i_rows(self, cur, by0: int, by1: int, qp_rd: int, out: FrameSymbols,
+                      qp_row_dev: torch.Tensor | None = None) -> FrameSymbols:
+        """so_encode_i_rows: block rows [by0, by1) of an I-frame; asynchronous."""
+        self._check_plane(cur, "cur")
+        rc = self.lib.so_encode_i_rows(
+            cur.data_ptr(), self.h, self.w, self.bs, self.sr, int(by0), int(by1), int(qp_rd), _lib.ptr(qp_row_dev),
+            int(self.vbs), self.lam, out.split.data_ptr(), out.mv.data_ptr(), out.qtc.data_ptr(),
+            out.tokens.data_ptr(), out.mae_num.data_ptr(), out.recon.data_ptr(), _lib.ptr(out.sse),
+            self.scratch.data_ptr(), _lib.stream_handle(self.device))
+        _lib.check(rc, "so_encode_i_rows")
+        out.frame_type, out.qp_rd = 0, int(qp_rd)
+        return out
+
     # ---- decode ---------------------------------------------------------------------------
     def recon_inter(self, refs: list, split, mv, qtc, qp: int, qp_row=None, out=None) -> torch.Tensor:
         out = out if out is not None else alloc_planes(1, self.h, self.w, self.device)[0]

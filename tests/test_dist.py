@@ -1,0 +1,150 @@
+"""Stripe-sharded GOP encode (streamoptima_amd/dist.py) under gloo on CPU.
+
+The per-stripe encoder here is the CPU oracle behind the same stripe methods the HIP Engine
+exposes (encode_p_rows / encode_i_rows / new_stripe_symbols), so these tests check the
+multi-GPU orchestration itself: row partition, the in-place all_gather of every
+reconstruction, the reference window, the RCFlag>1 all_reduce, and the rank-order symbol
+concatenation.  The result must equal the single-process oracle GOP (oracle/gop.py)
+bit for bit.  The HIP stripe kernels are checked against full-frame encodes in
+tests/test_gpu_parity.py.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from streamoptima_amd.dist import StripeGOPEncoder, stripe_rows
+from streamoptima_amd.engine import Engine
+
+H, W, F = 96, 64, 4
+
+
+def test_stripe_rows_partition():
+    for nby in (1, 5, 6, 17, 135):
+        for world in (1, 2, 3, 4, 8):
+            rows = []
+            rps = None
+            for r in range(world):
+                by0, by1, rps_r = stripe_rows(nby, world, r)
+                rps = rps_r
+                assert 0 <= by0 <= by1 <= nby and by1 - by0 <= rps
+                assert by0 == min(r * rps, nby)          # chunk r of the gathered plane
+                rows += list(range(by0, by1))
+            assert rows == list(range(nby))
+            assert world * rps >= nby
+
+
+class OracleStripeEngine:
+    """CPU stand-in for Engine's stripe methods, computed by the C oracle."""
+
+    def __init__(self, h, w, bs=16, sr=16, vbs=False, lam=0.015):
+        self.h, self.w, self.bs, self.sr, self.vbs, self.lam = h, w, bs, sr, vbs, lam
+        self.nbx, self.nby = w // bs, h // bs
+        self.device = torch.device("cpu")
+
+    new_stripe_symbols = Engine.new_stripe_symbols
+
+    def qp_row_tensor(self, q):
+        return torch.tensor(list(q), dtype=torch.int32)
+
+    def _fill(self, r, by0, by1, out):
+        b0, b1 = by0 * self.nbx, by1 * self.nbx
+        for name in ("split", "mv", "qtc", "tokens", "mae_num"):
+            out_t = getattr(out, name)
+            out_t.copy_(torch.from_numpy(np.ascontiguousarray(r[name][b0:b1]).astype(out_t.numpy().dtype)))
+        y0, y1 = by0 * self.bs, by1 * self.bs
+        out.recon[y0:y1].copy_(torch.from_numpy(r["recon"][y0:y1]))
+
+    def encode_p_rows(self, cur, refs, by0, by1, qp, out, qp_row_dev=None):
+        from oracle import oracle as O
+        qr = None if qp_row_dev is None else qp_row_dev.tolist()
+        r = O.inter_frame(cur.numpy(), [x.numpy() for x in refs], self.bs, self.sr, qp, qr, self.vbs, self.lam)
+        self._fill(r, by0, by1, out)
+        y0, y1 = by0 * self.bs, by1 * self.bs
+        d = cur.numpy()[y0:y1].astype(np.int64) - out.recon[y0:y1].numpy().astype(np.int64)
+        out.sse.zero_()
+        out.sse[0] = int((d * d).sum())
+        out.frame_type = 1
+        return out
+
+    def encode_i_rows(self, cur, by0, by1, qp, out, qp_row_dev=None):
+        from oracle import oracle as O
+        qr = None if qp_row_dev is None else qp_row_dev.tolist()
+        r = O.intra_frame(cur.numpy(), self.bs, self.sr, qp, qr, self.vbs, self.lam)
+        self._fill(r, by0, by1, out)
+        y0, y1 = by0 * self.bs, by1 * self.bs
+        d = cur.numpy()[y0:y1].astype(np.int64) - out.recon[y0:y1].numpy().astype(np.int64)
+        out.sse.zero_()
+        out.sse[0] = int((d * d).sum())
+        out.frame_type = 0
+        return out
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _frames():
+    from streamoptima_amd.synth import synth_sequence
+    return synth_sequence(F, H, W, seed=3)
+
+
+CASES = {
+    "plain": dict(vbs=False, qp=4, intra_dur=F, nref=1, rc=None),
+    "vbs_nref2": dict(vbs=True, qp=3, intra_dur=3, nref=2, rc=None),
+    "rc2": dict(vbs=True, qp=4, intra_dur=F, nref=1, rc=2, thresh=40),
+}
+
+
+def _rc_sched(case):
+    from oracle.gop import bitrate_per_row, row_qp_schedule
+    tables = [[9000, 6000, 4000, 2600, 1700, 1100, 700, 450, 300, 200]] * 2
+    return row_qp_schedule(bitrate_per_row("2 mbps", 30, H, 16), tables, H // 16), tables
+
+
+def _worker(rank, world, port, case_name, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        case = CASES[case_name]
+        frames = torch.from_numpy(_frames())
+        eng = OracleStripeEngine(H, W, vbs=case["vbs"])
+        enc = StripeGOPEncoder(eng)
+        sched = _rc_sched(case)[0] if case["rc"] else None
+        res = enc.encode(frames, case["intra_dur"], case["qp"], nref=case["nref"], qp_sched=sched,
+                         rc_flag=case["rc"], intra_thresh=case.get("thresh"))
+        full = [enc.gather_symbols(s) for s in res["symbols"]]
+        if rank == 0:
+            np.savez(os.path.join(outdir, "out.npz"), sse=res["sse"].numpy(),
+                     ftypes=np.array(res["frame_type"]),
+                     **{f"{k}_{i}": (v.numpy() if torch.is_tensor(v) else np.array(v))
+                        for i, g in enumerate(full) for k, v in g.items()})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,case_name", [(2, "plain"), (2, "vbs_nref2"), (2, "rc2"), (4, "plain")])
+def test_stripe_gop_matches_single_process_oracle(tmp_path, world, case_name):
+    from oracle.gop import encode_gop
+    mp.start_processes(_worker, args=(world, _free_port(), case_name, str(tmp_path)), nprocs=world,
+                       start_method="spawn")
+    got = np.load(tmp_path / "out.npz")
+    case = CASES[case_name]
+    rc_kw = {}
+    if case["rc"]:
+        _, tables = _rc_sched(case)
+        rc_kw = dict(rc=case["rc"], target="2 mbps", tables=tables, intra_thresh=case["thresh"])
+    ref = encode_gop(_frames(), case["qp"], case["intra_dur"], vbs=case["vbs"], nref=case["nref"], **rc_kw)
+    assert list(got["ftypes"]) == [r["frame_type"] for r in ref]
+    for i, r in enumerate(ref):
+        for k in ("split", "mv", "qtc", "tokens", "mae_num", "recon"):
+            np.testing.assert_array_equal(got[f"{k}_{i}"], np.asarray(r[k]).astype(got[f"{k}_{i}"].dtype),
+                                          err_msg=f"frame {i} {k}")
+        d = _frames()[i].astype(np.int64) - r["recon"].astype(np.int64)
+        assert int(got["sse"][i]) == int((d * d).sum())

@@ -277,3 +277,61 @@ def test_full_size_properties_4k(gpu):
     bx = np.arange(mv.shape[0]) % nbx * 16
     unsplit = sym.split.cpu().numpy() == 0
     assert ((bx + mv[:, 0, 0])[unsplit] < w - 16).all()
+
+
+# ---------------------------------------------------------------- stripes (multi-GPU sharding)
+@pytest.mark.parametrize("h,w,vbs,frame_type", [(256, 272, True, 1), (256, 272, False, 0), (208, 160, True, 0),
+                                                (2160, 3840, False, 1)])
+def test_stripes_concatenate_to_full_frame(gpu, h, w, vbs, frame_type):
+    """so_encode_p_rows / so_encode_i_rows over every rank's [by0, by1) for world sizes
+    2, 3 and 8: the rank-order concatenation equals so_encode_*_frame bit for bit, and
+    the stripe reconstructions tile the full one."""
+    from streamoptima_amd.dist import stripe_rows
+    from streamoptima_amd.engine import Engine, alloc_planes
+    from streamoptima_amd.synth import synth_sequence
+    seq = synth_sequence(2, h, w, seed=h + w)
+    eng = Engine(h, w, 16, 16, vbs, 0.015, gpu)
+    cur, ref = _plane(seq[1], gpu), _plane(seq[0], gpu)
+    qr = np.random.default_rng(w).integers(0, 7, size=h // 16).tolist()
+    qdev = eng.qp_row_tensor(qr)
+    full = eng.encode_p(cur, [ref], 3, qr) if frame_type else eng.encode_i(cur, 3, qr)
+    torch.cuda.synchronize()
+    for world in (2, 3, 8):
+        plane = alloc_planes(1, h, w, gpu, fill=0)[0]
+        parts = []
+        for rank in range(world):
+            by0, by1, _ = stripe_rows(eng.nby, world, rank)
+            if by1 == by0:
+                continue
+            s = eng.new_stripe_symbols(frame_type, by0, by1, plane)
+            if frame_type:
+                eng.encode_p_rows(cur, [ref], by0, by1, 3, s, qp_row_dev=qdev)
+            else:
+                eng.encode_i_rows(cur, by0, by1, 3, s, qp_row_dev=qdev)
+            parts.append(s)
+        torch.cuda.synchronize()
+        for k in ("split", "mv", "qtc", "tokens", "mae_num"):
+            cat = torch.cat([getattr(p, k) for p in parts])
+            assert torch.equal(cat, getattr(full, k)), (world, k)
+        assert torch.equal(plane, full.recon), world
+        assert sum(int(p.sse.sum()) for p in parts) == int(full.sse.sum())
+
+
+def test_stripe_gop_encoder_single_rank(gpu):
+    """StripeGOPEncoder with one rank (no process group) == Y_Video_codec.encode_device."""
+    from streamoptima_amd.Encoder import Y_Video_codec
+    from streamoptima_amd.dist import StripeGOPEncoder
+    from streamoptima_amd.engine import alloc_planes
+    from streamoptima_amd.synth import synth_sequence_torch
+    h, w, f = 128, 192, 4
+    codec = Y_Video_codec(h, w, f, 16, 16, 4, 3, 0, 0.015, True, y_only_frame_arr=None, device=gpu)
+    frames = alloc_planes(f, h, w, gpu)
+    frames.copy_(synth_sequence_torch(f, h, w, seed=2, device=gpu))
+    a = codec.encode_device(frames, 3)
+    b = StripeGOPEncoder(codec.engine()).encode(frames, 3, 4)
+    torch.cuda.synchronize()
+    assert torch.equal(a["sse"], b["sse"])
+    for sa, sb in zip(a["symbols"], b["symbols"]):
+        assert sa.frame_type == sb.frame_type
+        for k in ("split", "mv", "qtc", "tokens", "mae_num", "recon"):
+            assert torch.equal(getattr(sa, k), getattr(sb, k)), k

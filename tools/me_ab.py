@@ -1,4 +1,5 @@
-"""A/B of ME implementations in one process (interleaved rounds), 4K P-frame."""
+"""A/B of ME implementations in one process (interleaved rounds), 4K P-frame:
+me_tile_kernel (default) vs me_fast_kernel (SO_ME_IMPL=fast, round-1 kernel)."""
 import os, sys, time
 import numpy as np, torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -18,7 +19,7 @@ def main():
     res = {}
     for vbs in (False, True):
         outs = {}
-        for impl in ("sad", "wave", "sad", "wave", "sad", "wave"):
+        for impl in ("tile", "fast", "tile", "fast", "tile", "fast"):
             os.environ["SO_ME_IMPL"] = impl
             best = torch.empty((nb, 4), dtype=torch.int32, device=dev)
             sub = torch.empty((nb, 4, 4), dtype=torch.int32, device=dev) if vbs else None
@@ -30,7 +31,7 @@ def main():
             e1.record(); torch.cuda.synchronize()
             res.setdefault((vbs, impl), []).append(e0.elapsed_time(e1) / 20 * 1e3)
             outs[impl] = (best.cpu().numpy(), None if sub is None else sub.cpu().numpy())
-        same = (outs["sad"][0] == outs["wave"][0]).all() and (not vbs or (outs["sad"][1] == outs["wave"][1]).all())
+        same = (outs["tile"][0] == outs["fast"][0]).all() and (not vbs or (outs["tile"][1] == outs["fast"][1]).all())
         print(f"vbs={vbs} identical_outputs={same}")
     for k, v in res.items():
         print(f"vbs={k[0]} impl={k[1]:5s} us/launch: {['%.1f' % x for x in v]}  min {min(v):.1f}")
