@@ -49,9 +49,8 @@ SO_DEV void decode_key(uint64_t k, int sr, int32_t* out) {
 // 160 x 160 B) in LDS with coalesced 8-byte loads.  A task is (block, dx): 64 blocks x 33
 // dx = 2112 tasks = exactly 3 rounds of 704 lanes.
 //
-// A lane walks its block's 48 window rows once: each row is ONE unaligned ds_read_b128
-// (gfx950 LDS serves byte-unaligned b128 reads, so no v_alignbyte), and feeds up to 16
-// (cur row r, dy) pairs, each 4 v_sad_u8.  v_sad_u8 is the whole VALU budget: measured
+// A lane walks its block's window rows: each row is 5 aligned ds_read_b32 + 4 v_alignbyte
+// (win_read) and feeds up to 8 (cur row r, dy) pairs, each 4 v_sad_u8.  v_sad_u8 is the whole VALU budget: measured
 // 4.39 cycles per wave64 instruction (tools/ubench_sad.cpp), the same issue cost as any
 // other 32-bit VALU op, so the kernel is built to issue almost nothing else:
 //   * the current block is held 8 rows at a time (two passes of 40 window rows), which
@@ -75,17 +74,31 @@ struct MeGeo {
     static constexpr int NTHREADS = 704;                  // 11 waves; 33 * 64 = 3 * 704
 };
 
+// Aligned LDS row read of N dwords (ds_read_b128 / ds_read_b64).
 template <int N>
 SO_DEV void lds_read(const uint8_t* p, uint32_t (&v)[N]) {
     if constexpr (N == 4) {
-        uint4 t;
-        __builtin_memcpy(&t, p, 16);   // ds_read_b128, byte-unaligned allowed on gfx950
+        const uint4 t = *reinterpret_cast<const uint4*>(p);
         v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
     } else {
-        uint2 t;
-        __builtin_memcpy(&t, p, 8);    // ds_read_b64
+        const uint2 t = *reinterpret_cast<const uint2*>(p);
         v[0] = t.x; v[1] = t.y;
     }
+}
+
+// Window-row read of N dwords starting at ANY byte address p: aligned ds_read_b32 x (N+1)
+// and N v_alignbyte.  Measured alternatives (tools/me_ab.py, 4K P-frame, same outputs):
+// one byte-unaligned ds_read_b128 157.9 us, N byte-unaligned ds_read_b32 576.8 us -- gfx950
+// replays misaligned DS reads (cdna_hip_programming.md Guideline 17) -- vs 111.9 us here.
+template <int N>
+SO_DEV void win_read(const uint8_t* p, uint32_t (&v)[N]) {
+    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);   // keeps the LDS address space
+    uint32_t w[N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; ++k) w[k] = q[k];
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
 }
 
 // IR-level fence over the accumulators: the SADs of a window row are issued before any
@@ -118,10 +131,10 @@ SO_DEV uint32_t me_tile_task(const uint8_t* __restrict__ win, const uint8_t* __r
         for (int r = 0; r < RCH; ++r) lds_read<NDW>(curt + (crow + c0 + r) * CP + ccol, cr[r]);
         const uint8_t* p = win + (wrow + c0) * WP + wcol;
         uint32_t wc[NDW], wn[NDW];
-        lds_read<NDW>(p, wc);
+        win_read<NDW>(p, wc);
 #pragma unroll
         for (int jj = 0; jj < NR; ++jj) {
-            if (jj + 1 < NR) lds_read<NDW>(p + (jj + 1) * WP, wn);
+            if (jj + 1 < NR) win_read<NDW>(p + (jj + 1) * WP, wn);
 #pragma unroll
             for (int r = 0; r < RCH; ++r) {
                 const int di = jj - r;

@@ -1,9 +1,11 @@
 #!/bin/bash
+# ME A/B only (tools/me_ab.py), then the ME + stripe parity tests.
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 120 ./tools/ubench_sad > gpurun_out/ubench_sad.log 2>&1; rc=$?; echo "ubench rc=$rc"; cat gpurun_out/ubench_sad.log
+TAG=${1:-ab}
+timeout -k 10 300 python tools/me_ab.py > gpurun_out/me_ab_${TAG}.log 2>&1; rc=$?
+echo "me_ab rc=$rc"; grep -v amdgpu.ids gpurun_out/me_ab_${TAG}.log | tail -16
 [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python tools/me_ab.py > gpurun_out/me_ab.log 2>&1; rc=$?; echo "ab rc=$rc"; cat gpurun_out/me_ab.log | grep -v amdgpu.ids
-[ $rc -ne 0 ] && exit $rc
-timeout -k 10 600 python -m pytest tests -q -m gpu -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?
-echo "pytest rc=$rc"; grep -E "passed|failed|FAILED" gpurun_out/pytest_gpu.log | tail
+timeout -k 10 600 python -m pytest tests -q -m gpu -p no:cacheprovider -x > gpurun_out/pytest_gpu_${TAG}.log 2>&1; rc=$?
+echo "pytest rc=$rc"; grep -E "passed|failed|FAILED|ERROR" gpurun_out/pytest_gpu_${TAG}.log | tail -8
+exit $rc
