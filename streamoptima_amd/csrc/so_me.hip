@@ -14,7 +14,7 @@
 // Every kernel takes a block-row range [by0, by1) (stripe sharding across GPUs, DESIGN.md
 // §5); output records are indexed relative to by0.
 //
-// Tile path (sr == 16, bs in {16, 8}; default): see me_tile_kernel.
+// Wave path (sr == 16, bs in {16, 8}; default): see me_wave_kernel.
 // Generic path (any sr <= 64): one thread per (block, candidate) with a global atomicMin.
 #include <stdlib.h>
 #include <string.h>
@@ -41,27 +41,7 @@ SO_DEV void decode_key(uint64_t k, int sr, int32_t* out) {
     out[3] = (int)(k >> 32);
 }
 
-// ---------------------------------------------------------------------------------------
-// Tile path (default)
-//
-// A 704-thread workgroup (11 waves) owns a TB x TB tile of blocks (128 x 128 px).  It
-// stages the current tile (128 x 128 B) and the reference window (tile + 16-px halo,
-// 160 x 160 B) in LDS with coalesced 8-byte loads.  A task is (block, dx): 64 blocks x 33
-// dx = 2112 tasks = exactly 3 rounds of 704 lanes.
-//
-// A lane walks its block's window rows: each row is 5 aligned ds_read_b32 + 4 v_alignbyte
-// (win_read) and feeds up to 8 (cur row r, dy) pairs, each 4 v_sad_u8.  v_sad_u8 is the whole VALU budget: measured
-// 4.39 cycles per wave64 instruction (tools/ubench_sad.cpp), the same issue cost as any
-// other 32-bit VALU op, so the kernel is built to issue almost nothing else:
-//   * the current block is held 8 rows at a time (two passes of 40 window rows), which
-//     keeps ~80 VGPRs and 2 workgroups (22 waves) per CU so one tile's staging overlaps
-//     the other's SADs;
-//   * per-lane argmin on 32-bit keys (sad << 11 | |dy| << 6 | dy_index): one v_lshl_or
-//     and one v_min per candidate (dx and ref are fixed within a lane, so the order of
-//     these keys is the reference's order); dy bounds only for the frame's edge rows.
-// The lane's best is widened to the 64-bit key and merged with an LDS atomicMin.
-// With VBS the same launch also runs the 4 x 8x8 sub-block searches on the same window.
-// ---------------------------------------------------------------------------------------
+// Geometry of the round-1 kernel (me_fast_kernel, kept for A/B).
 template <int BS>
 struct MeGeo {
     static constexpr int SR = 16;
@@ -71,98 +51,95 @@ struct MeGeo {
     static constexpr int WP = TPX + 2 * SR;               // 160: window rows == pitch (bytes)
     static constexpr int CP = TPX;                        // current tile pitch
     static constexpr int NBLK = TB * TB;
-    static constexpr int NTHREADS = 704;                  // 11 waves; 33 * 64 = 3 * 704
+    static constexpr int NTHREADS = 704;                  // 11 waves
 };
 
-// Aligned LDS row read of N dwords (ds_read_b128 / ds_read_b64).
-template <int N>
-SO_DEV void lds_read(const uint8_t* p, uint32_t (&v)[N]) {
-    if constexpr (N == 4) {
-        const uint4 t = *reinterpret_cast<const uint4*>(p);
-        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-    } else {
-        const uint2 t = *reinterpret_cast<const uint2*>(p);
-        v[0] = t.x; v[1] = t.y;
+// ---------------------------------------------------------------------------------------
+// Wave path (default): one wavefront per block, current block in SGPRs, no v_alignbyte.
+//
+// gfx950 issue costs (tools/ubench_ops.cpp): every VOP3 instruction -- v_sad_u8,
+// v_alignbyte_b32, v_add3_u32 -- costs ~4.4 cycles per wave64, a VOP2 v_add ~2.5.  So the
+// kernel minimises VOP3 instructions other than v_sad_u8:
+//   * the block is wave-uniform: its pixels live in SGPRs (scalar loads, 8 rows per pass)
+//     and feed v_sad_u8 directly, so lanes hold only accumulators and one window row;
+//   * the window is staged in LDS as FOUR copies shifted by 0..3 bytes, so the 16 bytes at
+//     any column are four dword-aligned ds_read_b32 from copy (col & 3) -- the byte
+//     alignment is paid once per staged dword instead of once per row per lane (a b128 read
+//     would need 16-byte alignment: misaligned wide DS reads are replayed on gfx950);
+//   * copies are skewed by 16 banks.
+// Phase 1: lane = hh*32 + xi covers dx = xi - 16 (xi < 32) and dy = 16*hh + t - 16
+// (t < 17): the halves take dy in [-16, 0] and [0, 16] (dy 0 twice, 3% redundant).  The
+// lane slides over its 17 + 8 - 1 window rows per pass and adds every row into the t it
+// pairs with.  Phase 2: the dx = +16 column, lane = dy index (33 lanes), whose column is
+// 4-byte aligned (copy 0).
+// VBS: the lane keeps left/right-quadrant accumulators per pass (dwords 0-1 / 2-3), so
+// the 8x8 sub-block SADs come out of the same v_sad_u8 work and the 16x16 SAD is their sum.
+// Argmin: per-lane 32-bit keys (sad << 5 | ordered |dy| code), widened to the 64-bit key
+// and reduced across the wave.
+// ---------------------------------------------------------------------------------------
+template <int BS>
+struct MeWGeo {
+    static constexpr int SR = 16, D = 33, NT = 17;
+    static constexpr int TBX = 128 / BS;                  // blocks across (128 px)
+    static constexpr int TBY = (BS == 16) ? 2 : 4;        // blocks down (32 px)
+    static constexpr int TPX = 128, TPY = TBY * BS;
+    static constexpr int WR = TPY + 2 * SR;               // 64 window rows
+    static constexpr int RPD = (TPX + 2 * SR) / 4;        // 40 dwords per copy row
+    static constexpr int CSTRIDE = WR * RPD + 16;         // dwords per shifted copy (+16-bank skew)
+    static constexpr int NBLK = TBX * TBY;
+    static constexpr int NW = 8, NTHREADS = NW * 64;
+};
+
+typedef const __attribute__((address_space(4))) uint32_t* const_u32p;
+// LDS pointer type for volatile reads (address-space inference skips volatile accesses)
+typedef const volatile __attribute__((address_space(3))) uint32_t* lds_vu32p;
+
+// NR rows x NDW dwords of the current block into SGPRs (wave-uniform address).
+template <int NR, int NDW>
+SO_DEV void load_cur_sgpr(const uint8_t* __restrict__ cur, int W, int x, int y, uint32_t (&cr)[NR][NDW]) {
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const_u32p p = (const_u32p)(cur + (size_t)(y + r) * W + x);
+#pragma unroll
+        for (int k = 0; k < NDW; ++k) cr[r][k] = p[k];
     }
 }
 
-// Window-row read of N dwords starting at ANY byte address p: aligned ds_read_b32 x (N+1)
-// and N v_alignbyte.  Measured alternatives (tools/me_ab.py, 4K P-frame, same outputs):
-// one byte-unaligned ds_read_b128 157.9 us, N byte-unaligned ds_read_b32 576.8 us -- gfx950
-// replays misaligned DS reads (cdna_hip_programming.md Guideline 17) -- vs 111.9 us here.
-template <int N>
-SO_DEV void win_read(const uint8_t* p, uint32_t (&v)[N]) {
-    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);   // keeps the LDS address space
-    uint32_t w[N + 1];
+SO_DEV uint64_t wave_min_u64(uint64_t v) {
 #pragma unroll
-    for (int k = 0; k <= N; ++k) w[k] = q[k];
-#pragma unroll
-    for (int k = 0; k < N; ++k) v[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint32_t lo = __shfl_xor((uint32_t)v, m, 64), hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
+        const uint64_t o = ((uint64_t)hi << 32) | lo;
+        v = o < v ? o : v;
+    }
+    return v;
 }
 
-// IR-level fence over the accumulators: the SADs of a window row are issued before any
-// later row's LDS load is hoisted above them (bounds VGPRs to acc + cur + 2 rows).
-template <int D>
-SO_DEV void acc_fence(uint32_t (&a)[D]) {
-    static_assert(D == 33, "fence written for 33 accumulators");
+template <int N>
+SO_DEV void acc_fence_n(uint32_t (&a)[N]) {
+    static_assert(N == 17, "fence written for 17 accumulators");
     asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]),
                  "+v"(a[7]), "+v"(a[8]), "+v"(a[9]), "+v"(a[10]), "+v"(a[11]), "+v"(a[12]), "+v"(a[13]),
                  "+v"(a[14]), "+v"(a[15]), "+v"(a[16]) : : "memory");
-    asm volatile("" : "+v"(a[17]), "+v"(a[18]), "+v"(a[19]), "+v"(a[20]), "+v"(a[21]), "+v"(a[22]),
-                 "+v"(a[23]), "+v"(a[24]), "+v"(a[25]), "+v"(a[26]), "+v"(a[27]), "+v"(a[28]), "+v"(a[29]),
-                 "+v"(a[30]), "+v"(a[31]), "+v"(a[32]) : : "memory");
 }
 
-// One task: (sub-)block of size TBS whose top-left sits at window (wrow, wcol - dxi) and
-// current-tile (crow, ccol); wcol already includes dxi.  dy_index in [dlo, dhi] is valid.
-// Returns the lane's best 32-bit key, 0xFFFFFFFF if no dy is valid.
-template <int TBS, int WP, int CP>
-SO_DEV uint32_t me_tile_task(const uint8_t* __restrict__ win, const uint8_t* __restrict__ curt, int wrow,
-                             int wcol, int crow, int ccol, int dlo, int dhi) {
-    constexpr int D = 33, NDW = TBS / 4, RCH = 8, NR = RCH + D - 1;
-    uint32_t acc[D];
-#pragma unroll
-    for (int i = 0; i < D; ++i) acc[i] = 0;
-#pragma unroll
-    for (int c0 = 0; c0 < TBS; c0 += RCH) {
-        uint32_t cr[RCH][NDW];
-#pragma unroll
-        for (int r = 0; r < RCH; ++r) lds_read<NDW>(curt + (crow + c0 + r) * CP + ccol, cr[r]);
-        const uint8_t* p = win + (wrow + c0) * WP + wcol;
-        uint32_t wc[NDW], wn[NDW];
-        win_read<NDW>(p, wc);
-#pragma unroll
-        for (int jj = 0; jj < NR; ++jj) {
-            if (jj + 1 < NR) win_read<NDW>(p + (jj + 1) * WP, wn);
-#pragma unroll
-            for (int r = 0; r < RCH; ++r) {
-                const int di = jj - r;
-                if (di >= 0 && di < D) {
-#pragma unroll
-                    for (int k = 0; k < NDW; ++k) acc[di] = __builtin_amdgcn_sad_u8(cr[r][k], wc[k], acc[di]);
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < NDW; ++k) wc[k] = wn[k];
-            acc_fence<D>(acc);
-        }
-    }
+// Lane's best 32-bit key over its 17 phase-1 candidates t: (sad << 5) | (t ^ X), where
+// X = 31 for the dy <= 0 half (|dy| = 16 - t) and 0 for the other (|dy| = t) -- within a
+// lane dx and ref are fixed, so (sad, this code) orders exactly like (sad, |dx|+|dy|, scan).
+// di valid in [dlo, dhi] (di = 16*hh + t); `edge` selects the masked form.
+SO_DEV uint32_t lane_best17(const uint32_t (&a)[17], uint32_t X, int hh, int dlo, int dhi, bool edge) {
     uint32_t best = 0xFFFFFFFFu;
-    if (dlo == 0 && dhi == D - 1) {
+    if (!edge) {
 #pragma unroll
-        for (int di = 0; di < D; ++di) {
-            constexpr int SR = 16;
-            const uint32_t low = (uint32_t)(((di < SR ? SR - di : di - SR) << 6) | di);
-            const uint32_t k = (acc[di] << 11) | low;
+        for (int t = 0; t < 17; ++t) {
+            const uint32_t k = ((a[t] << 5) | (uint32_t)t) ^ X;
             best = k < best ? k : best;
         }
     } else {
 #pragma unroll
-        for (int di = 0; di < D; ++di) {
-            constexpr int SR = 16;
-            const uint32_t low = (uint32_t)(((di < SR ? SR - di : di - SR) << 6) | di);
-            uint32_t k = (acc[di] << 11) | low;
+        for (int t = 0; t < 17; ++t) {
+            const int di = 16 * hh + t;
+            uint32_t k = ((a[t] << 5) | (uint32_t)t) ^ X;
             k = (di < dlo || di > dhi) ? 0xFFFFFFFFu : k;
             best = k < best ? k : best;
         }
@@ -170,86 +147,196 @@ SO_DEV uint32_t me_tile_task(const uint8_t* __restrict__ win, const uint8_t* __r
     return best;
 }
 
+// Widen a lane's phase-1 best to the 64-bit reference key (kNoKey if none / dx invalid).
+SO_DEV uint64_t widen17(uint32_t b32, uint32_t X, int hh, int xi, bool xok, int ref) {
+    if (!xok || b32 == 0xFFFFFFFFu) return kNoKey;
+    const uint32_t t = (b32 & 31) ^ X, sad = b32 >> 5;
+    const int di = 16 * hh + (int)t, dy = di - 16, dx = xi - 16;
+    const uint32_t l1 = (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy));
+    return me_key(sad, l1, (uint32_t)ref, (uint32_t)(xi * 33 + di));
+}
+
 template <int BS, bool SUB>
-__global__ void __launch_bounds__(MeGeo<BS>::NTHREADS) __attribute__((amdgpu_waves_per_eu(6)))
-me_tile_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
+__global__ void __launch_bounds__(MeWGeo<BS>::NTHREADS) __attribute__((amdgpu_waves_per_eu(SUB ? 4 : 6)))
+me_wave_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
                int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub) {
-    using G = MeGeo<BS>;
-    constexpr int SR = G::SR, D = G::D, TB = G::TB, SB = BS / 2, WP = G::WP, CP = G::CP;
+    using G = MeWGeo<BS>;
+    constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RPD = G::RPD, CS = G::CSTRIDE, NT = G::NT;
+    constexpr int NDW = BS / 4, HALF = 8, NPASS = BS / HALF, NR = NT + HALF - 1;
     constexpr int NUNIT = G::NBLK * (SUB ? 5 : 1);
-    __shared__ uint32_t win32[WP * WP / 4];
-    __shared__ uint32_t cur32[G::TPX * CP / 4];
+    __shared__ uint32_t win[4 * CS];
     __shared__ unsigned long long keys[NUNIT];
-    uint8_t* win = reinterpret_cast<uint8_t*>(win32);
-    uint8_t* curt = reinterpret_cast<uint8_t*>(cur32);
 
     const int nbx = W / BS;
-    const int tiles_x = (nbx + TB - 1) / TB;
+    const int tiles_x = (nbx + TBX - 1) / TBX;
     const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
-    const int bx0 = tx * TB, byt0 = by0 + ty * TB;       // first block of the tile
+    const int bx0 = tx * TBX, byt0 = by0 + ty * TBY;
     const int x0 = bx0 * BS, y0 = byt0 * BS;
     const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
     for (int i = tid; i < NUNIT; i += G::NTHREADS) keys[i] = kNoKey;
-    // current tile: 128 rows x 16 chunks of 8 B (zero outside the frame)
-    for (int i = tid; i < G::TPX * (CP / 8); i += G::NTHREADS) {
-        const int r = i / (CP / 8), c = i % (CP / 8);
-        const int gy = y0 + r, gx = x0 + c * 8;
-        uint2 v = make_uint2(0, 0);
-        if (gy < H && gx + 8 <= W) v = *reinterpret_cast<const uint2*>(cur + (size_t)gy * W + gx);
-        *reinterpret_cast<uint2*>(curt + r * CP + c * 8) = v;
-    }
-
-    constexpr int NFULL = G::NBLK * D;
-    constexpr int NSUBT = SUB ? 4 * G::NBLK * D : 0;
-    constexpr int NTASK = NFULL + NSUBT;
-    static_assert(NTASK % G::NTHREADS == 0, "tasks must fill whole rounds");
-
     for (int r = 0; r < nref; ++r) {
         const uint8_t* ref = refs.p[r];
-        __syncthreads();  // previous reference's tasks are done with the window
-        for (int i = tid; i < WP * (WP / 8); i += G::NTHREADS) {
-            const int wr = i / (WP / 8), wc = i % (WP / 8);
-            const int gy = y0 - SR + wr, gx = x0 - SR + wc * 8;
-            uint2 v = make_uint2(0, 0);
-            if (gy >= 0 && gy < H && gx >= 0 && gx + 8 <= W)
-                v = *reinterpret_cast<const uint2*>(ref + (size_t)gy * W + gx);
-            *reinterpret_cast<uint2*>(win + wr * WP + wc * 8) = v;
+        __syncthreads();   // the previous reference's reads of the window are done
+        // stage: copy s row wr dword m = window bytes [4m + s, 4m + s + 4); zero off-frame
+        for (int i = tid; i < G::WR * RPD; i += G::NTHREADS) {
+            const int wr = i / RPD, m = i - wr * RPD;
+            const int gy = y0 - SR + wr, gx = x0 - SR + 4 * m;
+            uint32_t a = 0, b = 0;
+            if (gy >= 0 && gy < H) {
+                const uint8_t* rp = ref + (size_t)gy * W;
+                if (gx >= 0 && gx + 4 <= W) a = *reinterpret_cast<const uint32_t*>(rp + gx);
+                if (gx + 4 >= 0 && gx + 8 <= W) b = *reinterpret_cast<const uint32_t*>(rp + gx + 4);
+            }
+            uint32_t* d = win + wr * RPD + m;
+            d[0] = a;
+            d[CS] = __builtin_amdgcn_alignbyte(b, a, 1);
+            d[2 * CS] = __builtin_amdgcn_alignbyte(b, a, 2);
+            d[3 * CS] = __builtin_amdgcn_alignbyte(b, a, 3);
         }
         __syncthreads();
 #pragma unroll 1
-        for (int t = tid; t < NTASK; t += G::NTHREADS) {
-            int unit, tbs, dxi, ox, oy, blk;
-            if (t < NFULL) {
-                blk = t / D; dxi = t - blk * D; unit = blk; tbs = BS; ox = 0; oy = 0;
-            } else {
-                const int s = (t - NFULL) / D;
-                dxi = (t - NFULL) - s * D; blk = s >> 2; unit = G::NBLK + s; tbs = SB;
-                ox = (s & 1) * SB; oy = ((s >> 1) & 1) * SB;
+        for (int u = wave; u < G::NBLK; u += G::NW) {
+            const int bxl = u % TBX, byl = u / TBX;
+            if (bx0 + bxl >= nbx || byt0 + byl >= by1) continue;   // wave-uniform
+            const int x = x0 + bxl * BS, y = y0 + byl * BS;
+            // lane identity re-derived per block through an opaque asm: otherwise LICM hoists
+            // the ~17 per-lane (16*hh + t) edge constants out of this loop and spills them
+            int lane = tid & 63;
+            asm volatile("" : "+v"(lane));
+            const int xi = lane & 31, hh = lane >> 5;
+            const uint32_t X = hh ? 0u : 31u;
+            // phase-1 lane: window column bxl*BS + xi (dx = xi - 16) in copy xi & 3
+            const int q1 = (xi & 3) * CS + (byl * BS + 16 * hh) * RPD + ((bxl * BS + xi) >> 2);
+            // phase-2 lane: dx = +16 (column bxl*BS + 32, copy 0), dy index = lane (< 33)
+            const int d2 = lane < 33 ? lane : 32;
+            const int q2 = (byl * BS + d2) * RPD + ((bxl * BS + 32) >> 2);
+            uint32_t accL[NT], accR[NT], S[NT];
+            uint32_t a2L[NPASS], a2R[NPASS];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) S[t] = 0;
+            uint32_t subb[4];          // VBS: lane best 32-bit key per quadrant (phase 1)
+            uint32_t sub2[4];          // VBS: phase-2 quadrant SADs
+#pragma unroll
+            for (int pass = 0; pass < NPASS; ++pass) {
+                // the row index goes through an opaque asm so this pass's scalar loads cannot
+                // be hoisted above the previous pass (constant-space loads are otherwise free
+                // to move, and two passes of pixels overflow the SGPRs)
+                int ycur = y + pass * HALF;
+                asm volatile("" : "+s"(ycur));
+                uint32_t cr[HALF][NDW];
+                load_cur_sgpr<HALF, NDW>(cur, W, x, ycur, cr);
+                if (SUB || pass == 0) {   // without VBS accL accumulates the whole block
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) { accL[t] = 0; accR[t] = 0; }
+                }
+                // phase 1: rows pass*8 + jj of the lane's 24-row strip
+                // volatile: the four dwords stay four ds_read_b32 -- merged into one b128 they
+                // are 4-byte but not 16-byte aligned and the LDS replays them (Guideline 17)
+                int qo = q1 + pass * HALF * RPD;       // dword offsets into win[] keep the LDS
+                asm volatile("" : "+v"(qo));           // address space through the opaque asm
+                lds_vu32p qp = (lds_vu32p)(win + qo);
+                uint32_t wc[NDW], wn[NDW];
+#pragma unroll
+                for (int k = 0; k < NDW; ++k) wc[k] = qp[k];
+#pragma unroll
+                for (int jj = 0; jj < NR; ++jj) {
+                    if (jj + 1 < NR) {
+#pragma unroll
+                        for (int k = 0; k < NDW; ++k) wn[k] = qp[(jj + 1) * RPD + k];
+                    }
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) {
+                        const int rr = jj - t;
+                        if (rr >= 0 && rr < HALF) {
+#pragma unroll
+                            for (int k = 0; k < NDW; ++k) {
+                                if (SUB && k >= NDW / 2) accR[t] = __builtin_amdgcn_sad_u8(cr[rr][k], wc[k], accR[t]);
+                                else accL[t] = __builtin_amdgcn_sad_u8(cr[rr][k], wc[k], accL[t]);
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < NDW; ++k) wc[k] = wn[k];
+                    acc_fence_n<NT>(accL);
+                    if constexpr (SUB) acc_fence_n<NT>(accR);
+                }
+                // phase 2: the dx = +16 candidate of dy index d2, rows pass*8 .. +8
+                uint32_t l2 = 0, r2 = 0;
+                int q2o = q2 + pass * HALF * RPD;
+                asm volatile("" : "+v"(q2o));   // phase-2 reads stay after phase 1
+                lds_vu32p q2p = (lds_vu32p)(win + q2o);
+#pragma unroll
+                for (int rr = 0; rr < HALF; ++rr) {
+                    lds_vu32p w2 = q2p + rr * RPD;
+#pragma unroll
+                    for (int k = 0; k < NDW; ++k) {
+                        if (SUB && k >= NDW / 2) r2 = __builtin_amdgcn_sad_u8(cr[rr][k], w2[k], r2);
+                        else l2 = __builtin_amdgcn_sad_u8(cr[rr][k], w2[k], l2);
+                    }
+                    asm volatile("" : "+v"(l2), "+v"(r2) : : "memory");   // one row in flight
+                }
+                a2L[pass] = l2;
+                a2R[pass] = r2;
+                if constexpr (SUB) {
+                    // quadrants (pass 0: TL, TR; pass 1: BL, BR) -- per-lane bests now, the
+                    // accumulators are reused by the next pass
+                    const int ys = y + pass * HALF;
+                    int dlo = SR - ys;               dlo = dlo < 0 ? 0 : dlo;
+                    int dhi = H - 8 - ys + SR - 1; dhi = dhi > 32 ? 32 : dhi;
+                    const bool edge = dlo > 0 || dhi < 32;
+                    subb[2 * pass] = lane_best17(accL, X, hh, dlo, dhi, edge);
+                    subb[2 * pass + 1] = lane_best17(accR, X, hh, dlo, dhi, edge);
+                    sub2[2 * pass] = l2;
+                    sub2[2 * pass + 1] = r2;
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) S[t] += accL[t] + accR[t];
+                }
             }
-            const int bxl = blk % TB, byl = blk / TB;
-            if (bx0 + bxl >= nbx || byt0 + byl >= by1) continue;
-            const int x = x0 + bxl * BS + ox, y = y0 + byl * BS + oy;
-            int dlo = SR - y;               dlo = dlo < 0 ? 0 : dlo;
-            int dhi = H - tbs - y + SR - 1; dhi = dhi > D - 1 ? D - 1 : dhi;
-            const int wrow = byl * BS + oy, wcol = bxl * BS + ox + dxi;
-            uint32_t b32;
-            if (t < NFULL) b32 = me_tile_task<BS, WP, CP>(win, curt, wrow, wcol, wrow, bxl * BS + ox, dlo, dhi);
-            else if constexpr (SUB) b32 = me_tile_task<SB, WP, CP>(win, curt, wrow, wcol, wrow, bxl * BS + ox, dlo, dhi);
-            else b32 = 0xFFFFFFFFu;
-            const int dx = dxi - SR;
-            const bool xok = (x + dx >= 0) && (x + dx < W - tbs);
-            if (xok && b32 != 0xFFFFFFFFu) {
-                const uint32_t sad = b32 >> 11, ady = (b32 >> 6) & 31, di = b32 & 63;
-                const uint32_t adx = (uint32_t)(dx < 0 ? -dx : dx);
-                atomicMin(&keys[unit], (unsigned long long)me_key(sad, adx + ady, (uint32_t)r, (uint32_t)dxi * D + di));
+            if constexpr (!SUB) {
+#pragma unroll
+                for (int t = 0; t < NT; ++t) S[t] = accL[t];
+            }
+            // block keys: phase 1 (lane's 17 candidates) and phase 2 (dx = +16)
+            int dlo = SR - y;            dlo = dlo < 0 ? 0 : dlo;
+            int dhi = H - BS - y + SR - 1; dhi = dhi > 32 ? 32 : dhi;
+            const bool edge = dlo > 0 || dhi < 32;
+            const bool xok = (x + xi - 16 >= 0) && (x + xi - 16 < W - BS);
+            uint64_t k = widen17(lane_best17(S, X, hh, dlo, dhi, edge), X, hh, xi, xok, r);
+            {
+                uint32_t s2 = 0;
+#pragma unroll
+                for (int pass = 0; pass < NPASS; ++pass) s2 += a2L[pass] + a2R[pass];
+                const bool ok2 = lane < 33 && (x + 16 < W - BS) && d2 >= dlo && d2 <= dhi;
+                const uint64_t k2 = ok2 ? me_key(s2, (uint32_t)(16 + (d2 < 16 ? 16 - d2 : d2 - 16)), (uint32_t)r,
+                                                 (uint32_t)(32 * 33 + d2))
+                                        : kNoKey;
+                k = k2 < k ? k2 : k;
+            }
+            k = wave_min_u64(k);
+            if (lane == 0 && k < keys[u]) keys[u] = k;
+            if constexpr (SUB) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int xs = x + (j & 1) * 8, ys = y + (j >> 1) * 8;
+                    const bool sxok = (xs + xi - 16 >= 0) && (xs + xi - 16 < W - 8);
+                    uint64_t ks = widen17(subb[j], X, hh, xi, sxok, r);
+                    const bool ok2 = lane < 33 && (xs + 16 < W - 8) && (ys + d2 - 16 >= 0) && (ys + d2 - 16 < H - 8);
+                    const uint64_t k2 = ok2 ? me_key(sub2[j], (uint32_t)(16 + (d2 < 16 ? 16 - d2 : d2 - 16)),
+                                                     (uint32_t)r, (uint32_t)(32 * 33 + d2))
+                                            : kNoKey;
+                    ks = k2 < ks ? k2 : ks;
+                    ks = wave_min_u64(ks);
+                    if (lane == 0 && ks < keys[G::NBLK + 4 * u + j]) keys[G::NBLK + 4 * u + j] = ks;
+                }
             }
         }
     }
     __syncthreads();
     for (int i = tid; i < NUNIT; i += G::NTHREADS) {
         const int blk = i < G::NBLK ? i : (i - G::NBLK) >> 2;
-        const int gbx = bx0 + blk % TB, gby = byt0 + blk / TB;
+        const int gbx = bx0 + blk % TBX, gby = byt0 + blk / TBX;
         if (gbx >= nbx || gby >= by1) continue;
         const size_t b = (size_t)(gby - by0) * nbx + gbx;
         if (i < G::NBLK) decode_key(keys[i], SR, out_best + b * 4);
@@ -444,12 +531,27 @@ int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, in
     const int nbx = W / bs, nrows = by1 - by0;
     if (nrows <= 0) return SO_OK;
     if (sr == 16 && (bs == 16 || bs == 8) && (out_sub == nullptr || bs == 16)) {
-        // SO_ME_IMPL=fast selects the round-1 kernel (A/B only, tools/me_ab.py)
+        // SO_ME_IMPL=fast (A/B only, tools/me_ab.py) selects the round-1 kernel
         const char* impl = getenv("SO_ME_IMPL");
         const bool use_fast = impl && strcmp(impl, "fast") == 0;
         const int tb = bs == 16 ? MeGeo<16>::TB : MeGeo<8>::TB;
         const dim3 grid(((nbx + tb - 1) / tb) * ((nrows + tb - 1) / tb)), blk(MeGeo<16>::NTHREADS);
-        if (use_fast) {
+        if (!use_fast) {
+            const int tbx = bs == 16 ? MeWGeo<16>::TBX : MeWGeo<8>::TBX;
+            const int tby = bs == 16 ? MeWGeo<16>::TBY : MeWGeo<8>::TBY;
+            const dim3 wgrid(((nbx + tbx - 1) / tbx) * ((nrows + tby - 1) / tby)), wblk(MeWGeo<16>::NTHREADS);
+            if (bs == 16 && out_sub)
+                hipLaunchKernelGGL((me_wave_kernel<16, true>), wgrid, wblk, 0, st, cur, refs, nref, H, W, by0, by1,
+                                   out_best, out_sub);
+            else if (bs == 16)
+                hipLaunchKernelGGL((me_wave_kernel<16, false>), wgrid, wblk, 0, st, cur, refs, nref, H, W, by0, by1,
+                                   out_best, out_sub);
+            else
+                hipLaunchKernelGGL((me_wave_kernel<8, false>), wgrid, wblk, 0, st, cur, refs, nref, H, W, by0, by1,
+                                   out_best, nullptr);
+            return check_launch("me_wave_kernel");
+        }
+        {
             if (bs == 16 && out_sub)
                 hipLaunchKernelGGL((me_fast_kernel<16, true>), grid, blk, 0, st, cur, refs, nref, H, W, by0, by1,
                                    out_best, out_sub);
@@ -461,16 +563,6 @@ int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, in
                                    out_best, nullptr);
             return check_launch("me_fast_kernel");
         }
-        if (bs == 16 && out_sub)
-            hipLaunchKernelGGL((me_tile_kernel<16, true>), grid, blk, 0, st, cur, refs, nref, H, W, by0, by1,
-                               out_best, out_sub);
-        else if (bs == 16)
-            hipLaunchKernelGGL((me_tile_kernel<16, false>), grid, blk, 0, st, cur, refs, nref, H, W, by0, by1,
-                               out_best, out_sub);
-        else
-            hipLaunchKernelGGL((me_tile_kernel<8, false>), grid, blk, 0, st, cur, refs, nref, H, W, by0, by1,
-                               out_best, nullptr);
-        return check_launch("me_tile_kernel");
     }
     // generic
     const int d = 2 * sr + 1;

@@ -1,6 +1,6 @@
 """A/B of ME implementations in one process (interleaved rounds), 4K P-frame.
 
-Variants: me_tile_kernel (default) and the round-1 me_fast_kernel (SO_ME_IMPL=fast).  Checks every variant's output equals
+Variants: me_wave_kernel (default) and the round-1 me_fast_kernel (SO_ME_IMPL=fast).  Checks every variant's output equals
 the first one's, then prints us/launch per variant."""
 import os, sys
 import torch
@@ -9,7 +9,7 @@ from streamoptima_amd import _lib
 from streamoptima_amd.engine import alloc_planes
 from streamoptima_amd.synth import synth_sequence_torch
 
-VARIANTS = {"tile": {}, "fast": {"SO_ME_IMPL": "fast"}}
+VARIANTS = {"wave": {}, "fast": {"SO_ME_IMPL": "fast"}}
 
 
 def main():
