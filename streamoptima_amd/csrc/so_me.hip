@@ -77,17 +77,21 @@ struct MeGeo {
 // Argmin: per-lane 32-bit keys (sad << 5 | ordered |dy| code), widened to the 64-bit key
 // and reduced across the wave.
 // ---------------------------------------------------------------------------------------
-template <int BS>
+// Tile geometry.  Without VBS a lane needs ~40 VGPRs, so LDS sets the occupancy: a 128 x 64
+// tile (96-row window, 4 copies = 62 KB) with 16 waves gives 2 workgroups = 8 waves/SIMD.
+// With VBS (~126 VGPRs, 4 waves/SIMD) a 128 x 32 tile with 8 waves.
+template <int BS, bool SUB>
 struct MeWGeo {
     static constexpr int SR = 16, D = 33, NT = 17;
     static constexpr int TBX = 128 / BS;                  // blocks across (128 px)
-    static constexpr int TBY = (BS == 16) ? 2 : 4;        // blocks down (32 px)
-    static constexpr int TPX = 128, TPY = TBY * BS;
-    static constexpr int WR = TPY + 2 * SR;               // 64 window rows
+    static constexpr int TPY = SUB ? 32 : 64;             // pixel rows per tile
+    static constexpr int TBY = TPY / BS;
+    static constexpr int TPX = 128;
+    static constexpr int WR = TPY + 2 * SR;               // window rows
     static constexpr int RPD = (TPX + 2 * SR) / 4;        // 40 dwords per copy row
     static constexpr int CSTRIDE = WR * RPD + 16;         // dwords per shifted copy (+16-bank skew)
     static constexpr int NBLK = TBX * TBY;
-    static constexpr int NW = 8, NTHREADS = NW * 64;
+    static constexpr int NW = SUB ? 8 : 16, NTHREADS = NW * 64;
 };
 
 typedef const __attribute__((address_space(4))) uint32_t* const_u32p;
@@ -157,10 +161,10 @@ SO_DEV uint64_t widen17(uint32_t b32, uint32_t X, int hh, int xi, bool xok, int 
 }
 
 template <int BS, bool SUB>
-__global__ void __launch_bounds__(MeWGeo<BS>::NTHREADS) __attribute__((amdgpu_waves_per_eu(SUB ? 4 : 6)))
+__global__ void __launch_bounds__((MeWGeo<BS, SUB>::NTHREADS)) __attribute__((amdgpu_waves_per_eu(SUB ? 4 : 8)))
 me_wave_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
                int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub) {
-    using G = MeWGeo<BS>;
+    using G = MeWGeo<BS, SUB>;
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RPD = G::RPD, CS = G::CSTRIDE, NT = G::NT;
     constexpr int NDW = BS / 4, HALF = 8, NPASS = BS / HALF, NR = NT + HALF - 1;
     constexpr int NUNIT = G::NBLK * (SUB ? 5 : 1);
@@ -537,9 +541,11 @@ int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, in
         const int tb = bs == 16 ? MeGeo<16>::TB : MeGeo<8>::TB;
         const dim3 grid(((nbx + tb - 1) / tb) * ((nrows + tb - 1) / tb)), blk(MeGeo<16>::NTHREADS);
         if (!use_fast) {
-            const int tbx = bs == 16 ? MeWGeo<16>::TBX : MeWGeo<8>::TBX;
-            const int tby = bs == 16 ? MeWGeo<16>::TBY : MeWGeo<8>::TBY;
-            const dim3 wgrid(((nbx + tbx - 1) / tbx) * ((nrows + tby - 1) / tby)), wblk(MeWGeo<16>::NTHREADS);
+            const bool sub = out_sub != nullptr;
+            const int tbx = 128 / bs;
+            const int tby = (sub ? MeWGeo<16, true>::TPY : MeWGeo<16, false>::TPY) / bs;
+            const dim3 wgrid(((nbx + tbx - 1) / tbx) * ((nrows + tby - 1) / tby));
+            const dim3 wblk(sub ? MeWGeo<16, true>::NTHREADS : MeWGeo<16, false>::NTHREADS);
             if (bs == 16 && out_sub)
                 hipLaunchKernelGGL((me_wave_kernel<16, true>), wgrid, wblk, 0, st, cur, refs, nref, H, W, by0, by1,
                                    out_best, out_sub);
