@@ -99,7 +99,7 @@ def max_over_ranks(x: float, world: int) -> float:
 
 
 def me_kernel_name() -> str:
-    return "me_fast_kernel" if os.environ.get("SO_ME_IMPL") == "fast" else "me_tile_kernel"
+    return "me_fast_kernel" if os.environ.get("SO_ME_IMPL") == "fast" else "me_wave_kernel"
 
 
 def kernel_roofline(codec, frames_dev, reps: int) -> dict:

@@ -66,7 +66,7 @@ struct MeGeo {
 //     any column are four dword-aligned ds_read_b32 from copy (col & 3) -- the byte
 //     alignment is paid once per staged dword instead of once per row per lane (a b128 read
 //     would need 16-byte alignment: misaligned wide DS reads are replayed on gfx950);
-//   * copies are skewed by 16 banks.
+//   * copy strides are 8 (mod 32) dwords, so the 32-lane b32 reads are bank-conflict free.
 // Phase 1: lane = hh*32 + xi covers dx = xi - 16 (xi < 32) and dy = 16*hh + t - 16
 // (t < 17): the halves take dy in [-16, 0] and [0, 16] (dy 0 twice, 3% redundant).  The
 // lane slides over its 17 + 8 - 1 window rows per pass and adds every row into the t it
@@ -89,7 +89,9 @@ struct MeWGeo {
     static constexpr int TPX = 128;
     static constexpr int WR = TPY + 2 * SR;               // window rows
     static constexpr int RPD = (TPX + 2 * SR) / 4;        // 40 dwords per copy row
-    static constexpr int CSTRIDE = WR * RPD + 16;         // dwords per shifted copy (+16-bank skew)
+    // dwords per shifted copy: CSTRIDE = 8 (mod 32) puts the four copies 8 banks apart, so a
+    // 32-lane ds_read_b32 (bank = dword mod 32) of lanes xi hits 8*(xi&3) + (xi>>2): no conflict
+    static constexpr int CSTRIDE = WR * RPD + 8;
     static constexpr int NBLK = TBX * TBY;
     static constexpr int NW = SUB ? 8 : 16, NTHREADS = NW * 64;
 };
@@ -160,6 +162,146 @@ SO_DEV uint64_t widen17(uint32_t b32, uint32_t X, int hh, int xi, bool xok, int 
     return me_key(sad, l1, (uint32_t)ref, (uint32_t)(xi * 33 + di));
 }
 
+// Dense search of one block by one wavefront (phase 1 + phase 2 over the four shifted
+// window copies in `win`); merges the block key into keys[u] and, with VBS, the quadrant
+// keys into keys[nblk + 4u + j].  Shared by me_wave_kernel and me_sea_kernel's fallback.
+template <int BS, bool SUB, int RPD, int CS>
+SO_DEV void wave_dense_block(const uint32_t* win, unsigned long long* keys, int nblk, const uint8_t* __restrict__ cur,
+                             int W, int H, int x, int y, int bxl, int byl, int u, int tid, int r) {
+    constexpr int SR = 16, NT = 17;
+    constexpr int NDW = BS / 4, HALF = 8, NPASS = BS / HALF, NR = NT + HALF - 1;
+    // lane identity re-derived per block through an opaque asm: otherwise LICM hoists
+    // the ~17 per-lane (16*hh + t) edge constants out of this loop and spills them
+    int lane = tid & 63;
+    asm volatile("" : "+v"(lane));
+    const int xi = lane & 31, hh = lane >> 5;
+    const uint32_t X = hh ? 0u : 31u;
+    // phase-1 lane: window column bxl*BS + xi (dx = xi - 16) in copy xi & 3
+    const int q1 = (xi & 3) * CS + (byl * BS + 16 * hh) * RPD + ((bxl * BS + xi) >> 2);
+    // phase-2 lane: dx = +16 (column bxl*BS + 32, copy 0), dy index = lane (< 33)
+    const int d2 = lane < 33 ? lane : 32;
+    const int q2 = (byl * BS + d2) * RPD + ((bxl * BS + 32) >> 2);
+    uint32_t accL[NT], accR[NT], S[NT];
+    uint32_t a2L[NPASS], a2R[NPASS];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) S[t] = 0;
+    uint32_t subb[4];          // VBS: lane best 32-bit key per quadrant (phase 1)
+    uint32_t sub2[4];          // VBS: phase-2 quadrant SADs
+#pragma unroll
+    for (int pass = 0; pass < NPASS; ++pass) {
+        // the row index goes through an opaque asm so this pass's scalar loads cannot
+        // be hoisted above the previous pass (constant-space loads are otherwise free
+        // to move, and two passes of pixels overflow the SGPRs)
+        int ycur = y + pass * HALF;
+        asm volatile("" : "+s"(ycur));
+        uint32_t cr[HALF][NDW];
+        load_cur_sgpr<HALF, NDW>(cur, W, x, ycur, cr);
+        if (SUB || pass == 0) {   // without VBS accL accumulates the whole block
+#pragma unroll
+            for (int t = 0; t < NT; ++t) { accL[t] = 0; accR[t] = 0; }
+        }
+        // phase 1: rows pass*8 + jj of the lane's 24-row strip
+        // volatile: the four dwords stay four ds_read_b32 -- merged into one b128 they
+        // are 4-byte but not 16-byte aligned and the LDS replays them (Guideline 17)
+        int qo = q1 + pass * HALF * RPD;       // dword offsets into win[] keep the LDS
+        asm volatile("" : "+v"(qo));           // address space through the opaque asm
+        lds_vu32p qp = (lds_vu32p)(win + qo);
+        uint32_t wc[NDW], wn[NDW];
+#pragma unroll
+        for (int k = 0; k < NDW; ++k) wc[k] = qp[k];
+#pragma unroll
+        for (int jj = 0; jj < NR; ++jj) {
+            if (jj + 1 < NR) {
+#pragma unroll
+                for (int k = 0; k < NDW; ++k) wn[k] = qp[(jj + 1) * RPD + k];
+            }
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int rr = jj - t;
+                if (rr >= 0 && rr < HALF) {
+#pragma unroll
+                    for (int k = 0; k < NDW; ++k) {
+                        if (SUB && k >= NDW / 2) accR[t] = __builtin_amdgcn_sad_u8(cr[rr][k], wc[k], accR[t]);
+                        else accL[t] = __builtin_amdgcn_sad_u8(cr[rr][k], wc[k], accL[t]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < NDW; ++k) wc[k] = wn[k];
+            acc_fence_n<NT>(accL);
+            if constexpr (SUB) acc_fence_n<NT>(accR);
+        }
+        // phase 2: the dx = +16 candidate of dy index d2, rows pass*8 .. +8
+        uint32_t l2 = 0, r2 = 0;
+        int q2o = q2 + pass * HALF * RPD;
+        asm volatile("" : "+v"(q2o));   // phase-2 reads stay after phase 1
+        lds_vu32p q2p = (lds_vu32p)(win + q2o);
+#pragma unroll
+        for (int rr = 0; rr < HALF; ++rr) {
+            lds_vu32p w2 = q2p + rr * RPD;
+#pragma unroll
+            for (int k = 0; k < NDW; ++k) {
+                if (SUB && k >= NDW / 2) r2 = __builtin_amdgcn_sad_u8(cr[rr][k], w2[k], r2);
+                else l2 = __builtin_amdgcn_sad_u8(cr[rr][k], w2[k], l2);
+            }
+            asm volatile("" : "+v"(l2), "+v"(r2) : : "memory");   // one row in flight
+        }
+        a2L[pass] = l2;
+        a2R[pass] = r2;
+        if constexpr (SUB) {
+            // quadrants (pass 0: TL, TR; pass 1: BL, BR) -- per-lane bests now, the
+            // accumulators are reused by the next pass
+            const int ys = y + pass * HALF;
+            int dlo = SR - ys;               dlo = dlo < 0 ? 0 : dlo;
+            int dhi = H - 8 - ys + SR - 1; dhi = dhi > 32 ? 32 : dhi;
+            const bool edge = dlo > 0 || dhi < 32;
+            subb[2 * pass] = lane_best17(accL, X, hh, dlo, dhi, edge);
+            subb[2 * pass + 1] = lane_best17(accR, X, hh, dlo, dhi, edge);
+            sub2[2 * pass] = l2;
+            sub2[2 * pass + 1] = r2;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) S[t] += accL[t] + accR[t];
+        }
+    }
+    if constexpr (!SUB) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) S[t] = accL[t];
+    }
+    // block keys: phase 1 (lane's 17 candidates) and phase 2 (dx = +16)
+    int dlo = SR - y;            dlo = dlo < 0 ? 0 : dlo;
+    int dhi = H - BS - y + SR - 1; dhi = dhi > 32 ? 32 : dhi;
+    const bool edge = dlo > 0 || dhi < 32;
+    const bool xok = (x + xi - 16 >= 0) && (x + xi - 16 < W - BS);
+    uint64_t k = widen17(lane_best17(S, X, hh, dlo, dhi, edge), X, hh, xi, xok, r);
+    {
+        uint32_t s2 = 0;
+#pragma unroll
+        for (int pass = 0; pass < NPASS; ++pass) s2 += a2L[pass] + a2R[pass];
+        const bool ok2 = lane < 33 && (x + 16 < W - BS) && d2 >= dlo && d2 <= dhi;
+        const uint64_t k2 = ok2 ? me_key(s2, (uint32_t)(16 + (d2 < 16 ? 16 - d2 : d2 - 16)), (uint32_t)r,
+                                         (uint32_t)(32 * 33 + d2))
+                                : kNoKey;
+        k = k2 < k ? k2 : k;
+    }
+    k = wave_min_u64(k);
+    if (lane == 0 && k < keys[u]) keys[u] = k;
+    if constexpr (SUB) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int xs = x + (j & 1) * 8, ys = y + (j >> 1) * 8;
+            const bool sxok = (xs + xi - 16 >= 0) && (xs + xi - 16 < W - 8);
+            uint64_t ks = widen17(subb[j], X, hh, xi, sxok, r);
+            const bool ok2 = lane < 33 && (xs + 16 < W - 8) && (ys + d2 - 16 >= 0) && (ys + d2 - 16 < H - 8);
+            const uint64_t k2 = ok2 ? me_key(sub2[j], (uint32_t)(16 + (d2 < 16 ? 16 - d2 : d2 - 16)),
+                                             (uint32_t)r, (uint32_t)(32 * 33 + d2))
+                                    : kNoKey;
+            ks = k2 < ks ? k2 : ks;
+            ks = wave_min_u64(ks);
+            if (lane == 0 && ks < keys[nblk + 4 * u + j]) keys[nblk + 4 * u + j] = ks;
+        }
+    }
+}
+
 template <int BS, bool SUB>
 __global__ void __launch_bounds__((MeWGeo<BS, SUB>::NTHREADS)) __attribute__((amdgpu_waves_per_eu(SUB ? 4 : 8)))
 me_wave_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
@@ -205,136 +347,7 @@ me_wave_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
             const int bxl = u % TBX, byl = u / TBX;
             if (bx0 + bxl >= nbx || byt0 + byl >= by1) continue;   // wave-uniform
             const int x = x0 + bxl * BS, y = y0 + byl * BS;
-            // lane identity re-derived per block through an opaque asm: otherwise LICM hoists
-            // the ~17 per-lane (16*hh + t) edge constants out of this loop and spills them
-            int lane = tid & 63;
-            asm volatile("" : "+v"(lane));
-            const int xi = lane & 31, hh = lane >> 5;
-            const uint32_t X = hh ? 0u : 31u;
-            // phase-1 lane: window column bxl*BS + xi (dx = xi - 16) in copy xi & 3
-            const int q1 = (xi & 3) * CS + (byl * BS + 16 * hh) * RPD + ((bxl * BS + xi) >> 2);
-            // phase-2 lane: dx = +16 (column bxl*BS + 32, copy 0), dy index = lane (< 33)
-            const int d2 = lane < 33 ? lane : 32;
-            const int q2 = (byl * BS + d2) * RPD + ((bxl * BS + 32) >> 2);
-            uint32_t accL[NT], accR[NT], S[NT];
-            uint32_t a2L[NPASS], a2R[NPASS];
-#pragma unroll
-            for (int t = 0; t < NT; ++t) S[t] = 0;
-            uint32_t subb[4];          // VBS: lane best 32-bit key per quadrant (phase 1)
-            uint32_t sub2[4];          // VBS: phase-2 quadrant SADs
-#pragma unroll
-            for (int pass = 0; pass < NPASS; ++pass) {
-                // the row index goes through an opaque asm so this pass's scalar loads cannot
-                // be hoisted above the previous pass (constant-space loads are otherwise free
-                // to move, and two passes of pixels overflow the SGPRs)
-                int ycur = y + pass * HALF;
-                asm volatile("" : "+s"(ycur));
-                uint32_t cr[HALF][NDW];
-                load_cur_sgpr<HALF, NDW>(cur, W, x, ycur, cr);
-                if (SUB || pass == 0) {   // without VBS accL accumulates the whole block
-#pragma unroll
-                    for (int t = 0; t < NT; ++t) { accL[t] = 0; accR[t] = 0; }
-                }
-                // phase 1: rows pass*8 + jj of the lane's 24-row strip
-                // volatile: the four dwords stay four ds_read_b32 -- merged into one b128 they
-                // are 4-byte but not 16-byte aligned and the LDS replays them (Guideline 17)
-                int qo = q1 + pass * HALF * RPD;       // dword offsets into win[] keep the LDS
-                asm volatile("" : "+v"(qo));           // address space through the opaque asm
-                lds_vu32p qp = (lds_vu32p)(win + qo);
-                uint32_t wc[NDW], wn[NDW];
-#pragma unroll
-                for (int k = 0; k < NDW; ++k) wc[k] = qp[k];
-#pragma unroll
-                for (int jj = 0; jj < NR; ++jj) {
-                    if (jj + 1 < NR) {
-#pragma unroll
-                        for (int k = 0; k < NDW; ++k) wn[k] = qp[(jj + 1) * RPD + k];
-                    }
-#pragma unroll
-                    for (int t = 0; t < NT; ++t) {
-                        const int rr = jj - t;
-                        if (rr >= 0 && rr < HALF) {
-#pragma unroll
-                            for (int k = 0; k < NDW; ++k) {
-                                if (SUB && k >= NDW / 2) accR[t] = __builtin_amdgcn_sad_u8(cr[rr][k], wc[k], accR[t]);
-                                else accL[t] = __builtin_amdgcn_sad_u8(cr[rr][k], wc[k], accL[t]);
-                            }
-                        }
-                    }
-#pragma unroll
-                    for (int k = 0; k < NDW; ++k) wc[k] = wn[k];
-                    acc_fence_n<NT>(accL);
-                    if constexpr (SUB) acc_fence_n<NT>(accR);
-                }
-                // phase 2: the dx = +16 candidate of dy index d2, rows pass*8 .. +8
-                uint32_t l2 = 0, r2 = 0;
-                int q2o = q2 + pass * HALF * RPD;
-                asm volatile("" : "+v"(q2o));   // phase-2 reads stay after phase 1
-                lds_vu32p q2p = (lds_vu32p)(win + q2o);
-#pragma unroll
-                for (int rr = 0; rr < HALF; ++rr) {
-                    lds_vu32p w2 = q2p + rr * RPD;
-#pragma unroll
-                    for (int k = 0; k < NDW; ++k) {
-                        if (SUB && k >= NDW / 2) r2 = __builtin_amdgcn_sad_u8(cr[rr][k], w2[k], r2);
-                        else l2 = __builtin_amdgcn_sad_u8(cr[rr][k], w2[k], l2);
-                    }
-                    asm volatile("" : "+v"(l2), "+v"(r2) : : "memory");   // one row in flight
-                }
-                a2L[pass] = l2;
-                a2R[pass] = r2;
-                if constexpr (SUB) {
-                    // quadrants (pass 0: TL, TR; pass 1: BL, BR) -- per-lane bests now, the
-                    // accumulators are reused by the next pass
-                    const int ys = y + pass * HALF;
-                    int dlo = SR - ys;               dlo = dlo < 0 ? 0 : dlo;
-                    int dhi = H - 8 - ys + SR - 1; dhi = dhi > 32 ? 32 : dhi;
-                    const bool edge = dlo > 0 || dhi < 32;
-                    subb[2 * pass] = lane_best17(accL, X, hh, dlo, dhi, edge);
-                    subb[2 * pass + 1] = lane_best17(accR, X, hh, dlo, dhi, edge);
-                    sub2[2 * pass] = l2;
-                    sub2[2 * pass + 1] = r2;
-#pragma unroll
-                    for (int t = 0; t < NT; ++t) S[t] += accL[t] + accR[t];
-                }
-            }
-            if constexpr (!SUB) {
-#pragma unroll
-                for (int t = 0; t < NT; ++t) S[t] = accL[t];
-            }
-            // block keys: phase 1 (lane's 17 candidates) and phase 2 (dx = +16)
-            int dlo = SR - y;            dlo = dlo < 0 ? 0 : dlo;
-            int dhi = H - BS - y + SR - 1; dhi = dhi > 32 ? 32 : dhi;
-            const bool edge = dlo > 0 || dhi < 32;
-            const bool xok = (x + xi - 16 >= 0) && (x + xi - 16 < W - BS);
-            uint64_t k = widen17(lane_best17(S, X, hh, dlo, dhi, edge), X, hh, xi, xok, r);
-            {
-                uint32_t s2 = 0;
-#pragma unroll
-                for (int pass = 0; pass < NPASS; ++pass) s2 += a2L[pass] + a2R[pass];
-                const bool ok2 = lane < 33 && (x + 16 < W - BS) && d2 >= dlo && d2 <= dhi;
-                const uint64_t k2 = ok2 ? me_key(s2, (uint32_t)(16 + (d2 < 16 ? 16 - d2 : d2 - 16)), (uint32_t)r,
-                                                 (uint32_t)(32 * 33 + d2))
-                                        : kNoKey;
-                k = k2 < k ? k2 : k;
-            }
-            k = wave_min_u64(k);
-            if (lane == 0 && k < keys[u]) keys[u] = k;
-            if constexpr (SUB) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int xs = x + (j & 1) * 8, ys = y + (j >> 1) * 8;
-                    const bool sxok = (xs + xi - 16 >= 0) && (xs + xi - 16 < W - 8);
-                    uint64_t ks = widen17(subb[j], X, hh, xi, sxok, r);
-                    const bool ok2 = lane < 33 && (xs + 16 < W - 8) && (ys + d2 - 16 >= 0) && (ys + d2 - 16 < H - 8);
-                    const uint64_t k2 = ok2 ? me_key(sub2[j], (uint32_t)(16 + (d2 < 16 ? 16 - d2 : d2 - 16)),
-                                                     (uint32_t)r, (uint32_t)(32 * 33 + d2))
-                                            : kNoKey;
-                    ks = k2 < ks ? k2 : ks;
-                    ks = wave_min_u64(ks);
-                    if (lane == 0 && ks < keys[G::NBLK + 4 * u + j]) keys[G::NBLK + 4 * u + j] = ks;
-                }
-            }
+            wave_dense_block<BS, SUB, RPD, CS>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u, tid, r);
         }
     }
     __syncthreads();
@@ -345,6 +358,306 @@ me_wave_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
         const size_t b = (size_t)(gby - by0) * nbx + gbx;
         if (i < G::NBLK) decode_key(keys[i], SR, out_best + b * 4);
         else decode_key(keys[i], SR, out_sub + (b * 4 + ((i - G::NBLK) & 3)) * 4);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// SEA path (default for bs 16 without VBS): exact successive elimination.
+//
+// With S = a 4x4 pixel sum (0..4080) and q = S >> 4 (a byte), write S = 16q + r, r < 16.
+// Then |S_cur - S_ref| >= 16|q_cur - q_ref| - 15, so for a candidate c
+//     SAD(c) >= sum_k |S_cur(k) - S_ref(c, k)| >= 16 * LBq(c) - 240,
+//     LBq(c) = sum over the 16 4x4 sub-blocks k of |q_cur(k) - q_ref(c, k)|
+// (triangle inequality).  Per block:
+//   1. LBq for all 1089 candidates: lane (xi, hh) as in the dense phase 1 (17 dy each, plus
+//      the dx = +16 column on lanes 0..32); a candidate's four byte sums of one 4x4 row are
+//      one dword, so LBq costs 4 v_sad_u8 per candidate instead of 64 for its SAD;
+//   2. U = the full SAD of the valid candidate with the smallest LBq, so U >= min SAD;
+//   3. every valid candidate with 16 * LBq - 240 <= U gets its full SAD (survivors,
+//      compacted into an LDS list).  Any other candidate has SAD > U >= min SAD, so it can
+//      neither be the minimum nor tie it: the lexicographic key result is exactly the full
+//      search's.  More than CAP survivors (weak bounds: flat or noise-like content) falls
+//      back to the dense wave search of the block.
+// The reference's byte sums (B4) are built per tile in LDS from the shifted window copies
+// (one v_sad_u8 against 0 per row dword, sliding down each column), in a column layout
+// L(c) = (c&3)*40 + (c>>2) bytes that puts the sums at c, c+4, c+8, c+12 -- one 4x4 row of a
+// candidate -- in consecutive bytes.
+// ---------------------------------------------------------------------------------------
+struct SeaGeo {
+    static constexpr int BS = 16, SR = 16, NT = 17;
+    static constexpr int TBX = 8, TPY = 32, TBY = 2, TPX = 128;
+    static constexpr int WR = TPY + 2 * SR;               // 64 window rows
+    static constexpr int RPD = (TPX + 2 * SR) / 4;        // 40 dwords per copy row
+    static constexpr int CSTRIDE = WR * RPD + 8;           // = 8 (mod 32): see MeWGeo
+    static constexpr int B4R = WR - 3, B4C = TPX + 2 * SR - 3, B4P = 160;   // 61 x 157 byte sums (+4 pad)
+    static constexpr int NBLK = TBX * TBY;
+    static constexpr int NW = 8, NTHREADS = NW * 64;
+    static constexpr int CAP = 192;                       // survivors per block before fallback
+};
+
+
+SO_DEV uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint32_t o = __shfl_xor(v, m, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+SO_DEV uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+
+SO_DEV uint32_t lane_prefix(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__global__ void __launch_bounds__(SeaGeo::NTHREADS) __attribute__((amdgpu_waves_per_eu(4)))
+me_sea_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
+              int32_t* __restrict__ out_best) {
+    using G = SeaGeo;
+    constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RPD = G::RPD, CS = G::CSTRIDE, NT = G::NT;
+    constexpr int B4P = G::B4P, CAP = G::CAP, CP = G::TPX;
+    __shared__ uint32_t win[4 * CS];
+    __shared__ uint32_t b4w[(G::B4R * B4P + 4) / 4];
+    uint8_t* b4 = reinterpret_cast<uint8_t*>(b4w);
+    __shared__ uint32_t curt[G::TPY * CP / 4];      // current tile, 32 rows x 128 B
+    __shared__ uint32_t a4[G::NBLK * 4];           // per block: [j] = 4 byte sums (4x4 >> 4) of row j
+    __shared__ uint16_t list[G::NW * CAP];
+    __shared__ unsigned long long keys[G::NBLK];
+
+    const int nbx = W / 16;
+    const int tiles_x = (nbx + TBX - 1) / TBX;
+    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    const int bx0 = tx * TBX, byt0 = by0 + ty * TBY;
+    const int x0 = bx0 * 16, y0 = byt0 * 16;
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    for (int i = tid; i < G::NBLK; i += G::NTHREADS) keys[i] = kNoKey;
+    // current tile (zero outside the frame / stripe)
+    for (int i = tid; i < G::TPY * CP / 4; i += G::NTHREADS) {
+        const int rr = i / (CP / 4), m = i - rr * (CP / 4);
+        const int gy = y0 + rr, gx = x0 + 4 * m;
+        uint32_t v = 0;
+        if (gy < H && gx + 4 <= W) v = *reinterpret_cast<const uint32_t*>(cur + (size_t)gy * W + gx);
+        curt[i] = v;
+    }
+    __syncthreads();
+    // current blocks' 4x4 byte sums: item (block, j, ii) -> byte ii of a4[blk*4 + j]
+    for (int i = tid; i < G::NBLK * 16; i += G::NTHREADS) {
+        const int blk = i >> 4, j = (i >> 2) & 3, ii = i & 3;
+        const int rr = (blk / TBX) * 16 + 4 * j, m = (blk % TBX) * 4 + ii;
+        uint32_t sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sum = __builtin_amdgcn_sad_u8(curt[(rr + q) * (CP / 4) + m], 0u, sum);
+        reinterpret_cast<uint8_t*>(a4)[i] = (uint8_t)(sum >> 4);
+    }
+    for (int r = 0; r < nref; ++r) {
+        const uint8_t* ref = refs.p[r];
+        __syncthreads();
+        for (int i = tid; i < G::WR * RPD; i += G::NTHREADS) {
+            const int wr = i / RPD, m = i - wr * RPD;
+            const int gy = y0 - SR + wr, gx = x0 - SR + 4 * m;
+            uint32_t a = 0, b = 0;
+            if (gy >= 0 && gy < H) {
+                const uint8_t* rp = ref + (size_t)gy * W;
+                if (gx >= 0 && gx + 4 <= W) a = *reinterpret_cast<const uint32_t*>(rp + gx);
+                if (gx + 4 >= 0 && gx + 8 <= W) b = *reinterpret_cast<const uint32_t*>(rp + gx + 4);
+            }
+            uint32_t* d = win + wr * RPD + m;
+            d[0] = a;
+            d[CS] = __builtin_amdgcn_alignbyte(b, a, 1);
+            d[2 * CS] = __builtin_amdgcn_alignbyte(b, a, 2);
+            d[3 * CS] = __builtin_amdgcn_alignbyte(b, a, 3);
+        }
+        __syncthreads();
+        // B4(r, c): thread per (column, quarter of the rows) slides a 4-row sum of the
+        // horizontal 4-sums (one v_sad_u8 against 0 each) down its column
+        for (int i = tid; i < G::B4C * 4; i += G::NTHREADS) {
+            const int qtr = i / G::B4C, c = i - qtr * G::B4C;   // consecutive lanes: consecutive columns
+            const int r0 = qtr * 16, r1 = qtr == 3 ? G::B4R : r0 + 16;   // output rows [r0, r1)
+            const uint32_t* q = win + (c & 3) * CS + (c >> 2);
+            uint8_t* o = b4 + (c & 3) * 40 + (c >> 2);
+            uint32_t h0 = __builtin_amdgcn_sad_u8(q[r0 * RPD], 0u, 0u);
+            uint32_t h1 = __builtin_amdgcn_sad_u8(q[(r0 + 1) * RPD], 0u, 0u);
+            uint32_t h2 = __builtin_amdgcn_sad_u8(q[(r0 + 2) * RPD], 0u, 0u);
+            for (int rr = r0; rr < r1; ++rr) {
+                const uint32_t h3 = __builtin_amdgcn_sad_u8(q[(rr + 3) * RPD], 0u, 0u);
+                o[rr * B4P] = (uint8_t)((h0 + h1 + h2 + h3) >> 4);
+                h0 = h1; h1 = h2; h2 = h3;
+            }
+        }
+        __syncthreads();
+#pragma unroll 1
+        for (int u = wave; u < G::NBLK; u += G::NW) {
+            const int bxl = u % TBX, byl = u / TBX;
+            if (bx0 + bxl >= nbx || byt0 + byl >= by1) continue;   // wave-uniform
+            const int x = x0 + bxl * 16, y = y0 + byl * 16;
+            int lane = tid & 63;
+            asm volatile("" : "+v"(lane));
+            const int xi = lane & 31, hh = lane >> 5;
+            const int d2 = lane < 33 ? lane : 32;
+            uint32_t A[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) A[j] = a4[u * 4 + j];
+            // ---- 1. lower bounds ------------------------------------------------------------
+            const int cB = bxl * 16 + xi;
+            const int lb0 = (byl * 16 + 16 * hh) * B4P + (cB & 3) * 40 + (cB >> 2);   // byte offset
+            const uint32_t bsh = (uint32_t)lb0 & 3;
+            int lo1 = lb0 >> 2;
+            asm volatile("" : "+v"(lo1));
+            lds_vu32p p1 = (lds_vu32p)(b4w + lo1);
+            uint32_t lb[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) lb[t] = 0;
+#pragma unroll
+            for (int sr_ = 0; sr_ < NT + 12; ++sr_) {       // byte-sum rows of the lane's strip
+                const uint32_t w0 = p1[sr_ * (B4P / 4)], w1 = p1[sr_ * (B4P / 4) + 1];
+                const uint32_t P = __builtin_amdgcn_alignbyte(w1, w0, bsh);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int t = sr_ - 4 * j;
+                    if (t >= 0 && t < NT) lb[t] = __builtin_amdgcn_sad_u8(A[j], P, lb[t]);
+                }
+                acc_fence_n<NT>(lb);
+            }
+            uint32_t lb2 = 0;
+            {
+                // column c2 = bxl*16 + 32 = 0 (mod 4): its byte sums start dword-aligned
+                int lo2 = ((byl * 16 + d2) * B4P + ((bxl * 16 + 32) >> 2)) >> 2;
+                asm volatile("" : "+v"(lo2));
+                lds_vu32p p2 = (lds_vu32p)(b4w + lo2);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) lb2 = __builtin_amdgcn_sad_u8(A[j], p2[4 * j * (B4P / 4)], lb2);
+            }
+            // validity: dy index in [dlo, dhi], dx by lane; interior blocks need no masks
+            int dlo = SR - y;              dlo = dlo < 0 ? 0 : dlo;
+            int dhi = H - 16 - y + SR - 1; dhi = dhi > 32 ? 32 : dhi;
+            const bool xok = (x + xi - 16 >= 0) && (x + xi - 16 < W - 16);
+            const bool ok2 = lane < 33 && (x + 16 < W - 16) && d2 >= dlo && d2 <= dhi;
+            const bool edge = dlo > 0 || dhi < 32;
+            // ---- 2. U = SAD of the smallest-LB candidate ------------------------------------
+            uint32_t kt = 0xFFFFFFFFu;                         // (lb << 5 | t), lane-local
+            if (!edge) {
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    const uint32_t k = (lb[t] << 5) | (uint32_t)t;
+                    kt = k < kt ? k : kt;
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    const int di = 16 * hh + t;
+                    const uint32_t k = (di < dlo || di > dhi) ? 0xFFFFFFFFu : ((lb[t] << 5) | (uint32_t)t);
+                    kt = k < kt ? k : kt;
+                }
+            }
+            uint32_t kl = (xok && kt != 0xFFFFFFFFu) ? ((kt >> 5) << 11) | (uint32_t)(xi * 33 + 16 * hh + (kt & 31))
+                                                      : 0xFFFFFFFFu;
+            {
+                const uint32_t k2 = (lb2 << 11) | (uint32_t)(32 * 33 + d2);
+                kl = (ok2 && k2 < kl) ? k2 : kl;
+            }
+            const uint32_t kmin = __builtin_amdgcn_readfirstlane(wave_min_u32(kl));
+            if (kmin == 0xFFFFFFFFu) continue;                 // no valid candidate: key stays none
+            const int cs = (int)(kmin & 2047), cdx = cs / 33, cdi = cs - cdx * 33;
+            const int crow0 = byl * 16 * (CP / 4) + bxl * 4;   // current block in curt (dwords)
+            uint32_t U;
+            {
+                const int row = lane >> 2, kk = lane & 3;
+                const int col = bxl * 16 + cdx;
+                const uint32_t w = ((lds_vu32p)win)[(col & 3) * CS + (byl * 16 + cdi + row) * RPD + (col >> 2) + kk];
+                const uint32_t c = curt[crow0 + row * (CP / 4) + kk];
+                U = __builtin_amdgcn_readfirstlane(wave_sum_u32(__builtin_amdgcn_sad_u8(c, w, 0u)));
+            }
+            // ---- 3. survivors: 16 LBq - 240 <= U (per-t ballots; empty ones cost one v_cmp) --
+            const uint32_t qU = (U + 240) >> 4;
+            uint32_t nsur = 0;
+            uint16_t* mylist = list + wave * CAP;
+#pragma unroll
+            for (int t = 0; t <= NT; ++t) {
+                bool sv;
+                int cand;
+                if (t < NT) {
+                    const int di = 16 * hh + t;
+                    sv = xok && lb[t] <= qU && (!edge || (di >= dlo && di <= dhi));
+                    cand = xi * 33 + di;
+                } else {
+                    sv = ok2 && lb2 <= qU;
+                    cand = 32 * 33 + d2;
+                }
+                const uint64_t bal = __ballot(sv);
+                if (bal) {                                     // wave-uniform
+                    const uint32_t pos = nsur + lane_prefix(bal);
+                    if (sv && pos < (uint32_t)CAP) mylist[pos] = (uint16_t)cand;
+                    nsur += (uint32_t)__builtin_popcountll(bal);
+                }
+            }
+            if (nsur > (uint32_t)CAP) {
+                wave_dense_block<16, false, RPD, CS>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u, tid, r);
+                continue;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint64_t best = kNoKey;
+            if (nsur <= 4) {
+                // 16 lanes per survivor, one row each
+                const int sidx = lane >> 4, row = lane & 15;
+                const bool act = (uint32_t)sidx < nsur;
+                const int cand = act ? (int)mylist[sidx] : cs;
+                const int dxi = cand / 33, di = cand - dxi * 33;
+                const int col = bxl * 16 + dxi;
+                int wo = (col & 3) * CS + (byl * 16 + di + row) * RPD + (col >> 2);
+                asm volatile("" : "+v"(wo));
+                lds_vu32p wr_ = (lds_vu32p)(win + wo);       // 4-byte aligned only: keep b32 reads
+                const uint32_t* cr_ = curt + crow0 + row * (CP / 4);
+                uint32_t sad = 0;
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) sad = __builtin_amdgcn_sad_u8(cr_[kk], wr_[kk], sad);
+#pragma unroll
+                for (int m = 8; m >= 1; m >>= 1) sad += __shfl_xor(sad, m, 64);
+                const int dx = dxi - 16, dy = di - 16;
+                const uint64_t key = me_key(sad, (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)), (uint32_t)r,
+                                            (uint32_t)cand);
+                best = act ? key : kNoKey;
+            } else {
+#pragma unroll 1
+                for (uint32_t k0 = 0; k0 < nsur; k0 += 64) {
+                    const uint32_t idx = k0 + (uint32_t)lane;
+                    const int cand = idx < nsur ? (int)mylist[idx] : cs;
+                    const int dxi = cand / 33, di = cand - dxi * 33;
+                    const int col = bxl * 16 + dxi;
+                    int wo = (col & 3) * CS + (byl * 16 + di) * RPD + (col >> 2);
+                    asm volatile("" : "+v"(wo));
+                    lds_vu32p wp = (lds_vu32p)(win + wo);
+                    uint32_t sad = 0;
+#pragma unroll
+                    for (int rr = 0; rr < 16; ++rr) {
+#pragma unroll
+                        for (int kk = 0; kk < 4; ++kk)
+                            sad = __builtin_amdgcn_sad_u8(curt[crow0 + rr * (CP / 4) + kk], wp[rr * RPD + kk], sad);
+                        asm volatile("" : "+v"(sad) : : "memory");
+                    }
+                    const int dx = dxi - 16, dy = di - 16;
+                    const uint64_t key = me_key(sad, (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)),
+                                                (uint32_t)r, (uint32_t)cand);
+                    best = (idx < nsur && key < best) ? key : best;
+                }
+            }
+            best = wave_min_u64(best);
+            if (lane == 0 && best < keys[u]) keys[u] = best;
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < G::NBLK; i += G::NTHREADS) {
+        const int gbx = bx0 + i % TBX, gby = byt0 + i / TBX;
+        if (gbx >= nbx || gby >= by1) continue;
+        decode_key(keys[i], SR, out_best + ((size_t)(gby - by0) * nbx + gbx) * 4);
     }
 }
 
@@ -536,8 +849,16 @@ int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, in
     if (nrows <= 0) return SO_OK;
     if (sr == 16 && (bs == 16 || bs == 8) && (out_sub == nullptr || bs == 16)) {
         // SO_ME_IMPL=fast (A/B only, tools/me_ab.py) selects the round-1 kernel
+        // SO_ME_IMPL=dense selects the dense wave kernel where SEA would run (A/B, bench)
         const char* impl = getenv("SO_ME_IMPL");
         const bool use_fast = impl && strcmp(impl, "fast") == 0;
+        const bool use_dense = impl && strcmp(impl, "dense") == 0;
+        if (!use_fast && !use_dense && bs == 16 && out_sub == nullptr) {
+            const dim3 sgrid(((nbx + SeaGeo::TBX - 1) / SeaGeo::TBX) * ((nrows + SeaGeo::TBY - 1) / SeaGeo::TBY));
+            hipLaunchKernelGGL(me_sea_kernel, sgrid, dim3(SeaGeo::NTHREADS), 0, st, cur, refs, nref, H, W, by0, by1,
+                               out_best);
+            return check_launch("me_sea_kernel");
+        }
         const int tb = bs == 16 ? MeGeo<16>::TB : MeGeo<8>::TB;
         const dim3 grid(((nbx + tb - 1) / tb) * ((nrows + tb - 1) / tb)), blk(MeGeo<16>::NTHREADS);
         if (!use_fast) {

@@ -335,3 +335,34 @@ def test_stripe_gop_encoder_single_rank(gpu):
         assert sa.frame_type == sb.frame_type
         for k in ("split", "mv", "qtc", "tokens", "mae_num", "recon"):
             assert torch.equal(getattr(sa, k), getattr(sb, k)), k
+
+
+# ---------------------------------------------------------------- ME search paths (SEA / dense fallback)
+@pytest.mark.parametrize("kind", ["flat", "noise", "synth", "tie", "ramp"])
+def test_me_paths_vs_oracle(gpu, kind):
+    """The default bs-16 ME prunes candidates by 4x4-sum lower bounds (me_sea_kernel) and falls
+    back to the dense search when too many survive.  Flat frames make every candidate survive
+    (fallback), noise gives weak bounds, tie-heavy and ramp content stress the tie-break.
+    Every block's (dx, dy, ref, SAD) must equal the oracle's exhaustive search."""
+    from oracle import oracle as O
+    from streamoptima_amd.synth import synth_sequence, tie_heavy_sequence
+    h, w = 96, 160
+    rng = np.random.default_rng(7)
+    if kind == "flat":
+        seq = np.full((2, h, w), 77, np.uint8)
+    elif kind == "noise":
+        seq = rng.integers(0, 256, size=(2, h, w), dtype=np.uint8)
+    elif kind == "ramp":
+        yy, xx = np.mgrid[0:h, 0:w]
+        base = ((xx * 3 + yy * 5) % 256).astype(np.uint8)
+        seq = np.stack([base, np.roll(base, (2, -3), axis=(0, 1))])
+    elif kind == "tie":
+        seq = tie_heavy_sequence(2, h, w, 3)
+    else:
+        seq = synth_sequence(2, h, w, 5)
+    best, _ = _me(seq[1], [seq[0]], 16, 16, gpu)
+    nbx = w // 16
+    for b in range(best.shape[0]):
+        x, y = (b % nbx) * 16, (b // nbx) * 16
+        exp = O.me_block(seq[1], [seq[0]], x, y, 16, 16)
+        assert tuple(int(v) for v in best[b]) == exp, (kind, b, tuple(best[b]), exp)
