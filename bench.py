@@ -98,8 +98,13 @@ def max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
-def me_kernel_name() -> str:
-    return "me_fast_kernel" if os.environ.get("SO_ME_IMPL") == "fast" else "me_wave_kernel"
+def me_kernel_name(vbs: bool) -> str:
+    impl = os.environ.get("SO_ME_IMPL")
+    if impl == "fast":
+        return "me_fast_kernel"
+    if impl == "dense" or vbs:
+        return "me_wave_kernel<16, %s>" % ("true" if vbs else "false")
+    return "me_sea_kernel"
 
 
 def kernel_roofline(codec, frames_dev, reps: int) -> dict:
@@ -126,8 +131,19 @@ def kernel_roofline(codec, frames_dev, reps: int) -> dict:
                                          sym.qtc.data_ptr(), sym.tokens.data_ptr(), sym.mae_num.data_ptr(),
                                          sym.recon.data_ptr(), sym.sse.data_ptr(), st), "tq")
 
+    def me_dense():
+        old = os.environ.get("SO_ME_IMPL")
+        os.environ["SO_ME_IMPL"] = "dense"
+        try:
+            me()
+        finally:
+            if old is None:
+                os.environ.pop("SO_ME_IMPL")
+            else:
+                os.environ["SO_ME_IMPL"] = old
+
     out = {}
-    for name, fn in (("me", me), ("tq", tq)):
+    for name, fn in (("me", me), ("tq", tq), ("me_dense", me_dense)):
         for _ in range(3):
             fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -152,7 +168,7 @@ def kernel_roofline(codec, frames_dev, reps: int) -> dict:
     cands = int(vx.sum()) * int(vy.sum())
     me_bytes = 2 * h * w + 16 * nb
     tq_bytes = 5 * h * w + 8 * nb          # cur + pred + recon + QTC int16 + symbols
-    return {"me_s": out["me"], "tq_s": out["tq"], "me_bytes": me_bytes, "tq_bytes": tq_bytes,
+    return {"me_s": out["me"], "tq_s": out["tq"], "me_dense_s": out["me_dense"], "me_bytes": me_bytes, "tq_bytes": tq_bytes,
             "sad_ops": cands * bs * bs, "cands": cands, "d": d}
 
 
@@ -300,14 +316,20 @@ def main():
                    "search_range": 16, "qp": cfg["qp"], "vbs": bool(args.vbs), "nRefFrames": 1,
                    "transform": "fp64 pocketfft-exact DCT",
                    "parallelism": f"stripe x{world} (all_gather recon per frame)" if stripe else f"gop-per-rank x{world}"},
-        "roofline": {"bound": "hbm", "kernel": me_kernel_name(), "achieved": round(me_gbs, 2),
+        "roofline": {"bound": "hbm", "kernel": me_kernel_name(args.vbs), "achieved": round(me_gbs, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(me_gbs / HBM_PEAK_GBS, 5),
                      "traffic": traffic, "algorithmic_bytes": rl["me_bytes"],
                      "launch_us": round(rl["me_s"] * 1e6, 2),
-                     "valu_sad": {"achieved_ops": rl["sad_ops"] / rl["me_s"], "peak_ops": SAD_PEAK_OPS,
+                     # dense-equivalent |diff| rate: the exhaustive search's candidates x 256 per
+                     # launch time.  me_sea_kernel prunes exactly, so it can exceed
+                     # the v_sad_u8 issue peak; dense_me is the unpruned kernel on the same frame.
+                     "valu_sad": {"dense_equivalent_ops": rl["sad_ops"] / rl["me_s"], "peak_ops": SAD_PEAK_OPS,
                                   "frac": round(rl["sad_ops"] / rl["me_s"] / SAD_PEAK_OPS, 4),
                                   "measured_peak_ops": SAD_MEASURED_OPS,
                                   "candidates": rl["cands"]},
+                     "dense_me": {"kernel": "me_wave_kernel<16, %s>" % ("true" if args.vbs else "false"),
+                                  "launch_us": round(rl["me_dense_s"] * 1e6, 2),
+                                  "valu_sad_frac": round(rl["sad_ops"] / rl["me_dense_s"] / SAD_PEAK_OPS, 4)},
                      "tq_kernel": {"launch_us": round(rl["tq_s"] * 1e6, 2),
                                    "achieved_gbs": round(rl["tq_bytes"] / rl["tq_s"] / 1e9, 2)}},
         "cpu_baseline": cpu,

@@ -111,15 +111,7 @@ SO_DEV void load_cur_sgpr(const uint8_t* __restrict__ cur, int W, int x, int y, 
     }
 }
 
-SO_DEV uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        const uint32_t lo = __shfl_xor((uint32_t)v, m, 64), hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
-        const uint64_t o = ((uint64_t)hi << 32) | lo;
-        v = o < v ? o : v;
-    }
-    return v;
-}
+SO_DEV uint64_t wave_min_u64(uint64_t v);   // DPP version below (wave_min_u64_dpp)
 
 template <int N>
 SO_DEV void acc_fence_n(uint32_t (&a)[N]) {
@@ -396,20 +388,70 @@ struct SeaGeo {
 };
 
 
-SO_DEV uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        const uint32_t o = __shfl_xor(v, m, 64);
-        v = o < v ? o : v;
-    }
+// Cross-lane reductions with DPP (register-to-register VALU; no ds_bpermute round trips):
+// quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror leave every lane with its
+// 16-lane row's result; row_bcast15 (rows 1, 3) and row_bcast31 (rows 2, 3) carry it into
+// lane 63, which v_readlane broadcasts.  DPP lanes without a source keep `old`.
+constexpr int kDppQuad1032 = 0xB1, kDppQuad2301 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+constexpr int kDppBcast15 = 0x142, kDppBcast31 = 0x143;
+
+SO_DEV uint32_t row_min_u32(uint32_t v) {
+    uint32_t o;
+    o = __builtin_amdgcn_update_dpp(v, v, kDppQuad1032, 0xF, 0xF, false); v = o < v ? o : v;
+    o = __builtin_amdgcn_update_dpp(v, v, kDppQuad2301, 0xF, 0xF, false); v = o < v ? o : v;
+    o = __builtin_amdgcn_update_dpp(v, v, kDppHalfMirror, 0xF, 0xF, false); v = o < v ? o : v;
+    o = __builtin_amdgcn_update_dpp(v, v, kDppMirror, 0xF, 0xF, false); v = o < v ? o : v;
     return v;
 }
 
-SO_DEV uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+// wave-uniform minimum (SGPR)
+SO_DEV uint32_t wave_min_u32(uint32_t v) {
+    v = row_min_u32(v);
+    uint32_t o;
+    o = __builtin_amdgcn_update_dpp(v, v, kDppBcast15, 0xA, 0xF, false); v = o < v ? o : v;
+    o = __builtin_amdgcn_update_dpp(v, v, kDppBcast31, 0xC, 0xF, false); v = o < v ? o : v;
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+// sum over each 16-lane row, in every lane of the row
+SO_DEV uint32_t row_sum_u32(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, kDppQuad1032, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, kDppQuad2301, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, kDppHalfMirror, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, kDppMirror, 0xF, 0xF, false);
     return v;
 }
+
+// wave-uniform sum (SGPR)
+SO_DEV uint32_t wave_sum_u32(uint32_t v) {
+    v = row_sum_u32(v);
+    v += __builtin_amdgcn_update_dpp(0u, v, kDppBcast15, 0xA, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, kDppBcast31, 0xC, 0xF, false);
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+template <int CTRL, int RMASK>
+SO_DEV uint64_t dpp_min_step(uint64_t v) {
+    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    const uint32_t olo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, RMASK, 0xF, false);
+    const uint32_t ohi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, RMASK, 0xF, false);
+    const uint64_t o = ((uint64_t)ohi << 32) | olo;
+    return o < v ? o : v;
+}
+
+// wave-uniform 64-bit minimum
+SO_DEV uint64_t wave_min_u64_dpp(uint64_t v) {
+    v = dpp_min_step<kDppQuad1032, 0xF>(v);
+    v = dpp_min_step<kDppQuad2301, 0xF>(v);
+    v = dpp_min_step<kDppHalfMirror, 0xF>(v);
+    v = dpp_min_step<kDppMirror, 0xF>(v);
+    v = dpp_min_step<kDppBcast15, 0xA>(v);
+    v = dpp_min_step<kDppBcast31, 0xC>(v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, 63), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), 63);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+SO_DEV uint64_t wave_min_u64(uint64_t v) { return wave_min_u64_dpp(v); }
 
 SO_DEV uint32_t lane_prefix(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
@@ -514,9 +556,11 @@ me_sea_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int
             uint32_t lb[NT];
 #pragma unroll
             for (int t = 0; t < NT; ++t) lb[t] = 0;
+            uint32_t n0 = p1[0], n1 = p1[1];
 #pragma unroll
             for (int sr_ = 0; sr_ < NT + 12; ++sr_) {       // byte-sum rows of the lane's strip
-                const uint32_t w0 = p1[sr_ * (B4P / 4)], w1 = p1[sr_ * (B4P / 4) + 1];
+                const uint32_t w0 = n0, w1 = n1;
+                if (sr_ + 1 < NT + 12) { n0 = p1[(sr_ + 1) * (B4P / 4)]; n1 = p1[(sr_ + 1) * (B4P / 4) + 1]; }
                 const uint32_t P = __builtin_amdgcn_alignbyte(w1, w0, bsh);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -534,35 +578,32 @@ me_sea_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int
 #pragma unroll
                 for (int j = 0; j < 4; ++j) lb2 = __builtin_amdgcn_sad_u8(A[j], p2[4 * j * (B4P / 4)], lb2);
             }
-            // validity: dy index in [dlo, dhi], dx by lane; interior blocks need no masks
+            // validity: dy index in [dlo, dhi], dx by lane.  Edge blocks (uniform) overwrite the
+            // bounds of out-of-frame dy with kBig once; everything below is mask-free.
+            constexpr uint32_t kBig = 0x07FFFFFFu;            // (kBig << 5) | t never wraps
             int dlo = SR - y;              dlo = dlo < 0 ? 0 : dlo;
             int dhi = H - 16 - y + SR - 1; dhi = dhi > 32 ? 32 : dhi;
             const bool xok = (x + xi - 16 >= 0) && (x + xi - 16 < W - 16);
             const bool ok2 = lane < 33 && (x + 16 < W - 16) && d2 >= dlo && d2 <= dhi;
-            const bool edge = dlo > 0 || dhi < 32;
+            if (dlo > 0 || dhi < 32) {
+                const int tlo = dlo - 16 * hh, thi = dhi - 16 * hh;
+#pragma unroll
+                for (int t = 0; t < NT; ++t) lb[t] = (t < tlo || t > thi) ? kBig : lb[t];
+            }
             // ---- 2. U = SAD of the smallest-LB candidate ------------------------------------
             uint32_t kt = 0xFFFFFFFFu;                         // (lb << 5 | t), lane-local
-            if (!edge) {
 #pragma unroll
-                for (int t = 0; t < NT; ++t) {
-                    const uint32_t k = (lb[t] << 5) | (uint32_t)t;
-                    kt = k < kt ? k : kt;
-                }
-            } else {
-#pragma unroll
-                for (int t = 0; t < NT; ++t) {
-                    const int di = 16 * hh + t;
-                    const uint32_t k = (di < dlo || di > dhi) ? 0xFFFFFFFFu : ((lb[t] << 5) | (uint32_t)t);
-                    kt = k < kt ? k : kt;
-                }
+            for (int t = 0; t < NT; ++t) {
+                const uint32_t k = (lb[t] << 5) | (uint32_t)t;
+                kt = k < kt ? k : kt;
             }
-            uint32_t kl = (xok && kt != 0xFFFFFFFFu) ? ((kt >> 5) << 11) | (uint32_t)(xi * 33 + 16 * hh + (kt & 31))
+            uint32_t kl = (xok && (kt >> 5) != kBig) ? ((kt >> 5) << 11) | (uint32_t)(xi * 33 + 16 * hh + (kt & 31))
                                                       : 0xFFFFFFFFu;
             {
                 const uint32_t k2 = (lb2 << 11) | (uint32_t)(32 * 33 + d2);
                 kl = (ok2 && k2 < kl) ? k2 : kl;
             }
-            const uint32_t kmin = __builtin_amdgcn_readfirstlane(wave_min_u32(kl));
+            const uint32_t kmin = wave_min_u32(kl);
             if (kmin == 0xFFFFFFFFu) continue;                 // no valid candidate: key stays none
             const int cs = (int)(kmin & 2047), cdx = cs / 33, cdi = cs - cdx * 33;
             const int crow0 = byl * 16 * (CP / 4) + bxl * 4;   // current block in curt (dwords)
@@ -572,26 +613,19 @@ me_sea_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int
                 const int col = bxl * 16 + cdx;
                 const uint32_t w = ((lds_vu32p)win)[(col & 3) * CS + (byl * 16 + cdi + row) * RPD + (col >> 2) + kk];
                 const uint32_t c = curt[crow0 + row * (CP / 4) + kk];
-                U = __builtin_amdgcn_readfirstlane(wave_sum_u32(__builtin_amdgcn_sad_u8(c, w, 0u)));
+                U = wave_sum_u32(__builtin_amdgcn_sad_u8(c, w, 0u));
             }
-            // ---- 3. survivors: 16 LBq - 240 <= U (per-t ballots; empty ones cost one v_cmp) --
+            // ---- 3. survivors: 16 LBq - 240 <= U, i.e. LBq < qU1 (one v_cmp per t) -----------
             const uint32_t qU = (U + 240) >> 4;
+            const uint32_t qU1 = xok ? qU + 1 : 0u;            // dx-invalid lanes: nothing passes
             uint32_t nsur = 0;
             uint16_t* mylist = list + wave * CAP;
 #pragma unroll
             for (int t = 0; t <= NT; ++t) {
-                bool sv;
-                int cand;
-                if (t < NT) {
-                    const int di = 16 * hh + t;
-                    sv = xok && lb[t] <= qU && (!edge || (di >= dlo && di <= dhi));
-                    cand = xi * 33 + di;
-                } else {
-                    sv = ok2 && lb2 <= qU;
-                    cand = 32 * 33 + d2;
-                }
+                const bool sv = t < NT ? lb[t] < qU1 : (ok2 && lb2 <= qU);
                 const uint64_t bal = __ballot(sv);
-                if (bal) {                                     // wave-uniform
+                if (bal) {                                     // wave-uniform, rare
+                    const int cand = t < NT ? xi * 33 + 16 * hh + t : 32 * 33 + d2;
                     const uint32_t pos = nsur + lane_prefix(bal);
                     if (sv && pos < (uint32_t)CAP) mylist[pos] = (uint16_t)cand;
                     nsur += (uint32_t)__builtin_popcountll(bal);
@@ -619,8 +653,7 @@ me_sea_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int
                 uint32_t sad = 0;
 #pragma unroll
                 for (int kk = 0; kk < 4; ++kk) sad = __builtin_amdgcn_sad_u8(cr_[kk], wr_[kk], sad);
-#pragma unroll
-                for (int m = 8; m >= 1; m >>= 1) sad += __shfl_xor(sad, m, 64);
+                sad = row_sum_u32(sad);                        // 16 lanes = one DPP row
                 const int dx = dxi - 16, dy = di - 16;
                 const uint64_t key = me_key(sad, (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)), (uint32_t)r,
                                             (uint32_t)cand);
@@ -649,7 +682,7 @@ me_sea_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int
                     best = (idx < nsur && key < best) ? key : best;
                 }
             }
-            best = wave_min_u64(best);
+            best = wave_min_u64_dpp(best);
             if (lane == 0 && best < keys[u]) keys[u] = best;
         }
     }
