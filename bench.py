@@ -107,25 +107,33 @@ def me_kernel_name(vbs: bool) -> str:
     return "me_sea_kernel"
 
 
-def kernel_roofline(codec, frames_dev, reps: int) -> dict:
+def kernel_roofline(codec, frames_dev, symbols, reps: int) -> dict:
     """Average duration of the ME launch (the dominant kernel) and of the TQ launch for a
-    P-frame, measured with HIP events recorded on the launch stream."""
+    P-frame, measured with HIP events recorded on the launch stream.  The launches replay
+    the GOP's own P-frame work: launch k encodes frame i = 1 + k % (F-1) against the
+    reconstruction of frame i-1 from the timed GOP (the reference ME really searches, whose
+    content sets how much the successive-elimination bound prunes)."""
     from streamoptima_amd import _lib
     eng = codec.engine()
     lib = _lib.load()
     h, w, bs, sr = eng.h, eng.w, eng.bs, eng.sr
-    cur, ref = frames_dev[1], frames_dev[0]
-    refs = _lib.ref_array([ref])
+    nf = frames_dev.shape[0]
+    pairs = [(frames_dev[i], _lib.ref_array([symbols[i - 1].recon])) for i in range(1, nf)]
+    state = {"k": 0}
     best = torch.empty((eng.nb, 4), dtype=torch.int32, device=eng.device)
     sub = torch.empty((eng.nb, 4, 4), dtype=torch.int32, device=eng.device) if eng.vbs else None
     sym = eng.new_symbols(1)
     st = _lib.stream_handle(eng.device)
 
     def me():
+        cur, refs = pairs[state["k"] % len(pairs)]
+        state["k"] += 1
         _lib.check(lib.so_me_full_search(cur.data_ptr(), refs, 1, h, w, bs, sr, best.data_ptr(), _lib.ptr(sub), st),
                    "me")
 
     def tq():
+        cur, refs = pairs[state["k"] % len(pairs)]
+        state["k"] += 1
         _lib.check(lib.so_inter_tq_recon(cur.data_ptr(), refs, 1, h, w, bs, best.data_ptr(), _lib.ptr(sub),
                                          4, None, int(eng.vbs), eng.lam, sym.split.data_ptr(), sym.mv.data_ptr(),
                                          sym.qtc.data_ptr(), sym.tokens.data_ptr(), sym.mae_num.data_ptr(),
@@ -287,7 +295,7 @@ def main():
     sse = res["sse"].cpu().numpy()
     psnr_mean = float(np.mean([10 * np.log10(255 ** 2 / (s / (hp * w))) for s in sse if s > 0]))
 
-    rl = kernel_roofline(codec, frames, args.kernel_reps) if rank == 0 else None
+    rl = kernel_roofline(codec, frames, res["symbols"], args.kernel_reps) if rank == 0 else None
     delta = psnr_delta_vs_reference(dev) if rank == 0 else None
     pcie = pcie_inclusive(codec, cfg, frames) if rank == 0 and args.pcie and not stripe else None
     cpu = None
@@ -304,7 +312,9 @@ def main():
     pmc = os.path.join(ROOT, "profiles", "pmc_me_traffic.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get(args.config + ("_vbs" if args.vbs else ""), None)
+            kern = json.load(open(pmc)).get(args.config + ("_vbs" if args.vbs else ""), {}).get("kernels", {})
+            hit = kern.get("so::" + me_kernel_name(args.vbs))
+            traffic = round(hit["hbm_bytes"]) if hit else None
         except Exception:
             traffic = None
     line = {

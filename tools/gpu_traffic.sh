@@ -1,0 +1,17 @@
+#!/bin/bash
+# HBM traffic of every kernel in the bench command (MI355X_MICROARCH.md HBM section):
+# FETCH_SIZE and WRITE_SIZE in separate --pmc passes over a short bench run, then
+# tools/traffic_json.py writes profiles/pmc_me_traffic.json (bench.py roofline.traffic).
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out/traffic
+TAG=${1:-r01}
+CFG=${2:-4k}
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d gpurun_out/traffic/${TAG}_${CFG}_$c -o run -- \
+      python3 bench.py --config $CFG --steps 1 --warmup 1 --kernel-reps 5 --no-cpu-baseline \
+      > gpurun_out/traffic/${TAG}_${CFG}_$c.log 2>&1
+  rc=$?; echo "pmc $c rc=$rc"
+  [ $rc -ne 0 ] && { tail -5 gpurun_out/traffic/${TAG}_${CFG}_$c.log; exit $rc; }
+done
+exit 0
