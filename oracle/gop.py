@@ -28,9 +28,14 @@ def bitrate_per_row(target, frame_rate, h, bs):
 
 
 def encode_gop(frames, qp, intra_dur, bs=16, sr=16, vbs=False, lam=0.015, nref=1, rc=None,
-               target=None, tables=None, intra_thresh=None, frame_rate=30):
+               target=None, tables=None, intra_thresh=None, frame_rate=30, fast_me=False, fme=False,
+               parallel_mode=0):
     f, h, w = frames.shape
+    # the start reference is float64 all-128 (Encoder.py:1798): it matters only to the
+    # frac frame's uint8 wrap (oracle.fme_upsample)
     ref_frames = [np.full((h, w), 128, np.uint8)]
+    ref_float = [True]
+    me_mode = 0 if not fast_me else (2 if parallel_mode == 2 else 1)
     qp_sched = None
     if rc is not None and rc > 0:
         qp_sched = row_qp_schedule(bitrate_per_row(target, frame_rate, h, bs), tables, h // bs)
@@ -41,7 +46,8 @@ def encode_gop(frames, qp, intra_dur, bs=16, sr=16, vbs=False, lam=0.015, nref=1
             r = O.intra_frame(cur, bs, sr, qp, qp_sched, vbs, lam)
             ft = 0
         else:
-            r = O.inter_frame(cur, ref_frames, bs, sr, qp, qp_sched, vbs, lam)
+            r = O.inter_frame(cur, ref_frames, bs, sr, qp, qp_sched, vbs, lam, me_mode=me_mode, fme=fme,
+                              fme_wrap=not any(ref_float))
             ft = 1
             if rc is not None and rc > 1 and int(r["tokens"].sum()) > intra_thresh:
                 r = O.intra_frame(cur, bs, sr, qp_sched[-1], qp_sched, vbs, lam)
@@ -54,5 +60,7 @@ def encode_gop(frames, qp, intra_dur, bs=16, sr=16, vbs=False, lam=0.015, nref=1
         if i < f - 1:
             if len(ref_frames) >= nref:
                 ref_frames.pop(0)
+                ref_float.pop(0)
             ref_frames.append(r["recon"])
+            ref_float.append(False)
     return out

@@ -108,7 +108,11 @@ def _refs_array(refs):
 
 
 def inter_frame(cur: np.ndarray, refs, bs=16, sr=16, qp=4, qp_row=None, vbs=False,
-                lam=0.015) -> FrameResult:
+                lam=0.015, me_mode=0, fme=False, fme_wrap=True) -> FrameResult:
+    """complete_inter_flow for one frame (oc_inter_frame_ex).  me_mode 0 = full search,
+    1 = fast_me (serial predictor chain), 2 = fast_me under ParallelMode 2; fme = FMEEnable
+    with the frac frame's uint8 wrap `fme_wrap` (True unless the reference list still holds
+    the float64 start frame)."""
     cur = np.ascontiguousarray(cur, dtype=np.uint8)
     hp, wp = cur.shape
     h, w = refs[0].shape
@@ -118,12 +122,22 @@ def inter_frame(cur: np.ndarray, refs, bs=16, sr=16, qp=4, qp_row=None, vbs=Fals
                       qtc=np.zeros((nb, bs * bs), np.int16), tokens=np.zeros(nb, np.int32),
                       mae_num=np.zeros(nb, np.int64), recon=np.zeros((h, w), np.uint8))
     qr = None if qp_row is None else np.ascontiguousarray(qp_row, dtype=np.int32)
-    rc = lib().oc_inter_frame(_p(cur), hp, wp, ptrs, len(refs), h, w, bs, sr, qp,
-                              None if qr is None else _p(qr), int(vbs), ctypes.c_double(lam),
-                              _p(out["split"]), _p(out["mv"]), _p(out["qtc"]),
-                              _p(out["tokens"]), _p(out["mae_num"]), _p(out["recon"]))
+    rc = lib().oc_inter_frame_ex(_p(cur), hp, wp, ptrs, len(refs), h, w, bs, sr, qp,
+                                 None if qr is None else _p(qr), int(vbs), ctypes.c_double(lam),
+                                 int(me_mode), int(bool(fme)), int(bool(fme_wrap)),
+                                 _p(out["split"]), _p(out["mv"]), _p(out["qtc"]),
+                                 _p(out["tokens"]), _p(out["mae_num"]), _p(out["recon"]))
     if rc != 0:
-        raise ValueError(f"oc_inter_frame failed: {rc}")
+        raise ValueError(f"oc_inter_frame_ex failed: {rc}")
+    return out
+
+
+def fme_upsample(ref: np.ndarray, wrap=True) -> np.ndarray:
+    """frac_me_reference_frame of one reference (oc_fme_upsample)."""
+    ref = np.ascontiguousarray(ref, dtype=np.uint8)
+    h, w = ref.shape
+    out = np.zeros((2 * h - 1, 2 * w - 1), np.uint8)
+    lib().oc_fme_upsample(_p(ref), h, w, int(bool(wrap)), _p(out))
     return out
 
 
@@ -145,15 +159,15 @@ def intra_frame(cur: np.ndarray, bs=16, sr=16, qp=6, qp_row=None, vbs=False,
     return out
 
 
-def inter_recon(refs, split, mv, qtc, bs=16, qp=4, qp_row=None) -> np.ndarray:
+def inter_recon(refs, split, mv, qtc, bs=16, qp=4, qp_row=None, fme=False, fme_wrap=True) -> np.ndarray:
     h, w = refs[0].shape
     arrs, ptrs = _refs_array(refs)
     recon = np.zeros((h, w), np.uint8)
     qr = None if qp_row is None else np.ascontiguousarray(qp_row, dtype=np.int32)
-    lib().oc_inter_recon(ptrs, h, w, bs, qp, None if qr is None else _p(qr),
-                         _p(np.ascontiguousarray(split, np.uint8)),
-                         _p(np.ascontiguousarray(mv, np.int16)),
-                         _p(np.ascontiguousarray(qtc, np.int16)), _p(recon))
+    lib().oc_inter_recon_ex(ptrs, len(refs), h, w, bs, qp, None if qr is None else _p(qr), int(bool(fme)),
+                            int(bool(fme_wrap)), _p(np.ascontiguousarray(split, np.uint8)),
+                            _p(np.ascontiguousarray(mv, np.int16)),
+                            _p(np.ascontiguousarray(qtc, np.int16)), _p(recon))
     return recon
 
 

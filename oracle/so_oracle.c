@@ -23,6 +23,7 @@
 #include <string.h>
 
 #define EXPORT __attribute__((visibility("default")))
+#define SO_ORACLE_MAX_REF 16
 
 /* ------------------------------------------------------------------------------------ */
 /* pocketfft restatement (rfftp + T_dcst23), N in {8, 16}                                */
@@ -399,21 +400,6 @@ static om_mv find_best_match(const uint8_t *cur, int cstride, const uint8_t *con
     return best;
 }
 
-/* prediction fetch of calculate_inter_frame_residual / reconstruct_frame
- * (Encoder.py:444-456, 862-873, 907-919) incl. handle_boundary_conditions (:750-768). */
-static void fetch_pred(const uint8_t *ref, int H, int W, int px, int py, int bs, int32_t *pred) {
-    if (0 <= px && px < W - bs && 0 <= py && py < H - bs) {
-        for (int i = 0; i < bs; ++i)
-            for (int j = 0; j < bs; ++j) pred[i * bs + j] = ref[(py + i) * W + px + j];
-        return;
-    }
-    for (int i = 0; i < bs; ++i)
-        for (int j = 0; j < bs; ++j) {
-            int yy = py + i, xx = px + j;
-            pred[i * bs + j] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? ref[yy * W + xx] : 0;
-        }
-}
-
 static int block_tokens(const int16_t *q, int n) { return oc_rle(q, n, NULL); }
 
 /* calculate_RD_cost (Encoder.py:1133-1158) given token counts. */
@@ -433,29 +419,188 @@ static void tq_block(const int32_t *res, int n, int qp, int16_t *qtc) {
 
 static inline uint8_t wrap_u8(long v) { return (uint8_t)(v & 255); }
 
+/* ------------------------------------------------------------------------------------ */
+/* Fractional (half-pel) ME and fast ME                                                   */
+/* ------------------------------------------------------------------------------------ */
+
+/* frac_me_reference_frame (Encoder.py:388-403, decoder.py:468-483): a (2H-1) x (2W-1)
+ * frame.  Rows first: each row r becomes [r0, (r0+r1)/2, r1, ..., r_{W-1}] in float; then
+ * each column of that the same way, and np.ceil of the result.  Every value is a multiple
+ * of 1/4, so in integers:
+ *   F[2i][2j]     = r[i][j]
+ *   F[2i][2j+1]   = ceil(h(i,j) / 2)             h(i,j) = r[i][j] + r[i][j+1]
+ *   F[2i+1][2j]   = ceil((r[i][j] + r[i+1][j]) / 2)
+ *   F[2i+1][2j+1] = ceil((h(i,j) + h(i+1,j)) / 4)
+ * `wrap`: np.copy(ref_frames) is uint8 when every reference is a uint8 reconstruction, and
+ * then `row + np.roll(row, -1)` wraps mod 256 (h &= 255).  The column pass already runs in
+ * float64 (the rows were promoted by vstack), so it never wraps.  A list that still holds
+ * the float64 all-128 start frame (Encoder.py:1798) is float64: no wrap. */
+EXPORT void oc_fme_upsample(const uint8_t *ref, int H, int W, int wrap, uint8_t *out) {
+    const int W2 = 2 * W - 1;
+    for (int i = 0; i < H; ++i)
+        for (int j = 0; j < W; ++j) {
+            const int a = ref[(size_t)i * W + j];
+            out[(size_t)(2 * i) * W2 + 2 * j] = (uint8_t)a;
+            int h0 = 0;
+            if (j + 1 < W) {
+                h0 = a + ref[(size_t)i * W + j + 1];
+                if (wrap) h0 &= 255;
+                out[(size_t)(2 * i) * W2 + 2 * j + 1] = (uint8_t)((h0 + 1) >> 1);
+            }
+            if (i + 1 < H) {
+                const int c = ref[(size_t)(i + 1) * W + j];
+                out[(size_t)(2 * i + 1) * W2 + 2 * j] = (uint8_t)((a + c + 1) >> 1);
+                if (j + 1 < W) {
+                    int h1 = c + ref[(size_t)(i + 1) * W + j + 1];
+                    if (wrap) h1 &= 255;
+                    out[(size_t)(2 * i + 1) * W2 + 2 * j + 1] = (uint8_t)((h0 + h1 + 3) >> 2);
+                }
+            }
+        }
+}
+
+/* A search plane: the reference frame itself (step 1) or its frac_me frame (step 2, FME:
+ * the block is sampled every other row/column, Encoder.py:699-700). */
+typedef struct { const uint8_t *const *p; int H, W, step; } om_planes;
+
+static long plane_sad(const uint8_t *cur, int cstride, const uint8_t *pl, int PW, int X, int Y, int bs,
+                      int step) {
+    long sad = 0;
+    for (int i = 0; i < bs; ++i)
+        for (int j = 0; j < bs; ++j)
+            sad += labs((long)cur[i * cstride + j] - (long)pl[(size_t)(Y + step * i) * PW + X + step * j]);
+    return sad;
+}
+
+/* find_best_match (Encoder.py:678-717) incl. the FMEEnable branch (:697-705): at (X, Y)
+ * (= 2x, 2y with FME) over dx, dy in [-R, R] (R = 2 sr with FME, :1649); FME candidates
+ * also need 0 <= X+dx+2bs < W2-bs (and y), and compare the stride-2 sample. */
+static om_mv search_full(const uint8_t *cur, int cstride, om_planes P, int nref, int X, int Y, int bs,
+                         int R) {
+    om_mv best = {0, 0, 0, -1};
+    const int fme = P.step == 2;
+    for (int r = 0; r < nref; ++r)
+        for (int dx = -R; dx <= R; ++dx)
+            for (int dy = -R; dy <= R; ++dy) {
+                if (!(0 <= X + dx && X + dx < P.W - bs && 0 <= Y + dy && Y + dy < P.H - bs)) continue;
+                if (fme && !(0 <= X + dx + 2 * bs && X + dx + 2 * bs < P.W - bs && 0 <= Y + dy + 2 * bs &&
+                             Y + dy + 2 * bs < P.H - bs))
+                    continue;
+                const long sad = plane_sad(cur, cstride, P.p[r], P.W, X + dx, Y + dy, bs, P.step);
+                if (best.sad < 0 || sad < best.sad) {
+                    best.dx = dx; best.dy = dy; best.ref = r; best.sad = sad;
+                } else if (sad == best.sad) {
+                    int l1n = abs(dx) + abs(dy), l1b = abs(best.dx) + abs(best.dy);
+                    if (l1n < l1b || (l1n == l1b && r < best.ref)) {
+                        best.dx = dx; best.dy = dy; best.ref = r;
+                    }
+                }
+            }
+    return best;
+}
+
+/* fast_motion_estimation (Encoder.py:719-742): the 3x3 neighbourhood of the predictor
+ * mvp over refs[:nref]; a candidate needs the strict bound AND 0 <= X+dx+2bs < W-bs (and
+ * y) even without FME (:727); strictly smaller MAE wins (first found, no is_better_mv).
+ * Returns (best_mv, best_ref_idx): best_mv = mvp when nothing is valid, and the second
+ * value -- used by the caller as the block's MAE -- is the reference INDEX (:742).  Here
+ * .sad carries that index. */
+static om_mv search_fast(const uint8_t *cur, int cstride, om_planes P, int nref, int X, int Y, int bs,
+                         om_mv mvp) {
+    om_mv best = {mvp.dx, mvp.dy, mvp.ref, 0};
+    long best_sad = -1;
+    for (int r = 0; r < nref; ++r)
+        for (int dx = mvp.dx - 1; dx <= mvp.dx + 1; ++dx)
+            for (int dy = mvp.dy - 1; dy <= mvp.dy + 1; ++dy) {
+                if (!(0 <= X + dx && X + dx < P.W - bs && 0 <= Y + dy && Y + dy < P.H - bs)) continue;
+                if (!(0 <= X + dx + 2 * bs && X + dx + 2 * bs < P.W - bs && 0 <= Y + dy + 2 * bs &&
+                      Y + dy + 2 * bs < P.H - bs))
+                    continue;
+                const long sad = plane_sad(cur, cstride, P.p[r], P.W, X + dx, Y + dy, bs, P.step);
+                if (best_sad < 0 || sad < best_sad) {
+                    best_sad = sad;
+                    best.dx = dx; best.dy = dy; best.ref = r; best.sad = r;
+                }
+            }
+    return best;
+}
+
+/* Prediction of calculate_inter_frame_residual (Encoder.py:432-460) and reconstruct_frame
+ * (:831-932) on a search plane, at plane position (px, py), block size bs:
+ *   strict bound 0 <= px < W-bs (and y)  -> integer: the bs x bs block;
+ *                                           FME: if 0 <= px+ext < W-lim (and y) the
+ *                                           stride-2 sample, else all 128;
+ *   otherwise handle_boundary_conditions (:750-768): zero-filled contiguous overlap.
+ * (ext, lim) = (2bs, bs) in the residual and the unsplit recon; a split sub-block's recon
+ * uses (BS, BS) of the FULL block size (:908-909), stricter than its search. */
+static void fetch_pred2(const uint8_t *pl, int PH, int PW, int step, int px, int py, int bs, int ext, int lim,
+                        int32_t *pred) {
+    if (0 <= px && px < PW - bs && 0 <= py && py < PH - bs) {
+        if (step == 2) {
+            const int ok = 0 <= px + ext && px + ext < PW - lim && 0 <= py + ext && py + ext < PH - lim;
+            for (int i = 0; i < bs; ++i)
+                for (int j = 0; j < bs; ++j)
+                    pred[i * bs + j] = ok ? pl[(size_t)(py + 2 * i) * PW + px + 2 * j] : 128;
+        } else {
+            for (int i = 0; i < bs; ++i)
+                for (int j = 0; j < bs; ++j) pred[i * bs + j] = pl[(size_t)(py + i) * PW + px + j];
+        }
+        return;
+    }
+    for (int i = 0; i < bs; ++i)
+        for (int j = 0; j < bs; ++j) {
+            int yy = py + i, xx = px + j;
+            pred[i * bs + j] = (yy >= 0 && yy < PH && xx >= 0 && xx < PW) ? pl[(size_t)yy * PW + xx] : 0;
+        }
+}
+
 /*
  * One P-frame through complete_inter_flow (Encoder.py:1644-1709): inter_prediction
- * (:462-585, serial branch), per-block DCT/quant/tokens with the per-row QP (:1665-1697)
- * and reconstruct_frame (:831-932).
+ * (:462-585), per-block DCT/quant/tokens with the per-row QP (:1665-1697) and
+ * reconstruct_frame (:831-932).
  *
- *   cur    : padded current frame, Hp x Wp uint8 (pad_hw values)
- *   refs   : nref reference frames, H x W uint8 (H = Hp, W = Wp required)
- *   qp_rd  : QP in effect during inter_prediction (RD decisions)
- *   qp_row : per block-row QP (NULL => qp_rd everywhere)
+ *   cur     : padded current frame, Hp x Wp uint8 (pad_hw values)
+ *   refs    : nref reference frames, H x W uint8 (H = Hp, W = Wp required)
+ *   qp_rd   : QP in effect during inter_prediction (RD decisions)
+ *   qp_row  : per block-row QP (NULL => qp_rd everywhere)
+ *   me_mode : 0 find_best_match (full search);
+ *             1 fast_me, serial branch: the predictor is the previous block's mv in raster
+ *               order, starting at (0,0,0) (:462, :581), over all nref refs;
+ *             2 fast_me under ParallelMode 2 (inter_prediction_parallel :587-676): every
+ *               block's predictor is (0,0,0) and nRefFrames is 1 (:589-590, :641-642);
+ *               VBS is rejected there (the reference raises NameError on `mvp`, :609)
+ *   fme     : FMEEnable: search/predict on frac_me_reference_frame(refs) at (2x, 2y)
+ *             with range 2 sr, MVs in half-pel units (:1647-1651)
+ *   fme_wrap: the frac frame's uint8 wrap (oc_fme_upsample)
  * outputs (nb = Hp/bs * Wp/bs):
  *   split[nb], mv[nb][4][3], qtc[nb][bs*bs], tokens[nb], mae_num[nb] (MAE*bs*bs as an
  *   integer, -1 = inf), recon[H*W]
  */
-EXPORT int oc_inter_frame(const uint8_t *cur, int Hp, int Wp, const uint8_t *const *refs,
-                          int nref, int H, int W, int bs, int sr, int qp_rd,
-                          const int32_t *qp_row, int vbs, double lam, uint8_t *split,
-                          int16_t *mv, int16_t *qtc, int32_t *tokens, int64_t *mae_num,
-                          uint8_t *recon) {
+EXPORT int oc_inter_frame_ex(const uint8_t *cur, int Hp, int Wp, const uint8_t *const *refs,
+                             int nref, int H, int W, int bs, int sr, int qp_rd,
+                             const int32_t *qp_row, int vbs, double lam, int me_mode, int fme,
+                             int fme_wrap, uint8_t *split, int16_t *mv, int16_t *qtc,
+                             int32_t *tokens, int64_t *mae_num, uint8_t *recon) {
     if (bs != 16 && bs != 8) return -1;
     if (H != Hp || W != Wp) return -2;
+    if (me_mode == 2 && vbs) return -3;
     const int sb = bs / 2, nbx = Wp / bs, nby = Hp / bs, bb = bs * bs;
     int32_t res[256], pred[256], deq[256], idc[256];
     int16_t qfull[256], qsub[4][64];
+    uint8_t *up[SO_ORACLE_MAX_REF] = {0};
+    om_planes P = {refs, H, W, 1};
+    if (fme) {
+        for (int r = 0; r < nref; ++r) {
+            up[r] = (uint8_t *)malloc((size_t)(2 * H - 1) * (2 * W - 1));
+            oc_fme_upsample(refs[r], H, W, fme_wrap, up[r]);
+        }
+        P.p = (const uint8_t *const *)up;
+        P.H = 2 * H - 1; P.W = 2 * W - 1; P.step = 2;
+    }
+    const int k = fme ? 2 : 1;            /* block origin scale on the search plane */
+    const int R = fme ? 2 * sr : sr;
+    const int nref_fast = me_mode == 2 ? 1 : nref;
+    om_mv mvp = {0, 0, 0, 0};
     memset(recon, 0, (size_t)H * W);
     for (int by = 0; by < nby; ++by)
         for (int bx = 0; bx < nbx; ++bx) {
@@ -463,23 +608,41 @@ EXPORT int oc_inter_frame(const uint8_t *cur, int Hp, int Wp, const uint8_t *con
             const uint8_t *cb = cur + (size_t)y * Wp + x;
             const int qpr = qp_row ? qp_row[by] : qp_rd;
             const int eligible = vbs && x != 0 && y != 0;
+            if (me_mode == 2) { mvp.dx = 0; mvp.dy = 0; mvp.ref = 0; }
             om_mv sm[4];
             long vbs_sum = 0; int vbs_inf = 0;
             int32_t sres[4][64];
             if (eligible) {
                 for (int j = 0; j < 4; ++j) {
                     int xs = x + (j & 1) * sb, ys = y + (j >> 1) * sb;
-                    sm[j] = find_best_match(cur + (size_t)ys * Wp + xs, Wp, refs, nref, H, W, xs, ys, sb, sr);
-                    if (sm[j].sad < 0) vbs_inf = 1; else vbs_sum += sm[j].sad;
-                    fetch_pred(refs[sm[j].ref], H, W, xs + sm[j].dx, ys + sm[j].dy, sb, pred);
+                    const uint8_t *cs = cur + (size_t)ys * Wp + xs;
+                    if (me_mode) {
+                        sm[j] = search_fast(cs, Wp, P, nref_fast, k * xs, k * ys, sb, mvp);
+                        vbs_sum += sm[j].sad * sb * sb;     /* "mae" = ref index */
+                    } else {
+                        sm[j] = search_full(cs, Wp, P, nref, k * xs, k * ys, sb, R);
+                        if (sm[j].sad < 0) vbs_inf = 1; else vbs_sum += sm[j].sad;
+                    }
+                    fetch_pred2(P.p[sm[j].ref], P.H, P.W, P.step, k * xs + sm[j].dx, k * ys + sm[j].dy, sb, 2 * sb, sb,
+                                pred);
                     for (int i = 0; i < sb; ++i)
-                        for (int k = 0; k < sb; ++k)
-                            sres[j][i * sb + k] = (int32_t)cb[(size_t)((j >> 1) * sb + i) * Wp + (j & 1) * sb + k] - pred[i * sb + k];
+                        for (int q = 0; q < sb; ++q)
+                            sres[j][i * sb + q] = (int32_t)cb[(size_t)((j >> 1) * sb + i) * Wp + (j & 1) * sb + q] - pred[i * sb + q];
                 }
             }
-            om_mv m = find_best_match(cb, Wp, refs, nref, H, W, x, y, bs, sr);
+            om_mv m;
+            long mae_b_num;          /* MAE * bb */
+            int m_inf = 0;
+            if (me_mode) {
+                m = search_fast(cb, Wp, P, nref_fast, k * x, k * y, bs, mvp);
+                mae_b_num = m.sad * bb;
+            } else {
+                m = search_full(cb, Wp, P, nref, k * x, k * y, bs, R);
+                m_inf = m.sad < 0;
+                mae_b_num = m.sad;
+            }
             int32_t fpred[256];
-            fetch_pred(refs[m.ref], H, W, x + m.dx, y + m.dy, bs, fpred);
+            fetch_pred2(P.p[m.ref], P.H, P.W, P.step, k * x + m.dx, k * y + m.dy, bs, 2 * bs, bs, fpred);
             for (int i = 0; i < bb; ++i) res[i] = (int32_t)cb[(size_t)(i / bs) * Wp + i % bs] - fpred[i];
             int do_split = 0;
             if (eligible) {
@@ -487,15 +650,16 @@ EXPORT int oc_inter_frame(const uint8_t *cur, int Hp, int Wp, const uint8_t *con
                 tq_block(res, bs, qp_rd, qfull);
                 int tok_b = block_tokens(qfull, bs), tok_v = 0;
                 for (int j = 0; j < 4; ++j) { tq_block(sres[j], sb, qpm1_rd, qsub[j]); tok_v += block_tokens(qsub[j], sb); }
-                double mae_b = m.sad < 0 ? INFINITY : (double)m.sad / bb;
+                double mae_b = m_inf ? INFINITY : (double)mae_b_num / bb;
                 double mae_v = vbs_inf ? INFINITY : ((double)vbs_sum / (sb * sb)) / 4.0;
                 double c_v = rd_cost(1, 1, mae_v, tok_v, lam);
                 double c_b = rd_cost(1, 0, mae_b, tok_b, lam);
                 do_split = !(c_b < c_v);
                 mae_num[b] = vbs_inf ? -1 : vbs_sum;   /* mae = vbs_mae (:575) */
             } else {
-                mae_num[b] = m.sad;
+                mae_num[b] = m_inf ? -1 : mae_b_num;
             }
+            if (me_mode == 1) mvp = m;              /* mvp = mv (:581), the full block's */
             split[b] = (uint8_t)do_split;
             int16_t *mvb = mv + (size_t)b * 12;
             memset(mvb, 0, 12 * sizeof(int16_t));
@@ -507,8 +671,8 @@ EXPORT int oc_inter_frame(const uint8_t *cur, int Hp, int Wp, const uint8_t *con
                 dequantize(qb, deq, bs, qpr);
                 oc_apply_2d_idct(deq, idc, bs);
                 for (int i = 0; i < bs; ++i)
-                    for (int k = 0; k < bs; ++k)
-                        recon[(size_t)(y + i) * W + x + k] = wrap_u8((long)fpred[i * bs + k] + idc[i * bs + k]);
+                    for (int q = 0; q < bs; ++q)
+                        recon[(size_t)(y + i) * W + x + q] = wrap_u8((long)fpred[i * bs + q] + idc[i * bs + q]);
             } else {
                 const int qpm1 = qpr > 0 ? qpr - 1 : qpr;
                 int tk = 0;
@@ -518,17 +682,28 @@ EXPORT int oc_inter_frame(const uint8_t *cur, int Hp, int Wp, const uint8_t *con
                     tq_block(sres[j], sb, qpm1, qs);
                     tk += block_tokens(qs, sb);
                     int xs = x + (j & 1) * sb, ys = y + (j >> 1) * sb;
-                    fetch_pred(refs[sm[j].ref], H, W, xs + sm[j].dx, ys + sm[j].dy, sb, pred);
+                    fetch_pred2(P.p[sm[j].ref], P.H, P.W, P.step, k * xs + sm[j].dx, k * ys + sm[j].dy, sb, bs, bs,
+                                pred);
                     dequantize(qs, deq, sb, qpm1);
                     oc_apply_2d_idct(deq, idc, sb);
                     for (int i = 0; i < sb; ++i)
-                        for (int k = 0; k < sb; ++k)
-                            recon[(size_t)(ys + i) * W + xs + k] = wrap_u8((long)pred[i * sb + k] + idc[i * sb + k]);
+                        for (int q = 0; q < sb; ++q)
+                            recon[(size_t)(ys + i) * W + xs + q] = wrap_u8((long)pred[i * sb + q] + idc[i * sb + q]);
                 }
                 tokens[b] = tk;
             }
         }
+    for (int r = 0; r < nref; ++r) free(up[r]);
     return 0;
+}
+
+EXPORT int oc_inter_frame(const uint8_t *cur, int Hp, int Wp, const uint8_t *const *refs,
+                          int nref, int H, int W, int bs, int sr, int qp_rd,
+                          const int32_t *qp_row, int vbs, double lam, uint8_t *split,
+                          int16_t *mv, int16_t *qtc, int32_t *tokens, int64_t *mae_num,
+                          uint8_t *recon) {
+    return oc_inter_frame_ex(cur, Hp, Wp, refs, nref, H, W, bs, sr, qp_rd, qp_row, vbs, lam, 0, 0, 0, split, mv,
+                             qtc, tokens, mae_num, recon);
 }
 
 /* intra_find_best_match_horizontal (Encoder.py:1010-1045) on the in-loop canvas, which
@@ -674,12 +849,25 @@ EXPORT int oc_intra_frame(const uint8_t *cur, int Hp, int Wp, int bs, int sr, in
     return 0;
 }
 
-/* Decoder inter recon only (decoder.py:97-211 == reconstruct_frame :831-932). */
-EXPORT int oc_inter_recon(const uint8_t *const *refs, int H, int W, int bs, int qp_rd,
-                          const int32_t *qp_row, const uint8_t *split, const int16_t *mv,
-                          const int16_t *qtc, uint8_t *recon) {
+/* Decoder inter recon (decoder.py:97-211 == reconstruct_frame :831-932), with the FME
+ * branch (frac frames of the references, half-pel MVs; decoder.py:102-103, 121-141,
+ * 168-187): `fme_wrap` as in oc_fme_upsample. */
+EXPORT int oc_inter_recon_ex(const uint8_t *const *refs, int nref, int H, int W, int bs, int qp_rd,
+                             const int32_t *qp_row, int fme, int fme_wrap, const uint8_t *split,
+                             const int16_t *mv, const int16_t *qtc, uint8_t *recon) {
     const int sb = bs / 2, nbx = W / bs, nby = H / bs, bb = bs * bs;
     int32_t pred[256], deq[256], idc[256];
+    uint8_t *up[SO_ORACLE_MAX_REF] = {0};
+    om_planes P = {refs, H, W, 1};
+    if (fme) {
+        for (int r = 0; r < nref; ++r) {
+            up[r] = (uint8_t *)malloc((size_t)(2 * H - 1) * (2 * W - 1));
+            oc_fme_upsample(refs[r], H, W, fme_wrap, up[r]);
+        }
+        P.p = (const uint8_t *const *)up;
+        P.H = 2 * H - 1; P.W = 2 * W - 1; P.step = 2;
+    }
+    const int k = fme ? 2 : 1;
     memset(recon, 0, (size_t)H * W);
     for (int by = 0; by < nby; ++by)
         for (int bx = 0; bx < nbx; ++bx) {
@@ -688,26 +876,35 @@ EXPORT int oc_inter_recon(const uint8_t *const *refs, int H, int W, int bs, int 
             const int16_t *mvb = mv + (size_t)b * 12;
             const int16_t *qb = qtc + (size_t)b * bb;
             if (!split[b]) {
-                fetch_pred(refs[mvb[2]], H, W, x + mvb[0], y + mvb[1], bs, pred);
+                fetch_pred2(P.p[mvb[2]], P.H, P.W, P.step, k * x + mvb[0], k * y + mvb[1], bs, 2 * bs, bs, pred);
                 dequantize(qb, deq, bs, qpr);
                 oc_apply_2d_idct(deq, idc, bs);
                 for (int i = 0; i < bs; ++i)
-                    for (int k = 0; k < bs; ++k)
-                        recon[(size_t)(y + i) * W + x + k] = wrap_u8((long)pred[i * bs + k] + idc[i * bs + k]);
+                    for (int q = 0; q < bs; ++q)
+                        recon[(size_t)(y + i) * W + x + q] = wrap_u8((long)pred[i * bs + q] + idc[i * bs + q]);
             } else {
                 const int qpm1 = qpr > 0 ? qpr - 1 : qpr;
                 for (int j = 0; j < 4; ++j) {
                     int xs = x + (j & 1) * sb, ys = y + (j >> 1) * sb;
-                    fetch_pred(refs[mvb[3 * j + 2]], H, W, xs + mvb[3 * j], ys + mvb[3 * j + 1], sb, pred);
+                    fetch_pred2(P.p[mvb[3 * j + 2]], P.H, P.W, P.step, k * xs + mvb[3 * j], k * ys + mvb[3 * j + 1],
+                                sb, bs, bs, pred);
                     dequantize(qb + j * sb * sb, deq, sb, qpm1);
                     oc_apply_2d_idct(deq, idc, sb);
                     for (int i = 0; i < sb; ++i)
-                        for (int k = 0; k < sb; ++k)
-                            recon[(size_t)(ys + i) * W + xs + k] = wrap_u8((long)pred[i * sb + k] + idc[i * sb + k]);
+                        for (int q = 0; q < sb; ++q)
+                            recon[(size_t)(ys + i) * W + xs + q] = wrap_u8((long)pred[i * sb + q] + idc[i * sb + q]);
                 }
             }
         }
+    for (int r = 0; r < nref; ++r) free(up[r]);
     return 0;
+}
+
+EXPORT int oc_inter_recon(const uint8_t *const *refs, int H, int W, int bs, int qp_rd,
+                          const int32_t *qp_row, const uint8_t *split, const int16_t *mv,
+                          const int16_t *qtc, uint8_t *recon) {
+    int nref = 0;   /* the MVs name their reference; the plain path never upsamples */
+    return oc_inter_recon_ex(refs, nref, H, W, bs, qp_rd, qp_row, 0, 0, split, mv, qtc, recon);
 }
 
 /* sum of squared differences for PSNR (Encoder.py:934-935) */

@@ -83,13 +83,14 @@ def canvas_patch(Encoder, h, w):
 
 
 def make_codec(Encoder, frames_arr, qp, vbs=False, lam=0.015, rc=None, target=None,
-               tables=None, intra_thresh=None, intra_dur=None, nref=1, sr=16, bs=16):
+               tables=None, intra_thresh=None, intra_dur=None, nref=1, sr=16, bs=16,
+               fast_me=False, fme=False, parallel_mode=0):
     f, h, w = frames_arr.shape
     return Encoder.Y_Video_codec(h, w, f, bs, sr, qp, intra_dur or f, 0, lam, vbs,
                                  nRefFrames=nref, y_only_frame_arr=frames_arr,
-                                 fast_me=False, FMEEnable=False, RCFlag=rc,
+                                 fast_me=fast_me, FMEEnable=fme, RCFlag=rc,
                                  targetBR=target, frame_rate=30, qp_rate_tables=tables,
-                                 intra_thresh=intra_thresh, ParallelMode=0)
+                                 intra_thresh=intra_thresh, ParallelMode=parallel_mode)
 
 
 def canon_inter(mvs, qblocks, bs):
@@ -254,11 +255,11 @@ def gen_intra(Encoder, out, vbs, name, qp=6, h=288, w=352, seed=0):
 
 
 def gen_gop(Encoder, out, name, frames, intra_dur, qp, vbs, rc=None, target=None,
-            tables=None, intra_thresh=None, h=288, w=352, seed=0):
+            tables=None, intra_thresh=None, h=288, w=352, seed=0, **kw):
     """Golden vector 5: encode() of a short GOP plus the text bitstream lines."""
     seq = synth_sequence(frames, h, w, seed=seed)
     enc = make_codec(Encoder, seq, qp, vbs=vbs, rc=rc, target=target, tables=tables,
-                     intra_thresh=intra_thresh, intra_dur=intra_dur)
+                     intra_thresh=intra_thresh, intra_dur=intra_dur, **kw)
     with canvas_patch(Encoder, h, w), quiet():
         psnr = enc.encode(block_size=16)
     pkg = enc.encoded_package
@@ -288,6 +289,61 @@ def gen_gop(Encoder, out, name, frames, intra_dur, qp, vbs, rc=None, target=None
     import gzip
     with gzip.open(os.path.join(out, name + "_bitstream.json.gz"), "wt") as f:
         json.dump({"mv_lines": lines_mv, "residual_lines": lines_res}, f)
+
+
+def gen_fme_frames(Encoder, out):
+    """frac_me_reference_frame (Encoder.py:388-403) of a uint8 list (wrapping row sums) and
+    of a list that still holds the float64 all-128 start frame (no wrap)."""
+    rng = np.random.default_rng(77)
+    a = rng.integers(0, 256, size=(24, 40)).astype(np.uint8)
+    a[:4] = rng.integers(200, 256, size=(4, 40))         # row sums past 255
+    b = rng.integers(0, 256, size=(24, 40)).astype(np.uint8)
+    enc = make_codec(Encoder, np.zeros((1, 24, 40), np.uint8), 4)
+    up_u8 = enc.frac_me_reference_frame([a, b], 16)
+    up_f = enc.frac_me_reference_frame([np.ones((24, 40)) * 128, a], 16)
+    for f in up_u8 + up_f:
+        assert f.min() >= 0 and f.max() <= 255 and np.all(f == np.round(f))
+    np.savez_compressed(os.path.join(out, "fme_frames.npz"), a=a, b=b,
+                        up_u8_a=np.asarray(up_u8[0], np.uint8), up_u8_b=np.asarray(up_u8[1], np.uint8),
+                        up_f_128=np.asarray(up_f[0], np.uint8), up_f_a=np.asarray(up_f[1], np.uint8))
+
+
+def gen_inter_me_variants(Encoder, out):
+    """complete_inter_flow with FMEEnable and/or fast_me (Encoder.py:462-585, 678-742,
+    1644-1709), plus fast_me under ParallelMode 2 (inter_prediction_parallel :587-676)."""
+    cases = [
+        # name, h, w, sr, vbs, fast, fme, nref, parallel_mode
+        ("fme_cif_vbs0", 288, 352, 16, False, False, True, 1, 0),
+        ("fme_96x128_vbs1", 96, 128, 16, True, False, True, 1, 0),
+        ("fme_64x96_sr4_vbs1", 64, 96, 4, True, False, True, 1, 0),
+        ("fme_64x96_nref2", 64, 96, 8, True, False, True, 2, 0),
+        ("fast_cif_vbs0", 288, 352, 16, False, True, False, 1, 0),
+        ("fast_cif_vbs1", 288, 352, 16, True, True, False, 1, 0),
+        ("fast_cif_nref2_vbs1", 288, 352, 16, True, True, False, 2, 0),
+        ("fast_fme_cif_vbs1", 288, 352, 16, True, True, True, 1, 0),
+        ("fast_par2_cif", 288, 352, 16, False, True, False, 2, 2),
+    ]
+    res = {}
+    for name, h, w, sr, vbs, fast, fme, nref, pm in cases:
+        seq = synth_sequence(3, h, w, seed=11)
+        enc = make_codec(Encoder, seq, 4, vbs=vbs, sr=sr, fast_me=fast, fme=fme, nref=nref, parallel_mode=pm)
+        enc.set_Qp(4)
+        cur = enc.pad_hw(seq[2], 16, 128)
+        refs = [seq[0], seq[1]][-nref:] if nref > 1 else [seq[1]]
+        t0 = time.time()
+        with quiet():
+            mvs, avg_mae, qb, qprow, recon, rsize, stats = enc.complete_inter_flow(cur, list(refs), 16, sr)
+        split, mv, qtc = canon_inter(mvs, qb, 16)
+        tok = block_tokens(enc, qb, 16)
+        assert tok.sum() == rsize
+        for k, v in dict(split=split, mv=mv, qtc=qtc, tokens=tok, recon=recon).items():
+            res[f"{name}__{k}"] = v
+        res[f"{name}__avg_mae"] = np.float64(avg_mae)
+        res[f"{name}__cur"] = seq[2]
+        res[f"{name}__refs"] = np.stack(refs)
+        res[f"{name}__cfg"] = np.array([h, w, sr, int(vbs), int(fast), int(fme), nref, pm], np.int32)
+        print(f"  {name}: {time.time() - t0:.1f}s", flush=True)
+    np.savez_compressed(os.path.join(out, "inter_me_variants.npz"), **res)
 
 
 def gen_rc(Encoder, out):
@@ -386,6 +442,22 @@ def main():
         gen_gop(Encoder, out, "gop_small_rc2", frames=4, intra_dur=4, qp=3, vbs=True, rc=2,
                 target="1 mbps", tables=tables, intra_thresh=150, h=64, w=128, seed=7)
         print("gop2 done", flush=True)
+    if "fme" in todo:
+        gen_fme_frames(Encoder, out)
+        gen_inter_me_variants(Encoder, out)
+        print("fme/fast frames done", flush=True)
+    if "gopme" in todo:
+        gen_gop(Encoder, out, "gop_fme_vbs1", frames=3, intra_dur=3, qp=4, vbs=True, h=64, w=96, seed=4,
+                fme=True)
+        # (no nRefFrames > 1 GOP: the reference's closed-loop decode resets its reference
+        # list at every I-frame, decoder.py:520, and then indexes a missing reference,
+        # IndexError at decoder.py:117; the float-start no-wrap frac frame is pinned by
+        # fme_frames.npz instead)
+        gen_gop(Encoder, out, "gop_fast_vbs1", frames=4, intra_dur=4, qp=4, vbs=True, h=96, w=128, seed=6,
+                fast_me=True)
+        gen_gop(Encoder, out, "gop_fast_fme", frames=3, intra_dur=3, qp=4, vbs=False, h=64, w=96, seed=8,
+                fast_me=True, fme=True)
+        print("gop fme/fast done", flush=True)
     if args.large:
         gen_large(Encoder, out)
 

@@ -117,3 +117,58 @@ def test_large_1088p_hash():
         assert sha(out[i]["recon"]) == exp[f"recon{i}"]
         assert int(out[i]["tokens"].sum()) == exp[f"tokens{i}"]
         assert out[i]["psnr"] == pytest.approx(exp["psnr"][i], abs=1e-9)
+
+
+# ---- FME (half-pel) and fast ME: reference goldens (tests/golden/make_golden.py --only fme,gopme) ----
+def test_fme_upsample_golden():
+    """frac_me_reference_frame (Encoder.py:388-403): uint8 lists wrap the row sums mod 256,
+    a list holding the float64 start frame does not."""
+    g = golden("fme_frames.npz")
+    assert (O.fme_upsample(g["a"], wrap=True) == g["up_u8_a"]).all()
+    assert (O.fme_upsample(g["b"], wrap=True) == g["up_u8_b"]).all()
+    assert (O.fme_upsample(g["a"], wrap=False) == g["up_f_a"]).all()
+    assert (O.fme_upsample(np.full((24, 40), 128, np.uint8), wrap=False) == g["up_f_128"]).all()
+    assert not (O.fme_upsample(g["a"], wrap=True) == g["up_f_a"]).all()   # the wrap is observable
+
+
+ME_VARIANTS = ["fme_cif_vbs0", "fme_96x128_vbs1", "fme_64x96_sr4_vbs1", "fme_64x96_nref2", "fast_cif_vbs0",
+               "fast_cif_vbs1", "fast_cif_nref2_vbs1", "fast_fme_cif_vbs1", "fast_par2_cif"]
+
+
+def me_variant(name):
+    g = golden("inter_me_variants.npz")
+    h, w, sr, vbs, fast, fme, nref, pm = (int(v) for v in g[f"{name}__cfg"])
+    me_mode = 0 if not fast else (2 if pm == 2 else 1)
+    return g, dict(sr=sr, vbs=bool(vbs), me_mode=me_mode, fme=bool(fme), nref=nref)
+
+
+@pytest.mark.parametrize("name", ME_VARIANTS)
+def test_inter_frame_me_variants(name):
+    g, c = me_variant(name)
+    refs = list(g[f"{name}__refs"])
+    r = O.inter_frame(g[f"{name}__cur"], refs, sr=c["sr"], qp=4, vbs=c["vbs"], me_mode=c["me_mode"], fme=c["fme"])
+    for k in ("split", "mv", "qtc", "tokens", "recon"):
+        assert (r[k] == g[f"{name}__{k}"]).all(), k
+    avg = float("inf") if (r["mae_num"] < 0).any() else (r["mae_num"].sum() / 256) / len(r["mae_num"])
+    assert avg == float(g[f"{name}__avg_mae"])
+    if c["fme"]:
+        rec = O.inter_recon(refs, r["split"], r["mv"], r["qtc"], 16, 4, fme=True)
+        assert (rec == r["recon"]).all()
+
+
+@pytest.mark.parametrize("name,cfg", [
+    ("gop_fme_vbs1", dict(qp=4, intra_dur=3, vbs=True, fme=True)),
+    ("gop_fast_vbs1", dict(qp=4, intra_dur=4, vbs=True, fast_me=True)),
+    ("gop_fast_fme", dict(qp=4, intra_dur=3, vbs=False, fast_me=True, fme=True)),
+])
+def test_gop_me_variants(name, cfg):
+    g = golden(name + ".npz")
+    out = encode_gop(g["frames"], cfg["qp"], cfg["intra_dur"], vbs=cfg["vbs"], fast_me=cfg.get("fast_me", False),
+                     fme=cfg.get("fme", False))
+    assert [o["frame_type"] for o in out] == g["frame_type"].tolist()
+    for i, o in enumerate(out):
+        for k in ("split", "mv", "qtc", "tokens"):
+            assert (o[k] == g[f"{k}{i}"]).all(), (i, k)
+        assert (o["recon"] == g["recon"][i]).all()
+        assert o["psnr"] == pytest.approx(float(g["psnr"][i]), abs=1e-9)
+    assert (g["decoded"] == g["recon"]).all()
