@@ -142,6 +142,59 @@ int so_encode_i_rows(const uint8_t* cur, int H, int W, int bs, int sr, int by0, 
                      int32_t* out_mae_num, uint8_t* out_recon, int32_t* out_sse,
                      int32_t* scratch, void* stream);
 
+/*
+ * ---- ME variants: fast_me and FMEEnable (Encoder.py:388-406, 678-742, 1644-1651) -----------
+ *
+ * me_mode:
+ *   SO_ME_FULL      find_best_match, exhaustive +-sr (the default path above);
+ *   SO_ME_FAST      fast_me, serial branch of inter_prediction (:462-585): the 3x3
+ *                   neighbourhood of a predictor that is the previous block's mv in raster
+ *                   order (starting at (0,0,0)); a serial chain -- ONE wavefront walks the
+ *                   frame, so stripes (by0 > 0) are rejected;
+ *   SO_ME_FAST_PAR  fast_me under ParallelMode 2 (inter_prediction_parallel :587-676):
+ *                   predictor (0,0,0) for every block and nRefFrames 1 (VBS is rejected: the
+ *                   reference raises NameError there).
+ * fast_me's MAE is the chosen reference INDEX (:742): the ME record's last field is then
+ * ref * n^2 (and 0 when no candidate was valid, with mv = the predictor).
+ * fme: search the frac frame frac_me_reference_frame(refs) ((2H-1) x (2W-1)) at (2x, 2y) over
+ *   half-pel offsets in [-2sr, 2sr]; MVs are in half-pel units.  The library builds the
+ *   frame as four phase planes P_ab[i][j] = F[2i+a][2j+b] into the caller's workspace
+ *   `fme_planes` (so_fme_workspace_bytes) on every call, with
+ *   fme_wrap = 1 when every reference is a uint8 reconstruction (the reference's
+ *   `row + np.roll(row, -1)` then wraps mod 256), 0 while the list still holds the float64
+ *   all-128 start frame (Encoder.py:1798).
+ */
+#define SO_ME_FULL 0
+#define SO_ME_FAST 1
+#define SO_ME_FAST_PAR 2
+
+/* bytes of the FME workspace for nref references: nref * 4 planes of so_fme_plane_stride */
+size_t so_fme_plane_stride(int H, int W);
+size_t so_fme_workspace_bytes(int H, int W, int nref);
+
+/* The four phase planes of one reference's frac frame (frac_me_reference_frame,
+ * Encoder.py:388-403 / decoder.py:468-483) into out_planes (4 x so_fme_plane_stride). */
+int so_fme_planes(const uint8_t* ref, int H, int W, int wrap, uint8_t* out_planes, void* stream);
+
+/* so_me_full_search generalised by me_mode / fme (fme_planes: workspace, NULL unless fme). */
+int so_me_search_ex(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W, int bs,
+                    int sr, int me_mode, int fme, int fme_wrap, uint8_t* fme_planes,
+                    int32_t* out_best, int32_t* out_sub, void* stream);
+
+/* so_encode_p_rows generalised by me_mode / fme: the same outputs and scratch. */
+int so_encode_p_rows_ex(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W,
+                        int bs, int sr, int by0, int by1, int qp_rd, const int32_t* qp_row,
+                        int vbs, double lam, int me_mode, int fme, int fme_wrap,
+                        uint8_t* fme_planes, uint8_t* out_split, int16_t* out_mv,
+                        int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae_num,
+                        uint8_t* out_recon, int32_t* out_sse, int32_t* scratch, void* stream);
+
+/* Decoder P-frame reconstruction with FMEEnable (decoder.py:97-211 FME branches). */
+int so_inter_recon_ex(const uint8_t* const* refs, int nref, int H, int W, int bs, int qp,
+                      const int32_t* qp_row, int fme, int fme_wrap, uint8_t* fme_planes,
+                      const uint8_t* split, const int16_t* mv, const int16_t* qtc,
+                      uint8_t* out_recon, void* stream);
+
 /* Decoder: P-frame reconstruction from symbols (decoder.py:97-211). */
 int so_inter_recon(const uint8_t* const* refs, int nref, int H, int W, int bs, int qp,
                    const int32_t* qp_row, const uint8_t* split, const int16_t* mv,

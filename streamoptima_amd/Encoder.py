@@ -11,9 +11,13 @@ Deliberate, documented deviations ("Boundary"):
   * frames whose height/width are not multiples of block_size are padded with 128
     (pad_hw) and encoded at the padded size; the reference crashes there (Encoder.py:930);
   * the intra canvas is frame-sized (the reference hard-codes 288x352, Encoder.py:1248);
-  * fast_me, FMEEnable, intra_mode 1 and ParallelMode 1/3 raise NotImplementedError
-    (out of this round's scope; mode 1 changes semantics, mode 3 is broken upstream).
-    ParallelMode 2 is serial-identical in the reference and is accepted.
+  * intra_mode 1 and ParallelMode 1/3 raise NotImplementedError (mode 1 changes semantics,
+    mode 3 is broken upstream).  ParallelMode 2 is accepted: it is serial-identical in the
+    reference except under fast_me, where every block's predictor is (0,0,0) with one
+    reference (inter_prediction_parallel, Encoder.py:587-676) -- SO_ME_FAST_PAR; fast_me +
+    VBSEnable under ParallelMode 2 raises NameError in the reference and ValueError here.
+  * fast_me and FMEEnable run on the GPU (so_encode_p_rows_ex, so_fastme.hip / the FME
+    phase-plane search in so_me.hip).
 """
 from __future__ import annotations
 
@@ -46,10 +50,9 @@ class Y_Video_codec:
                  lam=None, VBSEnable=False, nRefFrames=1, yuv_file=None, y_only_frame_arr=None,
                  fast_me=False, FMEEnable=False, RCFlag=None, targetBR=None, frame_rate=30,
                  qp_rate_tables=None, intra_thresh=None, ParallelMode=0, device=None):
-        if fast_me:
-            raise NotImplementedError("fast_me (Encoder.py:719) is not in this round's scope")
-        if FMEEnable:
-            raise NotImplementedError("FMEEnable (fractional ME, Encoder.py:388) is not in this round's scope")
+        if fast_me and ParallelMode == 2 and VBSEnable:
+            raise ValueError("fast_me + VBSEnable under ParallelMode 2: the reference raises NameError on "
+                             "`mvp` (inter_prediction_parallel, Encoder.py:609)")
         if intra_mode not in (0,):
             raise NotImplementedError("only intra_mode 0 (horizontal) is built")
         if ParallelMode not in (0, 2):
@@ -199,8 +202,15 @@ class Y_Video_codec:
         hp, wp = self._geometry()
         if self._engine is None or (self._engine.h, self._engine.w) != (hp, wp):
             self._engine = Engine(hp, wp, self.block_size, self.search_range, self.VBSEnable, self.lam,
-                                  self.device)
+                                  self.device, me_mode=self._me_mode(), fme=bool(self.FMEEnable))
         return self._engine
+
+    def _me_mode(self) -> int:
+        """SO_ME_* of this configuration (include/streamoptima.h)."""
+        from . import _lib
+        if not self.fast_me:
+            return _lib.ME_FULL
+        return _lib.ME_FAST_PAR if self.ParallelMode == 2 else _lib.ME_FAST
 
     def _upload_padded(self, arr) -> torch.Tensor:
         """host frames -> [F, Hp, Wp] uint8 planes in HBM (pad_hw with 128)."""
@@ -233,7 +243,9 @@ class Y_Video_codec:
         refs = [self._upload_padded(np.asarray(r))[0] for r in ref_frames]
         qp_rd = self.Qp
         qp_row = self.row_qp_schedule(eng.nby) if self._rc_on() else None
-        sym = eng.encode_p(cur, refs, qp_rd, qp_row)
+        # frac frame wrap: the caller's list is uint8 unless it holds a float array
+        wrap = all(np.asarray(r).dtype == np.uint8 for r in ref_frames)
+        sym = eng.encode_p(cur, refs, qp_rd, qp_row, fme_wrap=wrap)
         if qp_row:
             self.set_Qp(qp_row[-1])
         return self._flow_tuple(sym, intra=False, stats=generate_row_wise_stats)
@@ -318,6 +330,9 @@ class Y_Video_codec:
         eng = self.engine()
         nframes = frames_dev.shape[0]
         ref_frames = [alloc_planes(1, eng.h, eng.w, self.device, fill=128)[0]]
+        # the start frame is float64 in the reference (Encoder.py:1798): while it is in the
+        # list the FME frac frame does not wrap its uint8 row sums (so_encode_p_rows_ex)
+        ref_float = [True]
         out_syms, ftypes, qp_rows = [], [], []
         rc_on = self._rc_on()
         qp_sched = self.row_qp_schedule(eng.nby) if rc_on else None
@@ -333,7 +348,7 @@ class Y_Video_codec:
             else:
                 sym = eng.encode_p(cur, ref_frames, self.Qp, qp_sched,
                                    out=pre if pre is not None and pre.frame_type == 1 else None,
-                                   qp_row_dev=qp_sched_dev)
+                                   qp_row_dev=qp_sched_dev, fme_wrap=not any(ref_float))
                 if self.RCFlag is not None and self.RCFlag > 1:
                     residual_size = int(sym.tokens.sum().item())
                     if residual_size > self.intra_thresh:
@@ -349,7 +364,9 @@ class Y_Video_codec:
             if i < nframes - 1:
                 if len(ref_frames) >= self.nRefFrames:
                     ref_frames.pop(0)
+                    ref_float.pop(0)
                 ref_frames.append(sym.recon)
+                ref_float.append(False)
         # per-block / per-row SSE came out of the encode kernels; one reduction per GOP
         sse = torch.stack([s.sse for s in out_syms]).sum(dim=1, dtype=torch.int64)
         return {"symbols": out_syms, "sse": sse, "frame_type": ftypes, "qp_rows": qp_rows}

@@ -46,7 +46,17 @@ _SIGS = {
     "so_inter_recon": ([_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "so_intra_recon": ([_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "so_sse_u8": ([_vp, _vp, ctypes.c_int64, _vp, _vp], _i),
+    "so_fme_plane_stride": ([_i, _i], _sz),
+    "so_fme_workspace_bytes": ([_i, _i, _i], _sz),
+    "so_fme_planes": ([_vp, _i, _i, _i, _vp, _vp], _i),
+    "so_me_search_ex": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp], _i),
+    "so_encode_p_rows_ex": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _d, _i, _i, _i, _vp, _vp, _vp,
+                             _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
+    "so_inter_recon_ex": ([_vp, _i, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp], _i),
 }
+
+# ME modes (include/streamoptima.h)
+ME_FULL, ME_FAST, ME_FAST_PAR = 0, 1, 2
 
 EXPORTED = tuple(_SIGS)
 

@@ -67,6 +67,41 @@ SO_DEV void fetch_row(const uint8_t* __restrict__ f, int W, int H, int px, int p
     }
 }
 
+// FME prediction row `row` of an NB x NB block at frac-frame position (px, py) -- the
+// FMEEnable branches of calculate_inter_frame_residual (Encoder.py:444-456) and
+// reconstruct_frame (:862-873, :907-919), on the reference's four phase planes
+// P_ab[i][j] = F[2i+a][2j+b] (`planes`, pstride bytes apart; so_me.hip FmePhase):
+//   0 <= px < W2-NB (and y)  and  0 <= px+ext < W2-lim (and y)  -> stride-2 sample of F,
+//                                                                = a row of P_ab;
+//   only the first                                              -> all 128;
+//   neither (handle_boundary_conditions :750-768)               -> F's contiguous bytes,
+//                                                                zero outside F.
+// (ext, lim) = (2 NB, NB) for the residual and the unsplit recon; a split sub-block's
+// recon uses the full block's (BS, BS).
+template <int NB>
+SO_DEV void fetch_row_fme(const uint8_t* __restrict__ planes, size_t pstride, int W, int H, int px, int py, int row,
+                          int ext, int lim, int* out) {
+    const int W2 = 2 * W - 1, H2 = 2 * H - 1;
+    if (0 <= px && px < W2 - NB && 0 <= py && py < H2 - NB) {
+        if (0 <= px + ext && px + ext < W2 - lim && 0 <= py + ext && py + ext < H2 - lim) {
+            const uint8_t* pl = planes + (size_t)(2 * (py & 1) + (px & 1)) * pstride;
+            fetch_row<NB>(pl, W, H, px >> 1, (py >> 1) + row, true, out);
+        } else {
+#pragma unroll
+            for (int k = 0; k < NB; ++k) out[k] = 128;
+        }
+    } else {
+        const int Y = py + row;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            const int X = px + k;
+            out[k] = (Y >= 0 && Y < H2 && X >= 0 && X < W2)
+                         ? planes[(size_t)(2 * (Y & 1) + (X & 1)) * pstride + (size_t)(Y >> 1) * W + (X >> 1)]
+                         : 0;
+        }
+    }
+}
+
 // aligned row of the current frame (x multiple of NB, W multiple of NB)
 template <int NB>
 SO_DEV void load_cur_row(const uint8_t* __restrict__ f, int W, int x, int y, int* out) {

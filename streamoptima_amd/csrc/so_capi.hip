@@ -19,13 +19,20 @@ void set_error(const char* fmt, ...) {
 
 int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, int bs, int sr, int by0, int by1,
               int32_t* out_best, int32_t* out_sub, hipStream_t st);
-int inter_tq_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int bs, int by0, int by1,
-                    const int32_t* best, const int32_t* sub, int qp_rd, const int32_t* qp_row, int vbs,
-                    double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
+int me_generic_launch(const uint8_t* cur, const RefSet& refs, const uint8_t* planes, size_t pstride, int nref, int H,
+                      int W, int bs, int sr, int by0, int by1, int32_t* out_best, int32_t* out_sub, hipStream_t st);
+int me_fme_launch(const uint8_t* cur, const uint8_t* planes, size_t pstride, int nref, int H, int W, int by0, int by1,
+                  int32_t* out_best, int32_t* out_sub, hipStream_t st);
+int fme_planes_launch(const uint8_t* ref, int H, int W, int wrap, uint8_t* out, size_t pstride, hipStream_t st);
+int me_fastpred_launch(const uint8_t* cur, const uint8_t* const* ptrs, int nptr, int nref, int H, int W, int bs,
+                       int fme, int by0, int by1, int serial, int32_t* out_best, int32_t* out_sub, hipStream_t st);
+int inter_tq_launch(const uint8_t* cur, const RefSet& refs, const uint8_t* planes, size_t pstride, int H, int W,
+                    int bs, int by0, int by1, const int32_t* best, const int32_t* sub, int qp_rd, const int32_t* qp_row,
+                    int vbs, double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
                     int32_t* out_mae, uint8_t* out_recon, int32_t* out_sse, hipStream_t st);
-int inter_recon_launch(const RefSet& refs, int H, int W, int bs, int qp, const int32_t* qp_row,
-                       const uint8_t* split, const int16_t* mv, const int16_t* qtc, uint8_t* out_recon,
-                       hipStream_t st);
+int inter_recon_launch(const RefSet& refs, const uint8_t* planes, size_t pstride, int H, int W, int bs, int qp,
+                       const int32_t* qp_row, const uint8_t* split, const int16_t* mv, const int16_t* qtc,
+                       uint8_t* out_recon, hipStream_t st);
 int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int by0, int by1, int qp_rd,
                         const int32_t* qp_row, int vbs, double lam, uint8_t* out_split, int16_t* out_mv,
                         int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon,
@@ -187,7 +194,7 @@ int so_inter_tq_recon(const uint8_t* cur, const uint8_t* const* refs, int nref, 
             set_error("%s: out_recon aliases refs[%d]", fn, i);
             return SO_E_INVALID;
         }
-    return inter_tq_launch(cur, rs, H, W, bs, 0, H / bs, best, vbs ? sub : nullptr, qp_rd, qp_row, vbs, lam,
+    return inter_tq_launch(cur, rs, nullptr, 0, H, W, bs, 0, H / bs, best, vbs ? sub : nullptr, qp_rd, qp_row, vbs, lam,
                            out_split, out_mv, out_qtc, out_tokens, out_mae_num, out_recon, out_sse,
                            (hipStream_t)stream);
 }
@@ -221,8 +228,8 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
     int32_t* sub = vbs ? scratch + nbs * 4 : nullptr;
     hipStream_t st = (hipStream_t)stream;
     SO_TRY(me_launch(cur, rs, nref, H, W, bs, sr, by0, by1, best, sub, st));
-    return inter_tq_launch(cur, rs, H, W, bs, by0, by1, best, sub, qp_rd, qp_row, vbs, lam, out_split, out_mv,
-                           out_qtc, out_tokens, out_mae_num, out_recon, out_sse, st);
+    return inter_tq_launch(cur, rs, nullptr, 0, H, W, bs, by0, by1, best, sub, qp_rd, qp_row, vbs, lam, out_split,
+                           out_mv, out_qtc, out_tokens, out_mae_num, out_recon, out_sse, st);
 }
 
 int so_encode_p_frame(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W, int bs, int sr,
@@ -279,7 +286,7 @@ int so_inter_recon(const uint8_t* const* refs, int nref, int H, int W, int bs, i
     SO_NEED(split, fn); SO_NEED(mv, fn); SO_NEED(qtc, fn); SO_NEED(out_recon, fn);
     RefSet rs;
     SO_TRY(make_refs(fn, refs, nref, &rs));
-    return inter_recon_launch(rs, H, W, bs, qp, qp_row, split, mv, qtc, out_recon, (hipStream_t)stream);
+    return inter_recon_launch(rs, nullptr, 0, H, W, bs, qp, qp_row, split, mv, qtc, out_recon, (hipStream_t)stream);
 }
 
 int so_intra_recon(int H, int W, int bs, int qp, const int32_t* qp_row, const uint8_t* split, const int16_t* mv,
@@ -291,6 +298,131 @@ int so_intra_recon(int H, int W, int bs, int qp, const int32_t* qp_row, const ui
     SO_NEED(split, fn); SO_NEED(mv, fn); SO_NEED(qtc, fn); SO_NEED(out_recon, fn); SO_NEED(scratch, fn);
     // the recon kernel only needs sr to size its ring: the largest reachable offset is 64
     return intra_recon_launch(H, W, bs, 64, qp, qp_row, split, mv, qtc, out_recon, scratch, (hipStream_t)stream);
+}
+
+size_t so_fme_plane_stride(int H, int W) {
+    if (H <= 0 || W <= 0) return 0;
+    return (((size_t)H * W + 64) + 255) & ~(size_t)255;   // 64 B of slack for aligned row reads
+}
+
+size_t so_fme_workspace_bytes(int H, int W, int nref) {
+    return nref <= 0 ? 0 : (size_t)nref * 4 * so_fme_plane_stride(H, W);
+}
+
+int so_fme_planes(const uint8_t* ref, int H, int W, int wrap, uint8_t* out_planes, void* stream) {
+    const char* fn = "so_fme_planes";
+    SO_NEED(ref, fn); SO_NEED(out_planes, fn);
+    if (H <= 1 || W <= 1 || W % 4) {
+        set_error("%s: frame %dx%d (W must be a multiple of 4)", fn, W, H);
+        return SO_E_INVALID;
+    }
+    return fme_planes_launch(ref, H, W, wrap, out_planes, so_fme_plane_stride(H, W), (hipStream_t)stream);
+}
+
+// shared validation + dispatch of the ME variants into best / sub
+static int me_ex(const char* fn, const uint8_t* cur, const uint8_t* const* refs, int nref, const RefSet& rs, int H,
+                 int W, int bs, int sr, int by0, int by1, int me_mode, int fme, int fme_wrap, uint8_t* planes,
+                 int32_t* best, int32_t* sub, hipStream_t st) {
+    if (me_mode < SO_ME_FULL || me_mode > SO_ME_FAST_PAR) {
+        set_error("%s: me_mode %d", fn, me_mode);
+        return SO_E_INVALID;
+    }
+    if (me_mode == SO_ME_FAST_PAR && sub) {
+        set_error("%s: fast_me under ParallelMode 2 with VBSEnable (the reference raises NameError, "
+                  "Encoder.py:609)", fn);
+        return SO_E_UNSUPPORTED;
+    }
+    if (me_mode == SO_ME_FAST && by0 != 0) {
+        set_error("%s: fast_me's predictor chain runs over the whole frame (no stripes)", fn);
+        return SO_E_UNSUPPORTED;
+    }
+    const size_t ps = so_fme_plane_stride(H, W);
+    if (fme) {
+        SO_NEED(planes, fn);
+        if (me_mode == SO_ME_FULL && sr > 63) {
+            set_error("%s: FME search_range %d > 63", fn, sr);
+            return SO_E_UNSUPPORTED;
+        }
+        for (int r = 0; r < nref; ++r)
+            SO_TRY(fme_planes_launch(refs[r], H, W, fme_wrap, planes + (size_t)r * 4 * ps, ps, st));
+    }
+    if (me_mode == SO_ME_FULL) {
+        if (!fme) return me_launch(cur, rs, nref, H, W, bs, sr, by0, by1, best, sub, st);
+        if (bs == 16 && sr == 16) return me_fme_launch(cur, planes, ps, nref, H, W, by0, by1, best, sub, st);
+        return me_generic_launch(cur, rs, planes, ps, nref, H, W, bs, sr, by0, by1, best, sub, st);
+    }
+    const uint8_t* ptrs[4 * kMaxRef];
+    const int nfast = me_mode == SO_ME_FAST_PAR ? 1 : nref;
+    int nptr = 0;
+    for (int r = 0; r < nfast; ++r) {
+        if (fme)
+            for (int p = 0; p < 4; ++p) ptrs[nptr++] = planes + (size_t)(4 * r + p) * ps;
+        else
+            ptrs[nptr++] = refs[r];
+    }
+    return me_fastpred_launch(cur, ptrs, nptr, nfast, H, W, bs, fme, by0, by1, me_mode == SO_ME_FAST, best, sub, st);
+}
+
+int so_me_search_ex(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W, int bs, int sr,
+                    int me_mode, int fme, int fme_wrap, uint8_t* fme_planes, int32_t* out_best, int32_t* out_sub,
+                    void* stream) {
+    const char* fn = "so_me_search_ex";
+    SO_TRY(check_geom(fn, H, W, bs, out_sub != nullptr));
+    SO_TRY(check_sr(fn, sr));
+    SO_NEED(cur, fn);
+    SO_NEED(out_best, fn);
+    RefSet rs;
+    SO_TRY(make_refs(fn, refs, nref, &rs));
+    return me_ex(fn, cur, refs, nref, rs, H, W, bs, sr, 0, H / bs, me_mode, fme, fme_wrap, fme_planes, out_best,
+                 out_sub, (hipStream_t)stream);
+}
+
+int so_encode_p_rows_ex(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W, int bs, int sr,
+                        int by0, int by1, int qp_rd, const int32_t* qp_row, int vbs, double lam, int me_mode, int fme,
+                        int fme_wrap, uint8_t* fme_planes, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc,
+                        int32_t* out_tokens, int32_t* out_mae_num, uint8_t* out_recon, int32_t* out_sse,
+                        int32_t* scratch, void* stream) {
+    const char* fn = "so_encode_p_rows_ex";
+    if (me_mode == SO_ME_FULL && !fme)
+        return so_encode_p_rows(cur, refs, nref, H, W, bs, sr, by0, by1, qp_rd, qp_row, vbs, lam, out_split, out_mv,
+                                out_qtc, out_tokens, out_mae_num, out_recon, out_sse, scratch, stream);
+    SO_TRY(check_geom(fn, H, W, bs, vbs));
+    SO_TRY(check_sr(fn, sr));
+    SO_TRY(check_qp(fn, qp_rd));
+    SO_TRY(check_rows(fn, H, bs, by0, by1));
+    SO_NEED(cur, fn); SO_NEED(scratch, fn); SO_NEED(out_split, fn); SO_NEED(out_mv, fn);
+    SO_NEED(out_qtc, fn); SO_NEED(out_tokens, fn); SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn);
+    RefSet rs;
+    SO_TRY(make_refs(fn, refs, nref, &rs));
+    for (int i = 0; i < nref; ++i)
+        if (refs[i] == out_recon) {
+            set_error("%s: out_recon aliases refs[%d]", fn, i);
+            return SO_E_INVALID;
+        }
+    const size_t nbs = (size_t)(W / bs) * (size_t)(by1 - by0);
+    int32_t* best = scratch;
+    int32_t* sub = vbs ? scratch + nbs * 4 : nullptr;
+    hipStream_t st = (hipStream_t)stream;
+    SO_TRY(me_ex(fn, cur, refs, nref, rs, H, W, bs, sr, by0, by1, me_mode, fme, fme_wrap, fme_planes, best, sub, st));
+    return inter_tq_launch(cur, rs, fme ? fme_planes : nullptr, so_fme_plane_stride(H, W), H, W, bs, by0, by1, best,
+                           sub, qp_rd, qp_row, vbs, lam, out_split, out_mv, out_qtc, out_tokens, out_mae_num, out_recon,
+                           out_sse, st);
+}
+
+int so_inter_recon_ex(const uint8_t* const* refs, int nref, int H, int W, int bs, int qp, const int32_t* qp_row,
+                      int fme, int fme_wrap, uint8_t* fme_planes, const uint8_t* split, const int16_t* mv,
+                      const int16_t* qtc, uint8_t* out_recon, void* stream) {
+    const char* fn = "so_inter_recon_ex";
+    if (!fme) return so_inter_recon(refs, nref, H, W, bs, qp, qp_row, split, mv, qtc, out_recon, stream);
+    SO_TRY(check_geom(fn, H, W, bs, 0));
+    SO_TRY(check_qp(fn, qp));
+    SO_NEED(split, fn); SO_NEED(mv, fn); SO_NEED(qtc, fn); SO_NEED(out_recon, fn); SO_NEED(fme_planes, fn);
+    RefSet rs;
+    SO_TRY(make_refs(fn, refs, nref, &rs));
+    const size_t ps = so_fme_plane_stride(H, W);
+    hipStream_t st = (hipStream_t)stream;
+    for (int r = 0; r < nref; ++r) SO_TRY(fme_planes_launch(refs[r], H, W, fme_wrap, fme_planes + (size_t)r * 4 * ps, ps, st));
+    return inter_recon_launch(rs, fme_planes, ps, H, W, bs, qp, qp_row, split, mv, qtc, out_recon, st);
 }
 
 int so_sse_u8(const uint8_t* a, const uint8_t* b, int64_t n, uint64_t* out_sse, void* stream) {

@@ -1,0 +1,174 @@
+// so_fastme.hip — fast_me (Encoder.py:719-742) for gfx950, integer-pel and FME.
+//
+// fast_motion_estimation searches the 3x3 neighbourhood of a predictor mvp over
+// refs[:nRefFrames], at (x, y) -- or (2x, 2y) on the frac frame with FME:
+//   * candidate (dx, dy) in mvp + {-1, 0, 1}^2 (ref outer, dx middle, dy inner) is valid iff
+//       0 <= X+dx < PW-n  and  0 <= X+dx+2n < PW-n   (and the same for y)
+//     -- the second test is the reference's FME bound, applied even without FME (:727);
+//   * the strictly smaller MAE wins: the first found minimum in scan order;
+//   * it returns (best_mv, best_ref_idx): best_mv = mvp when no candidate is valid, and the
+//     caller uses best_ref_idx AS THE BLOCK'S MAE (:742).  The kernels therefore write
+//     (dx, dy, ref, ref * n * n) into the ME record -- so_inter_tq_recon reads the last
+//     field as MAE * n^2 -- and (mvp.dx, mvp.dy, mvp.ref, 0) when nothing is valid.
+// The predictor chain of inter_prediction's serial branch (:462-585): mvp starts at
+// (0, 0, 0) and becomes each block's full-block mv in raster order (:581); the VBS
+// sub-blocks of a block use the same mvp as the block itself.  This is a true serial
+// dependence, so `serial` runs ONE wavefront along the frame; its loads for a block depend
+// only on the previous block's mv.  Under ParallelMode 2 (inter_prediction_parallel
+// :587-676) every block's mvp is (0, 0, 0) with nRefFrames 1: one wavefront per block.
+//
+// Lane mapping: a bs x bs block is (row i, dword c) -> lane i * (bs/4) + c; the four
+// (bs/2) sub-blocks of VBS take one 16-lane DPP row each (bs 16) with the same mapping.
+// A lane reads its 4 reference bytes as two aligned dwords + v_alignbyte (any column);
+// with FME the stride-2 sample of F at (X+dx, Y+dy) is 4 CONSECUTIVE bytes of phase plane
+// P_ab (a = (Y+dy) & 1, b = (X+dx) & 1), see so_me.hip FmePhase.
+#include "so_common.h"
+
+namespace so {
+
+struct FastRefs {
+    const uint8_t* p[4 * kMaxRef];   // integer: refs; FME: phase planes 4 r + 2a + b
+};
+
+SO_DEV uint32_t unaligned_u32(const uint8_t* p) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+    return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+}
+
+// sum over aligned groups of G lanes, result in every lane of the group
+template <int G>
+SO_DEV uint32_t group_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int m = 1; m < G; m <<= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+
+struct Mvp {
+    int dx, dy, ref;
+};
+
+// One fast search of an n x n block at frame position (x, y) by the lanes of a G-lane
+// group; (lane_i, lane_c) = the lane's block row / dword, `act` = the lane holds pixels.
+// Writes the record (dx, dy, ref, mae * n * n), identical in every lane of the group.
+template <bool FME, int G>
+SO_DEV void fast_search(const uint8_t* __restrict__ cur, const FastRefs& R, int nref, int H, int W, int x, int y,
+                        int n, Mvp mvp, int lane_i, int lane_c, bool act, int32_t out[4]) {
+    const int k = FME ? 2 : 1;
+    const int PW = FME ? 2 * W - 1 : W, PH = FME ? 2 * H - 1 : H;
+    const int X = k * x, Y = k * y;
+    uint32_t cw = 0;
+    if (act) cw = *reinterpret_cast<const uint32_t*>(cur + (size_t)(y + lane_i) * W + x + 4 * lane_c);
+    uint32_t best = 0xFFFFFFFFu;   // (sad << 8) | candidate index r * 9 + ci
+    for (int r = 0; r < nref; ++r) {
+#pragma unroll
+        for (int ci = 0; ci < 9; ++ci) {
+            const int dx = mvp.dx - 1 + ci / 3, dy = mvp.dy - 1 + ci % 3;
+            const int px = X + dx, py = Y + dy;
+            const bool ok = 0 <= px && px < PW - n && 0 <= py && py < PH - n && px + 2 * n < PW - n &&
+                            py + 2 * n < PH - n;   // uniform over the group
+            if (!ok) continue;
+            uint32_t s = 0;
+            if (act) {
+                const uint8_t* p;
+                if constexpr (FME) {
+                    p = R.p[4 * r + 2 * (py & 1) + (px & 1)] + (size_t)((py >> 1) + lane_i) * W + (px >> 1) +
+                        4 * lane_c;
+                } else {
+                    p = R.p[r] + (size_t)(py + lane_i) * W + px + 4 * lane_c;
+                }
+                s = __builtin_amdgcn_sad_u8(cw, unaligned_u32(p), 0u);
+            }
+            s = group_sum_u32<G>(s);
+            const uint32_t key = (s << 8) | (uint32_t)(r * 9 + ci);
+            best = key < best ? key : best;
+        }
+    }
+    if (best == 0xFFFFFFFFu) {
+        out[0] = mvp.dx; out[1] = mvp.dy; out[2] = mvp.ref; out[3] = 0;
+    } else {
+        const int c = (int)(best & 255), r = c / 9, ci = c % 9;
+        out[0] = mvp.dx - 1 + ci / 3; out[1] = mvp.dy - 1 + ci % 3; out[2] = r; out[3] = r * n * n;
+    }
+}
+
+// bs 16: full block on 64 lanes (row l >> 2, dword l & 3); sub-blocks on the four 16-lane
+// rows (sub j = l >> 4, row (l >> 1) & 7, dword l & 1).  bs 8: full block on lanes 0..15
+// (row l >> 1, dword l & 1); 4x4 sub-blocks on 4 lanes each (sub l >> 2, row l & 3).
+// Returns the full block's mv (the next predictor of the serial chain), uniform.
+template <bool FME, bool SUB, int BS>
+SO_DEV Mvp fast_block(const uint8_t* __restrict__ cur, const FastRefs& R, int nref, int H, int W, int x, int y,
+                      Mvp mvp, int lane, int32_t* __restrict__ ob, int32_t* __restrict__ os) {
+    constexpr int SBS = BS / 2;
+    if constexpr (SUB) {
+        if (x != 0 && y != 0) {
+            int32_t rec[4];
+            int j, i, c;
+            if constexpr (BS == 16) { j = lane >> 4; i = (lane >> 1) & 7; c = lane & 1; }
+            else { j = (lane >> 2) & 3; i = lane & 3; c = 0; }
+            const bool act = BS == 16 || lane < 16;
+            const int xs = x + (j & 1) * SBS, ys = y + (j >> 1) * SBS;
+            fast_search<FME, BS == 16 ? 16 : 4>(cur, R, nref, H, W, xs, ys, SBS, mvp, i, c, act, rec);
+            const int lj = BS == 16 ? 16 * j : 4 * j;
+            const int e = lane - lj;   // lanes lj .. lj+3 store the sub-block's record
+            const int32_t v = e == 0 ? rec[0] : e == 1 ? rec[1] : e == 2 ? rec[2] : rec[3];
+            if (act && e >= 0 && e < 4) os[j * 4 + e] = v;
+        }
+    }
+    int32_t rec[4];
+    const int i = BS == 16 ? lane >> 2 : lane >> 1, c = BS == 16 ? lane & 3 : lane & 1;
+    const bool act = BS == 16 || lane < 16;
+    fast_search<FME, BS == 16 ? 64 : 16>(cur, R, nref, H, W, x, y, BS, mvp, i, c, act, rec);
+    const int32_t v = lane == 0 ? rec[0] : lane == 1 ? rec[1] : lane == 2 ? rec[2] : rec[3];
+    if (lane < 4) ob[lane] = v;
+    // the record is identical in the lanes of the block's group; lane 0 is in it
+    return Mvp{__shfl(rec[0], 0, 64), __shfl(rec[1], 0, 64), __shfl(rec[2], 0, 64)};
+}
+
+template <bool FME, bool SUB, int BS>
+__global__ void __launch_bounds__(256)
+me_fastpred_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, int H, int W, int by0, int by1, int serial,
+                   int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub) {
+    const int nbx = W / BS, nb = nbx * (by1 - by0);
+    const int lane = threadIdx.x & 63;
+    if (serial) {
+        // one wavefront walks the range in raster order; mvp = the previous block's mv
+        if (blockIdx.x != 0 || threadIdx.x >= 64) return;
+        Mvp mvp{0, 0, 0};
+        for (int b = 0; b < nb; ++b) {
+            const int x = (b % nbx) * BS, y = (by0 + b / nbx) * BS;
+            mvp = fast_block<FME, SUB, BS>(cur, R, nref, H, W, x, y, mvp, lane, out_best + (size_t)b * 4,
+                                           out_sub ? out_sub + (size_t)b * 16 : nullptr);
+        }
+        return;
+    }
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);   // one wave per block, mvp (0,0,0)
+    if (b >= nb) return;
+    const int x = (b % nbx) * BS, y = (by0 + b / nbx) * BS;
+    fast_block<FME, SUB, BS>(cur, R, nref, H, W, x, y, Mvp{0, 0, 0}, lane, out_best + (size_t)b * 4,
+                             out_sub ? out_sub + (size_t)b * 16 : nullptr);
+}
+
+int me_fastpred_launch(const uint8_t* cur, const uint8_t* const* ptrs, int nptr, int nref, int H, int W, int bs,
+                       int fme, int by0, int by1, int serial, int32_t* out_best, int32_t* out_sub, hipStream_t st) {
+    FastRefs R{};
+    for (int i = 0; i < nptr && i < 4 * kMaxRef; ++i) R.p[i] = ptrs[i];
+    const int nb = (W / bs) * (by1 - by0);
+    if (nb <= 0) return SO_OK;
+    const dim3 grid(serial ? 1 : (nb + 3) / 4), blk(serial ? 64 : 256);
+    const bool sub = out_sub != nullptr;
+#define SO_FASTPRED(F, S, B)                                                                                 \
+    hipLaunchKernelGGL((me_fastpred_kernel<F, S, B>), grid, blk, 0, st, cur, R, nref, H, W, by0, by1, serial, \
+                       out_best, out_sub)
+    if (bs == 16) {
+        if (fme) { if (sub) SO_FASTPRED(true, true, 16); else SO_FASTPRED(true, false, 16); }
+        else { if (sub) SO_FASTPRED(false, true, 16); else SO_FASTPRED(false, false, 16); }
+    } else {
+        if (fme) { if (sub) SO_FASTPRED(true, true, 8); else SO_FASTPRED(true, false, 8); }
+        else { if (sub) SO_FASTPRED(false, true, 8); else SO_FASTPRED(false, false, 8); }
+    }
+#undef SO_FASTPRED
+    return check_launch("me_fastpred_kernel");
+}
+
+}  // namespace so

@@ -125,7 +125,11 @@ SO_DEV void acc_fence_n(uint32_t (&a)[N]) {
 // X = 31 for the dy <= 0 half (|dy| = 16 - t) and 0 for the other (|dy| = t) -- within a
 // lane dx and ref are fixed, so (sad, this code) orders exactly like (sad, |dx|+|dy|, scan).
 // di valid in [dlo, dhi] (di = 16*hh + t); `edge` selects the masked form.
-SO_DEV uint32_t lane_best17(const uint32_t (&a)[17], uint32_t X, int hh, int dlo, int dhi, bool edge) {
+// `ex16`: drop t = 16 of the lower half (the duplicate dy = 0 row) -- the FME row phase
+// a = 1 maps it to dy = +1 half-pel, which the upper half's t = 0 already covers, and
+// keeping it would break the lane's |dy| order (|-1| == |+1| at t = 15 and t = 16).
+SO_DEV uint32_t lane_best17(const uint32_t (&a)[17], uint32_t X, int hh, int dlo, int dhi, bool edge,
+                            bool ex16 = false) {
     uint32_t best = 0xFFFFFFFFu;
     if (!edge) {
 #pragma unroll
@@ -138,11 +142,43 @@ SO_DEV uint32_t lane_best17(const uint32_t (&a)[17], uint32_t X, int hh, int dlo
         for (int t = 0; t < 17; ++t) {
             const int di = 16 * hh + t;
             uint32_t k = ((a[t] << 5) | (uint32_t)t) ^ X;
-            k = (di < dlo || di > dhi) ? 0xFFFFFFFFu : k;
+            k = (di < dlo || di > dhi || (t == 16 && ex16 && hh == 0)) ? 0xFFFFFFFFu : k;
             best = k < best ? k : best;
         }
     }
     return best;
+}
+
+// ---- FME (FMEEnable, Encoder.py:388-403, 697-705, 1647-1651) ---------------------------------
+// The frac frame F ((2H-1) x (2W-1)) is searched at (2x, 2y) over half-pel offsets in
+// [-2sr, 2sr] with the block sampled every other row and column.  Candidate (dxh, dyh)
+// reads F[2y+dyh+2i][2x+dxh+2j] = P_ab[y+v+i][x+u+j] with dyh = 2v+a, dxh = 2u+b and the
+// phase planes P_ab[i][j] = F[2i+a][2j+b] (so_fme_planes).  So the half-pel search is four
+// integer-pel searches (u, v in [-16, 16]) over the four planes, with a candidate map:
+//   valid   |dxh| <= 2sr and 0 <= 2x+dxh <= 2W-3bs-2 (the reference's strict bound plus
+//           its FME bound 0 <= X+dx+2bs < W2-bs, :698); the same for y;
+//   key     (SAD, |dxh|+|dyh|, ref, (dxh+2sr)(4sr+1)+(dyh+2sr)), decoded with sr' = 2sr.
+struct FmePhase {
+    int a, b;
+};
+
+SO_DEV bool fme_xok(int x, int dxi, int b, int W, int bsz) {
+    const int dxh = 2 * (dxi - 16) + b;
+    return dxh >= -32 && dxh <= 32 && 2 * x + dxh >= 0 && 2 * x + dxh <= 2 * W - 3 * bsz - 2;
+}
+
+// valid dy indices di in [dlo, dhi] (dyh = 2(di-16)+a)
+SO_DEV void fme_drange(int y, int a, int H, int bsz, int& dlo, int& dhi) {
+    int lo = -2 * y;             lo = lo < -32 ? -32 : lo;
+    int hi = 2 * H - 3 * bsz - 2 - 2 * y; hi = hi > 32 ? 32 : hi;
+    dlo = (lo + 33 - a) >> 1;    // ceil((lo + 32 - a) / 2)
+    dhi = (hi + 32 - a) >> 1;    // floor, arithmetic shift
+}
+
+SO_DEV uint64_t fme_key(uint32_t sad, int dxi, int di, FmePhase ph, int ref) {
+    const int dxh = 2 * (dxi - 16) + ph.b, dyh = 2 * (di - 16) + ph.a;
+    const uint32_t l1 = (uint32_t)((dxh < 0 ? -dxh : dxh) + (dyh < 0 ? -dyh : dyh));
+    return me_key(sad, l1, (uint32_t)ref, (uint32_t)((dxh + 32) * 65 + (dyh + 32)));
 }
 
 // Widen a lane's phase-1 best to the 64-bit reference key (kNoKey if none / dx invalid).
@@ -154,12 +190,19 @@ SO_DEV uint64_t widen17(uint32_t b32, uint32_t X, int hh, int xi, bool xok, int 
     return me_key(sad, l1, (uint32_t)ref, (uint32_t)(xi * 33 + di));
 }
 
+SO_DEV uint64_t widen17_fme(uint32_t b32, uint32_t X, int hh, int xi, bool xok, int ref, FmePhase ph) {
+    if (!xok || b32 == 0xFFFFFFFFu) return kNoKey;
+    const uint32_t t = (b32 & 31) ^ X, sad = b32 >> 5;
+    return fme_key(sad, xi, 16 * hh + (int)t, ph, ref);
+}
+
 // Dense search of one block by one wavefront (phase 1 + phase 2 over the four shifted
 // window copies in `win`); merges the block key into keys[u] and, with VBS, the quadrant
 // keys into keys[nblk + 4u + j].  Shared by me_wave_kernel and me_sea_kernel's fallback.
-template <int BS, bool SUB, int RPD, int CS>
+template <int BS, bool SUB, int RPD, int CS, bool FME = false>
 SO_DEV void wave_dense_block(const uint32_t* win, unsigned long long* keys, int nblk, const uint8_t* __restrict__ cur,
-                             int W, int H, int x, int y, int bxl, int byl, int u, int tid, int r) {
+                             int W, int H, int x, int y, int bxl, int byl, int u, int tid, int r,
+                             FmePhase ph = FmePhase{0, 0}) {
     constexpr int SR = 16, NT = 17;
     constexpr int NDW = BS / 4, HALF = 8, NPASS = BS / HALF, NR = NT + HALF - 1;
     // lane identity re-derived per block through an opaque asm: otherwise LICM hoists
@@ -244,11 +287,16 @@ SO_DEV void wave_dense_block(const uint32_t* win, unsigned long long* keys, int 
             // quadrants (pass 0: TL, TR; pass 1: BL, BR) -- per-lane bests now, the
             // accumulators are reused by the next pass
             const int ys = y + pass * HALF;
-            int dlo = SR - ys;               dlo = dlo < 0 ? 0 : dlo;
-            int dhi = H - 8 - ys + SR - 1; dhi = dhi > 32 ? 32 : dhi;
-            const bool edge = dlo > 0 || dhi < 32;
-            subb[2 * pass] = lane_best17(accL, X, hh, dlo, dhi, edge);
-            subb[2 * pass + 1] = lane_best17(accR, X, hh, dlo, dhi, edge);
+            int dlo, dhi;
+            if constexpr (FME) {
+                fme_drange(ys, ph.a, H, 8, dlo, dhi);
+            } else {
+                dlo = SR - ys;          dlo = dlo < 0 ? 0 : dlo;
+                dhi = H - 8 - ys + SR - 1; dhi = dhi > 32 ? 32 : dhi;
+            }
+            const bool edge = FME || dlo > 0 || dhi < 32;
+            subb[2 * pass] = lane_best17(accL, X, hh, dlo, dhi, edge, FME && ph.a);
+            subb[2 * pass + 1] = lane_best17(accR, X, hh, dlo, dhi, edge, FME && ph.a);
             sub2[2 * pass] = l2;
             sub2[2 * pass + 1] = r2;
 #pragma unroll
@@ -260,19 +308,34 @@ SO_DEV void wave_dense_block(const uint32_t* win, unsigned long long* keys, int 
         for (int t = 0; t < NT; ++t) S[t] = accL[t];
     }
     // block keys: phase 1 (lane's 17 candidates) and phase 2 (dx = +16)
-    int dlo = SR - y;            dlo = dlo < 0 ? 0 : dlo;
-    int dhi = H - BS - y + SR - 1; dhi = dhi > 32 ? 32 : dhi;
-    const bool edge = dlo > 0 || dhi < 32;
-    const bool xok = (x + xi - 16 >= 0) && (x + xi - 16 < W - BS);
-    uint64_t k = widen17(lane_best17(S, X, hh, dlo, dhi, edge), X, hh, xi, xok, r);
+    int dlo, dhi;
+    bool xok, x2ok;
+    if constexpr (FME) {
+        fme_drange(y, ph.a, H, BS, dlo, dhi);
+        xok = fme_xok(x, xi, ph.b, W, BS);
+        x2ok = fme_xok(x, 32, ph.b, W, BS);
+    } else {
+        dlo = SR - y;            dlo = dlo < 0 ? 0 : dlo;
+        dhi = H - BS - y + SR - 1; dhi = dhi > 32 ? 32 : dhi;
+        xok = (x + xi - 16 >= 0) && (x + xi - 16 < W - BS);
+        x2ok = x + 16 < W - BS;
+    }
+    const bool edge = FME || dlo > 0 || dhi < 32;
+    const uint32_t lb = lane_best17(S, X, hh, dlo, dhi, edge, FME && ph.a);
+    uint64_t k;
+    if constexpr (FME) k = widen17_fme(lb, X, hh, xi, xok, r, ph);
+    else k = widen17(lb, X, hh, xi, xok, r);
     {
         uint32_t s2 = 0;
 #pragma unroll
         for (int pass = 0; pass < NPASS; ++pass) s2 += a2L[pass] + a2R[pass];
-        const bool ok2 = lane < 33 && (x + 16 < W - BS) && d2 >= dlo && d2 <= dhi;
-        const uint64_t k2 = ok2 ? me_key(s2, (uint32_t)(16 + (d2 < 16 ? 16 - d2 : d2 - 16)), (uint32_t)r,
-                                         (uint32_t)(32 * 33 + d2))
-                                : kNoKey;
+        const bool ok2 = lane < 33 && x2ok && d2 >= dlo && d2 <= dhi;
+        uint64_t k2 = kNoKey;
+        if constexpr (FME) {
+            if (ok2) k2 = fme_key(s2, 32, d2, ph, r);
+        } else {
+            if (ok2) k2 = me_key(s2, (uint32_t)(16 + (d2 < 16 ? 16 - d2 : d2 - 16)), (uint32_t)r, (uint32_t)(32 * 33 + d2));
+        }
         k = k2 < k ? k2 : k;
     }
     k = wave_min_u64(k);
@@ -281,12 +344,19 @@ SO_DEV void wave_dense_block(const uint32_t* win, unsigned long long* keys, int 
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int xs = x + (j & 1) * 8, ys = y + (j >> 1) * 8;
-            const bool sxok = (xs + xi - 16 >= 0) && (xs + xi - 16 < W - 8);
-            uint64_t ks = widen17(subb[j], X, hh, xi, sxok, r);
-            const bool ok2 = lane < 33 && (xs + 16 < W - 8) && (ys + d2 - 16 >= 0) && (ys + d2 - 16 < H - 8);
-            const uint64_t k2 = ok2 ? me_key(sub2[j], (uint32_t)(16 + (d2 < 16 ? 16 - d2 : d2 - 16)),
-                                             (uint32_t)r, (uint32_t)(32 * 33 + d2))
-                                    : kNoKey;
+            uint64_t ks, k2 = kNoKey;
+            if constexpr (FME) {
+                int sdlo, sdhi;
+                fme_drange(ys, ph.a, H, 8, sdlo, sdhi);
+                ks = widen17_fme(subb[j], X, hh, xi, fme_xok(xs, xi, ph.b, W, 8), r, ph);
+                if (lane < 33 && fme_xok(xs, 32, ph.b, W, 8) && d2 >= sdlo && d2 <= sdhi) k2 = fme_key(sub2[j], 32, d2, ph, r);
+            } else {
+                const bool sxok = (xs + xi - 16 >= 0) && (xs + xi - 16 < W - 8);
+                ks = widen17(subb[j], X, hh, xi, sxok, r);
+                const bool ok2 = lane < 33 && (xs + 16 < W - 8) && (ys + d2 - 16 >= 0) && (ys + d2 - 16 < H - 8);
+                if (ok2) k2 = me_key(sub2[j], (uint32_t)(16 + (d2 < 16 ? 16 - d2 : d2 - 16)), (uint32_t)r,
+                                     (uint32_t)(32 * 33 + d2));
+            }
             ks = k2 < ks ? k2 : ks;
             ks = wave_min_u64(ks);
             if (lane == 0 && ks < keys[nblk + 4 * u + j]) keys[nblk + 4 * u + j] = ks;
@@ -299,8 +369,7 @@ __global__ void __launch_bounds__((MeWGeo<BS, SUB>::NTHREADS)) __attribute__((am
 me_wave_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
                int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub) {
     using G = MeWGeo<BS, SUB>;
-    constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RPD = G::RPD, CS = G::CSTRIDE, NT = G::NT;
-    constexpr int NDW = BS / 4, HALF = 8, NPASS = BS / HALF, NR = NT + HALF - 1;
+    constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RPD = G::RPD, CS = G::CSTRIDE;
     constexpr int NUNIT = G::NBLK * (SUB ? 5 : 1);
     __shared__ uint32_t win[4 * CS];
     __shared__ unsigned long long keys[NUNIT];
@@ -351,6 +420,129 @@ me_wave_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
         if (i < G::NBLK) decode_key(keys[i], SR, out_best + b * 4);
         else decode_key(keys[i], SR, out_sub + (b * 4 + ((i - G::NBLK) & 3)) * 4);
     }
+}
+
+// FME search (FMEEnable): me_wave_kernel's dense wave search over the four phase planes of
+// every reference (virtual references vr = 4 r + 2a + b, planes + vr * pstride; see
+// FmePhase above).  Keys are the half-pel keys, decoded with sr' = 2 sr = 32.
+template <bool SUB>
+__global__ void __launch_bounds__((MeWGeo<16, SUB>::NTHREADS)) __attribute__((amdgpu_waves_per_eu(SUB ? 4 : 8)))
+me_fme_kernel(const uint8_t* __restrict__ cur, const uint8_t* __restrict__ planes, size_t pstride, int nref, int H,
+              int W, int by0, int by1, int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub) {
+    using G = MeWGeo<16, SUB>;
+    constexpr int BS = 16, SR = G::SR, TBX = G::TBX, TBY = G::TBY, RPD = G::RPD, CS = G::CSTRIDE;
+    constexpr int NUNIT = G::NBLK * (SUB ? 5 : 1);
+    __shared__ uint32_t win[4 * CS];
+    __shared__ unsigned long long keys[NUNIT];
+
+    const int nbx = W / BS;
+    const int tiles_x = (nbx + TBX - 1) / TBX;
+    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    const int bx0 = tx * TBX, byt0 = by0 + ty * TBY;
+    const int x0 = bx0 * BS, y0 = byt0 * BS;
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    for (int i = tid; i < NUNIT; i += G::NTHREADS) keys[i] = kNoKey;
+    for (int vr = 0; vr < 4 * nref; ++vr) {
+        const uint8_t* ref = planes + (size_t)vr * pstride;
+        const FmePhase ph{(vr >> 1) & 1, vr & 1};
+        const int r = vr >> 2;
+        __syncthreads();
+        for (int i = tid; i < G::WR * RPD; i += G::NTHREADS) {
+            const int wr = i / RPD, m = i - wr * RPD;
+            const int gy = y0 - SR + wr, gx = x0 - SR + 4 * m;
+            uint32_t a = 0, b = 0;
+            if (gy >= 0 && gy < H) {
+                const uint8_t* rp = ref + (size_t)gy * W;
+                if (gx >= 0 && gx + 4 <= W) a = *reinterpret_cast<const uint32_t*>(rp + gx);
+                if (gx + 4 >= 0 && gx + 8 <= W) b = *reinterpret_cast<const uint32_t*>(rp + gx + 4);
+            }
+            uint32_t* d = win + wr * RPD + m;
+            d[0] = a;
+            d[CS] = __builtin_amdgcn_alignbyte(b, a, 1);
+            d[2 * CS] = __builtin_amdgcn_alignbyte(b, a, 2);
+            d[3 * CS] = __builtin_amdgcn_alignbyte(b, a, 3);
+        }
+        __syncthreads();
+#pragma unroll 1
+        for (int u = wave; u < G::NBLK; u += G::NW) {
+            const int bxl = u % TBX, byl = u / TBX;
+            if (bx0 + bxl >= nbx || byt0 + byl >= by1) continue;   // wave-uniform
+            const int x = x0 + bxl * BS, y = y0 + byl * BS;
+            wave_dense_block<BS, SUB, RPD, CS, true>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u, tid, r, ph);
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < NUNIT; i += G::NTHREADS) {
+        const int blk = i < G::NBLK ? i : (i - G::NBLK) >> 2;
+        const int gbx = bx0 + blk % TBX, gby = byt0 + blk / TBX;
+        if (gbx >= nbx || gby >= by1) continue;
+        const size_t b = (size_t)(gby - by0) * nbx + gbx;
+        if (i < G::NBLK) decode_key(keys[i], 2 * SR, out_best + b * 4);
+        else decode_key(keys[i], 2 * SR, out_sub + (b * 4 + ((i - G::NBLK) & 3)) * 4);
+    }
+}
+
+// Phase planes of frac_me_reference_frame (Encoder.py:388-403): P_ab[i][j] = F[2i+a][2j+b],
+//   P00 = r,  P01 = ceil(h/2),  P10 = ceil((r[i][j] + r[i+1][j]) / 2),  P11 = ceil((h + h') / 4)
+// with h = r[i][j] + r[i][j+1] (mod 256 when `wrap`: the uint8 row sum of the reference,
+// see oracle oc_fme_upsample) and h' the same one row down.  Entries past F (last column of
+// P01/P11, last row of P10/P11) are 0 and never read by a valid candidate.  One thread per
+// 4 pixels of a row: one dword of r and of the next row, plus the next byte of each.
+__global__ void __launch_bounds__(256)
+fme_planes_kernel(const uint8_t* __restrict__ ref, int H, int W, int wrap, uint8_t* __restrict__ out, size_t pstride) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    const int qpr = W >> 2;
+    if (q >= qpr * H) return;
+    const int i = q / qpr, j0 = (q - i * qpr) * 4;
+    const uint8_t* r0 = ref + (size_t)i * W + j0;
+    const bool down = i + 1 < H;
+    const uint8_t* r1 = down ? r0 + W : r0;
+    uint32_t p00 = 0, p01 = 0, p10 = 0, p11 = 0;
+    const uint32_t w0 = *reinterpret_cast<const uint32_t*>(r0), w1 = *reinterpret_cast<const uint32_t*>(r1);
+    const bool right = j0 + 4 < W;
+    const int e0 = right ? r0[4] : 0, e1 = right ? r1[4] : 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int a = (w0 >> (8 * k)) & 255, c = (w1 >> (8 * k)) & 255;
+        const bool rk = j0 + k + 1 < W;
+        const int a2 = k < 3 ? (int)((w0 >> (8 * k + 8)) & 255) : e0;
+        const int c2 = k < 3 ? (int)((w1 >> (8 * k + 8)) & 255) : e1;
+        int h0 = a + a2, h1 = c + c2;
+        if (wrap) { h0 &= 255; h1 &= 255; }
+        p00 |= (uint32_t)a << (8 * k);
+        if (rk) p01 |= (uint32_t)((h0 + 1) >> 1) << (8 * k);
+        if (down) p10 |= (uint32_t)((a + c + 1) >> 1) << (8 * k);
+        if (down && rk) p11 |= (uint32_t)((h0 + h1 + 3) >> 2) << (8 * k);
+    }
+    const size_t o = (size_t)i * W + j0;
+    *reinterpret_cast<uint32_t*>(out + o) = p00;
+    *reinterpret_cast<uint32_t*>(out + pstride + o) = p01;
+    *reinterpret_cast<uint32_t*>(out + 2 * pstride + o) = p10;
+    *reinterpret_cast<uint32_t*>(out + 3 * pstride + o) = p11;
+}
+
+int fme_planes_launch(const uint8_t* ref, int H, int W, int wrap, uint8_t* out, size_t pstride, hipStream_t st) {
+    const int n = (W / 4) * H;
+    hipLaunchKernelGGL(fme_planes_kernel, dim3((n + 255) / 256), dim3(256), 0, st, ref, H, W, wrap, out, pstride);
+    return check_launch("fme_planes_kernel");
+}
+
+int me_fme_launch(const uint8_t* cur, const uint8_t* planes, size_t pstride, int nref, int H, int W, int by0, int by1,
+                  int32_t* out_best, int32_t* out_sub, hipStream_t st) {
+    const int nbx = W / 16, nrows = by1 - by0;
+    if (nrows <= 0) return SO_OK;
+    const bool sub = out_sub != nullptr;
+    const int tby = (sub ? MeWGeo<16, true>::TPY : MeWGeo<16, false>::TPY) / 16;
+    const dim3 grid(((nbx + 7) / 8) * ((nrows + tby - 1) / tby));
+    if (sub)
+        hipLaunchKernelGGL((me_fme_kernel<true>), grid, dim3(MeWGeo<16, true>::NTHREADS), 0, st, cur, planes, pstride,
+                           nref, H, W, by0, by1, out_best, out_sub);
+    else
+        hipLaunchKernelGGL((me_fme_kernel<false>), grid, dim3(MeWGeo<16, false>::NTHREADS), 0, st, cur, planes,
+                           pstride, nref, H, W, by0, by1, out_best, out_sub);
+    return check_launch("me_fme_kernel");
 }
 
 // ---------------------------------------------------------------------------------------
@@ -837,11 +1029,16 @@ __global__ void me_generic_init(unsigned long long* keys, int n) {
     if (i < n) keys[2 * (size_t)i] = kNoKey;
 }
 
-__global__ void me_generic_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H,
-                                  int W, int bs, int by0, int nrows, int sb_mode, int sr,
-                                  unsigned long long* __restrict__ keys) {
+// `planes` != NULL: FME (FmePhase above) -- the candidates are the half-pel offsets in
+// [-2sr, 2sr] at (2x, 2y) on the frac frame, read from its phase planes, with the
+// reference's FME bound (find_best_match :697-705); the scan index runs over that range.
+__global__ void me_generic_kernel(const uint8_t* __restrict__ cur, RefSet refs, const uint8_t* __restrict__ planes,
+                                  size_t pstride, int nref, int H, int W, int bs, int by0, int nrows, int sb_mode,
+                                  int sr, unsigned long long* __restrict__ keys) {
     // sb_mode 0: full blocks (size bs); 1: sub-blocks (size bs/2, 4 per block)
-    const int d = 2 * sr + 1;
+    const bool fme = planes != nullptr;
+    const int R = fme ? 2 * sr : sr;
+    const int d = 2 * R + 1;
     const int nbx = W / bs;
     const int nunit = nbx * nrows * (sb_mode ? 4 : 1);
     const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -855,15 +1052,28 @@ __global__ void me_generic_kernel(const uint8_t* __restrict__ cur, RefSet refs, 
     int x = (b % nbx) * bs, y = (by0 + b / nbx) * bs;
     if (sb_mode) { x += (u & 1) * tbs; y += ((u >> 1) & 1) * tbs; }
     const int dxi = cand / d, di = cand % d;
-    const int dx = dxi - sr, dy = di - sr;
-    if (!(x + dx >= 0 && x + dx < W - tbs && y + dy >= 0 && y + dy < H - tbs)) return;
-    const uint8_t* ref = refs.p[r];
+    const int dx = dxi - R, dy = di - R;
     uint32_t sad = 0;
-    for (int i = 0; i < tbs; ++i)
-        for (int j = 0; j < tbs; ++j) {
-            int a = cur[(size_t)(y + i) * W + x + j], c = ref[(size_t)(y + dy + i) * W + x + dx + j];
-            sad += (uint32_t)(a > c ? a - c : c - a);
-        }
+    if (fme) {
+        const int W2 = 2 * W - 1, H2 = 2 * H - 1, px = 2 * x + dx, py = 2 * y + dy;
+        if (!(px >= 0 && px < W2 - tbs && py >= 0 && py < H2 - tbs && px + 2 * tbs < W2 - tbs &&
+              py + 2 * tbs < H2 - tbs))
+            return;
+        const uint8_t* pl = planes + (size_t)(4 * r + 2 * (py & 1) + (px & 1)) * pstride;
+        for (int i = 0; i < tbs; ++i)
+            for (int j = 0; j < tbs; ++j) {
+                int a = cur[(size_t)(y + i) * W + x + j], c = pl[(size_t)((py >> 1) + i) * W + (px >> 1) + j];
+                sad += (uint32_t)(a > c ? a - c : c - a);
+            }
+    } else {
+        if (!(x + dx >= 0 && x + dx < W - tbs && y + dy >= 0 && y + dy < H - tbs)) return;
+        const uint8_t* ref = refs.p[r];
+        for (int i = 0; i < tbs; ++i)
+            for (int j = 0; j < tbs; ++j) {
+                int a = cur[(size_t)(y + i) * W + x + j], c = ref[(size_t)(y + dy + i) * W + x + dx + j];
+                sad += (uint32_t)(a > c ? a - c : c - a);
+            }
+    }
     const uint32_t l1 = (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy));
     atomicMin(&keys[2 * (size_t)u], (unsigned long long)me_key(sad, l1, (uint32_t)r, (uint32_t)cand));
 }
@@ -875,6 +1085,9 @@ __global__ void me_generic_finalize(int n, int sr, int32_t* __restrict__ out) {
         decode_key(k, sr, out + (size_t)i * 4);
     }
 }
+
+int me_generic_launch(const uint8_t* cur, const RefSet& refs, const uint8_t* planes, size_t pstride, int nref, int H,
+                      int W, int bs, int sr, int by0, int by1, int32_t* out_best, int32_t* out_sub, hipStream_t st);
 
 int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, int bs, int sr, int by0, int by1,
               int32_t* out_best, int32_t* out_sub, hipStream_t st) {
@@ -924,8 +1137,15 @@ int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, in
             return check_launch("me_fast_kernel");
         }
     }
-    // generic
-    const int d = 2 * sr + 1;
+    return me_generic_launch(cur, refs, nullptr, 0, nref, H, W, bs, sr, by0, by1, out_best, out_sub, st);
+}
+
+int me_generic_launch(const uint8_t* cur, const RefSet& refs, const uint8_t* planes, size_t pstride, int nref, int H,
+                      int W, int bs, int sr, int by0, int by1, int32_t* out_best, int32_t* out_sub, hipStream_t st) {
+    const int nbx = W / bs, nrows = by1 - by0;
+    if (nrows <= 0) return SO_OK;
+    const int R = planes ? 2 * sr : sr;
+    const int d = 2 * R + 1;
     for (int mode = 0; mode < (out_sub ? 2 : 1); ++mode) {
         const int nunit = nbx * nrows * (mode ? 4 : 1);
         int32_t* out = mode ? out_sub : out_best;
@@ -933,9 +1153,9 @@ int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, in
         hipLaunchKernelGGL(me_generic_init, dim3((nunit + 255) / 256), dim3(256), 0, st, keys, nunit);
         const long long ntot = (long long)nunit * nref * d * d;
         hipLaunchKernelGGL(me_generic_kernel, dim3((unsigned)((ntot + 255) / 256)), dim3(256), 0, st,
-                           cur, refs, nref, H, W, bs, by0, nrows, mode, sr, keys);
+                           cur, refs, planes, pstride, nref, H, W, bs, by0, nrows, mode, sr, keys);
         hipLaunchKernelGGL(me_generic_finalize, dim3((nunit + 255) / 256), dim3(256), 0, st, nunit,
-                           sr, out);
+                           R, out);
     }
     return check_launch("me_generic_kernel");
 }

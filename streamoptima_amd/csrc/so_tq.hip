@@ -14,9 +14,10 @@
 
 namespace so {
 
-template <int BS, bool VBS>
+template <int BS, bool VBS, bool FME>
 __global__ void __launch_bounds__(256)
-inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W, int by0, int nrows,
+inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, const uint8_t* __restrict__ planes, size_t pstride,
+                int H, int W, int by0, int nrows,
                 const int32_t* __restrict__ best, const int32_t* __restrict__ sub, int qp_rd,
                 const int32_t* __restrict__ qp_row, double lam, uint8_t* __restrict__ out_split,
                 int16_t* __restrict__ out_mv, int16_t* __restrict__ out_qtc,
@@ -37,9 +38,13 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W, int 
 
     const int32_t* bb = best + (size_t)b * 4;
     const int dx = bb[0], dy = bb[1], rf = bb[2], sad = bb[3];
-    const bool fast = (0 <= x + dx) && (x + dx < W - BS) && (0 <= y + dy) && (y + dy < H - BS);
     int pred[BS], crow[BS], res[BS];
-    fetch_row<BS>(refs.p[rf], W, H, x + dx, y + dy + l, fast, pred);
+    if constexpr (FME) {
+        fetch_row_fme<BS>(planes + (size_t)rf * 4 * pstride, pstride, W, H, 2 * x + dx, 2 * y + dy, l, 2 * BS, BS, pred);
+    } else {
+        const bool fast = (0 <= x + dx) && (x + dx < W - BS) && (0 <= y + dy) && (y + dy < H - BS);
+        fetch_row<BS>(refs.p[rf], W, H, x + dx, y + dy + l, fast, pred);
+    }
     load_cur_row<BS>(cur, W, x, y + l, crow);
 #pragma unroll
     for (int c = 0; c < BS; ++c) res[c] = crow[c] - pred[c];
@@ -67,7 +72,11 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W, int 
             for (int h = 0; h < 2; ++h) {
                 const int row = r0 + 4 * h;
                 int scur[8];
-                fetch_row<8>(refs.p[sref], W, H, xs + sdx, ys + sdy + row, sfast, spred[h]);
+                if constexpr (FME)
+                    fetch_row_fme<8>(planes + (size_t)sref * 4 * pstride, pstride, W, H, 2 * xs + sdx, 2 * ys + sdy,
+                                     row, 16, 8, spred[h]);
+                else
+                    fetch_row<8>(refs.p[sref], W, H, xs + sdx, ys + sdy + row, sfast, spred[h]);
                 load_cur_row<8>(cur, W, xs, ys + row, scur);
 #pragma unroll
                 for (int c = 0; c < 8; ++c) sres[h][c] = scur[c] - spred[h][c];
@@ -135,6 +144,14 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W, int 
             }
             double srd[2][8];
             xform2d_sub<true>(dl, l, sdq, srd);
+            if constexpr (FME) {
+                // the split recon predicts with the FULL block's FME bound (Encoder.py:908-909),
+                // stricter than the sub-block search: those sub-blocks reconstruct on 128
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    fetch_row_fme<8>(planes + (size_t)sref * 4 * pstride, pstride, W, H, 2 * xs + sdx, 2 * ys + sdy,
+                                     r0 + 4 * h, BS, BS, spred[h]);
+            }
             sse = 0;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -165,9 +182,10 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W, int 
 
 // Decoder: reconstruct a P-frame from (split, mv, qtc) — decoder.py:97-211, which is the
 // same arithmetic as reconstruct_frame (Encoder.py:831-932).
-template <int BS, bool VBS>
+template <int BS, bool VBS, bool FME>
 __global__ void __launch_bounds__(256)
-inter_recon_kernel(RefSet refs, int H, int W, int qp, const int32_t* __restrict__ qp_row,
+inter_recon_kernel(RefSet refs, const uint8_t* __restrict__ planes, size_t pstride, int H, int W, int qp,
+                   const int32_t* __restrict__ qp_row,
                    const uint8_t* __restrict__ split, const int16_t* __restrict__ mv,
                    const int16_t* __restrict__ qtc, uint8_t* __restrict__ out_recon) {
     constexpr int G = BS, BPW = 256 / G, SB = BS / 2;
@@ -183,9 +201,14 @@ inter_recon_kernel(RefSet refs, int H, int W, int qp, const int32_t* __restrict_
     const int16_t* m = mv + (size_t)b * 12;
     if (!VBS || !split[b]) {
         const int dx = m[0], dy = m[1], rf = m[2];
-        const bool fast = (0 <= x + dx) && (x + dx < W - BS) && (0 <= y + dy) && (y + dy < H - BS);
         int pred[BS], q[BS], dq[BS], rec[BS];
-        fetch_row<BS>(refs.p[rf], W, H, x + dx, y + dy + l, fast, pred);
+        if constexpr (FME) {
+            fetch_row_fme<BS>(planes + (size_t)rf * 4 * pstride, pstride, W, H, 2 * x + dx, 2 * y + dy, l, 2 * BS, BS,
+                              pred);
+        } else {
+            const bool fast = (0 <= x + dx) && (x + dx < W - BS) && (0 <= y + dy) && (y + dy < H - BS);
+            fetch_row<BS>(refs.p[rf], W, H, x + dx, y + dy + l, fast, pred);
+        }
         load_row_i16<BS>(qtc + (size_t)b * BS * BS + l * BS, q);
         dequant_row<BS>(q, l, qpr, dq);
         double rd[BS];
@@ -203,7 +226,11 @@ inter_recon_kernel(RefSet refs, int H, int W, int qp, const int32_t* __restrict_
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             int qv[8];
-            fetch_row<8>(refs.p[sref], W, H, xs + sdx, ys + sdy + r0 + 4 * h, sfast, spred[h]);
+            if constexpr (FME)
+                fetch_row_fme<8>(planes + (size_t)sref * 4 * pstride, pstride, W, H, 2 * xs + sdx, 2 * ys + sdy,
+                                 r0 + 4 * h, BS, BS, spred[h]);
+            else
+                fetch_row<8>(refs.p[sref], W, H, xs + sdx, ys + sdy + r0 + 4 * h, sfast, spred[h]);
             load_row_i16<8>(qtc + (size_t)b * BS * BS + j * 64 + (r0 + 4 * h) * 8, qv);
             dequant_row<8>(qv, r0 + 4 * h, qpm1, sdq[h]);
         }
@@ -219,39 +246,40 @@ inter_recon_kernel(RefSet refs, int H, int W, int qp, const int32_t* __restrict_
     }
 }
 
-int inter_tq_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int bs, int by0, int by1,
-                    const int32_t* best, const int32_t* sub, int qp_rd, const int32_t* qp_row, int vbs,
-                    double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
+int inter_tq_launch(const uint8_t* cur, const RefSet& refs, const uint8_t* planes, size_t pstride, int H, int W,
+                    int bs, int by0, int by1, const int32_t* best, const int32_t* sub, int qp_rd, const int32_t* qp_row,
+                    int vbs, double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
                     int32_t* out_mae, uint8_t* out_recon, int32_t* out_sse, hipStream_t st) {
     const int nrows = by1 - by0;
     if (nrows <= 0) return SO_OK;
     const int nb = (W / bs) * nrows;
     const int bpw = 256 / bs;
     dim3 grid((nb + bpw - 1) / bpw), blk(256);
-    if (bs == 16 && vbs)
-        hipLaunchKernelGGL((inter_tq_kernel<16, true>), grid, blk, 0, st, cur, refs, H, W, by0, nrows, best, sub, qp_rd,
-                           qp_row, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon, out_sse);
-    else if (bs == 16)
-        hipLaunchKernelGGL((inter_tq_kernel<16, false>), grid, blk, 0, st, cur, refs, H, W, by0, nrows, best, sub, qp_rd,
-                           qp_row, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon, out_sse);
-    else
-        hipLaunchKernelGGL((inter_tq_kernel<8, false>), grid, blk, 0, st, cur, refs, H, W, by0, nrows, best, sub, qp_rd,
-                           qp_row, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon, out_sse);
+#define SO_TQ(B, V, F)                                                                                             \
+    hipLaunchKernelGGL((inter_tq_kernel<B, V, F>), grid, blk, 0, st, cur, refs, planes, pstride, H, W, by0, nrows,   \
+                       best, sub, qp_rd, qp_row, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon,    \
+                       out_sse)
+    const bool fme = planes != nullptr;
+    if (bs == 16 && vbs) { if (fme) SO_TQ(16, true, true); else SO_TQ(16, true, false); }
+    else if (bs == 16) { if (fme) SO_TQ(16, false, true); else SO_TQ(16, false, false); }
+    else { if (fme) SO_TQ(8, false, true); else SO_TQ(8, false, false); }
+#undef SO_TQ
     return check_launch("inter_tq_kernel");
 }
 
-int inter_recon_launch(const RefSet& refs, int H, int W, int bs, int qp, const int32_t* qp_row,
-                       const uint8_t* split, const int16_t* mv, const int16_t* qtc, uint8_t* out_recon,
-                       hipStream_t st) {
+int inter_recon_launch(const RefSet& refs, const uint8_t* planes, size_t pstride, int H, int W, int bs, int qp,
+                       const int32_t* qp_row, const uint8_t* split, const int16_t* mv, const int16_t* qtc,
+                       uint8_t* out_recon, hipStream_t st) {
     const int nb = (W / bs) * (H / bs);
     const int bpw = 256 / bs;
     dim3 grid((nb + bpw - 1) / bpw), blk(256);
-    if (bs == 16)
-        hipLaunchKernelGGL((inter_recon_kernel<16, true>), grid, blk, 0, st, refs, H, W, qp, qp_row, split, mv,
-                           qtc, out_recon);
-    else
-        hipLaunchKernelGGL((inter_recon_kernel<8, false>), grid, blk, 0, st, refs, H, W, qp, qp_row, split, mv,
-                           qtc, out_recon);
+#define SO_REC(B, V, F)                                                                                          \
+    hipLaunchKernelGGL((inter_recon_kernel<B, V, F>), grid, blk, 0, st, refs, planes, pstride, H, W, qp, qp_row, \
+                       split, mv, qtc, out_recon)
+    const bool fme = planes != nullptr;
+    if (bs == 16) { if (fme) SO_REC(16, true, true); else SO_REC(16, true, false); }
+    else { if (fme) SO_REC(8, false, true); else SO_REC(8, false, false); }
+#undef SO_REC
     return check_launch("inter_recon_kernel");
 }
 

@@ -2,7 +2,9 @@
 
 decode() reconstructs frames from symbols with the same gfx950 kernels as the encoder's
 reconstruction (decoder.py:97-211 inter, :330-432 intra mode 0, :487-545 GOP loop incl.
-its reference-list handling: an I-frame CLEARS the list, decoder.py:520).
+its reference-list handling: an I-frame CLEARS the list, decoder.py:520).  With
+FMEEnable the references are the frac frames (decoder.py:102-103, 468-483); after the
+I-frame reset the list holds uint8 reconstructions only, so their row sums always wrap.
 """
 from __future__ import annotations
 
@@ -66,7 +68,7 @@ class decoder:
         hp = -(-self.h_pixels // bs) * bs
         wp = -(-self.w_pixels // bs) * bs
         if self._engine is None:
-            self._engine = Engine(hp, wp, bs, 16, False, 0.0, self.device)
+            self._engine = Engine(hp, wp, bs, 16, False, 0.0, self.device, fme=bool(self.FMEEnable))
         return self._engine
 
     def _rc(self):

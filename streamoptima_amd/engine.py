@@ -47,7 +47,7 @@ class Engine:
     """Kernels for one frame geometry on one device."""
 
     def __init__(self, height: int, width: int, block_size: int = 16, search_range: int = 16,
-                 vbs: bool = False, lam: float | None = None, device=None):
+                 vbs: bool = False, lam: float | None = None, device=None, me_mode: int = 0, fme: bool = False):
         if height % block_size or width % block_size:
             raise ValueError(f"frame {width}x{height} is not a multiple of block_size {block_size}")
         self.h, self.w, self.bs, self.sr = height, width, block_size, search_range
@@ -64,6 +64,17 @@ class Engine:
         ps = self.lib.so_p_frame_scratch_elems(height, width, block_size, int(self.vbs))
         is_ = self.lib.so_i_frame_scratch_elems(height, width, block_size)
         self.scratch = torch.empty(max(ps, is_), dtype=torch.int32, device=self.device)
+        # ME variant (include/streamoptima.h SO_ME_*): fast_me / FMEEnable
+        self.me_mode = int(me_mode)
+        self.fme = bool(fme)
+        self._fme_ws = None
+
+    def fme_workspace(self, nref: int) -> torch.Tensor:
+        """Phase planes of the references' frac frames (rebuilt by every FME call)."""
+        need = self.lib.so_fme_workspace_bytes(self.h, self.w, nref)
+        if self._fme_ws is None or self._fme_ws.numel() < need:
+            self._fme_ws = torch.zeros(need, dtype=torch.uint8, device=self.device)
+        return self._fme_ws
 
     # ---- allocation ----------------------------------------------------------------------
     def new_symbols(self, frame_type: int) -> FrameSymbols:
@@ -94,8 +105,10 @@ class Engine:
 
     # ---- encode -------------------------------------------------------------------------
     def encode_p(self, cur: torch.Tensor, refs: list, qp_rd: int, qp_row=None,
-                 out: FrameSymbols | None = None, qp_row_dev: torch.Tensor | None = None) -> FrameSymbols:
-        """complete_inter_flow (Encoder.py:1644) for one frame; asynchronous."""
+                 out: FrameSymbols | None = None, qp_row_dev: torch.Tensor | None = None,
+                 fme_wrap: bool = True) -> FrameSymbols:
+        """complete_inter_flow (Encoder.py:1644) for one frame; asynchronous.  `fme_wrap`:
+        see so_encode_p_rows_ex (False while refs hold the float64 all-128 start frame)."""
         self._check_plane(cur, "cur")
         for k, r in enumerate(refs):
             self._check_plane(r, f"refs[{k}]")
@@ -103,12 +116,22 @@ class Engine:
             raise ValueError(f"nRefFrames must be in [1, {_lib.MAX_REF}]")
         out = out or self.new_symbols(1)
         qr = qp_row_dev if qp_row_dev is not None else self.qp_row_tensor(qp_row)
-        rc = self.lib.so_encode_p_frame(
-            cur.data_ptr(), _lib.ref_array(refs), len(refs), self.h, self.w, self.bs, self.sr,
-            int(qp_rd), _lib.ptr(qr), int(self.vbs), self.lam, out.split.data_ptr(),
-            out.mv.data_ptr(), out.qtc.data_ptr(), out.tokens.data_ptr(), out.mae_num.data_ptr(),
-            out.recon.data_ptr(), _lib.ptr(out.sse), self.scratch.data_ptr(), _lib.stream_handle(self.device))
-        _lib.check(rc, "so_encode_p_frame")
+        if self.me_mode == _lib.ME_FULL and not self.fme:
+            rc = self.lib.so_encode_p_frame(
+                cur.data_ptr(), _lib.ref_array(refs), len(refs), self.h, self.w, self.bs, self.sr,
+                int(qp_rd), _lib.ptr(qr), int(self.vbs), self.lam, out.split.data_ptr(),
+                out.mv.data_ptr(), out.qtc.data_ptr(), out.tokens.data_ptr(), out.mae_num.data_ptr(),
+                out.recon.data_ptr(), _lib.ptr(out.sse), self.scratch.data_ptr(), _lib.stream_handle(self.device))
+            _lib.check(rc, "so_encode_p_frame")
+        else:
+            ws = self.fme_workspace(len(refs)) if self.fme else None
+            rc = self.lib.so_encode_p_rows_ex(
+                cur.data_ptr(), _lib.ref_array(refs), len(refs), self.h, self.w, self.bs, self.sr, 0, self.nby,
+                int(qp_rd), _lib.ptr(qr), int(self.vbs), self.lam, self.me_mode, int(self.fme), int(bool(fme_wrap)),
+                _lib.ptr(ws), out.split.data_ptr(), out.mv.data_ptr(), out.qtc.data_ptr(), out.tokens.data_ptr(),
+                out.mae_num.data_ptr(), out.recon.data_ptr(), _lib.ptr(out.sse), self.scratch.data_ptr(),
+                _lib.stream_handle(self.device))
+            _lib.check(rc, "so_encode_p_rows_ex")
         out.frame_type, out.qp_rd = 1, int(qp_rd)
         out.qp_row = None if qp_row is None else list(qp_row)
         return out
@@ -147,17 +170,19 @@ class Engine:
                             extra={"by0": by0, "by1": by1})
 
     def encode_p_rows(self, cur, refs, by0: int, by1: int, qp_rd: int, out: FrameSymbols,
-                      qp_row_dev: torch.Tensor | None = None) -> FrameSymbols:
-        """so_encode_p_rows: block rows [by0, by1) of a P-frame; asynchronous."""
+                      qp_row_dev: torch.Tensor | None = None, fme_wrap: bool = True) -> FrameSymbols:
+        """so_encode_p_rows(_ex): block rows [by0, by1) of a P-frame; asynchronous."""
         self._check_plane(cur, "cur")
         for k, r in enumerate(refs):
             self._check_plane(r, f"refs[{k}]")
-        rc = self.lib.so_encode_p_rows(
+        ws = self.fme_workspace(len(refs)) if self.fme else None
+        rc = self.lib.so_encode_p_rows_ex(
             cur.data_ptr(), _lib.ref_array(refs), len(refs), self.h, self.w, self.bs, self.sr, int(by0), int(by1),
-            int(qp_rd), _lib.ptr(qp_row_dev), int(self.vbs), self.lam, out.split.data_ptr(), out.mv.data_ptr(),
-            out.qtc.data_ptr(), out.tokens.data_ptr(), out.mae_num.data_ptr(), out.recon.data_ptr(),
-            _lib.ptr(out.sse), self.scratch.data_ptr(), _lib.stream_handle(self.device))
-        _lib.check(rc, "so_encode_p_rows")
+            int(qp_rd), _lib.ptr(qp_row_dev), int(self.vbs), self.lam, self.me_mode, int(self.fme),
+            int(bool(fme_wrap)), _lib.ptr(ws), out.split.data_ptr(), out.mv.data_ptr(), out.qtc.data_ptr(),
+            out.tokens.data_ptr(), out.mae_num.data_ptr(), out.recon.data_ptr(), _lib.ptr(out.sse),
+            self.scratch.data_ptr(), _lib.stream_handle(self.device))
+        _lib.check(rc, "so_encode_p_rows_ex")
         out.frame_type, out.qp_rd = 1, int(qp_rd)
         return out
 
@@ -175,9 +200,18 @@ class Engine:
         return out
 
     # ---- decode ---------------------------------------------------------------------------
-    def recon_inter(self, refs: list, split, mv, qtc, qp: int, qp_row=None, out=None) -> torch.Tensor:
+    def recon_inter(self, refs: list, split, mv, qtc, qp: int, qp_row=None, out=None,
+                    fme_wrap: bool = True) -> torch.Tensor:
         out = out if out is not None else alloc_planes(1, self.h, self.w, self.device)[0]
         qr = self.qp_row_tensor(qp_row)
+        if self.fme:
+            ws = self.fme_workspace(len(refs))
+            rc = self.lib.so_inter_recon_ex(_lib.ref_array(refs), len(refs), self.h, self.w, self.bs, int(qp),
+                                            _lib.ptr(qr), 1, int(bool(fme_wrap)), ws.data_ptr(), split.data_ptr(),
+                                            mv.data_ptr(), qtc.data_ptr(), out.data_ptr(),
+                                            _lib.stream_handle(self.device))
+            _lib.check(rc, "so_inter_recon_ex")
+            return out
         rc = self.lib.so_inter_recon(_lib.ref_array(refs), len(refs), self.h, self.w, self.bs, int(qp),
                                      _lib.ptr(qr), split.data_ptr(), mv.data_ptr(), qtc.data_ptr(),
                                      out.data_ptr(), _lib.stream_handle(self.device))

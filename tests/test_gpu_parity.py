@@ -366,3 +366,124 @@ def test_me_paths_vs_oracle(gpu, kind):
         x, y = (b % nbx) * 16, (b // nbx) * 16
         exp = O.me_block(seq[1], [seq[0]], x, y, 16, 16)
         assert tuple(int(v) for v in best[b]) == exp, (kind, b, tuple(best[b]), exp)
+
+
+# ---------------------------------------------------------------- FME and fast ME
+# reference goldens (tests/golden/make_golden.py --only fme,gopme) and the C oracle
+ME_VARIANTS = ["fme_cif_vbs0", "fme_96x128_vbs1", "fme_64x96_sr4_vbs1", "fme_64x96_nref2", "fast_cif_vbs0",
+               "fast_cif_vbs1", "fast_cif_nref2_vbs1", "fast_fme_cif_vbs1", "fast_par2_cif"]
+
+
+def _me_mode(fast, pm):
+    return 0 if not fast else (2 if pm == 2 else 1)
+
+
+@pytest.mark.parametrize("name", ME_VARIANTS)
+def test_inter_me_variants_golden(gpu, name):
+    """complete_inter_flow with FMEEnable / fast_me (and fast_me under ParallelMode 2)."""
+    from streamoptima_amd.engine import Engine
+    g = golden("inter_me_variants.npz")
+    h, w, sr, vbs, fast, fme, nref, pm = (int(v) for v in g[f"{name}__cfg"])
+    eng = Engine(h, w, 16, sr, bool(vbs), 0.015, gpu, me_mode=_me_mode(fast, pm), fme=bool(fme))
+    refs = [_plane(r, gpu) for r in g[f"{name}__refs"]]
+    sym = eng.encode_p(_plane(g[f"{name}__cur"], gpu), refs, 4)
+    torch.cuda.synchronize()
+    hs = _sym_host(sym)
+    _assert_frame(hs, {k: g[f"{name}__{k}"] for k in ("split", "mv", "qtc", "tokens", "recon")})
+    m = hs["mae_num"]
+    avg = float("inf") if (m < 0).any() else (int(m.sum()) / 256) / len(m)
+    assert avg == float(g[f"{name}__avg_mae"])
+    if fme:   # the decoder's FME recon of the same symbols
+        rec = eng.recon_inter(refs, sym.split, sym.mv, sym.qtc, 4)
+        torch.cuda.synchronize()
+        assert (rec.cpu().numpy() == g[f"{name}__recon"]).all()
+
+
+def test_fme_planes_golden(gpu):
+    """so_fme_planes == frac_me_reference_frame, interleaved back (wrap and no-wrap)."""
+    from streamoptima_amd import _lib
+    lib = _lib.load()
+    g = golden("fme_frames.npz")
+    h, w = g["a"].shape
+    ps = lib.so_fme_plane_stride(h, w)
+    for src, wrap, key in ((g["a"], 1, "up_u8_a"), (g["b"], 1, "up_u8_b"), (g["a"], 0, "up_f_a"),
+                           (np.full((h, w), 128, np.uint8), 0, "up_f_128")):
+        out = torch.zeros(4 * ps, dtype=torch.uint8, device=gpu)
+        _lib.check(lib.so_fme_planes(_plane(src, gpu).data_ptr(), h, w, wrap, out.data_ptr(), _lib.stream_handle()),
+                   "so_fme_planes")
+        torch.cuda.synchronize()
+        o = out.cpu().numpy()
+        F = np.zeros((2 * h - 1, 2 * w - 1), np.uint8)
+        for a in (0, 1):
+            for b in (0, 1):
+                p = o[(2 * a + b) * ps:(2 * a + b) * ps + h * w].reshape(h, w)
+                F[a::2, b::2] = p[: h - a, : w - b]
+        assert (F == g[key]).all(), key
+
+
+ME_GOPS = [
+    ("gop_fme_vbs1", dict(qp=4, intra_dur=3, vbs=True, fme=True)),
+    ("gop_fast_vbs1", dict(qp=4, intra_dur=4, vbs=True, fast_me=True)),
+    ("gop_fast_fme", dict(qp=4, intra_dur=3, vbs=False, fast_me=True, fme=True)),
+]
+
+
+@pytest.mark.parametrize("name,cfg", ME_GOPS)
+def test_gop_me_variants_golden(gpu, name, cfg, tmp_path, monkeypatch):
+    from streamoptima_amd.Encoder import Y_Video_codec
+    g = golden(name + ".npz")
+    frames = g["frames"]
+    f, h, w = frames.shape
+    monkeypatch.chdir(tmp_path)
+    enc = Y_Video_codec(h, w, f, 16, 16, cfg["qp"], cfg["intra_dur"], 0, 0.015, cfg["vbs"], nRefFrames=1,
+                        y_only_frame_arr=frames, fast_me=cfg.get("fast_me", False), FMEEnable=cfg.get("fme", False),
+                        device=gpu)
+    psnr = enc.encode(block_size=16)
+    assert np.allclose(psnr, g["psnr"], rtol=0, atol=1e-9), (psnr, g["psnr"])
+    for i in range(f):
+        _assert_frame(_sym_host(enc._symbols[i]), {"split": g[f"split{i}"], "mv": g[f"mv{i}"], "qtc": g[f"qtc{i}"],
+                                                   "tokens": g[f"tokens{i}"], "recon": g["recon"][i]})
+        assert (enc.decoded_device[i].cpu().numpy() == g["decoded"][i]).all()
+    import gzip
+    js = json.load(gzip.open(os.path.join(GOLDEN, name + "_bitstream.json.gz"), "rt"))
+    pkg = enc.encoded_package
+    for i in range(f):
+        ft = pkg["frame_type_seq"][i]
+        line = f"{ft}|" + enc.differential_encoder_frame(ft, pkg["MVS per Frame"][i], pkg["Qp_per_row_per_frame"][i])
+        assert line == js["mv_lines"][i]
+
+
+ME_VAR_CASES = [
+    # (h, w, bs, sr, vbs, nref, me_mode, fme, wrap, kind)
+    (64, 64, 16, 16, True, 2, 0, True, True, "tie"),
+    (48, 80, 16, 16, False, 1, 0, True, False, "synth"),
+    (64, 64, 8, 6, False, 1, 0, True, True, "synth"),      # bs 8 FME: generic kernel
+    (16, 32, 16, 16, True, 1, 0, True, True, "synth"),     # no valid FME candidate: 128 prediction
+    (256, 272, 16, 16, True, 1, 0, True, True, "synth"),   # several FME tiles
+    (64, 96, 16, 16, True, 3, 1, False, True, "tie"),
+    (64, 48, 8, 16, False, 2, 1, False, True, "synth"),    # bs 8 fast chain, two refs
+    (96, 128, 16, 16, True, 2, 1, True, True, "synth"),
+    (80, 64, 16, 16, False, 1, 2, False, True, "synth"),
+    (80, 64, 8, 16, False, 1, 2, True, True, "tie"),
+]
+
+
+@pytest.mark.parametrize("h,w,bs,sr,vbs,nref,me_mode,fme,wrap,kind", ME_VAR_CASES)
+def test_inter_me_variants_vs_oracle(gpu, h, w, bs, sr, vbs, nref, me_mode, fme, wrap, kind):
+    from oracle import oracle as O
+    from streamoptima_amd.engine import Engine
+    seq = _frames(kind, h, w, 5 + h + 3 * w, n=nref + 1)
+    cur, refs = seq[nref], [seq[k] for k in range(nref)]
+    exp = O.inter_frame(cur, refs, bs, sr, 3, None, vbs, 0.015, me_mode=me_mode, fme=fme, fme_wrap=wrap)
+    eng = Engine(h, w, bs, sr, vbs, 0.015, gpu, me_mode=me_mode, fme=fme)
+    rp = [_plane(r, gpu) for r in refs]
+    sym = eng.encode_p(_plane(cur, gpu), rp, 3, fme_wrap=wrap)
+    torch.cuda.synchronize()
+    hs = _sym_host(sym)
+    _assert_frame(hs, exp)
+    assert (hs["mae_num"] == exp["mae_num"]).all()
+    if fme:
+        rec = eng.recon_inter(rp, sym.split, sym.mv, sym.qtc, 3, fme_wrap=wrap)
+        torch.cuda.synchronize()
+        assert (rec.cpu().numpy() == O.inter_recon(refs, exp["split"], exp["mv"], exp["qtc"], bs, 3, fme=True,
+                                                   fme_wrap=wrap)).all()

@@ -89,11 +89,24 @@ def test_unsupported_modes_raise():
     from streamoptima_amd.Encoder import Y_Video_codec
     z = np.zeros((1, 32, 32), np.uint8)
     with pytest.raises(NotImplementedError):
-        Y_Video_codec(32, 32, 1, 16, 16, 4, 1, 0, 0.015, False, y_only_frame_arr=z, FMEEnable=True)
-    with pytest.raises(NotImplementedError):
         Y_Video_codec(32, 32, 1, 16, 16, 4, 1, 1, 0.015, False, y_only_frame_arr=z)
+    with pytest.raises(ValueError):      # NameError on `mvp` in the reference (Encoder.py:609)
+        Y_Video_codec(32, 32, 1, 16, 16, 4, 1, 0, 0.015, True, y_only_frame_arr=z, fast_me=True, ParallelMode=2)
     with pytest.raises(NotImplementedError):
         Y_Video_codec(32, 32, 1, 16, 16, 4, 1, 0, 0.015, False, y_only_frame_arr=z, ParallelMode=3)
+
+
+def test_me_mode_selection():
+    """fast_me / FMEEnable / ParallelMode pick the C-ABI ME mode (include/streamoptima.h)."""
+    from streamoptima_amd import _lib
+    from streamoptima_amd.Encoder import Y_Video_codec
+    z = np.zeros((1, 32, 32), np.uint8)
+    mk = lambda **k: Y_Video_codec(32, 32, 1, 16, 16, 4, 1, 0, 0.015, False, y_only_frame_arr=z, **k)  # noqa: E731
+    assert mk()._me_mode() == _lib.ME_FULL
+    assert mk(fast_me=True)._me_mode() == _lib.ME_FAST
+    assert mk(fast_me=True, ParallelMode=2)._me_mode() == _lib.ME_FAST_PAR
+    assert mk(ParallelMode=2)._me_mode() == _lib.ME_FULL
+    assert mk(FMEEnable=True).FMEEnable
 
 
 def test_engine_refuses_cpu_device():
