@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--kernel-reps", type=int, default=20)
     ap.add_argument("--shard", choices=("gop", "stripe"), default="gop",
                     help="multi-GPU: independent GOP per rank (weak) or block-row stripes of one GOP (strong)")
+    ap.add_argument("--me", choices=("full", "fme", "fast", "fastpar", "fast_fme"), default="full",
+                    help="ME variant: full search (headline), FMEEnable, fast_me (serial chain), fast_me under "
+                         "ParallelMode 2, fast_me + FMEEnable")
     ap.add_argument("--pcie", action="store_true",
                     help="also time the PCIe-inclusive path (pinned host frames in, symbols out)")
     return ap.parse_args()
@@ -98,7 +101,11 @@ def max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
-def me_kernel_name(vbs: bool) -> str:
+def me_kernel_name(vbs: bool, me: str = "full") -> str:
+    if me != "full":
+        f = "true" if "fme" in me else "false"
+        s = "true" if vbs else "false"
+        return {"fme": f"me_fme_kernel<{s}>"}.get(me, f"me_fastpred_kernel<{f}, {s}, 16>")
     impl = os.environ.get("SO_ME_IMPL")
     if impl == "fast":
         return "me_fast_kernel"
@@ -107,7 +114,7 @@ def me_kernel_name(vbs: bool) -> str:
     return "me_sea_kernel"
 
 
-def kernel_roofline(codec, frames_dev, symbols, reps: int) -> dict:
+def kernel_roofline(codec, frames_dev, symbols, reps: int, me_variant: str = "full") -> dict:
     """Average duration of the ME launch (the dominant kernel) and of the TQ launch for a
     P-frame, measured with HIP events recorded on the launch stream.  The launches replay
     the GOP's own P-frame work: launch k encodes frame i = 1 + k % (F-1) against the
@@ -125,11 +132,17 @@ def kernel_roofline(codec, frames_dev, symbols, reps: int) -> dict:
     sym = eng.new_symbols(1)
     st = _lib.stream_handle(eng.device)
 
+    ws = eng.fme_workspace(1) if eng.fme else None
+
     def me():
         cur, refs = pairs[state["k"] % len(pairs)]
         state["k"] += 1
-        _lib.check(lib.so_me_full_search(cur.data_ptr(), refs, 1, h, w, bs, sr, best.data_ptr(), _lib.ptr(sub), st),
-                   "me")
+        if me_variant == "full":
+            _lib.check(lib.so_me_full_search(cur.data_ptr(), refs, 1, h, w, bs, sr, best.data_ptr(), _lib.ptr(sub),
+                                             st), "me")
+        else:   # ME variant incl. its phase-plane build (FME)
+            _lib.check(lib.so_me_search_ex(cur.data_ptr(), refs, 1, h, w, bs, sr, eng.me_mode, int(eng.fme), 1,
+                                           _lib.ptr(ws), best.data_ptr(), _lib.ptr(sub), st), "me_ex")
 
     def tq():
         cur, refs = pairs[state["k"] % len(pairs)]
@@ -150,8 +163,9 @@ def kernel_roofline(codec, frames_dev, symbols, reps: int) -> dict:
             else:
                 os.environ["SO_ME_IMPL"] = old
 
-    out = {}
-    for name, fn in (("me", me), ("tq", tq), ("me_dense", me_dense)):
+    todo = (("me", me), ("tq", tq), ("me_dense", me_dense)) if me_variant == "full" else (("me", me), ("tq", tq))
+    out = {"me_dense": float("nan")}
+    for name, fn in todo:
         for _ in range(3):
             fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -263,7 +277,10 @@ def main():
     dev = torch.device("cuda", local)
     h, w, f = cfg["h"], cfg["w"], cfg["frames"]
     hp = -(-h // 16) * 16
-    codec = Y_Video_codec(h, w, f, 16, 16, cfg["qp"], f, 0, 0.015, args.vbs, y_only_frame_arr=None, device=dev)
+    me_kw = {"full": {}, "fme": dict(FMEEnable=True), "fast": dict(fast_me=True),
+             "fastpar": dict(fast_me=True, ParallelMode=2), "fast_fme": dict(fast_me=True, FMEEnable=True)}[args.me]
+    codec = Y_Video_codec(h, w, f, 16, 16, cfg["qp"], f, 0, 0.015, args.vbs, y_only_frame_arr=None, device=dev,
+                          **me_kw)
     eng = codec.engine()
     stripe = args.shard == "stripe"
     frames = alloc_planes(f, hp, w, dev, fill=128)
@@ -295,7 +312,7 @@ def main():
     sse = res["sse"].cpu().numpy()
     psnr_mean = float(np.mean([10 * np.log10(255 ** 2 / (s / (hp * w))) for s in sse if s > 0]))
 
-    rl = kernel_roofline(codec, frames, res["symbols"], args.kernel_reps) if rank == 0 else None
+    rl = kernel_roofline(codec, frames, res["symbols"], args.kernel_reps, args.me) if rank == 0 else None
     delta = psnr_delta_vs_reference(dev) if rank == 0 else None
     pcie = pcie_inclusive(codec, cfg, frames) if rank == 0 and args.pcie and not stripe else None
     cpu = None
@@ -313,7 +330,7 @@ def main():
     if os.path.exists(pmc):
         try:
             kern = json.load(open(pmc)).get(args.config + ("_vbs" if args.vbs else ""), {}).get("kernels", {})
-            hit = kern.get("so::" + me_kernel_name(args.vbs))
+            hit = kern.get("so::" + me_kernel_name(args.vbs, args.me))
             traffic = round(hit["hbm_bytes"]) if hit else None
         except Exception:
             traffic = None
@@ -323,10 +340,10 @@ def main():
         "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "strong" if stripe else "weak",
         "vs_baseline": None, "dtype": "u8", "data": "synthetic (splitmix64 texture, +2/+1 px/frame motion)",
         "config": {"workload": cfg["workload"], "width": w, "height": h, "frames": f, "block_size": 16,
-                   "search_range": 16, "qp": cfg["qp"], "vbs": bool(args.vbs), "nRefFrames": 1,
+                   "search_range": 16, "qp": cfg["qp"], "vbs": bool(args.vbs), "nRefFrames": 1, "me": args.me,
                    "transform": "fp64 pocketfft-exact DCT",
                    "parallelism": f"stripe x{world} (all_gather recon per frame)" if stripe else f"gop-per-rank x{world}"},
-        "roofline": {"bound": "hbm", "kernel": me_kernel_name(args.vbs), "achieved": round(me_gbs, 2),
+        "roofline": {"bound": "hbm", "kernel": me_kernel_name(args.vbs, args.me), "achieved": round(me_gbs, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(me_gbs / HBM_PEAK_GBS, 5),
                      "traffic": traffic, "algorithmic_bytes": rl["me_bytes"],
                      "launch_us": round(rl["me_s"] * 1e6, 2),
@@ -346,6 +363,10 @@ def main():
         "psnr_mean_db": round(psnr_mean, 4),
         "psnr_delta_vs_reference": delta,
     }
+    if args.me != "full":
+        # the SAD-op accounting above is the integer full search's; the variants report time only
+        line["roofline"]["valu_sad"] = None
+        line["roofline"]["dense_me"] = None
     if pcie:
         line.update(pcie)
     if cpu:

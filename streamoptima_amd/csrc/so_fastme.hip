@@ -23,6 +23,7 @@
 // with FME the stride-2 sample of F at (X+dx, Y+dy) is 4 CONSECUTIVE bytes of phase plane
 // P_ab (a = (Y+dy) & 1, b = (X+dx) & 1), see so_me.hip FmePhase.
 #include "so_common.h"
+#include "so_dpp.h"
 
 namespace so {
 
@@ -36,12 +37,13 @@ SO_DEV uint32_t unaligned_u32(const uint8_t* p) {
     return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
 }
 
-// sum over aligned groups of G lanes, result in every lane of the group
+// sum over aligned groups of G lanes (4: quads, 16: DPP rows, 64: the wave), result in
+// every lane of the group
 template <int G>
 SO_DEV uint32_t group_sum_u32(uint32_t v) {
-#pragma unroll
-    for (int m = 1; m < G; m <<= 1) v += __shfl_xor(v, m, 64);
-    return v;
+    if constexpr (G == 64) return wave_sum_u32(v);
+    else if constexpr (G == 16) return row_sum_u32(v);
+    else return quad_sum_u32(v);
 }
 
 struct Mvp {
@@ -57,31 +59,39 @@ SO_DEV void fast_search(const uint8_t* __restrict__ cur, const FastRefs& R, int 
     const int k = FME ? 2 : 1;
     const int PW = FME ? 2 * W - 1 : W, PH = FME ? 2 * H - 1 : H;
     const int X = k * x, Y = k * y;
-    uint32_t cw = 0;
-    if (act) cw = *reinterpret_cast<const uint32_t*>(cur + (size_t)(y + lane_i) * W + x + 4 * lane_c);
+    const uint32_t cw = *reinterpret_cast<const uint32_t*>(cur + (size_t)(y + (act ? lane_i : 0)) * W + x +
+                                                           4 * (act ? lane_c : 0));
     uint32_t best = 0xFFFFFFFFu;   // (sad << 8) | candidate index r * 9 + ci
+#pragma unroll 1
     for (int r = 0; r < nref; ++r) {
+        // all nine candidates' bytes are loaded before any is used (one latency per ref):
+        // the addresses are clamped into the plane, invalid candidates are masked below
+        uint32_t wv[9];
 #pragma unroll
         for (int ci = 0; ci < 9; ++ci) {
-            const int dx = mvp.dx - 1 + ci / 3, dy = mvp.dy - 1 + ci % 3;
-            const int px = X + dx, py = Y + dy;
+            const int px = X + mvp.dx - 1 + ci / 3, py = Y + mvp.dy - 1 + ci % 3;
+            const uint8_t* p;
+            if constexpr (FME) {
+                int row = (py >> 1) + lane_i, col = (px >> 1) + 4 * lane_c;
+                row = row < 0 ? 0 : (row > H - 1 ? H - 1 : row);
+                col = col < 0 ? 0 : (col > W - 4 ? W - 4 : col);
+                p = R.p[4 * r + 2 * (py & 1) + (px & 1)] + (size_t)row * W + col;
+            } else {
+                int row = py + lane_i, col = px + 4 * lane_c;
+                row = row < 0 ? 0 : (row > H - 1 ? H - 1 : row);
+                col = col < 0 ? 0 : (col > W - 4 ? W - 4 : col);
+                p = R.p[r] + (size_t)row * W + col;
+            }
+            wv[ci] = unaligned_u32(p);
+        }
+#pragma unroll
+        for (int ci = 0; ci < 9; ++ci) {
+            const int px = X + mvp.dx - 1 + ci / 3, py = Y + mvp.dy - 1 + ci % 3;
             const bool ok = 0 <= px && px < PW - n && 0 <= py && py < PH - n && px + 2 * n < PW - n &&
                             py + 2 * n < PH - n;   // uniform over the group
-            if (!ok) continue;
-            uint32_t s = 0;
-            if (act) {
-                const uint8_t* p;
-                if constexpr (FME) {
-                    p = R.p[4 * r + 2 * (py & 1) + (px & 1)] + (size_t)((py >> 1) + lane_i) * W + (px >> 1) +
-                        4 * lane_c;
-                } else {
-                    p = R.p[r] + (size_t)(py + lane_i) * W + px + 4 * lane_c;
-                }
-                s = __builtin_amdgcn_sad_u8(cw, unaligned_u32(p), 0u);
-            }
-            s = group_sum_u32<G>(s);
+            const uint32_t s = group_sum_u32<G>(act ? __builtin_amdgcn_sad_u8(cw, wv[ci], 0u) : 0u);
             const uint32_t key = (s << 8) | (uint32_t)(r * 9 + ci);
-            best = key < best ? key : best;
+            best = (ok && key < best) ? key : best;
         }
     }
     if (best == 0xFFFFFFFFu) {

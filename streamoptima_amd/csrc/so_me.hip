@@ -20,6 +20,7 @@
 #include <string.h>
 
 #include "so_common.h"
+#include "so_dpp.h"
 
 namespace so {
 
@@ -111,7 +112,6 @@ SO_DEV void load_cur_sgpr(const uint8_t* __restrict__ cur, int W, int x, int y, 
     }
 }
 
-SO_DEV uint64_t wave_min_u64(uint64_t v);   // DPP version below (wave_min_u64_dpp)
 
 template <int N>
 SO_DEV void acc_fence_n(uint32_t (&a)[N]) {
@@ -580,74 +580,6 @@ struct SeaGeo {
 };
 
 
-// Cross-lane reductions with DPP (register-to-register VALU; no ds_bpermute round trips):
-// quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror leave every lane with its
-// 16-lane row's result; row_bcast15 (rows 1, 3) and row_bcast31 (rows 2, 3) carry it into
-// lane 63, which v_readlane broadcasts.  DPP lanes without a source keep `old`.
-constexpr int kDppQuad1032 = 0xB1, kDppQuad2301 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
-constexpr int kDppBcast15 = 0x142, kDppBcast31 = 0x143;
-
-SO_DEV uint32_t row_min_u32(uint32_t v) {
-    uint32_t o;
-    o = __builtin_amdgcn_update_dpp(v, v, kDppQuad1032, 0xF, 0xF, false); v = o < v ? o : v;
-    o = __builtin_amdgcn_update_dpp(v, v, kDppQuad2301, 0xF, 0xF, false); v = o < v ? o : v;
-    o = __builtin_amdgcn_update_dpp(v, v, kDppHalfMirror, 0xF, 0xF, false); v = o < v ? o : v;
-    o = __builtin_amdgcn_update_dpp(v, v, kDppMirror, 0xF, 0xF, false); v = o < v ? o : v;
-    return v;
-}
-
-// wave-uniform minimum (SGPR)
-SO_DEV uint32_t wave_min_u32(uint32_t v) {
-    v = row_min_u32(v);
-    uint32_t o;
-    o = __builtin_amdgcn_update_dpp(v, v, kDppBcast15, 0xA, 0xF, false); v = o < v ? o : v;
-    o = __builtin_amdgcn_update_dpp(v, v, kDppBcast31, 0xC, 0xF, false); v = o < v ? o : v;
-    return __builtin_amdgcn_readlane(v, 63);
-}
-
-// sum over each 16-lane row, in every lane of the row
-SO_DEV uint32_t row_sum_u32(uint32_t v) {
-    v += __builtin_amdgcn_update_dpp(0u, v, kDppQuad1032, 0xF, 0xF, false);
-    v += __builtin_amdgcn_update_dpp(0u, v, kDppQuad2301, 0xF, 0xF, false);
-    v += __builtin_amdgcn_update_dpp(0u, v, kDppHalfMirror, 0xF, 0xF, false);
-    v += __builtin_amdgcn_update_dpp(0u, v, kDppMirror, 0xF, 0xF, false);
-    return v;
-}
-
-// wave-uniform sum (SGPR)
-SO_DEV uint32_t wave_sum_u32(uint32_t v) {
-    v = row_sum_u32(v);
-    v += __builtin_amdgcn_update_dpp(0u, v, kDppBcast15, 0xA, 0xF, false);
-    v += __builtin_amdgcn_update_dpp(0u, v, kDppBcast31, 0xC, 0xF, false);
-    return __builtin_amdgcn_readlane(v, 63);
-}
-
-template <int CTRL, int RMASK>
-SO_DEV uint64_t dpp_min_step(uint64_t v) {
-    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-    const uint32_t olo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, RMASK, 0xF, false);
-    const uint32_t ohi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, RMASK, 0xF, false);
-    const uint64_t o = ((uint64_t)ohi << 32) | olo;
-    return o < v ? o : v;
-}
-
-// wave-uniform 64-bit minimum
-SO_DEV uint64_t wave_min_u64_dpp(uint64_t v) {
-    v = dpp_min_step<kDppQuad1032, 0xF>(v);
-    v = dpp_min_step<kDppQuad2301, 0xF>(v);
-    v = dpp_min_step<kDppHalfMirror, 0xF>(v);
-    v = dpp_min_step<kDppMirror, 0xF>(v);
-    v = dpp_min_step<kDppBcast15, 0xA>(v);
-    v = dpp_min_step<kDppBcast31, 0xC>(v);
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, 63), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), 63);
-    return ((uint64_t)hi << 32) | lo;
-}
-
-SO_DEV uint64_t wave_min_u64(uint64_t v) { return wave_min_u64_dpp(v); }
-
-SO_DEV uint32_t lane_prefix(uint64_t mask) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
 
 __global__ void __launch_bounds__(SeaGeo::NTHREADS) __attribute__((amdgpu_waves_per_eu(4)))
 me_sea_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
