@@ -11,6 +11,8 @@
 """
 from __future__ import annotations
 
+import ast
+import re
 from functools import lru_cache
 
 import numpy as np
@@ -129,3 +131,86 @@ def entropy_encoder_frame(frame_residuals, block_size) -> str:
                 else:
                     parts.append(t + ",")
     return "".join(parts)
+
+
+# ---- parsers (decoder.py:547-690) ------------------------------------------------------------
+# The reference parses with eval(); the tokens are int / tuple / list literals -- numpy 2
+# prints the package's values as np.int64(v) -- so unwrapping those and ast.literal_eval
+# read exactly the same values without executing anything.
+_NP_SCALAR = re.compile(r"np\.u?int(?:8|16|32|64)\((-?\d+)\)")
+
+
+def _literal(text: str):
+    return ast.literal_eval(_NP_SCALAR.sub(r"\1", text))
+
+def entropy_decoder_block(encoded_block, block_size) -> list:
+    """decoder.py:547-586: RLE tokens -> block_size x block_size list of lists (anti-diagonal
+    scan; a zero token ends the block, trailing positions stay 0)."""
+    arr = []
+    i = 0
+    while i < len(encoded_block):
+        t = encoded_block[i]
+        if t < 0:
+            arr.extend(encoded_block[i + 1:i + 1 - t])
+            i += -t
+        else:
+            if t == 0:
+                break
+            arr.extend([0] * t)
+        i += 1
+    out = np.zeros(block_size * block_size, dtype=int)
+    order = scan_order(block_size)
+    m = min(len(arr), len(order))
+    out[order[:m]] = arr[:m]
+    return out.reshape(block_size, block_size).tolist()
+
+
+def differential_decoder_frame(line: str, rc_flag, num_blocks_per_row):
+    """decoder.py:589-644: '<type>|...' -> (frame_type, per-block mvs, per-row QPs)."""
+    rc = rc_flag is not None and rc_flag > 0
+    raw = line.strip().split("|")
+    frame_type = int(raw[0])
+    mvs, qps = [], []
+    ref_qp = 0
+    ref = 0 if frame_type == 0 else (0, 0, 0)
+    for j, tok in enumerate(raw[1].split(";")):
+        if rc and j % num_blocks_per_row == 0:
+            q, tok = tok.split("@")
+            ref_qp = ref_qp + int(_literal(q))
+            qps.append(ref_qp)
+        split, body = tok.split("'")
+        v = _literal(body)
+        if frame_type == 0:
+            if split == "0":
+                ref = ref + int(v)
+                mvs.append((0, ref))
+            else:
+                sub = []
+                for d in v:
+                    ref = ref + d
+                    sub.append(ref)
+                mvs.append((1, sub))
+        else:
+            if split == "0":
+                ref = (ref[0] + v[0], ref[1] + v[1], ref[2] + v[2])
+                mvs.append((0, ref))
+            else:
+                sub = []
+                for d in v:
+                    ref = (ref[0] + d[0], ref[1] + d[1], ref[2] + d[2])
+                    sub.append(ref)
+                mvs.append((1, sub))
+    return frame_type, mvs, qps
+
+
+def entropy_decoder_frame(line: str, block_size) -> list:
+    """decoder.py:646-664: residual RLE line -> [(0, QTC) | (1, [QTC x 4])]."""
+    out = []
+    for tok in line.strip().split(";"):
+        split, body = tok.split("'")
+        v = _literal(body)
+        if split == "0":
+            out.append((0, np.array(entropy_decoder_block(v, block_size))))
+        else:
+            out.append((1, [np.array(entropy_decoder_block(sb, block_size // 2)) for sb in v]))
+    return out

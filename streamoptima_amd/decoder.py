@@ -11,6 +11,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from . import bitstream as _bs
 from .bitstream import entropy_encoder_block  # noqa: F401  (API parity helpers live there)
 from .engine import Engine, alloc_planes
 
@@ -124,6 +125,40 @@ class decoder:
             self.decoded_vid_f = True
             self.decoded_vid = host
         return host
+
+    # ---- text bitstream (decoder.py:547-710) ----------------------------------------------
+    def entropy_decoder_block(self, encoded_block, block_size):
+        return _bs.entropy_decoder_block(encoded_block, block_size)
+
+    def differential_decoder_frame(self, mv_for_frame):
+        return _bs.differential_decoder_frame(mv_for_frame, self.RCFlag, self.num_blocks_per_row)
+
+    def entropy_decoder_frame(self, residual_for_frame, block_size):
+        return _bs.entropy_decoder_frame(residual_for_frame, block_size)
+
+    def decode_differential_entropy(self, all_mv_f, all_residual_f, block_size):
+        """decoder.py:666-684: the two text files -> per-frame symbol lists."""
+        frame_type_seq, mv_for_vid, qp_for_vid, res_for_vid = [], [], [], []
+        with open(all_mv_f) as f:
+            for line in f:
+                ft, mvs, qps = self.differential_decoder_frame(line)
+                frame_type_seq.append(ft)
+                mv_for_vid.append(mvs)
+                qp_for_vid.append(qps)
+        with open(all_residual_f) as f:
+            for line in f:
+                res_for_vid.append(self.entropy_decoder_frame(line, block_size))
+        return frame_type_seq, mv_for_vid, qp_for_vid, res_for_vid
+
+    def decode_bitstream(self, mv_file, residual_file, intra_mode=None, intra_dur=None, block_size=None, frames=None,
+                         width=None, height=None, save_decoded_frames=True):
+        """decoder.py:686-709: parse the transmitted text bitstream (transmit_bitstream)
+        on the host, reconstruct every frame on the GPU."""
+        bs = block_size or self.block_size
+        ft, mvs, qps, res = self.decode_differential_entropy(mv_file, residual_file, bs)
+        self.mv_per_frame = mvs
+        self.residuals_per_frame = res
+        return self.decode(ft, res, qps, mvs, intra_mode, intra_dur, bs, frames, width, height, save_decoded_frames)
 
     def save_decoded_frames(self, filename="yuv/decoded_bitstream_frames.yuv"):
         if not self.decoded_vid_f:
