@@ -181,19 +181,56 @@ int so_me_search_ex(const uint8_t* cur, const uint8_t* const* refs, int nref, in
                     int sr, int me_mode, int fme, int fme_wrap, uint8_t* fme_planes,
                     int32_t* out_best, int32_t* out_sub, void* stream);
 
-/* so_encode_p_rows generalised by me_mode / fme: the same outputs and scratch. */
+/*
+ * so_encode_p_rows generalised by me_mode / fme, a per-block QP map and flags; the same
+ * outputs and scratch.
+ *   qp_map  device int32 [H/bs * W/bs] per-block QP (full-frame, raster) or NULL; it
+ *           replaces qp_row / qp_rd for the quantisation and reconstruction of each block
+ *           (the VBS RD decision keeps qp_rd, like the reference's); see so_qp_map
+ *   flags   SO_REUSE_ME: skip the ME; `scratch` (and fme_planes) still hold the ME records
+ *           of a previous call on the same cur / refs / rows (pass 2 of two-pass RC)
+ */
+#define SO_REUSE_ME 1
 int so_encode_p_rows_ex(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W,
                         int bs, int sr, int by0, int by1, int qp_rd, const int32_t* qp_row,
-                        int vbs, double lam, int me_mode, int fme, int fme_wrap,
-                        uint8_t* fme_planes, uint8_t* out_split, int16_t* out_mv,
+                        const int32_t* qp_map, int vbs, double lam, int me_mode, int fme,
+                        int fme_wrap, uint8_t* fme_planes, int flags, uint8_t* out_split,
+                        int16_t* out_mv,
                         int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae_num,
                         uint8_t* out_recon, int32_t* out_sse, int32_t* scratch, void* stream);
 
-/* Decoder P-frame reconstruction with FMEEnable (decoder.py:97-211 FME branches). */
+/* Decoder P-frame reconstruction with FMEEnable (decoder.py:97-211 FME branches) and a
+ * per-block QP map (NULL: qp_row / qp). */
 int so_inter_recon_ex(const uint8_t* const* refs, int nref, int H, int W, int bs, int qp,
-                      const int32_t* qp_row, int fme, int fme_wrap, uint8_t* fme_planes,
+                      const int32_t* qp_row, const int32_t* qp_map, int fme, int fme_wrap,
+                      uint8_t* fme_planes,
                       const uint8_t* split, const int16_t* mv, const int16_t* qtc,
                       uint8_t* out_recon, void* stream);
+
+/* so_encode_i_rows / so_intra_recon with a per-block QP map (NULL: qp_row / qp_rd). */
+int so_encode_i_rows_ex(const uint8_t* cur, int H, int W, int bs, int sr, int by0, int by1,
+                        int qp_rd, const int32_t* qp_row, const int32_t* qp_map, int vbs,
+                        double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc,
+                        int32_t* out_tokens, int32_t* out_mae_num, uint8_t* out_recon,
+                        int32_t* out_sse, int32_t* scratch, void* stream);
+int so_intra_recon_ex(int H, int W, int bs, int qp, const int32_t* qp_row, const int32_t* qp_map,
+                      const uint8_t* split, const int16_t* mv, const int16_t* qtc,
+                      uint8_t* out_recon, int32_t* scratch, void* stream);
+
+/*
+ * ROI and two-pass rate control (BASELINE configs[4]; a build extension -- the reference
+ * computes per-row stats in complete_*_flow and discards them, Encoder.py:1627-1640,
+ * 1696-1707, and has no ROI).  Writes the per-block QP map of block rows [by0, by1):
+ *   qp = clamp(base + delta + roi, qp_lo, qp_hi),  base = qp_row[by] or qp_rd,
+ *   delta in [-2, 2] from the block's pass-1 token count t against its row's sum m over n
+ *   blocks: [t n >= 2m] + [t n >= 4m] - [2 t n < m] - [4 t n < m]  (0 when tokens == NULL).
+ *   tokens  device int32 stripe-local pass-1 token counts (so_encode_*_rows out_tokens), or NULL
+ *   roi     device int32 [H/bs * W/bs] QP offsets (negative = finer), or NULL
+ *   out_qp_map  device int32 [H/bs * W/bs] (rows outside [by0, by1) untouched)
+ */
+int so_qp_map(const int32_t* tokens, int H, int W, int bs, int by0, int by1, int qp_rd,
+              const int32_t* qp_row, const int32_t* roi, int qp_lo, int qp_hi,
+              int32_t* out_qp_map, void* stream);
 
 /* Decoder: P-frame reconstruction from symbols (decoder.py:97-211). */
 int so_inter_recon(const uint8_t* const* refs, int nref, int H, int W, int bs, int qp,

@@ -29,7 +29,10 @@ def bitrate_per_row(target, frame_rate, h, bs):
 
 def encode_gop(frames, qp, intra_dur, bs=16, sr=16, vbs=False, lam=0.015, nref=1, rc=None,
                target=None, tables=None, intra_thresh=None, frame_rate=30, fast_me=False, fme=False,
-               parallel_mode=0):
+               parallel_mode=0, roi=None, qp_clamp=(0, 12)):
+    """encode() (Encoder.py:1790-1898) over the C oracle.  Build extensions restated from
+    streamoptima_amd/Encoder.py: rc = 3 is two-pass RC (pass-1 tokens -> oc_qp_map -> pass
+    2), roi = flat per-block QP offsets (or None); r["qp_map"] holds the per-block QPs."""
     f, h, w = frames.shape
     # the start reference is float64 all-128 (Encoder.py:1798): it matters only to the
     # frac frame's uint8 wrap (oracle.fme_upsample)
@@ -39,18 +42,35 @@ def encode_gop(frames, qp, intra_dur, bs=16, sr=16, vbs=False, lam=0.015, nref=1
     qp_sched = None
     if rc is not None and rc > 0:
         qp_sched = row_qp_schedule(bitrate_per_row(target, frame_rate, h, bs), tables, h // bs)
+    nbx, nby = w // bs, h // bs
+    two_pass = rc is not None and rc >= 3
+    lo, hi = qp_clamp
+
+    def enc(cur, intra, qp_rd, wrap):
+        run = (lambda qm: O.intra_frame(cur, bs, sr, qp_rd, qp_sched, vbs, lam, qp_map=qm)) if intra else (
+            lambda qm: O.inter_frame(cur, ref_frames, bs, sr, qp_rd, qp_sched, vbs, lam, me_mode=me_mode, fme=fme,
+                                     fme_wrap=wrap, qp_map=qm))
+        qm = None
+        if two_pass:
+            r1 = run(None)
+            qm = O.qp_map(r1["tokens"], nbx, nby, qp_rd, qp_sched, roi, lo, hi)
+        elif roi is not None:
+            qm = O.qp_map(None, nbx, nby, qp_rd, qp_sched, roi, lo, hi)
+        r = run(qm)
+        r["qp_map"] = qm
+        return r
+
     out = []
     for i in range(f):
         cur = frames[i]
         if i % intra_dur == 0:
-            r = O.intra_frame(cur, bs, sr, qp, qp_sched, vbs, lam)
+            r = enc(cur, True, qp, True)
             ft = 0
         else:
-            r = O.inter_frame(cur, ref_frames, bs, sr, qp, qp_sched, vbs, lam, me_mode=me_mode, fme=fme,
-                              fme_wrap=not any(ref_float))
+            r = enc(cur, False, qp, not any(ref_float))
             ft = 1
             if rc is not None and rc > 1 and int(r["tokens"].sum()) > intra_thresh:
-                r = O.intra_frame(cur, bs, sr, qp_sched[-1], qp_sched, vbs, lam)
+                r = enc(cur, True, qp_sched[-1], True)
                 ft = 0
         r["frame_type"] = ft
         r["qp_row"] = list(qp_sched) if qp_sched else []

@@ -107,8 +107,12 @@ def _refs_array(refs):
     return arrs, ptrs
 
 
+def _i32(a):
+    return None if a is None else np.ascontiguousarray(a, dtype=np.int32)
+
+
 def inter_frame(cur: np.ndarray, refs, bs=16, sr=16, qp=4, qp_row=None, vbs=False,
-                lam=0.015, me_mode=0, fme=False, fme_wrap=True) -> FrameResult:
+                lam=0.015, me_mode=0, fme=False, fme_wrap=True, qp_map=None) -> FrameResult:
     """complete_inter_flow for one frame (oc_inter_frame_ex).  me_mode 0 = full search,
     1 = fast_me (serial predictor chain), 2 = fast_me under ParallelMode 2; fme = FMEEnable
     with the frac frame's uint8 wrap `fme_wrap` (True unless the reference list still holds
@@ -122,8 +126,10 @@ def inter_frame(cur: np.ndarray, refs, bs=16, sr=16, qp=4, qp_row=None, vbs=Fals
                       qtc=np.zeros((nb, bs * bs), np.int16), tokens=np.zeros(nb, np.int32),
                       mae_num=np.zeros(nb, np.int64), recon=np.zeros((h, w), np.uint8))
     qr = None if qp_row is None else np.ascontiguousarray(qp_row, dtype=np.int32)
+    qm = _i32(qp_map)
     rc = lib().oc_inter_frame_ex(_p(cur), hp, wp, ptrs, len(refs), h, w, bs, sr, qp,
-                                 None if qr is None else _p(qr), int(vbs), ctypes.c_double(lam),
+                                 None if qr is None else _p(qr), None if qm is None else _p(qm), int(vbs),
+                                 ctypes.c_double(lam),
                                  int(me_mode), int(bool(fme)), int(bool(fme_wrap)),
                                  _p(out["split"]), _p(out["mv"]), _p(out["qtc"]),
                                  _p(out["tokens"]), _p(out["mae_num"]), _p(out["recon"]))
@@ -142,7 +148,7 @@ def fme_upsample(ref: np.ndarray, wrap=True) -> np.ndarray:
 
 
 def intra_frame(cur: np.ndarray, bs=16, sr=16, qp=6, qp_row=None, vbs=False,
-                lam=0.015) -> FrameResult:
+                lam=0.015, qp_map=None) -> FrameResult:
     cur = np.ascontiguousarray(cur, dtype=np.uint8)
     hp, wp = cur.shape
     nb = (hp // bs) * (wp // bs)
@@ -150,8 +156,9 @@ def intra_frame(cur: np.ndarray, bs=16, sr=16, qp=6, qp_row=None, vbs=False,
                       qtc=np.zeros((nb, bs * bs), np.int16), tokens=np.zeros(nb, np.int32),
                       mae_num=np.zeros(nb, np.int64), recon=np.zeros((hp, wp), np.uint8))
     qr = None if qp_row is None else np.ascontiguousarray(qp_row, dtype=np.int32)
-    rc = lib().oc_intra_frame(_p(cur), hp, wp, bs, sr, qp, None if qr is None else _p(qr),
-                              int(vbs), ctypes.c_double(lam), _p(out["split"]), _p(out["mv"]),
+    qm = _i32(qp_map)
+    rc = lib().oc_intra_frame_ex(_p(cur), hp, wp, bs, sr, qp, None if qr is None else _p(qr),
+                                 None if qm is None else _p(qm), int(vbs), ctypes.c_double(lam), _p(out["split"]), _p(out["mv"]),
                               _p(out["qtc"]), _p(out["tokens"]), _p(out["mae_num"]),
                               _p(out["recon"]))
     if rc != 0:
@@ -159,16 +166,28 @@ def intra_frame(cur: np.ndarray, bs=16, sr=16, qp=6, qp_row=None, vbs=False,
     return out
 
 
-def inter_recon(refs, split, mv, qtc, bs=16, qp=4, qp_row=None, fme=False, fme_wrap=True) -> np.ndarray:
+def inter_recon(refs, split, mv, qtc, bs=16, qp=4, qp_row=None, fme=False, fme_wrap=True,
+                qp_map=None) -> np.ndarray:
     h, w = refs[0].shape
     arrs, ptrs = _refs_array(refs)
     recon = np.zeros((h, w), np.uint8)
     qr = None if qp_row is None else np.ascontiguousarray(qp_row, dtype=np.int32)
-    lib().oc_inter_recon_ex(ptrs, len(refs), h, w, bs, qp, None if qr is None else _p(qr), int(bool(fme)),
+    qm = _i32(qp_map)
+    lib().oc_inter_recon_ex(ptrs, len(refs), h, w, bs, qp, None if qr is None else _p(qr),
+                            None if qm is None else _p(qm), int(bool(fme)),
                             int(bool(fme_wrap)), _p(np.ascontiguousarray(split, np.uint8)),
                             _p(np.ascontiguousarray(mv, np.int16)),
                             _p(np.ascontiguousarray(qtc, np.int16)), _p(recon))
     return recon
+
+
+def qp_map(tokens, nbx, nby, qp_rd, qp_row=None, roi=None, qp_lo=0, qp_hi=12) -> np.ndarray:
+    """Per-block QP map of ROI / two-pass RC (oc_qp_map); tokens/roi flat [nby*nbx] or None."""
+    out = np.zeros(nbx * nby, np.int32)
+    t, r, qr = _i32(tokens), _i32(roi), _i32(qp_row)
+    lib().oc_qp_map(None if t is None else _p(t), nbx, nby, qp_rd, None if qr is None else _p(qr),
+                    None if r is None else _p(r), qp_lo, qp_hi, _p(out))
+    return out
 
 
 def sse(a: np.ndarray, b: np.ndarray) -> int:

@@ -563,6 +563,7 @@ static void fetch_pred2(const uint8_t *pl, int PH, int PW, int step, int px, int
  *   refs    : nref reference frames, H x W uint8 (H = Hp, W = Wp required)
  *   qp_rd   : QP in effect during inter_prediction (RD decisions)
  *   qp_row  : per block-row QP (NULL => qp_rd everywhere)
+ *   qp_map  : per-block QP (build extension: ROI / two-pass RC, oc_qp_map); overrides qp_row
  *   me_mode : 0 find_best_match (full search);
  *             1 fast_me, serial branch: the predictor is the previous block's mv in raster
  *               order, starting at (0,0,0) (:462, :581), over all nref refs;
@@ -578,7 +579,7 @@ static void fetch_pred2(const uint8_t *pl, int PH, int PW, int step, int px, int
  */
 EXPORT int oc_inter_frame_ex(const uint8_t *cur, int Hp, int Wp, const uint8_t *const *refs,
                              int nref, int H, int W, int bs, int sr, int qp_rd,
-                             const int32_t *qp_row, int vbs, double lam, int me_mode, int fme,
+                             const int32_t *qp_row, const int32_t *qp_map, int vbs, double lam, int me_mode, int fme,
                              int fme_wrap, uint8_t *split, int16_t *mv, int16_t *qtc,
                              int32_t *tokens, int64_t *mae_num, uint8_t *recon) {
     if (bs != 16 && bs != 8) return -1;
@@ -606,7 +607,7 @@ EXPORT int oc_inter_frame_ex(const uint8_t *cur, int Hp, int Wp, const uint8_t *
         for (int bx = 0; bx < nbx; ++bx) {
             const int b = by * nbx + bx, x = bx * bs, y = by * bs;
             const uint8_t *cb = cur + (size_t)y * Wp + x;
-            const int qpr = qp_row ? qp_row[by] : qp_rd;
+            const int qpr = qp_map ? qp_map[b] : (qp_row ? qp_row[by] : qp_rd);
             const int eligible = vbs && x != 0 && y != 0;
             if (me_mode == 2) { mvp.dx = 0; mvp.dy = 0; mvp.ref = 0; }
             om_mv sm[4];
@@ -702,7 +703,7 @@ EXPORT int oc_inter_frame(const uint8_t *cur, int Hp, int Wp, const uint8_t *con
                           const int32_t *qp_row, int vbs, double lam, uint8_t *split,
                           int16_t *mv, int16_t *qtc, int32_t *tokens, int64_t *mae_num,
                           uint8_t *recon) {
-    return oc_inter_frame_ex(cur, Hp, Wp, refs, nref, H, W, bs, sr, qp_rd, qp_row, vbs, lam, 0, 0, 0, split, mv,
+    return oc_inter_frame_ex(cur, Hp, Wp, refs, nref, H, W, bs, sr, qp_rd, qp_row, NULL, vbs, lam, 0, 0, 0, split, mv,
                              qtc, tokens, mae_num, recon);
 }
 
@@ -754,10 +755,10 @@ static void intra_search(const uint8_t *cur, int Wp, int x, int y, int bx0, int 
  * final astype(uint8) == mod-256 wrap).
  * mv[nb][4]: dx per (sub-)block, -1 for x == 0.
  */
-EXPORT int oc_intra_frame(const uint8_t *cur, int Hp, int Wp, int bs, int sr, int qp_rd,
-                          const int32_t *qp_row, int vbs, double lam, uint8_t *split,
-                          int16_t *mv, int16_t *qtc, int32_t *tokens, int64_t *mae_num,
-                          uint8_t *recon) {
+EXPORT int oc_intra_frame_ex(const uint8_t *cur, int Hp, int Wp, int bs, int sr, int qp_rd,
+                             const int32_t *qp_row, const int32_t *qp_map, int vbs, double lam,
+                             uint8_t *split, int16_t *mv, int16_t *qtc, int32_t *tokens,
+                             int64_t *mae_num, uint8_t *recon) {
     if (bs != 16 && bs != 8) return -1;
     const int sb = bs / 2, nbx = Wp / bs, nby = Hp / bs, bb = bs * bs;
     int32_t res[256], sres[4][64], deq[256];
@@ -766,7 +767,7 @@ EXPORT int oc_intra_frame(const uint8_t *cur, int Hp, int Wp, int bs, int sr, in
     for (int by = 0; by < nby; ++by)
         for (int bx = 0; bx < nbx; ++bx) {
             const int b = by * nbx + bx, x = bx * bs, y = by * bs;
-            const int qpr = qp_row ? qp_row[by] : qp_rd;
+            const int qpr = qp_map ? qp_map[(size_t)by * nbx + bx] : (qp_row ? qp_row[by] : qp_rd);
             const int eligible = vbs && x != 0 && y != 0;
             int smv[4]; long ssad[4]; long vsum = 0;
             if (eligible)
@@ -852,8 +853,16 @@ EXPORT int oc_intra_frame(const uint8_t *cur, int Hp, int Wp, int bs, int sr, in
 /* Decoder inter recon (decoder.py:97-211 == reconstruct_frame :831-932), with the FME
  * branch (frac frames of the references, half-pel MVs; decoder.py:102-103, 121-141,
  * 168-187): `fme_wrap` as in oc_fme_upsample. */
+EXPORT int oc_intra_frame(const uint8_t *cur, int Hp, int Wp, int bs, int sr, int qp_rd,
+                          const int32_t *qp_row, int vbs, double lam, uint8_t *split,
+                          int16_t *mv, int16_t *qtc, int32_t *tokens, int64_t *mae_num,
+                          uint8_t *recon) {
+    return oc_intra_frame_ex(cur, Hp, Wp, bs, sr, qp_rd, qp_row, NULL, vbs, lam, split, mv, qtc, tokens, mae_num,
+                             recon);
+}
+
 EXPORT int oc_inter_recon_ex(const uint8_t *const *refs, int nref, int H, int W, int bs, int qp_rd,
-                             const int32_t *qp_row, int fme, int fme_wrap, const uint8_t *split,
+                             const int32_t *qp_row, const int32_t *qp_map, int fme, int fme_wrap, const uint8_t *split,
                              const int16_t *mv, const int16_t *qtc, uint8_t *recon) {
     const int sb = bs / 2, nbx = W / bs, nby = H / bs, bb = bs * bs;
     int32_t pred[256], deq[256], idc[256];
@@ -872,7 +881,7 @@ EXPORT int oc_inter_recon_ex(const uint8_t *const *refs, int nref, int H, int W,
     for (int by = 0; by < nby; ++by)
         for (int bx = 0; bx < nbx; ++bx) {
             const int b = by * nbx + bx, x = bx * bs, y = by * bs;
-            const int qpr = qp_row ? qp_row[by] : qp_rd;
+            const int qpr = qp_map ? qp_map[b] : (qp_row ? qp_row[by] : qp_rd);
             const int16_t *mvb = mv + (size_t)b * 12;
             const int16_t *qb = qtc + (size_t)b * bb;
             if (!split[b]) {
@@ -904,7 +913,7 @@ EXPORT int oc_inter_recon(const uint8_t *const *refs, int H, int W, int bs, int 
                           const int32_t *qp_row, const uint8_t *split, const int16_t *mv,
                           const int16_t *qtc, uint8_t *recon) {
     int nref = 0;   /* the MVs name their reference; the plain path never upsamples */
-    return oc_inter_recon_ex(refs, nref, H, W, bs, qp_rd, qp_row, 0, 0, split, mv, qtc, recon);
+    return oc_inter_recon_ex(refs, nref, H, W, bs, qp_rd, qp_row, NULL, 0, 0, split, mv, qtc, recon);
 }
 
 /* sum of squared differences for PSNR (Encoder.py:934-935) */
@@ -919,4 +928,27 @@ EXPORT void oc_me_block(const uint8_t *cur, int cstride, const uint8_t *const *r
                         int W, int x, int y, int bs, int sr, int32_t *out) {
     om_mv m = find_best_match(cur + (size_t)y * cstride + x, cstride, refs, nref, H, W, x, y, bs, sr);
     out[0] = m.dx; out[1] = m.dy; out[2] = m.ref; out[3] = (int32_t)m.sad;
+}
+
+/* Per-block QP map of ROI / two-pass rate control (build extension; restates
+ * so_capi.hip qp_map_kernel): tokens = pass-1 token counts [nby*nbx] or NULL,
+ * roi = offsets [nby*nbx] or NULL. */
+EXPORT void oc_qp_map(const int32_t *tokens, int nbx, int nby, int qp_rd, const int32_t *qp_row,
+                      const int32_t *roi, int qp_lo, int qp_hi, int32_t *out) {
+    for (int by = 0; by < nby; ++by) {
+        long long m = 0;
+        if (tokens)
+            for (int bx = 0; bx < nbx; ++bx) m += tokens[(size_t)by * nbx + bx];
+        const int base = qp_row ? qp_row[by] : qp_rd;
+        for (int bx = 0; bx < nbx; ++bx) {
+            int d = 0;
+            if (tokens) {
+                const long long tn = (long long)tokens[(size_t)by * nbx + bx] * nbx;
+                d = (tn >= 2 * m) + (tn >= 4 * m) - (2 * tn < m) - (4 * tn < m);
+            }
+            int q = base + d + (roi ? roi[(size_t)by * nbx + bx] : 0);
+            q = q < qp_lo ? qp_lo : (q > qp_hi ? qp_hi : q);
+            out[(size_t)by * nbx + bx] = q;
+        }
+    }
 }

@@ -49,7 +49,7 @@ class Y_Video_codec:
     def __init__(self, h_pixels, w_pixels, frames, block_size, search_range, Qp, intra_dur, intra_mode,
                  lam=None, VBSEnable=False, nRefFrames=1, yuv_file=None, y_only_frame_arr=None,
                  fast_me=False, FMEEnable=False, RCFlag=None, targetBR=None, frame_rate=30,
-                 qp_rate_tables=None, intra_thresh=None, ParallelMode=0, device=None):
+                 qp_rate_tables=None, intra_thresh=None, ParallelMode=0, device=None, roi=None, qp_clamp=(0, 12)):
         if fast_me and ParallelMode == 2 and VBSEnable:
             raise ValueError("fast_me + VBSEnable under ParallelMode 2: the reference raises NameError on "
                              "`mvp` (inter_prediction_parallel, Encoder.py:609)")
@@ -57,6 +57,8 @@ class Y_Video_codec:
             raise NotImplementedError("only intra_mode 0 (horizontal) is built")
         if ParallelMode not in (0, 2):
             raise NotImplementedError("ParallelMode 1 changes semantics and 3 is broken in the reference")
+        if RCFlag is not None and RCFlag > 3:
+            raise ValueError(f"RCFlag {RCFlag}: 0-2 are the reference's, 3 is two-pass RC (build extension)")
         self.h_pixels = h_pixels
         self.w_pixels = w_pixels
         self.frames = frames
@@ -99,8 +101,30 @@ class Y_Video_codec:
             self.y_only_f_arr = self.read_yuv(yuv_file, h_pixels, w_pixels, frames)
         else:
             self.y_only_f_arr = y_only_frame_arr
+        # build extension (BASELINE configs[4], DESIGN.md "ROI and two-pass rate control"):
+        # roi = per-block QP offsets ([H/bs, W/bs] array) or rectangles (x0, y0, x1, y1, offset)
+        # in pixels -- a block takes the offset of the last rectangle holding its centre;
+        # RCFlag 3 = two-pass RC (pass-1 token counts -> per-block QP map, so_qp_map)
+        self.roi = roi
+        self.qp_clamp = tuple(qp_clamp)
         self._engine = None
         self._symbols = None
+
+    def roi_block_offsets(self):
+        """ROI as int32 [nb] per-block QP offsets (raster order), or None."""
+        if self.roi is None:
+            return None
+        bs = self.block_size
+        nby, nbx = math.ceil(self.h_pixels / bs), math.ceil(self.w_pixels / bs)
+        a = np.asarray(self.roi)
+        if a.ndim == 2 and a.shape == (nby, nbx):
+            return a.astype(np.int32).reshape(-1)
+        out = np.zeros((nby, nbx), np.int32)
+        cy = np.arange(nby)[:, None] * bs + bs / 2
+        cx = np.arange(nbx)[None, :] * bs + bs / 2
+        for x0, y0, x1, y1, off in self.roi:
+            out[(cy >= y0) & (cy < y1) & (cx >= x0) & (cx < x1)] = int(off)
+        return out.reshape(-1)
 
     # ---- host helpers with the reference's semantics ---------------------------------------
     def set_target_bitrate(self, targetBR):
@@ -317,6 +341,8 @@ class Y_Video_codec:
         # closed-loop decode of the same symbols (Encoder.py:1873); result kept on device
         self.decoded_device = self.decoder.decode_symbols(syms, eng)
         pkg = LazyPackage(self, syms, psnr_per_frame, result["frame_type"], result["qp_rows"])
+        if any("qp_map" in s.extra for s in syms):
+            pkg["QP map per frame"] = [s.extra["qp_map"].cpu().numpy() if "qp_map" in s.extra else None for s in syms]
         self.encoded_package_f = True
         if save_enc_pkg:
             self.encoded_package = pkg
@@ -337,27 +363,52 @@ class Y_Video_codec:
         rc_on = self._rc_on()
         qp_sched = self.row_qp_schedule(eng.nby) if rc_on else None
         qp_sched_dev = eng.qp_row_tensor(qp_sched) if rc_on else None
-        q_persist = self.const_init_Qp
+        two_pass = self.RCFlag is not None and self.RCFlag >= 3
+        roi = self.roi_block_offsets()
+        roi_dev = torch.from_numpy(roi).to(self.device) if roi is not None else None
+        use_map = two_pass or roi_dev is not None
+        lo, hi = self.qp_clamp
+
+        def frame(cur, intra, qp_rd, out, wrap):
+            """one frame: plain, ROI map, or two-pass (pass 1 -> so_qp_map -> pass 2)"""
+            qmap = torch.empty(eng.nb, dtype=torch.int32, device=self.device) if use_map else None
+            if intra:
+                enc = lambda o, qm: eng.encode_i(cur, qp_rd, qp_sched, out=o, qp_row_dev=qp_sched_dev,  # noqa: E731
+                                                 qp_map_dev=qm)
+            else:
+                enc = lambda o, qm, reuse=False: eng.encode_p(  # noqa: E731
+                    cur, ref_frames, qp_rd, qp_sched, out=o, qp_row_dev=qp_sched_dev, fme_wrap=wrap, qp_map_dev=qm,
+                    **({"reuse_me": reuse} if reuse else {}))
+            if two_pass:
+                sym = enc(out, None)
+                eng.qp_map(sym.tokens, qp_rd, qp_sched_dev, roi_dev, qmap, qp_lo=lo, qp_hi=hi)
+                sym = enc(sym, qmap) if intra else enc(sym, qmap, True)
+            elif roi_dev is not None:
+                eng.qp_map(None, qp_rd, qp_sched_dev, roi_dev, qmap, qp_lo=lo, qp_hi=hi)
+                sym = enc(out, qmap)
+            else:
+                sym = enc(out, None)
+            if qmap is not None:
+                sym.extra["qp_map"] = qmap
+            return sym
+
         for i in range(nframes):
             cur = frames_dev[i]
             pre = symbols[i] if symbols is not None else None
             self.set_Qp(self.const_init_Qp)
             if i % intra_dur == 0:
-                sym = eng.encode_i(cur, self.Qp, qp_sched, out=pre if pre is not None and pre.frame_type == 0 else None,
-                                   qp_row_dev=qp_sched_dev)
+                sym = frame(cur, True, self.Qp, pre if pre is not None and pre.frame_type == 0 else None, True)
             else:
-                sym = eng.encode_p(cur, ref_frames, self.Qp, qp_sched,
-                                   out=pre if pre is not None and pre.frame_type == 1 else None,
-                                   qp_row_dev=qp_sched_dev, fme_wrap=not any(ref_float))
+                sym = frame(cur, False, self.Qp, pre if pre is not None and pre.frame_type == 1 else None,
+                            not any(ref_float))
                 if self.RCFlag is not None and self.RCFlag > 1:
                     residual_size = int(sym.tokens.sum().item())
                     if residual_size > self.intra_thresh:
                         # self.Q still holds the last row's QP of the inter pass (quirk
                         # of Encoder.py:1851-1856 after the per-row set_Qp calls)
-                        sym = eng.encode_i(cur, qp_sched[-1], qp_sched, qp_row_dev=qp_sched_dev)
+                        sym = frame(cur, True, qp_sched[-1], None, True)
             if rc_on:
-                q_persist = qp_sched[-1]
-                self.set_Qp(q_persist)
+                self.set_Qp(qp_sched[-1])
             out_syms.append(sym)
             ftypes.append(sym.frame_type)
             qp_rows.append(list(qp_sched) if rc_on else [])
@@ -387,10 +438,12 @@ class Y_Video_codec:
     def get_encoded_package(self):
         return self.encoded_package
 
-    def transmit_bitstream(self, intra_dur=None, block_size=None, mv_file=None, residual_file=None):
+    def transmit_bitstream(self, intra_dur=None, block_size=None, mv_file=None, residual_file=None,
+                           qp_map_file=None):
         """Encoder.py:1544-1573, writing the differential MV/QP lines and the RLE residual
         lines (entropy_encoder_frame) — the reference writes str(residuals) instead, which
-        its own parser cannot read."""
+        its own parser cannot read.  With ROI / two-pass RC (build extension)
+        `qp_map_file` receives one line per frame of per-block QP deltas against the row QP."""
         if not self.encoded_package_f:
             print("[ERROR] No encoded package available, please run encode() first")
             return
@@ -401,3 +454,11 @@ class Y_Video_codec:
                 fm.write(str(ft) + "|" + self.differential_encoder_frame(ft, pkg["MVS per Frame"][i],
                                                                          pkg["Qp_per_row_per_frame"][i]) + "\n")
                 fr.write(self.entropy_encoder_frame(pkg["approx residual"][i], block_size or self.block_size) + "\n")
+        if qp_map_file is not None:
+            from .bitstream import qp_map_line
+            maps = pkg["QP map per frame"] if "QP map per frame" in pkg else None
+            with open(qp_map_file, "w") as fq:
+                for i in range(len(pkg["frame_type_seq"])):
+                    m = maps[i] if maps is not None else None
+                    fq.write(("" if m is None else qp_map_line(m, pkg["Qp_per_row_per_frame"][i], self.const_init_Qp,
+                                                                self.num_blocks_per_row)) + "\n")

@@ -50,13 +50,18 @@ _SIGS = {
     "so_fme_workspace_bytes": ([_i, _i, _i], _sz),
     "so_fme_planes": ([_vp, _i, _i, _i, _vp, _vp], _i),
     "so_me_search_ex": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp], _i),
-    "so_encode_p_rows_ex": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _d, _i, _i, _i, _vp, _vp, _vp,
-                             _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
-    "so_inter_recon_ex": ([_vp, _i, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp], _i),
+    "so_encode_p_rows_ex": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _d, _i, _i, _i, _vp, _i,
+                             _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
+    "so_inter_recon_ex": ([_vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp], _i),
+    "so_encode_i_rows_ex": ([_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _d, _vp, _vp, _vp, _vp, _vp, _vp,
+                             _vp, _vp, _vp], _i),
+    "so_intra_recon_ex": ([_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
+    "so_qp_map": ([_vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp], _i),
 }
 
 # ME modes (include/streamoptima.h)
 ME_FULL, ME_FAST, ME_FAST_PAR = 0, 1, 2
+REUSE_ME = 1   # so_encode_p_rows_ex flags
 
 EXPORTED = tuple(_SIGS)
 

@@ -214,3 +214,20 @@ def entropy_decoder_frame(line: str, block_size) -> list:
         else:
             out.append((1, [np.array(entropy_decoder_block(sb, block_size // 2)) for sb in v]))
     return out
+
+
+# ---- per-block QP map line (build extension: ROI / two-pass RC) --------------------------------
+def qp_map_line(qp_map, qp_rows, base_qp, num_blocks_per_row) -> str:
+    """Per-block QPs as comma-separated deltas against the row's QP (the per-row QP the
+    reference line already carries, or the frame QP without rate control)."""
+    nbx = int(num_blocks_per_row)
+    q = np.asarray(qp_map).reshape(-1, nbx)
+    base = np.asarray(qp_rows if qp_rows else [base_qp] * q.shape[0]).reshape(-1, 1)
+    return ",".join(str(int(v)) for v in (q - base).reshape(-1))
+
+
+def parse_qp_map_line(line: str, qp_rows, base_qp, num_blocks_per_row) -> np.ndarray:
+    nbx = int(num_blocks_per_row)
+    d = np.array([int(t) for t in line.strip().split(",")], np.int32).reshape(-1, nbx)
+    base = np.asarray(qp_rows if qp_rows else [base_qp] * d.shape[0], np.int32).reshape(-1, 1)
+    return (d + base).reshape(-1).astype(np.int32)

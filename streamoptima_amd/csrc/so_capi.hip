@@ -28,16 +28,17 @@ int me_fastpred_launch(const uint8_t* cur, const uint8_t* const* ptrs, int nptr,
                        int fme, int by0, int by1, int serial, int32_t* out_best, int32_t* out_sub, hipStream_t st);
 int inter_tq_launch(const uint8_t* cur, const RefSet& refs, const uint8_t* planes, size_t pstride, int H, int W,
                     int bs, int by0, int by1, const int32_t* best, const int32_t* sub, int qp_rd, const int32_t* qp_row,
-                    int vbs, double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
+                    const int32_t* qp_map, int vbs, double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
                     int32_t* out_mae, uint8_t* out_recon, int32_t* out_sse, hipStream_t st);
 int inter_recon_launch(const RefSet& refs, const uint8_t* planes, size_t pstride, int H, int W, int bs, int qp,
-                       const int32_t* qp_row, const uint8_t* split, const int16_t* mv, const int16_t* qtc,
+                       const int32_t* qp_row, const int32_t* qp_map, const uint8_t* split, const int16_t* mv, const int16_t* qtc,
                        uint8_t* out_recon, hipStream_t st);
 int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int by0, int by1, int qp_rd,
-                        const int32_t* qp_row, int vbs, double lam, uint8_t* out_split, int16_t* out_mv,
+                        const int32_t* qp_row, const int32_t* qp_map, int vbs, double lam, uint8_t* out_split, int16_t* out_mv,
                         int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon,
                         int32_t* out_sse, int32_t* idres, hipStream_t st);
-int intra_recon_launch(int H, int W, int bs, int sr, int qp, const int32_t* qp_row, const uint8_t* split,
+int intra_recon_launch(int H, int W, int bs, int sr, int qp, const int32_t* qp_row, const int32_t* qp_map,
+                       const uint8_t* split,
                        const int16_t* mv, const int16_t* qtc, uint8_t* out_recon, int32_t* idres,
                        hipStream_t st);
 
@@ -155,6 +156,41 @@ __global__ void __launch_bounds__(256) sse_kernel(const uint8_t* __restrict__ a,
     if (threadIdx.x == 0) atomicAdd(out, part[0] + part[1] + part[2] + part[3]);
 }
 
+// Per-block QP map (build extension, DESIGN.md "ROI and two-pass rate control"): one
+// workgroup per block row.  Two-pass: with pass-1 token counts t (stripe-local records) the
+// row mean is m / n (m = sum, n = blocks per row) and
+//   delta = [t n >= 2m] + [t n >= 4m] - [2 t n < m] - [4 t n < m]      (in [-2, 2], exact)
+// i.e. blocks at >= 2x / 4x the row's mean bits are quantised 1 / 2 QP coarser and blocks at
+// < 1/2 / < 1/4 of it 1 / 2 QP finer.  qp = clamp(base + delta + roi, qp_lo, qp_hi) with
+// base = qp_row[by] (rate-control schedule) or qp_rd.  tokens == NULL: ROI only (delta 0).
+__global__ void __launch_bounds__(256)
+qp_map_kernel(const int32_t* __restrict__ tokens, int nbx, int by0, int qp_rd, const int32_t* __restrict__ qp_row,
+              const int32_t* __restrict__ roi, int qp_lo, int qp_hi, int32_t* __restrict__ out) {
+    __shared__ long long part[4];
+    const int by = by0 + blockIdx.x;
+    const int32_t* t = tokens ? tokens + (size_t)blockIdx.x * nbx : nullptr;
+    long long m = 0;
+    if (t) {
+        for (int bx = threadIdx.x; bx < nbx; bx += blockDim.x) m += t[bx];
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1) m += __shfl_xor(m, s, 64);
+        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
+        __syncthreads();
+        m = part[0] + part[1] + part[2] + part[3];
+    }
+    const int base = qp_row ? qp_row[by] : qp_rd;
+    for (int bx = threadIdx.x; bx < nbx; bx += blockDim.x) {
+        int d = 0;
+        if (t) {
+            const long long tn = (long long)t[bx] * nbx;
+            d = (tn >= 2 * m) + (tn >= 4 * m) - (2 * tn < m) - (4 * tn < m);
+        }
+        int q = base + d + (roi ? roi[(size_t)by * nbx + bx] : 0);
+        q = q < qp_lo ? qp_lo : (q > qp_hi ? qp_hi : q);
+        out[(size_t)by * nbx + bx] = q;
+    }
+}
+
 }  // namespace so
 
 using namespace so;
@@ -194,7 +230,7 @@ int so_inter_tq_recon(const uint8_t* cur, const uint8_t* const* refs, int nref, 
             set_error("%s: out_recon aliases refs[%d]", fn, i);
             return SO_E_INVALID;
         }
-    return inter_tq_launch(cur, rs, nullptr, 0, H, W, bs, 0, H / bs, best, vbs ? sub : nullptr, qp_rd, qp_row, vbs, lam,
+    return inter_tq_launch(cur, rs, nullptr, 0, H, W, bs, 0, H / bs, best, vbs ? sub : nullptr, qp_rd, qp_row, nullptr, vbs, lam,
                            out_split, out_mv, out_qtc, out_tokens, out_mae_num, out_recon, out_sse,
                            (hipStream_t)stream);
 }
@@ -228,7 +264,7 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
     int32_t* sub = vbs ? scratch + nbs * 4 : nullptr;
     hipStream_t st = (hipStream_t)stream;
     SO_TRY(me_launch(cur, rs, nref, H, W, bs, sr, by0, by1, best, sub, st));
-    return inter_tq_launch(cur, rs, nullptr, 0, H, W, bs, by0, by1, best, sub, qp_rd, qp_row, vbs, lam, out_split,
+    return inter_tq_launch(cur, rs, nullptr, 0, H, W, bs, by0, by1, best, sub, qp_rd, qp_row, nullptr, vbs, lam, out_split,
                            out_mv, out_qtc, out_tokens, out_mae_num, out_recon, out_sse, st);
 }
 
@@ -262,7 +298,7 @@ int so_encode_i_rows(const uint8_t* cur, int H, int W, int bs, int sr, int by0, 
     SO_TRY(check_rows(fn, H, bs, by0, by1));
     SO_NEED(cur, fn); SO_NEED(out_split, fn); SO_NEED(out_mv, fn); SO_NEED(out_qtc, fn);
     SO_NEED(out_tokens, fn); SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn); SO_NEED(scratch, fn);
-    return intra_encode_launch(cur, H, W, bs, sr, by0, by1, qp_rd, qp_row, vbs, lam, out_split, out_mv, out_qtc,
+    return intra_encode_launch(cur, H, W, bs, sr, by0, by1, qp_rd, qp_row, nullptr, vbs, lam, out_split, out_mv, out_qtc,
                                out_tokens, out_mae_num, out_recon, out_sse, scratch, (hipStream_t)stream);
 }
 
@@ -286,7 +322,8 @@ int so_inter_recon(const uint8_t* const* refs, int nref, int H, int W, int bs, i
     SO_NEED(split, fn); SO_NEED(mv, fn); SO_NEED(qtc, fn); SO_NEED(out_recon, fn);
     RefSet rs;
     SO_TRY(make_refs(fn, refs, nref, &rs));
-    return inter_recon_launch(rs, nullptr, 0, H, W, bs, qp, qp_row, split, mv, qtc, out_recon, (hipStream_t)stream);
+    return inter_recon_launch(rs, nullptr, 0, H, W, bs, qp, qp_row, nullptr, split, mv, qtc, out_recon,
+                              (hipStream_t)stream);
 }
 
 int so_intra_recon(int H, int W, int bs, int qp, const int32_t* qp_row, const uint8_t* split, const int16_t* mv,
@@ -297,7 +334,8 @@ int so_intra_recon(int H, int W, int bs, int qp, const int32_t* qp_row, const ui
     SO_TRY(check_qp(fn, qp));
     SO_NEED(split, fn); SO_NEED(mv, fn); SO_NEED(qtc, fn); SO_NEED(out_recon, fn); SO_NEED(scratch, fn);
     // the recon kernel only needs sr to size its ring: the largest reachable offset is 64
-    return intra_recon_launch(H, W, bs, 64, qp, qp_row, split, mv, qtc, out_recon, scratch, (hipStream_t)stream);
+    return intra_recon_launch(H, W, bs, 64, qp, qp_row, nullptr, split, mv, qtc, out_recon, scratch,
+                              (hipStream_t)stream);
 }
 
 size_t so_fme_plane_stride(int H, int W) {
@@ -378,12 +416,12 @@ int so_me_search_ex(const uint8_t* cur, const uint8_t* const* refs, int nref, in
 }
 
 int so_encode_p_rows_ex(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W, int bs, int sr,
-                        int by0, int by1, int qp_rd, const int32_t* qp_row, int vbs, double lam, int me_mode, int fme,
-                        int fme_wrap, uint8_t* fme_planes, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc,
+                        int by0, int by1, int qp_rd, const int32_t* qp_row, const int32_t* qp_map, int vbs, double lam,
+                        int me_mode, int fme, int fme_wrap, uint8_t* fme_planes, int flags, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc,
                         int32_t* out_tokens, int32_t* out_mae_num, uint8_t* out_recon, int32_t* out_sse,
                         int32_t* scratch, void* stream) {
     const char* fn = "so_encode_p_rows_ex";
-    if (me_mode == SO_ME_FULL && !fme)
+    if (me_mode == SO_ME_FULL && !fme && !qp_map && !(flags & SO_REUSE_ME))
         return so_encode_p_rows(cur, refs, nref, H, W, bs, sr, by0, by1, qp_rd, qp_row, vbs, lam, out_split, out_mv,
                                 out_qtc, out_tokens, out_mae_num, out_recon, out_sse, scratch, stream);
     SO_TRY(check_geom(fn, H, W, bs, vbs));
@@ -403,26 +441,82 @@ int so_encode_p_rows_ex(const uint8_t* cur, const uint8_t* const* refs, int nref
     int32_t* best = scratch;
     int32_t* sub = vbs ? scratch + nbs * 4 : nullptr;
     hipStream_t st = (hipStream_t)stream;
-    SO_TRY(me_ex(fn, cur, refs, nref, rs, H, W, bs, sr, by0, by1, me_mode, fme, fme_wrap, fme_planes, best, sub, st));
+    if (flags & SO_REUSE_ME) {
+        // pass 2 of two-pass RC: the ME records (and FME planes) of the previous call stay
+        if (fme) SO_NEED(fme_planes, fn);
+    } else {
+        SO_TRY(me_ex(fn, cur, refs, nref, rs, H, W, bs, sr, by0, by1, me_mode, fme, fme_wrap, fme_planes, best, sub,
+                     st));
+    }
     return inter_tq_launch(cur, rs, fme ? fme_planes : nullptr, so_fme_plane_stride(H, W), H, W, bs, by0, by1, best,
-                           sub, qp_rd, qp_row, vbs, lam, out_split, out_mv, out_qtc, out_tokens, out_mae_num, out_recon,
+                           sub, qp_rd, qp_row, qp_map, vbs, lam, out_split, out_mv, out_qtc, out_tokens, out_mae_num, out_recon,
                            out_sse, st);
 }
 
 int so_inter_recon_ex(const uint8_t* const* refs, int nref, int H, int W, int bs, int qp, const int32_t* qp_row,
-                      int fme, int fme_wrap, uint8_t* fme_planes, const uint8_t* split, const int16_t* mv,
+                      const int32_t* qp_map, int fme, int fme_wrap, uint8_t* fme_planes, const uint8_t* split, const int16_t* mv,
                       const int16_t* qtc, uint8_t* out_recon, void* stream) {
     const char* fn = "so_inter_recon_ex";
-    if (!fme) return so_inter_recon(refs, nref, H, W, bs, qp, qp_row, split, mv, qtc, out_recon, stream);
     SO_TRY(check_geom(fn, H, W, bs, 0));
     SO_TRY(check_qp(fn, qp));
-    SO_NEED(split, fn); SO_NEED(mv, fn); SO_NEED(qtc, fn); SO_NEED(out_recon, fn); SO_NEED(fme_planes, fn);
+    SO_NEED(split, fn); SO_NEED(mv, fn); SO_NEED(qtc, fn); SO_NEED(out_recon, fn);
+    if (fme) SO_NEED(fme_planes, fn);
     RefSet rs;
     SO_TRY(make_refs(fn, refs, nref, &rs));
     const size_t ps = so_fme_plane_stride(H, W);
     hipStream_t st = (hipStream_t)stream;
-    for (int r = 0; r < nref; ++r) SO_TRY(fme_planes_launch(refs[r], H, W, fme_wrap, fme_planes + (size_t)r * 4 * ps, ps, st));
-    return inter_recon_launch(rs, fme_planes, ps, H, W, bs, qp, qp_row, split, mv, qtc, out_recon, st);
+    if (fme)
+        for (int r = 0; r < nref; ++r)
+            SO_TRY(fme_planes_launch(refs[r], H, W, fme_wrap, fme_planes + (size_t)r * 4 * ps, ps, st));
+    return inter_recon_launch(rs, fme ? fme_planes : nullptr, ps, H, W, bs, qp, qp_row, qp_map, split, mv, qtc,
+                              out_recon, st);
+}
+
+int so_encode_i_rows_ex(const uint8_t* cur, int H, int W, int bs, int sr, int by0, int by1, int qp_rd,
+                        const int32_t* qp_row, const int32_t* qp_map, int vbs, double lam, uint8_t* out_split,
+                        int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae_num,
+                        uint8_t* out_recon, int32_t* out_sse, int32_t* scratch, void* stream) {
+    const char* fn = "so_encode_i_rows_ex";
+    SO_TRY(check_geom(fn, H, W, bs, vbs));
+    SO_TRY(check_intra_width(fn, W));
+    SO_TRY(check_sr(fn, sr));
+    SO_TRY(check_qp(fn, qp_rd));
+    SO_TRY(check_rows(fn, H, bs, by0, by1));
+    SO_NEED(cur, fn); SO_NEED(out_split, fn); SO_NEED(out_mv, fn); SO_NEED(out_qtc, fn);
+    SO_NEED(out_tokens, fn); SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn); SO_NEED(scratch, fn);
+    return intra_encode_launch(cur, H, W, bs, sr, by0, by1, qp_rd, qp_row, qp_map, vbs, lam, out_split, out_mv,
+                               out_qtc, out_tokens, out_mae_num, out_recon, out_sse, scratch, (hipStream_t)stream);
+}
+
+int so_intra_recon_ex(int H, int W, int bs, int qp, const int32_t* qp_row, const int32_t* qp_map,
+                      const uint8_t* split, const int16_t* mv, const int16_t* qtc, uint8_t* out_recon,
+                      int32_t* scratch, void* stream) {
+    const char* fn = "so_intra_recon_ex";
+    SO_TRY(check_geom(fn, H, W, bs, 0));
+    SO_TRY(check_intra_width(fn, W));
+    SO_TRY(check_qp(fn, qp));
+    SO_NEED(split, fn); SO_NEED(mv, fn); SO_NEED(qtc, fn); SO_NEED(out_recon, fn); SO_NEED(scratch, fn);
+    return intra_recon_launch(H, W, bs, 64, qp, qp_row, qp_map, split, mv, qtc, out_recon, scratch,
+                              (hipStream_t)stream);
+}
+
+int so_qp_map(const int32_t* tokens, int H, int W, int bs, int by0, int by1, int qp_rd, const int32_t* qp_row,
+              const int32_t* roi, int qp_lo, int qp_hi, int32_t* out_qp_map, void* stream) {
+    const char* fn = "so_qp_map";
+    if (bs <= 0 || H <= 0 || W <= 0 || H % bs || W % bs) {
+        set_error("%s: bad geometry", fn);
+        return SO_E_INVALID;
+    }
+    SO_TRY(check_rows(fn, H, bs, by0, by1));
+    SO_NEED(out_qp_map, fn);
+    if (qp_lo < 0 || qp_hi > 20 || qp_lo > qp_hi) {
+        set_error("%s: QP clamp [%d, %d] outside [0, 20]", fn, qp_lo, qp_hi);
+        return SO_E_INVALID;
+    }
+    if (by1 <= by0) return SO_OK;
+    hipLaunchKernelGGL(qp_map_kernel, dim3(by1 - by0), dim3(256), 0, (hipStream_t)stream, tokens, W / bs, by0, qp_rd,
+                       qp_row, roi, qp_lo, qp_hi, out_qp_map);
+    return check_launch("qp_map_kernel");
 }
 
 int so_sse_u8(const uint8_t* a, const uint8_t* b, int64_t n, uint64_t* out_sse, void* stream) {

@@ -31,7 +31,8 @@ SO_DEV int canvas_at(const uint8_t* left /* LDS row: cols x0-sr .. x0-1 */, int 
 template <int BS, bool VBS>
 __global__ void __launch_bounds__(256)
 intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int by0, int nrows, int sr, int qp_rd,
-                const int32_t* __restrict__ qp_row, double lam, uint8_t* __restrict__ out_split,
+                const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map, double lam,
+                uint8_t* __restrict__ out_split,
                 int16_t* __restrict__ out_mv, int16_t* __restrict__ out_qtc,
                 int32_t* __restrict__ out_tokens, int32_t* __restrict__ out_mae,
                 int32_t* __restrict__ idres) {
@@ -48,7 +49,7 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int by0, int nrow
     uint8_t* fl = ldsf + g * BS * BS;
     uint8_t* left = ldsl + g * BS * kIntraMaxSr;
     const int bx = b % nbx, by = by0 + b / nbx, x = bx * BS, y = by * BS;
-    const int qpr = qp_row ? qp_row[by] : qp_rd;
+    const int qpr = qp_map ? qp_map[(size_t)by * nbx + bx] : (qp_row ? qp_row[by] : qp_rd);
 
     // stage the original pixels left of the block (cols x-sr .. x-1, 0 where < 0)
     uint8_t* lrow = left + l * kIntraMaxSr;
@@ -266,7 +267,7 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int by0, int nrow
 // rescale_QTC + apply_2d_idct of every block (decoder.py:347-365 / Encoder.py:1358-1376)
 template <int BS, bool VBS>
 __global__ void __launch_bounds__(256)
-dequant_idct_kernel(int H, int W, int qp, const int32_t* __restrict__ qp_row,
+dequant_idct_kernel(int H, int W, int qp, const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map,
                     const uint8_t* __restrict__ split, const int16_t* __restrict__ qtc,
                     int32_t* __restrict__ idres) {
     constexpr int G = BS, BPW = 256 / G;
@@ -278,7 +279,7 @@ dequant_idct_kernel(int H, int W, int qp, const int32_t* __restrict__ qp_row,
     if (b >= nb) return;
     double* dl = ldsd + g * LDS_D;
     const int by = b / nbx;
-    const int qpr = qp_row ? qp_row[by] : qp;
+    const int qpr = qp_map ? qp_map[b] : (qp_row ? qp_row[by] : qp);
     int32_t* rb = idres + (size_t)b * BS * BS;
     if (!VBS || !split[b]) {
         int q[BS], dq[BS];
@@ -377,7 +378,7 @@ intra_recon_kernel(int H, int W, int by0, const uint8_t* __restrict__ split, con
 }
 
 int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int by0, int by1, int qp_rd,
-                        const int32_t* qp_row, int vbs, double lam, uint8_t* out_split, int16_t* out_mv,
+                        const int32_t* qp_row, const int32_t* qp_map, int vbs, double lam, uint8_t* out_split, int16_t* out_mv,
                         int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon,
                         int32_t* out_sse, int32_t* idres, hipStream_t st) {
     const int nrows = by1 - by0;
@@ -386,13 +387,16 @@ int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int by
     const int bpw = 256 / bs;
     dim3 grid((nb + bpw - 1) / bpw), blk(256);
     if (bs == 16 && vbs)
-        hipLaunchKernelGGL((intra_tq_kernel<16, true>), grid, blk, 0, st, cur, H, W, by0, nrows, sr, qp_rd, qp_row, lam,
+        hipLaunchKernelGGL((intra_tq_kernel<16, true>), grid, blk, 0, st, cur, H, W, by0, nrows, sr, qp_rd, qp_row, qp_map,
+                           lam,
                            out_split, out_mv, out_qtc, out_tokens, out_mae, idres);
     else if (bs == 16)
-        hipLaunchKernelGGL((intra_tq_kernel<16, false>), grid, blk, 0, st, cur, H, W, by0, nrows, sr, qp_rd, qp_row, lam,
+        hipLaunchKernelGGL((intra_tq_kernel<16, false>), grid, blk, 0, st, cur, H, W, by0, nrows, sr, qp_rd, qp_row, qp_map,
+                           lam,
                            out_split, out_mv, out_qtc, out_tokens, out_mae, idres);
     else
-        hipLaunchKernelGGL((intra_tq_kernel<8, false>), grid, blk, 0, st, cur, H, W, by0, nrows, sr, qp_rd, qp_row, lam,
+        hipLaunchKernelGGL((intra_tq_kernel<8, false>), grid, blk, 0, st, cur, H, W, by0, nrows, sr, qp_rd, qp_row, qp_map,
+                           lam,
                            out_split, out_mv, out_qtc, out_tokens, out_mae, idres);
     int rc = check_launch("intra_tq_kernel");
     if (rc) return rc;
@@ -405,16 +409,19 @@ int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int by
     return check_launch("intra_recon_kernel");
 }
 
-int intra_recon_launch(int H, int W, int bs, int sr, int qp, const int32_t* qp_row, const uint8_t* split,
+int intra_recon_launch(int H, int W, int bs, int sr, int qp, const int32_t* qp_row, const int32_t* qp_map,
+                       const uint8_t* split,
                        const int16_t* mv, const int16_t* qtc, uint8_t* out_recon, int32_t* idres,
                        hipStream_t st) {
     const int nb = (W / bs) * (H / bs);
     const int bpw = 256 / bs;
     dim3 grid((nb + bpw - 1) / bpw), blk(256);
     if (bs == 16)
-        hipLaunchKernelGGL((dequant_idct_kernel<16, true>), grid, blk, 0, st, H, W, qp, qp_row, split, qtc, idres);
+        hipLaunchKernelGGL((dequant_idct_kernel<16, true>), grid, blk, 0, st, H, W, qp, qp_row, qp_map, split, qtc,
+                           idres);
     else
-        hipLaunchKernelGGL((dequant_idct_kernel<8, false>), grid, blk, 0, st, H, W, qp, qp_row, split, qtc, idres);
+        hipLaunchKernelGGL((dequant_idct_kernel<8, false>), grid, blk, 0, st, H, W, qp, qp_row, qp_map, split, qtc,
+                           idres);
     int rc = check_launch("dequant_idct_kernel");
     if (rc) return rc;
     if (bs == 16)

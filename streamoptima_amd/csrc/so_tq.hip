@@ -19,7 +19,8 @@ __global__ void __launch_bounds__(256)
 inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, const uint8_t* __restrict__ planes, size_t pstride,
                 int H, int W, int by0, int nrows,
                 const int32_t* __restrict__ best, const int32_t* __restrict__ sub, int qp_rd,
-                const int32_t* __restrict__ qp_row, double lam, uint8_t* __restrict__ out_split,
+                const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map, double lam,
+                uint8_t* __restrict__ out_split,
                 int16_t* __restrict__ out_mv, int16_t* __restrict__ out_qtc,
                 int32_t* __restrict__ out_tokens, int32_t* __restrict__ out_mae,
                 uint8_t* __restrict__ out_recon, int32_t* __restrict__ out_sse) {
@@ -34,7 +35,8 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, const uint8_t* __r
     double* dl = ldsd + g * LDS_D;
     uint8_t* fl = ldsf + g * BS * BS;
     const int bx = b % nbx, by = by0 + b / nbx, x = bx * BS, y = by * BS;
-    const int qpr = qp_row ? qp_row[by] : qp_rd;
+    // per-block QP map (ROI / two-pass RC) > per-row RC QP > the frame QP
+    const int qpr = qp_map ? qp_map[(size_t)by * nbx + bx] : (qp_row ? qp_row[by] : qp_rd);
 
     const int32_t* bb = best + (size_t)b * 4;
     const int dx = bb[0], dy = bb[1], rf = bb[2], sad = bb[3];
@@ -185,7 +187,7 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, const uint8_t* __r
 template <int BS, bool VBS, bool FME>
 __global__ void __launch_bounds__(256)
 inter_recon_kernel(RefSet refs, const uint8_t* __restrict__ planes, size_t pstride, int H, int W, int qp,
-                   const int32_t* __restrict__ qp_row,
+                   const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map,
                    const uint8_t* __restrict__ split, const int16_t* __restrict__ mv,
                    const int16_t* __restrict__ qtc, uint8_t* __restrict__ out_recon) {
     constexpr int G = BS, BPW = 256 / G, SB = BS / 2;
@@ -197,7 +199,7 @@ inter_recon_kernel(RefSet refs, const uint8_t* __restrict__ planes, size_t pstri
     if (b >= nb) return;
     double* dl = ldsd + g * LDS_D;
     const int bx = b % nbx, by = b / nbx, x = bx * BS, y = by * BS;
-    const int qpr = qp_row ? qp_row[by] : qp;
+    const int qpr = qp_map ? qp_map[b] : (qp_row ? qp_row[by] : qp);
     const int16_t* m = mv + (size_t)b * 12;
     if (!VBS || !split[b]) {
         const int dx = m[0], dy = m[1], rf = m[2];
@@ -248,7 +250,7 @@ inter_recon_kernel(RefSet refs, const uint8_t* __restrict__ planes, size_t pstri
 
 int inter_tq_launch(const uint8_t* cur, const RefSet& refs, const uint8_t* planes, size_t pstride, int H, int W,
                     int bs, int by0, int by1, const int32_t* best, const int32_t* sub, int qp_rd, const int32_t* qp_row,
-                    int vbs, double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
+                    const int32_t* qp_map, int vbs, double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
                     int32_t* out_mae, uint8_t* out_recon, int32_t* out_sse, hipStream_t st) {
     const int nrows = by1 - by0;
     if (nrows <= 0) return SO_OK;
@@ -257,8 +259,8 @@ int inter_tq_launch(const uint8_t* cur, const RefSet& refs, const uint8_t* plane
     dim3 grid((nb + bpw - 1) / bpw), blk(256);
 #define SO_TQ(B, V, F)                                                                                             \
     hipLaunchKernelGGL((inter_tq_kernel<B, V, F>), grid, blk, 0, st, cur, refs, planes, pstride, H, W, by0, nrows,   \
-                       best, sub, qp_rd, qp_row, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon,    \
-                       out_sse)
+                       best, sub, qp_rd, qp_row, qp_map, lam, out_split, out_mv, out_qtc, out_tokens, out_mae,       \
+                       out_recon, out_sse)
     const bool fme = planes != nullptr;
     if (bs == 16 && vbs) { if (fme) SO_TQ(16, true, true); else SO_TQ(16, true, false); }
     else if (bs == 16) { if (fme) SO_TQ(16, false, true); else SO_TQ(16, false, false); }
@@ -268,14 +270,14 @@ int inter_tq_launch(const uint8_t* cur, const RefSet& refs, const uint8_t* plane
 }
 
 int inter_recon_launch(const RefSet& refs, const uint8_t* planes, size_t pstride, int H, int W, int bs, int qp,
-                       const int32_t* qp_row, const uint8_t* split, const int16_t* mv, const int16_t* qtc,
+                       const int32_t* qp_row, const int32_t* qp_map, const uint8_t* split, const int16_t* mv, const int16_t* qtc,
                        uint8_t* out_recon, hipStream_t st) {
     const int nb = (W / bs) * (H / bs);
     const int bpw = 256 / bs;
     dim3 grid((nb + bpw - 1) / bpw), blk(256);
 #define SO_REC(B, V, F)                                                                                          \
     hipLaunchKernelGGL((inter_recon_kernel<B, V, F>), grid, blk, 0, st, refs, planes, pstride, H, W, qp, qp_row, \
-                       split, mv, qtc, out_recon)
+                       qp_map, split, mv, qtc, out_recon)
     const bool fme = planes != nullptr;
     if (bs == 16) { if (fme) SO_REC(16, true, true); else SO_REC(16, true, false); }
     else { if (fme) SO_REC(8, false, true); else SO_REC(8, false, false); }

@@ -83,11 +83,12 @@ class decoder:
         n = len(symbols)
         for i, s in enumerate(symbols):
             qp_row = s.qp_row if self._rc() else None
+            qm = s.extra.get("qp_map")      # ROI / two-pass per-block QP (build extension)
             if s.frame_type == 0:
-                rec = eng.recon_intra(s.split, s.mv, s.qtc, self.Qp, qp_row)
+                rec = eng.recon_intra(s.split, s.mv, s.qtc, self.Qp, qp_row, qp_map_dev=qm)
                 ref_frames = []
             else:
-                rec = eng.recon_inter(ref_frames, s.split, s.mv, s.qtc, self.Qp, qp_row)
+                rec = eng.recon_inter(ref_frames, s.split, s.mv, s.qtc, self.Qp, qp_row, qp_map_dev=qm)
             out.append(rec)
             if i < n - 1:
                 if len(ref_frames) >= self.nRefFrames:
@@ -96,8 +97,9 @@ class decoder:
         return out
 
     def decode(self, frame_type_seq, residual_file, Qp_per_row_per_frame, mv_file, intra_mode=None, intra_dur=None,
-               block_size=None, frames=None, width=None, height=None, save_decoded_frames=True):
-        """decoder.py:487-545 with the per-frame lists of the encoded package."""
+               block_size=None, frames=None, width=None, height=None, save_decoded_frames=True, qp_maps=None):
+        """decoder.py:487-545 with the per-frame lists of the encoded package.  qp_maps: per
+        frame per-block QPs (ROI / two-pass RC build extension) or None."""
         bs = block_size or self.block_size
         frames = frames or self.frames
         eng = self._eng()
@@ -110,11 +112,14 @@ class decoder:
             mv_d = torch.from_numpy(mv).to(eng.device)
             qtc_d = torch.from_numpy(qtc).to(eng.device)
             qp_row = Qp_per_row_per_frame[i] if self._rc() else None
+            qm = None
+            if qp_maps is not None and qp_maps[i] is not None:
+                qm = torch.as_tensor(np.asarray(qp_maps[i], np.int32)).to(eng.device)
             if ft == 0:
-                rec = eng.recon_intra(split_d, mv_d, qtc_d, self.Qp, qp_row)
+                rec = eng.recon_intra(split_d, mv_d, qtc_d, self.Qp, qp_row, qp_map_dev=qm)
                 ref_frames = []
             else:
-                rec = eng.recon_inter(ref_frames, split_d, mv_d, qtc_d, self.Qp, qp_row)
+                rec = eng.recon_inter(ref_frames, split_d, mv_d, qtc_d, self.Qp, qp_row, qp_map_dev=qm)
             decoded.append(rec)
             if i < frames - 1:
                 if len(ref_frames) >= self.nRefFrames:
@@ -151,14 +156,21 @@ class decoder:
         return frame_type_seq, mv_for_vid, qp_for_vid, res_for_vid
 
     def decode_bitstream(self, mv_file, residual_file, intra_mode=None, intra_dur=None, block_size=None, frames=None,
-                         width=None, height=None, save_decoded_frames=True):
+                         width=None, height=None, save_decoded_frames=True, qp_map_file=None):
         """decoder.py:686-709: parse the transmitted text bitstream (transmit_bitstream)
-        on the host, reconstruct every frame on the GPU."""
+        on the host, reconstruct every frame on the GPU.  qp_map_file: the per-block QP
+        lines of ROI / two-pass RC (build extension)."""
         bs = block_size or self.block_size
         ft, mvs, qps, res = self.decode_differential_entropy(mv_file, residual_file, bs)
         self.mv_per_frame = mvs
         self.residuals_per_frame = res
-        return self.decode(ft, res, qps, mvs, intra_mode, intra_dur, bs, frames, width, height, save_decoded_frames)
+        maps = None
+        if qp_map_file is not None:
+            with open(qp_map_file) as f:
+                maps = [(_bs.parse_qp_map_line(line, qps[i] if self._rc() else None, self.Qp, self.num_blocks_per_row)
+                         if line.strip() else None) for i, line in enumerate(f)]
+        return self.decode(ft, res, qps, mvs, intra_mode, intra_dur, bs, frames, width, height, save_decoded_frames,
+                           qp_maps=maps)
 
     def save_decoded_frames(self, filename="yuv/decoded_bitstream_frames.yuv"):
         if not self.decoded_vid_f:

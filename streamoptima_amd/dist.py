@@ -76,9 +76,13 @@ class StripeGOPEncoder:
 
     # ---- GOP -----------------------------------------------------------------------------
     def encode(self, frames: torch.Tensor, intra_dur: int, qp: int, nref: int = 1, qp_sched=None,
-               rc_flag=None, intra_thresh=None):
+               rc_flag=None, intra_thresh=None, roi=None, qp_clamp=(0, 12)):
         """The encode() loop over frames [F, H, W] resident on this rank's device.
 
+        rc_flag 3 = two-pass RC and `roi` (flat int32 per-block QP offsets) = ROI (build
+        extensions, Encoder.py facade): a block row lies inside one stripe, so each rank
+        builds the per-block QP map of its own rows from its own pass-1 tokens (so_qp_map);
+        the map never crosses ranks.
         Returns per frame the stripe-local FrameSymbols (recon = the full, exchanged plane),
         the frame types, and the whole-frame SSE (int64 [F], summed over ranks).
         """
@@ -87,28 +91,51 @@ class StripeGOPEncoder:
         _, init = self.new_plane(fill=128)
         refs = [init]
         qp_dev = e.qp_row_tensor(qp_sched) if qp_sched is not None else None
+        two_pass = rc_flag is not None and rc_flag >= 3
+        roi_dev = torch.as_tensor(roi, dtype=torch.int32).to(e.device) if roi is not None else None
+        use_map = two_pass or roi_dev is not None
+        lo, hi = qp_clamp
+
+        def stripe(cur, intra, qp_rd, plane):
+            sym = e.new_stripe_symbols(0 if intra else 1, self.by0, self.by1, plane)
+            if self.by1 <= self.by0:            # a rank past the last block row idles
+                return sym
+            qmap = torch.empty(e.nb, dtype=torch.int32, device=e.device) if use_map else None
+
+            def run(qm, reuse=False):
+                if intra:
+                    e.encode_i_rows(cur, self.by0, self.by1, qp_rd, sym, qp_row_dev=qp_dev, qp_map_dev=qm)
+                else:
+                    e.encode_p_rows(cur, refs, self.by0, self.by1, qp_rd, sym, qp_row_dev=qp_dev, qp_map_dev=qm,
+                                    reuse_me=reuse)
+            if two_pass:
+                run(None)
+                e.qp_map(sym.tokens, qp_rd, qp_dev, roi_dev, qmap, self.by0, self.by1, lo, hi)
+                run(qmap, reuse=not intra)
+            elif roi_dev is not None:
+                e.qp_map(None, qp_rd, qp_dev, roi_dev, qmap, self.by0, self.by1, lo, hi)
+                run(qmap)
+            else:
+                run(None)
+            if qmap is not None:
+                sym.extra["qp_map"] = qmap      # valid on this rank's rows only
+            return sym
+
         syms, ftypes = [], []
         for i in range(nframes):
             cur = frames[i]
             flat, plane = self.new_plane()
-            work = self.by1 > self.by0          # a rank past the last block row idles
             if i % intra_dur == 0:
-                sym = e.new_stripe_symbols(0, self.by0, self.by1, plane)
-                if work:
-                    e.encode_i_rows(cur, self.by0, self.by1, qp, sym, qp_row_dev=qp_dev)
+                sym = stripe(cur, True, qp, plane)
             else:
-                sym = e.new_stripe_symbols(1, self.by0, self.by1, plane)
-                if work:
-                    e.encode_p_rows(cur, refs, self.by0, self.by1, qp, sym, qp_row_dev=qp_dev)
+                sym = stripe(cur, False, qp, plane)
                 if rc_flag is not None and rc_flag > 1:
                     total = sym.tokens.sum(dtype=torch.int64).reshape(1)
                     if self.world > 1:
                         dist.all_reduce(total, group=self.group)
                     if int(total.item()) > intra_thresh:
                         # Encoder.py:1851-1856: redo as intra with the last row's QP
-                        sym = e.new_stripe_symbols(0, self.by0, self.by1, plane)
-                        if work:
-                            e.encode_i_rows(cur, self.by0, self.by1, qp_sched[-1], sym, qp_row_dev=qp_dev)
+                        sym = stripe(cur, True, qp_sched[-1], plane)
             sym.qp_row = list(qp_sched) if qp_sched is not None else None
             sym.extra["flat"] = flat
             self.exchange(flat)

@@ -106,50 +106,32 @@ class Engine:
     # ---- encode -------------------------------------------------------------------------
     def encode_p(self, cur: torch.Tensor, refs: list, qp_rd: int, qp_row=None,
                  out: FrameSymbols | None = None, qp_row_dev: torch.Tensor | None = None,
-                 fme_wrap: bool = True) -> FrameSymbols:
-        """complete_inter_flow (Encoder.py:1644) for one frame; asynchronous.  `fme_wrap`:
-        see so_encode_p_rows_ex (False while refs hold the float64 all-128 start frame)."""
-        self._check_plane(cur, "cur")
-        for k, r in enumerate(refs):
-            self._check_plane(r, f"refs[{k}]")
-        if not 1 <= len(refs) <= _lib.MAX_REF:
-            raise ValueError(f"nRefFrames must be in [1, {_lib.MAX_REF}]")
-        out = out or self.new_symbols(1)
-        qr = qp_row_dev if qp_row_dev is not None else self.qp_row_tensor(qp_row)
-        if self.me_mode == _lib.ME_FULL and not self.fme:
-            rc = self.lib.so_encode_p_frame(
-                cur.data_ptr(), _lib.ref_array(refs), len(refs), self.h, self.w, self.bs, self.sr,
-                int(qp_rd), _lib.ptr(qr), int(self.vbs), self.lam, out.split.data_ptr(),
-                out.mv.data_ptr(), out.qtc.data_ptr(), out.tokens.data_ptr(), out.mae_num.data_ptr(),
-                out.recon.data_ptr(), _lib.ptr(out.sse), self.scratch.data_ptr(), _lib.stream_handle(self.device))
-            _lib.check(rc, "so_encode_p_frame")
-        else:
-            ws = self.fme_workspace(len(refs)) if self.fme else None
-            rc = self.lib.so_encode_p_rows_ex(
-                cur.data_ptr(), _lib.ref_array(refs), len(refs), self.h, self.w, self.bs, self.sr, 0, self.nby,
-                int(qp_rd), _lib.ptr(qr), int(self.vbs), self.lam, self.me_mode, int(self.fme), int(bool(fme_wrap)),
-                _lib.ptr(ws), out.split.data_ptr(), out.mv.data_ptr(), out.qtc.data_ptr(), out.tokens.data_ptr(),
-                out.mae_num.data_ptr(), out.recon.data_ptr(), _lib.ptr(out.sse), self.scratch.data_ptr(),
-                _lib.stream_handle(self.device))
-            _lib.check(rc, "so_encode_p_rows_ex")
-        out.frame_type, out.qp_rd = 1, int(qp_rd)
-        out.qp_row = None if qp_row is None else list(qp_row)
-        return out
+                 fme_wrap: bool = True, qp_map_dev: torch.Tensor | None = None,
+                 reuse_me: bool = False) -> FrameSymbols:
+        """complete_inter_flow (Encoder.py:1644) for one frame; asynchronous.
+        fme_wrap: see so_encode_p_rows_ex (False while refs hold the float64 start frame);
+        qp_map_dev: per-block QP (ROI / two-pass RC); reuse_me: keep the ME records of the
+        previous encode_p of the same frame (pass 2)."""
+        return self.encode_p_rows(cur, refs, 0, self.nby, qp_rd, out or self.new_symbols(1),
+                                  qp_row_dev if qp_row_dev is not None else self.qp_row_tensor(qp_row),
+                                  fme_wrap=fme_wrap, qp_map_dev=qp_map_dev, reuse_me=reuse_me, qp_row=qp_row)
 
     def encode_i(self, cur: torch.Tensor, qp_rd: int, qp_row=None, out: FrameSymbols | None = None,
-                 qp_row_dev: torch.Tensor | None = None) -> FrameSymbols:
+                 qp_row_dev: torch.Tensor | None = None, qp_map_dev: torch.Tensor | None = None) -> FrameSymbols:
         """complete_intra_flow (Encoder.py:1582), intra_mode 0, for one frame; asynchronous."""
-        self._check_plane(cur, "cur")
-        out = out or self.new_symbols(0)
-        qr = qp_row_dev if qp_row_dev is not None else self.qp_row_tensor(qp_row)
-        rc = self.lib.so_encode_i_frame(
-            cur.data_ptr(), self.h, self.w, self.bs, self.sr, int(qp_rd), _lib.ptr(qr), int(self.vbs),
-            self.lam, out.split.data_ptr(), out.mv.data_ptr(), out.qtc.data_ptr(), out.tokens.data_ptr(),
-            out.mae_num.data_ptr(), out.recon.data_ptr(), _lib.ptr(out.sse), self.scratch.data_ptr(),
-            _lib.stream_handle(self.device))
-        _lib.check(rc, "so_encode_i_frame")
-        out.frame_type, out.qp_rd = 0, int(qp_rd)
-        out.qp_row = None if qp_row is None else list(qp_row)
+        return self.encode_i_rows(cur, 0, self.nby, qp_rd, out or self.new_symbols(0),
+                                  qp_row_dev if qp_row_dev is not None else self.qp_row_tensor(qp_row),
+                                  qp_map_dev=qp_map_dev, qp_row=qp_row)
+
+    def qp_map(self, tokens: torch.Tensor | None, qp_rd: int, qp_row_dev: torch.Tensor | None,
+               roi_dev: torch.Tensor | None, out: torch.Tensor, by0: int = 0, by1: int | None = None,
+               qp_lo: int = 0, qp_hi: int = 12) -> torch.Tensor:
+        """so_qp_map: the per-block QP map of ROI / two-pass RC into `out` (int32 [nb])."""
+        by1 = self.nby if by1 is None else by1
+        rc = self.lib.so_qp_map(_lib.ptr(tokens), self.h, self.w, self.bs, int(by0), int(by1), int(qp_rd),
+                                _lib.ptr(qp_row_dev), _lib.ptr(roi_dev), int(qp_lo), int(qp_hi), out.data_ptr(),
+                                _lib.stream_handle(self.device))
+        _lib.check(rc, "so_qp_map")
         return out
 
     # ---- stripes (multi-GPU sharding, DESIGN.md §5) --------------------------------------
@@ -170,61 +152,71 @@ class Engine:
                             extra={"by0": by0, "by1": by1})
 
     def encode_p_rows(self, cur, refs, by0: int, by1: int, qp_rd: int, out: FrameSymbols,
-                      qp_row_dev: torch.Tensor | None = None, fme_wrap: bool = True) -> FrameSymbols:
+                      qp_row_dev: torch.Tensor | None = None, fme_wrap: bool = True,
+                      qp_map_dev: torch.Tensor | None = None, reuse_me: bool = False, qp_row=None) -> FrameSymbols:
         """so_encode_p_rows(_ex): block rows [by0, by1) of a P-frame; asynchronous."""
         self._check_plane(cur, "cur")
         for k, r in enumerate(refs):
             self._check_plane(r, f"refs[{k}]")
-        ws = self.fme_workspace(len(refs)) if self.fme else None
-        rc = self.lib.so_encode_p_rows_ex(
-            cur.data_ptr(), _lib.ref_array(refs), len(refs), self.h, self.w, self.bs, self.sr, int(by0), int(by1),
-            int(qp_rd), _lib.ptr(qp_row_dev), int(self.vbs), self.lam, self.me_mode, int(self.fme),
-            int(bool(fme_wrap)), _lib.ptr(ws), out.split.data_ptr(), out.mv.data_ptr(), out.qtc.data_ptr(),
-            out.tokens.data_ptr(), out.mae_num.data_ptr(), out.recon.data_ptr(), _lib.ptr(out.sse),
-            self.scratch.data_ptr(), _lib.stream_handle(self.device))
-        _lib.check(rc, "so_encode_p_rows_ex")
+        if not 1 <= len(refs) <= _lib.MAX_REF:
+            raise ValueError(f"nRefFrames must be in [1, {_lib.MAX_REF}]")
+        st = _lib.stream_handle(self.device)
+        if self.me_mode == _lib.ME_FULL and not self.fme and qp_map_dev is None and not reuse_me:
+            rc = self.lib.so_encode_p_rows(
+                cur.data_ptr(), _lib.ref_array(refs), len(refs), self.h, self.w, self.bs, self.sr, int(by0), int(by1),
+                int(qp_rd), _lib.ptr(qp_row_dev), int(self.vbs), self.lam, out.split.data_ptr(), out.mv.data_ptr(),
+                out.qtc.data_ptr(), out.tokens.data_ptr(), out.mae_num.data_ptr(), out.recon.data_ptr(),
+                _lib.ptr(out.sse), self.scratch.data_ptr(), st)
+            _lib.check(rc, "so_encode_p_rows")
+        else:
+            ws = self.fme_workspace(len(refs)) if self.fme else None
+            rc = self.lib.so_encode_p_rows_ex(
+                cur.data_ptr(), _lib.ref_array(refs), len(refs), self.h, self.w, self.bs, self.sr, int(by0), int(by1),
+                int(qp_rd), _lib.ptr(qp_row_dev), _lib.ptr(qp_map_dev), int(self.vbs), self.lam, self.me_mode,
+                int(self.fme), int(bool(fme_wrap)), _lib.ptr(ws), _lib.REUSE_ME if reuse_me else 0,
+                out.split.data_ptr(), out.mv.data_ptr(), out.qtc.data_ptr(), out.tokens.data_ptr(),
+                out.mae_num.data_ptr(), out.recon.data_ptr(), _lib.ptr(out.sse), self.scratch.data_ptr(), st)
+            _lib.check(rc, "so_encode_p_rows_ex")
         out.frame_type, out.qp_rd = 1, int(qp_rd)
+        out.qp_row = None if qp_row is None else list(qp_row)
         return out
 
     def encode_i_rows(self, cur, by0: int, by1: int, qp_rd: int, out: FrameSymbols,
-                      qp_row_dev: torch.Tensor | None = None) -> FrameSymbols:
-        """so_encode_i_rows: block rows [by0, by1) of an I-frame; asynchronous."""
+                      qp_row_dev: torch.Tensor | None = None, qp_map_dev: torch.Tensor | None = None,
+                      qp_row=None) -> FrameSymbols:
+        """so_encode_i_rows_ex: block rows [by0, by1) of an I-frame; asynchronous."""
         self._check_plane(cur, "cur")
-        rc = self.lib.so_encode_i_rows(
+        rc = self.lib.so_encode_i_rows_ex(
             cur.data_ptr(), self.h, self.w, self.bs, self.sr, int(by0), int(by1), int(qp_rd), _lib.ptr(qp_row_dev),
-            int(self.vbs), self.lam, out.split.data_ptr(), out.mv.data_ptr(), out.qtc.data_ptr(),
-            out.tokens.data_ptr(), out.mae_num.data_ptr(), out.recon.data_ptr(), _lib.ptr(out.sse),
-            self.scratch.data_ptr(), _lib.stream_handle(self.device))
-        _lib.check(rc, "so_encode_i_rows")
+            _lib.ptr(qp_map_dev), int(self.vbs), self.lam, out.split.data_ptr(), out.mv.data_ptr(),
+            out.qtc.data_ptr(), out.tokens.data_ptr(), out.mae_num.data_ptr(), out.recon.data_ptr(),
+            _lib.ptr(out.sse), self.scratch.data_ptr(), _lib.stream_handle(self.device))
+        _lib.check(rc, "so_encode_i_rows_ex")
         out.frame_type, out.qp_rd = 0, int(qp_rd)
+        out.qp_row = None if qp_row is None else list(qp_row)
         return out
 
     # ---- decode ---------------------------------------------------------------------------
     def recon_inter(self, refs: list, split, mv, qtc, qp: int, qp_row=None, out=None,
-                    fme_wrap: bool = True) -> torch.Tensor:
+                    fme_wrap: bool = True, qp_map_dev: torch.Tensor | None = None) -> torch.Tensor:
         out = out if out is not None else alloc_planes(1, self.h, self.w, self.device)[0]
         qr = self.qp_row_tensor(qp_row)
-        if self.fme:
-            ws = self.fme_workspace(len(refs))
-            rc = self.lib.so_inter_recon_ex(_lib.ref_array(refs), len(refs), self.h, self.w, self.bs, int(qp),
-                                            _lib.ptr(qr), 1, int(bool(fme_wrap)), ws.data_ptr(), split.data_ptr(),
-                                            mv.data_ptr(), qtc.data_ptr(), out.data_ptr(),
-                                            _lib.stream_handle(self.device))
-            _lib.check(rc, "so_inter_recon_ex")
-            return out
-        rc = self.lib.so_inter_recon(_lib.ref_array(refs), len(refs), self.h, self.w, self.bs, int(qp),
-                                     _lib.ptr(qr), split.data_ptr(), mv.data_ptr(), qtc.data_ptr(),
-                                     out.data_ptr(), _lib.stream_handle(self.device))
-        _lib.check(rc, "so_inter_recon")
+        ws = self.fme_workspace(len(refs)) if self.fme else None
+        rc = self.lib.so_inter_recon_ex(_lib.ref_array(refs), len(refs), self.h, self.w, self.bs, int(qp),
+                                        _lib.ptr(qr), _lib.ptr(qp_map_dev), int(self.fme), int(bool(fme_wrap)),
+                                        _lib.ptr(ws), split.data_ptr(), mv.data_ptr(), qtc.data_ptr(), out.data_ptr(),
+                                        _lib.stream_handle(self.device))
+        _lib.check(rc, "so_inter_recon_ex")
         return out
 
-    def recon_intra(self, split, mv, qtc, qp: int, qp_row=None, out=None) -> torch.Tensor:
+    def recon_intra(self, split, mv, qtc, qp: int, qp_row=None, out=None,
+                    qp_map_dev: torch.Tensor | None = None) -> torch.Tensor:
         out = out if out is not None else alloc_planes(1, self.h, self.w, self.device)[0]
         qr = self.qp_row_tensor(qp_row)
-        rc = self.lib.so_intra_recon(self.h, self.w, self.bs, int(qp), _lib.ptr(qr), split.data_ptr(),
-                                     mv.data_ptr(), qtc.data_ptr(), out.data_ptr(), self.scratch.data_ptr(),
-                                     _lib.stream_handle(self.device))
-        _lib.check(rc, "so_intra_recon")
+        rc = self.lib.so_intra_recon_ex(self.h, self.w, self.bs, int(qp), _lib.ptr(qr), _lib.ptr(qp_map_dev),
+                                        split.data_ptr(), mv.data_ptr(), qtc.data_ptr(), out.data_ptr(),
+                                        self.scratch.data_ptr(), _lib.stream_handle(self.device))
+        _lib.check(rc, "so_intra_recon_ex")
         return out
 
     # ---- metrics ---------------------------------------------------------------------------

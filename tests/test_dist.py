@@ -44,7 +44,20 @@ class OracleStripeEngine:
     def __init__(self, h, w, bs=16, sr=16, vbs=False, lam=0.015):
         self.h, self.w, self.bs, self.sr, self.vbs, self.lam = h, w, bs, sr, vbs, lam
         self.nbx, self.nby = w // bs, h // bs
+        self.nb = self.nbx * self.nby
         self.device = torch.device("cpu")
+
+    def qp_map(self, tokens, qp_rd, qp_row_dev, roi_dev, out, by0=0, by1=None, qp_lo=0, qp_hi=12):
+        """so_qp_map on the stripe's rows (stripe-local tokens) via the oracle restatement."""
+        from oracle import oracle as O
+        by1 = self.nby if by1 is None else by1
+        n = (by1 - by0) * self.nbx
+        t = None if tokens is None else tokens.numpy()[:n]
+        qr = None if qp_row_dev is None else qp_row_dev.numpy()[by0:by1]
+        roi = None if roi_dev is None else roi_dev.numpy()[by0 * self.nbx:by1 * self.nbx]
+        m = O.qp_map(t, self.nbx, by1 - by0, qp_rd, qr, roi, qp_lo, qp_hi)
+        out[by0 * self.nbx:by1 * self.nbx] = torch.from_numpy(m)
+        return out
 
     new_stripe_symbols = Engine.new_stripe_symbols
 
@@ -59,10 +72,15 @@ class OracleStripeEngine:
         y0, y1 = by0 * self.bs, by1 * self.bs
         out.recon[y0:y1].copy_(torch.from_numpy(r["recon"][y0:y1]))
 
-    def encode_p_rows(self, cur, refs, by0, by1, qp, out, qp_row_dev=None):
+    def encode_p_rows(self, cur, refs, by0, by1, qp, out, qp_row_dev=None, qp_map_dev=None, reuse_me=False):
         from oracle import oracle as O
         qr = None if qp_row_dev is None else qp_row_dev.tolist()
-        r = O.inter_frame(cur.numpy(), [x.numpy() for x in refs], self.bs, self.sr, qp, qr, self.vbs, self.lam)
+        qm = None if qp_map_dev is None else qp_map_dev.numpy().copy()
+        if qm is not None:   # rows outside the stripe are not this rank's: fill with qp (unused)
+            qm[: by0 * self.nbx] = qp
+            qm[by1 * self.nbx:] = qp
+        r = O.inter_frame(cur.numpy(), [x.numpy() for x in refs], self.bs, self.sr, qp, qr, self.vbs, self.lam,
+                          qp_map=qm)
         self._fill(r, by0, by1, out)
         y0, y1 = by0 * self.bs, by1 * self.bs
         d = cur.numpy()[y0:y1].astype(np.int64) - out.recon[y0:y1].numpy().astype(np.int64)
@@ -71,10 +89,14 @@ class OracleStripeEngine:
         out.frame_type = 1
         return out
 
-    def encode_i_rows(self, cur, by0, by1, qp, out, qp_row_dev=None):
+    def encode_i_rows(self, cur, by0, by1, qp, out, qp_row_dev=None, qp_map_dev=None):
         from oracle import oracle as O
         qr = None if qp_row_dev is None else qp_row_dev.tolist()
-        r = O.intra_frame(cur.numpy(), self.bs, self.sr, qp, qr, self.vbs, self.lam)
+        qm = None if qp_map_dev is None else qp_map_dev.numpy().copy()
+        if qm is not None:
+            qm[: by0 * self.nbx] = qp
+            qm[by1 * self.nbx:] = qp
+        r = O.intra_frame(cur.numpy(), self.bs, self.sr, qp, qr, self.vbs, self.lam, qp_map=qm)
         self._fill(r, by0, by1, out)
         y0, y1 = by0 * self.bs, by1 * self.bs
         d = cur.numpy()[y0:y1].astype(np.int64) - out.recon[y0:y1].numpy().astype(np.int64)
@@ -99,7 +121,17 @@ CASES = {
     "plain": dict(vbs=False, qp=4, intra_dur=F, nref=1, rc=None),
     "vbs_nref2": dict(vbs=True, qp=3, intra_dur=3, nref=2, rc=None),
     "rc2": dict(vbs=True, qp=4, intra_dur=F, nref=1, rc=2, thresh=40),
+    # two-pass RC (RCFlag 3) + ROI (build extension, BASELINE configs[4])
+    "rc3_roi": dict(vbs=True, qp=4, intra_dur=3, nref=1, rc=3, thresh=10 ** 9, roi=True),
+    "roi_only": dict(vbs=False, qp=4, intra_dur=F, nref=1, rc=None, roi=True),
 }
+
+
+def _roi():
+    r = np.zeros((H // 16, W // 16), np.int32)
+    r[1:4, 1:3] = -2
+    r[0, :] = 1
+    return r.reshape(-1)
 
 
 def _rc_sched(case):
@@ -118,7 +150,8 @@ def _worker(rank, world, port, case_name, outdir):
         enc = StripeGOPEncoder(eng)
         sched = _rc_sched(case)[0] if case["rc"] else None
         res = enc.encode(frames, case["intra_dur"], case["qp"], nref=case["nref"], qp_sched=sched,
-                         rc_flag=case["rc"], intra_thresh=case.get("thresh"))
+                         rc_flag=case["rc"], intra_thresh=case.get("thresh"),
+                         roi=_roi() if case.get("roi") else None)
         full = [enc.gather_symbols(s) for s in res["symbols"]]
         if rank == 0:
             np.savez(os.path.join(outdir, "out.npz"), sse=res["sse"].numpy(),
@@ -129,7 +162,8 @@ def _worker(rank, world, port, case_name, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,case_name", [(2, "plain"), (2, "vbs_nref2"), (2, "rc2"), (4, "plain")])
+@pytest.mark.parametrize("world,case_name", [(2, "plain"), (2, "vbs_nref2"), (2, "rc2"), (4, "plain"),
+                                             (2, "rc3_roi"), (3, "roi_only")])
 def test_stripe_gop_matches_single_process_oracle(tmp_path, world, case_name):
     from oracle.gop import encode_gop
     mp.start_processes(_worker, args=(world, _free_port(), case_name, str(tmp_path)), nprocs=world,
@@ -140,6 +174,8 @@ def test_stripe_gop_matches_single_process_oracle(tmp_path, world, case_name):
     if case["rc"]:
         _, tables = _rc_sched(case)
         rc_kw = dict(rc=case["rc"], target="2 mbps", tables=tables, intra_thresh=case["thresh"])
+    if case.get("roi"):
+        rc_kw["roi"] = _roi()
     ref = encode_gop(_frames(), case["qp"], case["intra_dur"], vbs=case["vbs"], nref=case["nref"], **rc_kw)
     assert list(got["ftypes"]) == [r["frame_type"] for r in ref]
     for i, r in enumerate(ref):

@@ -525,3 +525,98 @@ def test_transmit_then_decode_bitstream(gpu, tmp_path, monkeypatch):
     out = dec.decode_bitstream(str(tmp_path / "mv.txt"), str(tmp_path / "res.txt"))
     for i in range(4):
         assert (out[i] == enc._symbols[i].recon.cpu().numpy()).all(), i
+
+
+# ---------------------------------------------------------------- ROI and two-pass RC (configs[4])
+# Build extension: no reference counterpart -- parity against the C oracle's
+# restatement (oracle/gop.py encode_gop rc=3 / roi, oracle oc_qp_map).
+def test_qp_map_kernel_vs_oracle(gpu):
+    from oracle import oracle as O
+    from streamoptima_amd.engine import Engine
+    eng = Engine(96, 160, 16, 16, False, 0.015, gpu)
+    rng = np.random.default_rng(5)
+    tok = rng.integers(1, 400, size=eng.nb).astype(np.int32)
+    roi = rng.integers(-3, 3, size=eng.nb).astype(np.int32)
+    qr = rng.integers(0, 8, size=eng.nby).astype(np.int32)
+    out = torch.full((eng.nb,), -7, dtype=torch.int32, device=gpu)
+    for t, r, q in ((tok, roi, qr), (tok, None, None), (None, roi, qr)):
+        eng.qp_map(_dev(t, gpu) if t is not None else None, 4, _dev(q, gpu) if q is not None else None,
+                   _dev(r, gpu) if r is not None else None, out, qp_lo=1, qp_hi=9)
+        torch.cuda.synchronize()
+        assert (out.cpu().numpy() == O.qp_map(t, eng.nbx, eng.nby, 4, q, r, 1, 9)).all()
+    # stripe rows only: rows outside [2, 4) keep their previous values
+    out.fill_(-7)
+    eng.qp_map(_dev(tok[2 * eng.nbx:4 * eng.nbx], gpu), 4, None, None, out, 2, 4)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy().reshape(eng.nby, eng.nbx)
+    assert (o[:2] == -7).all() and (o[4:] == -7).all()
+    assert (o[2:4].reshape(-1) == O.qp_map(tok[2 * eng.nbx:4 * eng.nbx], eng.nbx, 2, 4)).all()
+
+
+RC_GOPS = [
+    # (name, vbs, rc, roi, fast, fme)
+    ("two_pass_vbs", True, 3, False, False, False),
+    ("two_pass_roi", False, 3, True, False, False),
+    ("roi_rc1", True, 1, True, False, False),
+    ("roi_only_fme", False, None, True, False, True),
+    ("two_pass_fast", True, 3, True, True, False),
+]
+
+
+@pytest.mark.parametrize("name,vbs,rc,roi,fast,fme", RC_GOPS)
+def test_gop_two_pass_roi_vs_oracle(gpu, name, vbs, rc, roi, fast, fme, tmp_path, monkeypatch):
+    from oracle.gop import encode_gop
+    from streamoptima_amd.Encoder import Y_Video_codec
+    from streamoptima_amd.synth import synth_sequence
+    monkeypatch.chdir(tmp_path)
+    h, w, f = 96, 128, 5
+    seq = synth_sequence(f, h, w, seed=31)
+    # mixed complexity (two-pass needs blocks far from their row's mean): a smooth ramp on
+    # the left quarter, a flat patch, texture elsewhere
+    seq[:, :, : w // 4] = (np.arange(w // 4)[None, None, :] * 3 + np.arange(h)[None, :, None]).astype(np.uint8)
+    seq[:, 32:64, 64:96] = 90
+    tables = json.load(open(os.path.join(GOLDEN, "rc_schedule.json")))["tables"]
+    roi_map = None
+    if roi:
+        roi_map = np.zeros((h // 16, w // 16), np.int32)
+        roi_map[2:5, 2:6] = -2
+        roi_map[0] = 2
+    kw = dict(RCFlag=rc, targetBR="200 kbps" if rc else None, qp_rate_tables=tables if rc else None,
+              intra_thresh=10 ** 9 if rc and rc > 1 else None)
+    enc = Y_Video_codec(h, w, f, 16, 16, 4, 3, 0, 0.015, vbs, y_only_frame_arr=seq, fast_me=fast, FMEEnable=fme,
+                        roi=roi_map, device=gpu, **kw)
+    psnr = enc.encode()
+    exp = encode_gop(seq, 4, 3, vbs=vbs, rc=rc, target=kw["targetBR"], tables=tables,
+                     intra_thresh=kw["intra_thresh"], fast_me=fast, fme=fme,
+                     roi=roi_map.reshape(-1) if roi else None)
+    pkg = enc.encoded_package
+    for i in range(f):
+        _assert_frame(_sym_host(enc._symbols[i]), exp[i])
+        assert (pkg["QP map per frame"][i] == exp[i]["qp_map"]).all()
+        assert psnr[i] == exp[i]["psnr"]
+        assert (enc.decoded_device[i].cpu().numpy() == exp[i]["recon"]).all()
+    if rc == 3:   # the map really moved QPs (two-pass is not a no-op on this content)
+        assert any(len(np.unique(pkg["QP map per frame"][i])) > 2 for i in range(f))
+
+
+def test_two_pass_roi_bitstream_round_trip(gpu, tmp_path, monkeypatch):
+    """RCFlag 3 + ROI: transmit_bitstream (+ the QP-map line) -> decode_bitstream == recon."""
+    from streamoptima_amd.Encoder import Y_Video_codec
+    from streamoptima_amd.decoder import decoder
+    from streamoptima_amd.synth import synth_sequence
+    monkeypatch.chdir(tmp_path)
+    h, w, f = 96, 128, 4
+    seq = synth_sequence(f, h, w, seed=8)
+    seq[:, :, :48] = 60
+    tables = json.load(open(os.path.join(GOLDEN, "rc_schedule.json")))["tables"]
+    roi = [(32, 16, 96, 64, -2)]
+    enc = Y_Video_codec(h, w, f, 16, 16, 4, 2, 0, 0.015, True, y_only_frame_arr=seq, RCFlag=3, targetBR="200 kbps",
+                        qp_rate_tables=tables, intra_thresh=10 ** 9, roi=roi, device=gpu)
+    enc.encode()
+    files = [str(tmp_path / n) for n in ("mv.txt", "res.txt", "qp.txt")]
+    enc.transmit_bitstream(mv_file=files[0], residual_file=files[1], qp_map_file=files[2])
+    dec = decoder(0, 2, 16, f, h, w, 4, 1, False, 0.015, True, RCFlag=3, targetBR="200 kbps", qp_rate_tables=tables,
+                  device=gpu)
+    out = dec.decode_bitstream(files[0], files[1], qp_map_file=files[2])
+    for i in range(f):
+        assert (out[i] == enc._symbols[i].recon.cpu().numpy()).all(), i
