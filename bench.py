@@ -49,7 +49,13 @@ CONFIGS = {
     "1080p": dict(workload="1080p 30-frame I+P GOP (configs[1], 1920x1088 internal)", h=1080, w=1920,
                   frames=30, qp=4),
     "4k120": dict(workload="4K 120-frame I+P GOP (configs[3])", h=2160, w=3840, frames=120, qp=4),
+    # configs[4]: ROI + two-pass RC (RCFlag 3, build extension); a centred ROI rectangle at
+    # -2 QP, 50 mbps against a QP-rate table scaled to 4K rows (rc_schedule.json table x 11)
+    "4k_rc2pass": dict(workload="4K 30-frame ROI + two-pass RC GOP (configs[4])", h=2160, w=3840, frames=30, qp=4,
+                       rc=3, target="50 mbps", roi=[(1280, 720, 2560, 1440, -2)]),
 }
+RC_TABLES = [[v * 11 for v in (9000, 6000, 4000, 2600, 1700, 1100, 700, 450, 300, 200)],
+             [v * 11 for v in (7000, 4500, 3000, 2000, 1300, 850, 550, 350, 230, 150)]]
 
 
 def parse():
@@ -279,6 +285,9 @@ def main():
     hp = -(-h // 16) * 16
     me_kw = {"full": {}, "fme": dict(FMEEnable=True), "fast": dict(fast_me=True),
              "fastpar": dict(fast_me=True, ParallelMode=2), "fast_fme": dict(fast_me=True, FMEEnable=True)}[args.me]
+    if cfg.get("rc"):
+        # RCFlag 3 without intra_thresh: no P->I switch, so no host read per frame
+        me_kw.update(RCFlag=cfg["rc"], targetBR=cfg["target"], qp_rate_tables=RC_TABLES, roi=cfg.get("roi"))
     codec = Y_Video_codec(h, w, f, 16, 16, cfg["qp"], f, 0, 0.015, args.vbs, y_only_frame_arr=None, device=dev,
                           **me_kw)
     eng = codec.engine()
@@ -291,7 +300,9 @@ def main():
         senc = StripeGOPEncoder(eng)
 
         def step():
-            return senc.encode(frames, f, cfg["qp"])
+            rc = cfg.get("rc")
+            return senc.encode(frames, f, cfg["qp"], qp_sched=codec.row_qp_schedule(eng.nby) if rc else None,
+                               rc_flag=rc, intra_thresh=None, roi=codec.roi_block_offsets())
     else:
         def step():
             return codec.encode_device(frames, f, symbols=pre)

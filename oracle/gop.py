@@ -69,7 +69,8 @@ def encode_gop(frames, qp, intra_dur, bs=16, sr=16, vbs=False, lam=0.015, nref=1
         else:
             r = enc(cur, False, qp, not any(ref_float))
             ft = 1
-            if rc is not None and rc > 1 and int(r["tokens"].sum()) > intra_thresh:
+            if (rc is not None and rc > 1 and (rc == 2 or intra_thresh is not None)
+                    and int(r["tokens"].sum()) > intra_thresh):
                 r = enc(cur, True, qp_sched[-1], True)
                 ft = 0
         r["frame_type"] = ft

@@ -401,7 +401,9 @@ class Y_Video_codec:
             else:
                 sym = frame(cur, False, self.Qp, pre if pre is not None and pre.frame_type == 1 else None,
                             not any(ref_float))
-                if self.RCFlag is not None and self.RCFlag > 1:
+                # RCFlag 2 (and 3 given an intra_thresh): P->I switch on the residual size,
+                # one host read per P-frame (Encoder.py:1851-1856)
+                if self.RCFlag is not None and self.RCFlag > 1 and (self.RCFlag == 2 or self.intra_thresh is not None):
                     residual_size = int(sym.tokens.sum().item())
                     if residual_size > self.intra_thresh:
                         # self.Q still holds the last row's QP of the inter pass (quirk

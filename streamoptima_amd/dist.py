@@ -129,7 +129,7 @@ class StripeGOPEncoder:
                 sym = stripe(cur, True, qp, plane)
             else:
                 sym = stripe(cur, False, qp, plane)
-                if rc_flag is not None and rc_flag > 1:
+                if rc_flag is not None and rc_flag > 1 and (rc_flag == 2 or intra_thresh is not None):
                     total = sym.tokens.sum(dtype=torch.int64).reshape(1)
                     if self.world > 1:
                         dist.all_reduce(total, group=self.group)
