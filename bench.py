@@ -117,7 +117,7 @@ def me_kernel_name(vbs: bool, me: str = "full") -> str:
         return "me_fast_kernel"
     if impl == "dense" or vbs:
         return "me_wave_kernel<16, %s>" % ("true" if vbs else "false")
-    return "me_sea_kernel"
+    return "me_sea2_kernel" if impl != "sea1" else "me_sea_kernel"
 
 
 def kernel_roofline(codec, frames_dev, symbols, reps: int, me_variant: str = "full") -> dict:

@@ -89,7 +89,9 @@ struct MeWGeo {
     static constexpr int TBY = TPY / BS;
     static constexpr int TPX = 128;
     static constexpr int WR = TPY + 2 * SR;               // window rows
-    static constexpr int RPD = (TPX + 2 * SR) / 4;        // 40 dwords per copy row
+    // copy row pitch: 40 dwords of window + 1 pad, so reads that walk down a column (dy
+    // lanes, survivor rows) hit 32 different banks (41 r mod 32) instead of 4 (40 r mod 32)
+    static constexpr int RPD = (TPX + 2 * SR) / 4 + 1;
     // dwords per shifted copy: CSTRIDE = 8 (mod 32) puts the four copies 8 banks apart, so a
     // 32-lane ds_read_b32 (bank = dword mod 32) of lanes xi hits 8*(xi&3) + (xi>>2): no conflict
     static constexpr int CSTRIDE = WR * RPD + 8;
@@ -112,6 +114,40 @@ SO_DEV void load_cur_sgpr(const uint8_t* __restrict__ cur, int W, int x, int y, 
     }
 }
 
+
+// Stage a WR x (4 RPD) byte window of `ref` at (gx0, gy0) into LDS as four copies shifted
+// by 0..3 bytes (copy s, row r, dword m = window bytes [4m + s, 4m + s + 4); zero outside
+// the frame).  Every thread issues all its global loads before any LDS store, so a
+// workgroup pays one memory latency for the window instead of one per loop trip.
+template <int WR, int RPD, int CS, int NT>
+SO_DEV void stage_window(uint32_t* win, const uint8_t* __restrict__ ref, int H, int W, int gx0, int gy0, int tid) {
+    constexpr int N = WR * RPD, IT = (N + NT - 1) / NT;
+    uint32_t a[IT], b[IT];
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const int i = tid + k * NT;
+        const int wr = i / RPD, m = i - wr * RPD;
+        const int gy = gy0 + wr, gx = gx0 + 4 * m;
+        a[k] = 0;
+        b[k] = 0;
+        if (i < N && gy >= 0 && gy < H) {
+            const uint8_t* rp = ref + (size_t)gy * W;
+            if (gx >= 0 && gx + 4 <= W) a[k] = *reinterpret_cast<const uint32_t*>(rp + gx);
+            if (gx + 4 >= 0 && gx + 8 <= W) b[k] = *reinterpret_cast<const uint32_t*>(rp + gx + 4);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const int i = tid + k * NT;
+        if (i < N) {
+            uint32_t* d = win + i;     // == wr * RPD + m
+            d[0] = a[k];
+            d[CS] = __builtin_amdgcn_alignbyte(b[k], a[k], 1);
+            d[2 * CS] = __builtin_amdgcn_alignbyte(b[k], a[k], 2);
+            d[3 * CS] = __builtin_amdgcn_alignbyte(b[k], a[k], 3);
+        }
+    }
+}
 
 template <int N>
 SO_DEV void acc_fence_n(uint32_t (&a)[N]) {
@@ -199,7 +235,9 @@ SO_DEV uint64_t widen17_fme(uint32_t b32, uint32_t X, int hh, int xi, bool xok, 
 // Dense search of one block by one wavefront (phase 1 + phase 2 over the four shifted
 // window copies in `win`); merges the block key into keys[u] and, with VBS, the quadrant
 // keys into keys[nblk + 4u + j].  Shared by me_wave_kernel and me_sea_kernel's fallback.
-template <int BS, bool SUB, int RPD, int CS, bool FME = false>
+// ONE: the window is a single copy (me_sea2_kernel): the lane's 16 bytes at any column are
+// five ds_read_b32 + four v_alignbyte per row instead of four reads of its shifted copy.
+template <int BS, bool SUB, int RPD, int CS, bool FME = false, bool ONE = false>
 SO_DEV void wave_dense_block(const uint32_t* win, unsigned long long* keys, int nblk, const uint8_t* __restrict__ cur,
                              int W, int H, int x, int y, int bxl, int byl, int u, int tid, int r,
                              FmePhase ph = FmePhase{0, 0}) {
@@ -212,7 +250,8 @@ SO_DEV void wave_dense_block(const uint32_t* win, unsigned long long* keys, int 
     const int xi = lane & 31, hh = lane >> 5;
     const uint32_t X = hh ? 0u : 31u;
     // phase-1 lane: window column bxl*BS + xi (dx = xi - 16) in copy xi & 3
-    const int q1 = (xi & 3) * CS + (byl * BS + 16 * hh) * RPD + ((bxl * BS + xi) >> 2);
+    const int q1 = (ONE ? 0 : (xi & 3) * CS) + (byl * BS + 16 * hh) * RPD + ((bxl * BS + xi) >> 2);
+    const uint32_t sh1 = (uint32_t)((bxl * BS + xi) & 3);   // ONE: byte shift of the lane's column
     // phase-2 lane: dx = +16 (column bxl*BS + 32, copy 0), dy index = lane (< 33)
     const int d2 = lane < 33 ? lane : 32;
     const int q2 = (byl * BS + d2) * RPD + ((bxl * BS + 32) >> 2);
@@ -242,13 +281,29 @@ SO_DEV void wave_dense_block(const uint32_t* win, unsigned long long* keys, int 
         asm volatile("" : "+v"(qo));           // address space through the opaque asm
         lds_vu32p qp = (lds_vu32p)(win + qo);
         uint32_t wc[NDW], wn[NDW];
+        if constexpr (ONE) {
+            uint32_t t[NDW + 1];
 #pragma unroll
-        for (int k = 0; k < NDW; ++k) wc[k] = qp[k];
+            for (int k = 0; k <= NDW; ++k) t[k] = qp[k];
+#pragma unroll
+            for (int k = 0; k < NDW; ++k) wc[k] = __builtin_amdgcn_alignbyte(t[k + 1], t[k], sh1);
+        } else {
+#pragma unroll
+            for (int k = 0; k < NDW; ++k) wc[k] = qp[k];
+        }
 #pragma unroll
         for (int jj = 0; jj < NR; ++jj) {
             if (jj + 1 < NR) {
+                if constexpr (ONE) {
+                    uint32_t t[NDW + 1];
 #pragma unroll
-                for (int k = 0; k < NDW; ++k) wn[k] = qp[(jj + 1) * RPD + k];
+                    for (int k = 0; k <= NDW; ++k) t[k] = qp[(jj + 1) * RPD + k];
+#pragma unroll
+                    for (int k = 0; k < NDW; ++k) wn[k] = __builtin_amdgcn_alignbyte(t[k + 1], t[k], sh1);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < NDW; ++k) wn[k] = qp[(jj + 1) * RPD + k];
+                }
             }
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
@@ -387,21 +442,7 @@ me_wave_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
         const uint8_t* ref = refs.p[r];
         __syncthreads();   // the previous reference's reads of the window are done
         // stage: copy s row wr dword m = window bytes [4m + s, 4m + s + 4); zero off-frame
-        for (int i = tid; i < G::WR * RPD; i += G::NTHREADS) {
-            const int wr = i / RPD, m = i - wr * RPD;
-            const int gy = y0 - SR + wr, gx = x0 - SR + 4 * m;
-            uint32_t a = 0, b = 0;
-            if (gy >= 0 && gy < H) {
-                const uint8_t* rp = ref + (size_t)gy * W;
-                if (gx >= 0 && gx + 4 <= W) a = *reinterpret_cast<const uint32_t*>(rp + gx);
-                if (gx + 4 >= 0 && gx + 8 <= W) b = *reinterpret_cast<const uint32_t*>(rp + gx + 4);
-            }
-            uint32_t* d = win + wr * RPD + m;
-            d[0] = a;
-            d[CS] = __builtin_amdgcn_alignbyte(b, a, 1);
-            d[2 * CS] = __builtin_amdgcn_alignbyte(b, a, 2);
-            d[3 * CS] = __builtin_amdgcn_alignbyte(b, a, 3);
-        }
+        stage_window<G::WR, RPD, CS, G::NTHREADS>(win, ref, H, W, x0 - SR, y0 - SR, tid);
         __syncthreads();
 #pragma unroll 1
         for (int u = wave; u < G::NBLK; u += G::NW) {
@@ -449,21 +490,7 @@ me_fme_kernel(const uint8_t* __restrict__ cur, const uint8_t* __restrict__ plane
         const FmePhase ph{(vr >> 1) & 1, vr & 1};
         const int r = vr >> 2;
         __syncthreads();
-        for (int i = tid; i < G::WR * RPD; i += G::NTHREADS) {
-            const int wr = i / RPD, m = i - wr * RPD;
-            const int gy = y0 - SR + wr, gx = x0 - SR + 4 * m;
-            uint32_t a = 0, b = 0;
-            if (gy >= 0 && gy < H) {
-                const uint8_t* rp = ref + (size_t)gy * W;
-                if (gx >= 0 && gx + 4 <= W) a = *reinterpret_cast<const uint32_t*>(rp + gx);
-                if (gx + 4 >= 0 && gx + 8 <= W) b = *reinterpret_cast<const uint32_t*>(rp + gx + 4);
-            }
-            uint32_t* d = win + wr * RPD + m;
-            d[0] = a;
-            d[CS] = __builtin_amdgcn_alignbyte(b, a, 1);
-            d[2 * CS] = __builtin_amdgcn_alignbyte(b, a, 2);
-            d[3 * CS] = __builtin_amdgcn_alignbyte(b, a, 3);
-        }
+        stage_window<G::WR, RPD, CS, G::NTHREADS>(win, ref, H, W, x0 - SR, y0 - SR, tid);
         __syncthreads();
 #pragma unroll 1
         for (int u = wave; u < G::NBLK; u += G::NW) {
@@ -571,7 +598,9 @@ struct SeaGeo {
     static constexpr int BS = 16, SR = 16, NT = 17;
     static constexpr int TBX = 8, TPY = 32, TBY = 2, TPX = 128;
     static constexpr int WR = TPY + 2 * SR;               // 64 window rows
-    static constexpr int RPD = (TPX + 2 * SR) / 4;        // 40 dwords per copy row
+    // copy row pitch: 40 dwords of window + 1 pad, so reads that walk down a column (dy
+    // lanes, survivor rows) hit 32 different banks (41 r mod 32) instead of 4 (40 r mod 32)
+    static constexpr int RPD = (TPX + 2 * SR) / 4 + 1;
     static constexpr int CSTRIDE = WR * RPD + 8;           // = 8 (mod 32): see MeWGeo
     static constexpr int B4R = WR - 3, B4C = TPX + 2 * SR - 3, B4P = 160;   // 61 x 157 byte sums (+4 pad)
     static constexpr int NBLK = TBX * TBY;
@@ -583,7 +612,7 @@ struct SeaGeo {
 
 __global__ void __launch_bounds__(SeaGeo::NTHREADS) __attribute__((amdgpu_waves_per_eu(4)))
 me_sea_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
-              int32_t* __restrict__ out_best) {
+              int32_t* __restrict__ out_best, int probe) {
     using G = SeaGeo;
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RPD = G::RPD, CS = G::CSTRIDE, NT = G::NT;
     constexpr int B4P = G::B4P, CAP = G::CAP, CP = G::TPX;
@@ -605,12 +634,20 @@ me_sea_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int
 
     for (int i = tid; i < G::NBLK; i += G::NTHREADS) keys[i] = kNoKey;
     // current tile (zero outside the frame / stripe)
-    for (int i = tid; i < G::TPY * CP / 4; i += G::NTHREADS) {
-        const int rr = i / (CP / 4), m = i - rr * (CP / 4);
-        const int gy = y0 + rr, gx = x0 + 4 * m;
-        uint32_t v = 0;
-        if (gy < H && gx + 4 <= W) v = *reinterpret_cast<const uint32_t*>(cur + (size_t)gy * W + gx);
-        curt[i] = v;
+    {
+        constexpr int N = G::TPY * CP / 4, IT = (N + G::NTHREADS - 1) / G::NTHREADS;
+        uint32_t v[IT];
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            const int i = tid + k * G::NTHREADS;
+            const int rr = i / (CP / 4), m = i - rr * (CP / 4);
+            const int gy = y0 + rr, gx = x0 + 4 * m;
+            v[k] = 0;
+            if (i < N && gy < H && gx + 4 <= W) v[k] = *reinterpret_cast<const uint32_t*>(cur + (size_t)gy * W + gx);
+        }
+#pragma unroll
+        for (int k = 0; k < IT; ++k)
+            if (tid + k * G::NTHREADS < N) curt[tid + k * G::NTHREADS] = v[k];
     }
     __syncthreads();
     // current blocks' 4x4 byte sums: item (block, j, ii) -> byte ii of a4[blk*4 + j]
@@ -625,21 +662,7 @@ me_sea_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int
     for (int r = 0; r < nref; ++r) {
         const uint8_t* ref = refs.p[r];
         __syncthreads();
-        for (int i = tid; i < G::WR * RPD; i += G::NTHREADS) {
-            const int wr = i / RPD, m = i - wr * RPD;
-            const int gy = y0 - SR + wr, gx = x0 - SR + 4 * m;
-            uint32_t a = 0, b = 0;
-            if (gy >= 0 && gy < H) {
-                const uint8_t* rp = ref + (size_t)gy * W;
-                if (gx >= 0 && gx + 4 <= W) a = *reinterpret_cast<const uint32_t*>(rp + gx);
-                if (gx + 4 >= 0 && gx + 8 <= W) b = *reinterpret_cast<const uint32_t*>(rp + gx + 4);
-            }
-            uint32_t* d = win + wr * RPD + m;
-            d[0] = a;
-            d[CS] = __builtin_amdgcn_alignbyte(b, a, 1);
-            d[2 * CS] = __builtin_amdgcn_alignbyte(b, a, 2);
-            d[3 * CS] = __builtin_amdgcn_alignbyte(b, a, 3);
-        }
+        stage_window<G::WR, RPD, CS, G::NTHREADS>(win, ref, H, W, x0 - SR, y0 - SR, tid);
         __syncthreads();
         // B4(r, c): thread per (column, quarter of the rows) slides a 4-row sum of the
         // horizontal 4-sums (one v_sad_u8 against 0 each) down its column
@@ -658,6 +681,7 @@ me_sea_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int
             }
         }
         __syncthreads();
+        if (probe == 1) continue;   // timing probe (tools/me_ab2.py): staging + byte sums only
 #pragma unroll 1
         for (int u = wave; u < G::NBLK; u += G::NW) {
             const int bxl = u % TBX, byl = u / TBX;
@@ -739,6 +763,10 @@ me_sea_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int
                 const uint32_t c = curt[crow0 + row * (CP / 4) + kk];
                 U = wave_sum_u32(__builtin_amdgcn_sad_u8(c, w, 0u));
             }
+            if (probe == 2) {          // timing probe: bounds + U, no survivor search
+                if (lane == 0 && U < keys[u]) keys[u] = U;
+                continue;
+            }
             // ---- 3. survivors: 16 LBq - 240 <= U, i.e. LBq < qU1 (one v_cmp per t) -----------
             const uint32_t qU = (U + 240) >> 4;
             const uint32_t qU1 = xok ? qU + 1 : 0u;            // dx-invalid lanes: nothing passes
@@ -756,33 +784,42 @@ me_sea_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int
                 }
             }
             if (nsur > (uint32_t)CAP) {
+                if (probe == 3) continue;   // timing probe: no dense fallback
                 wave_dense_block<16, false, RPD, CS>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u, tid, r);
                 continue;
             }
+            if (probe == 4) continue;       // timing probe: bounds, U and the survivor list only
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             uint64_t best = kNoKey;
-            if (nsur <= 4) {
-                // 16 lanes per survivor, one row each
+            if (nsur <= 8) {
+                // few survivors: four per pass, 16 lanes (one DPP row) per survivor, one block
+                // row per lane
                 const int sidx = lane >> 4, row = lane & 15;
-                const bool act = (uint32_t)sidx < nsur;
-                const int cand = act ? (int)mylist[sidx] : cs;
-                const int dxi = cand / 33, di = cand - dxi * 33;
-                const int col = bxl * 16 + dxi;
-                int wo = (col & 3) * CS + (byl * 16 + di + row) * RPD + (col >> 2);
-                asm volatile("" : "+v"(wo));
-                lds_vu32p wr_ = (lds_vu32p)(win + wo);       // 4-byte aligned only: keep b32 reads
                 const uint32_t* cr_ = curt + crow0 + row * (CP / 4);
-                uint32_t sad = 0;
-#pragma unroll
-                for (int kk = 0; kk < 4; ++kk) sad = __builtin_amdgcn_sad_u8(cr_[kk], wr_[kk], sad);
-                sad = row_sum_u32(sad);                        // 16 lanes = one DPP row
-                const int dx = dxi - 16, dy = di - 16;
-                const uint64_t key = me_key(sad, (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)), (uint32_t)r,
-                                            (uint32_t)cand);
-                best = act ? key : kNoKey;
+                const uint32_t c0 = cr_[0], c1 = cr_[1], c2 = cr_[2], c3 = cr_[3];
+#pragma unroll 1
+                for (uint32_t s0 = 0; s0 < nsur; s0 += 4) {
+                    const bool act = s0 + (uint32_t)sidx < nsur;
+                    const int cand = act ? (int)mylist[s0 + sidx] : cs;
+                    const int dxi = cand / 33, di = cand - dxi * 33;
+                    const int col = bxl * 16 + dxi;
+                    int wo = (col & 3) * CS + (byl * 16 + di + row) * RPD + (col >> 2);
+                    asm volatile("" : "+v"(wo));
+                    lds_vu32p wr_ = (lds_vu32p)(win + wo);   // 4-byte aligned only: keep b32 reads
+                    uint32_t sad = __builtin_amdgcn_sad_u8(c0, wr_[0], 0u);
+                    sad = __builtin_amdgcn_sad_u8(c1, wr_[1], sad);
+                    sad = __builtin_amdgcn_sad_u8(c2, wr_[2], sad);
+                    sad = __builtin_amdgcn_sad_u8(c3, wr_[3], sad);
+                    sad = row_sum_u32(sad);                    // 16 lanes = one DPP row
+                    const int dx = dxi - 16, dy = di - 16;
+                    const uint64_t key = me_key(sad, (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)),
+                                                (uint32_t)r, (uint32_t)cand);
+                    best = (act && key < best) ? key : best;
+                }
             } else {
+                // many: one survivor per lane, 64 at a time
 #pragma unroll 1
                 for (uint32_t k0 = 0; k0 < nsur; k0 += 64) {
                     const uint32_t idx = k0 + (uint32_t)lane;
@@ -799,6 +836,324 @@ me_sea_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int
                         for (int kk = 0; kk < 4; ++kk)
                             sad = __builtin_amdgcn_sad_u8(curt[crow0 + rr * (CP / 4) + kk], wp[rr * RPD + kk], sad);
                         asm volatile("" : "+v"(sad) : : "memory");
+                    }
+                    const int dx = dxi - 16, dy = di - 16;
+                    const uint64_t key = me_key(sad, (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)),
+                                                (uint32_t)r, (uint32_t)cand);
+                    best = (idx < nsur && key < best) ? key : best;
+                }
+            }
+            best = wave_min_u64_dpp(best);
+            if (lane == 0 && best < keys[u]) keys[u] = best;
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < G::NBLK; i += G::NTHREADS) {
+        const int gbx = bx0 + i % TBX, gby = byt0 + i / TBX;
+        if (gbx >= nbx || gby >= by1) continue;
+        decode_key(keys[i], SR, out_best + ((size_t)(gby - by0) * nbx + gbx) * 4);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// SEA, single-copy window (me_sea2_kernel, the default for bs 16 without VBS).
+//
+// Same exact successive elimination as me_sea_kernel (bound, U, survivors, fallback), with
+// the per-block overheads cut -- the old kernel spent 23 of its 66 us per 4K P-frame
+// staging and 17 us compacting survivors (tools/me_ab2.py timing probes):
+//   * ONE copy of the window in LDS (pitch 41 dwords: column walks are conflict free); the
+//     byte-shifted reads the search needs are two ds_read_b32 + v_alignbyte.  LDS per
+//     workgroup drops from 59 KB to 28 KB, so three workgroups (6 waves/SIMD) share a CU;
+//   * the window's loads are all issued before any LDS store;
+//   * the 4x4 byte sums are built by threads owning 4 adjacent columns and 6 output rows,
+//     all their LDS reads issued up front;
+//   * survivors are compacted with one LDS atomic per lane (its popcount) instead of a
+//     ballot per candidate row -- the list order is irrelevant, the key decides;
+//   * more than CAP survivors: every valid candidate's SAD, one per lane (no dense kernel).
+// ---------------------------------------------------------------------------------------
+struct Sea2Geo {
+    static constexpr int SR = 16, NT = 17;
+    static constexpr int TBX = 8, TPY = 32, TBY = 2, TPX = 128;
+    static constexpr int WR = TPY + 2 * SR;               // 64 window rows
+    static constexpr int WD = (TPX + 2 * SR) / 4;         // 40 data dwords per row
+    static constexpr int RP = WD + 1;                     // pitch 41
+    static constexpr int B4R = WR - 3, B4C = TPX + 2 * SR - 3, B4P = 160;
+    static constexpr int B4BAND = 6, B4NB = (B4R + B4BAND - 1) / B4BAND;   // 11 bands of output rows
+    static constexpr int NBLK = TBX * TBY;
+    static constexpr int NW = 8, NTHREADS = NW * 64;
+    static constexpr int CAP = 192;
+};
+
+// 4 bytes of window row `row` starting at byte column `col` (single copy, pitch RP dwords)
+template <int RP>
+SO_DEV uint32_t win_u32(const uint32_t* win, int row, int col) {
+    lds_vu32p p = (lds_vu32p)(win + row * RP + (col >> 2));
+    return __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)(col & 3));
+}
+
+__global__ void __launch_bounds__(Sea2Geo::NTHREADS) __attribute__((amdgpu_waves_per_eu(6)))
+me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
+               int32_t* __restrict__ out_best, int probe) {
+    using G = Sea2Geo;
+    constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RP = G::RP, NT = G::NT;
+    constexpr int B4P = G::B4P, CAP = G::CAP, CP = G::TPX;
+    __shared__ uint32_t win[G::WR * RP + 4];
+    __shared__ uint32_t b4w[(G::B4R * B4P + 4) / 4];
+    uint8_t* b4 = reinterpret_cast<uint8_t*>(b4w);
+    __shared__ uint32_t curt[G::TPY * CP / 4];      // current tile, 32 rows x 128 B
+    __shared__ uint32_t a4[G::NBLK * 4];           // per block: [j] = 4 byte sums (4x4 >> 4) of row j
+    __shared__ uint16_t list[G::NW * CAP];
+    __shared__ uint32_t lcount[G::NW];
+    __shared__ unsigned long long keys[G::NBLK];
+
+    const int nbx = W / 16;
+    const int tiles_x = (nbx + TBX - 1) / TBX;
+    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    const int bx0 = tx * TBX, byt0 = by0 + ty * TBY;
+    const int x0 = bx0 * 16, y0 = byt0 * 16;
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    for (int i = tid; i < G::NBLK; i += G::NTHREADS) keys[i] = kNoKey;
+    {   // current tile (zero outside the frame / stripe)
+        constexpr int N = G::TPY * CP / 4, IT = (N + G::NTHREADS - 1) / G::NTHREADS;
+        uint32_t v[IT];
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            const int i = tid + k * G::NTHREADS;
+            const int rr = i / (CP / 4), m = i - rr * (CP / 4);
+            const int gy = y0 + rr, gx = x0 + 4 * m;
+            v[k] = 0;
+            if (i < N && gy < H && gx + 4 <= W) v[k] = *reinterpret_cast<const uint32_t*>(cur + (size_t)gy * W + gx);
+        }
+#pragma unroll
+        for (int k = 0; k < IT; ++k)
+            if (tid + k * G::NTHREADS < N) curt[tid + k * G::NTHREADS] = v[k];
+    }
+    __syncthreads();
+    for (int i = tid; i < G::NBLK * 16; i += G::NTHREADS) {   // (block, j, ii) -> byte ii of a4[blk*4 + j]
+        const int blk = i >> 4, j = (i >> 2) & 3, ii = i & 3;
+        const int rr = (blk / TBX) * 16 + 4 * j, m = (blk % TBX) * 4 + ii;
+        uint32_t sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sum = __builtin_amdgcn_sad_u8(curt[(rr + q) * (CP / 4) + m], 0u, sum);
+        reinterpret_cast<uint8_t*>(a4)[i] = (uint8_t)(sum >> 4);
+    }
+    for (int r = 0; r < nref; ++r) {
+        const uint8_t* ref = refs.p[r];
+        __syncthreads();
+        {   // window: all loads first, then the LDS stores
+            constexpr int N = G::WR * RP, IT = (N + G::NTHREADS - 1) / G::NTHREADS;
+            uint32_t v[IT];
+#pragma unroll
+            for (int k = 0; k < IT; ++k) {
+                const int i = tid + k * G::NTHREADS;
+                const int wr = i / RP, m = i - wr * RP;
+                const int gy = y0 - SR + wr, gx = x0 - SR + 4 * m;
+                v[k] = 0;
+                if (i < N && gy >= 0 && gy < H && gx >= 0 && gx + 4 <= W)
+                    v[k] = *reinterpret_cast<const uint32_t*>(ref + (size_t)gy * W + gx);
+            }
+#pragma unroll
+            for (int k = 0; k < IT; ++k)
+                if (tid + k * G::NTHREADS < N) win[tid + k * G::NTHREADS] = v[k];
+        }
+        __syncthreads();
+        // 4x4 byte sums B4(row, c) = (sum of the 4x4 window block at (row, c)) >> 4, stored at
+        // b4[row * B4P + (c & 3) * 40 + (c >> 2)] (a candidate's four sums of one 4x4 row --
+        // columns c, c+4, c+8, c+12 -- are then consecutive bytes).  Thread = (dword column m:
+        // columns 4m..4m+3, band of B4BAND output rows).
+        if (tid < G::WD * G::B4NB) {
+            const int m = tid % G::WD, band = tid / G::WD;
+            const int r0 = band * G::B4BAND;
+            constexpr int NR = G::B4BAND + 3;
+            uint32_t h[NR][4];
+#pragma unroll
+            for (int i = 0; i < NR; ++i) {
+                const int row = r0 + i < G::WR ? r0 + i : G::WR - 1;
+                lds_vu32p p = (lds_vu32p)(win + row * RP + m);
+                const uint32_t w0 = p[0], w1 = p[1];
+                h[i][0] = __builtin_amdgcn_sad_u8(w0, 0u, 0u);
+                h[i][1] = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w1, w0, 1), 0u, 0u);
+                h[i][2] = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w1, w0, 2), 0u, 0u);
+                h[i][3] = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w1, w0, 3), 0u, 0u);
+            }
+#pragma unroll
+            for (int i = 0; i < G::B4BAND; ++i) {
+                const int orow = r0 + i;
+                if (orow < G::B4R) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (4 * m + k < G::B4C)
+                            b4[orow * B4P + k * 40 + m] = (uint8_t)((h[i][k] + h[i + 1][k] + h[i + 2][k] + h[i + 3][k]) >> 4);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (probe == 1) continue;   // timing probe (tools/me_ab2.py): staging + byte sums only
+#pragma unroll 1
+        for (int u = wave; u < G::NBLK; u += G::NW) {
+            const int bxl = u % TBX, byl = u / TBX;
+            if (bx0 + bxl >= nbx || byt0 + byl >= by1) continue;   // wave-uniform
+            const int x = x0 + bxl * 16, y = y0 + byl * 16;
+            int lane = tid & 63;
+            asm volatile("" : "+v"(lane));
+            const int xi = lane & 31, hh = lane >> 5;
+            const int d2 = lane < 33 ? lane : 32;
+            uint32_t A[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) A[j] = a4[u * 4 + j];
+            // ---- 1. lower bounds (as me_sea_kernel) ------------------------------------------
+            const int cB = bxl * 16 + xi;
+            const int lb0 = (byl * 16 + 16 * hh) * B4P + (cB & 3) * 40 + (cB >> 2);   // byte offset
+            const uint32_t bsh = (uint32_t)lb0 & 3;
+            int lo1 = lb0 >> 2;
+            asm volatile("" : "+v"(lo1));
+            lds_vu32p p1 = (lds_vu32p)(b4w + lo1);
+            uint32_t lb[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) lb[t] = 0;
+            uint32_t n0 = p1[0], n1 = p1[1];
+#pragma unroll
+            for (int sr_ = 0; sr_ < NT + 12; ++sr_) {
+                const uint32_t w0 = n0, w1 = n1;
+                if (sr_ + 1 < NT + 12) { n0 = p1[(sr_ + 1) * (B4P / 4)]; n1 = p1[(sr_ + 1) * (B4P / 4) + 1]; }
+                const uint32_t P = __builtin_amdgcn_alignbyte(w1, w0, bsh);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int t = sr_ - 4 * j;
+                    if (t >= 0 && t < NT) lb[t] = __builtin_amdgcn_sad_u8(A[j], P, lb[t]);
+                }
+                acc_fence_n<NT>(lb);
+            }
+            uint32_t lb2 = 0;
+            {
+                int lo2 = ((byl * 16 + d2) * B4P + ((bxl * 16 + 32) >> 2)) >> 2;
+                asm volatile("" : "+v"(lo2));
+                lds_vu32p p2 = (lds_vu32p)(b4w + lo2);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) lb2 = __builtin_amdgcn_sad_u8(A[j], p2[4 * j * (B4P / 4)], lb2);
+            }
+            constexpr uint32_t kBig = 0x07FFFFFFu;
+            int dlo = SR - y;              dlo = dlo < 0 ? 0 : dlo;
+            int dhi = H - 16 - y + SR - 1; dhi = dhi > 32 ? 32 : dhi;
+            const bool xok = (x + xi - 16 >= 0) && (x + xi - 16 < W - 16);
+            const bool x2ok = x + 16 < W - 16;
+            const bool ok2 = lane < 33 && x2ok && d2 >= dlo && d2 <= dhi;
+            if (dlo > 0 || dhi < 32) {
+                const int tlo = dlo - 16 * hh, thi = dhi - 16 * hh;
+#pragma unroll
+                for (int t = 0; t < NT; ++t) lb[t] = (t < tlo || t > thi) ? kBig : lb[t];
+            }
+            // ---- 2. U = SAD of the smallest-bound candidate ----------------------------------
+            uint32_t kt = 0xFFFFFFFFu;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const uint32_t k = (lb[t] << 5) | (uint32_t)t;
+                kt = k < kt ? k : kt;
+            }
+            uint32_t kl = (xok && (kt >> 5) != kBig) ? ((kt >> 5) << 11) | (uint32_t)(xi * 33 + 16 * hh + (kt & 31))
+                                                      : 0xFFFFFFFFu;
+            {
+                const uint32_t k2 = (lb2 << 11) | (uint32_t)(32 * 33 + d2);
+                kl = (ok2 && k2 < kl) ? k2 : kl;
+            }
+            const uint32_t kmin = wave_min_u32(kl);
+            if (kmin == 0xFFFFFFFFu) continue;                 // no valid candidate: key stays none
+            const int cs = (int)(kmin & 2047), cdx = cs / 33, cdi = cs - cdx * 33;
+            const int crow0 = byl * 16 * (CP / 4) + bxl * 4;   // current block in curt (dwords)
+            uint32_t U;
+            {
+                const int row = lane >> 2, kk = lane & 3;
+                const uint32_t w = win_u32<RP>(win, byl * 16 + cdi + row, bxl * 16 + cdx + 4 * kk);
+                U = wave_sum_u32(__builtin_amdgcn_sad_u8(curt[crow0 + row * (CP / 4) + kk], w, 0u));
+            }
+            if (probe == 2) {
+                if (lane == 0 && U < keys[u]) keys[u] = U;
+                continue;
+            }
+            // ---- 3. survivors: 16 LBq - 240 <= U, i.e. LBq < qU1 ------------------------------
+            const uint32_t qU = (U + 240) >> 4;
+            const uint32_t qU1 = xok ? qU + 1 : 0u;            // dx-invalid lanes: nothing passes
+            uint32_t msk = (ok2 && lb2 <= qU) ? (1u << NT) : 0u;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) msk |= (lb[t] < qU1 ? 1u : 0u) << t;
+            const uint32_t nmine = (uint32_t)__builtin_popcount(msk);
+            const uint32_t nsur = wave_sum_u32(nmine);
+            uint16_t* mylist = list + wave * CAP;
+            if (nsur > (uint32_t)CAP) {
+                if (probe == 3) continue;
+                // fallback: the dense wave search on the single-copy window
+                wave_dense_block<16, false, RP, 0, false, true>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u, tid,
+                                                                r);
+                continue;
+            }
+            if (probe == 4) continue;
+            // compaction: one LDS atomic per lane reserves its slots (the order is irrelevant:
+            // the packed key decides, ties included)
+            if (lane == 0) lcount[wave] = 0;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (nmine) {
+                uint32_t pos = atomicAdd(&lcount[wave], nmine);
+                uint32_t mm = msk;
+                while (mm) {
+                    const int t = __builtin_ctz(mm);
+                    mm &= mm - 1;
+                    mylist[pos++] = (uint16_t)(t < NT ? xi * 33 + 16 * hh + t : 32 * 33 + d2);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint64_t best = kNoKey;
+            if (nsur <= 8) {
+                // four survivors per pass: 16 lanes (one DPP row) per survivor, a row per lane
+                const int sidx = lane >> 4, row = lane & 15;
+                const uint32_t* cr_ = curt + crow0 + row * (CP / 4);
+                const uint32_t c0 = cr_[0], c1 = cr_[1], c2 = cr_[2], c3 = cr_[3];
+#pragma unroll 1
+                for (uint32_t s0 = 0; s0 < nsur; s0 += 4) {
+                    const bool act = s0 + (uint32_t)sidx < nsur;
+                    const int cand = act ? (int)mylist[s0 + sidx] : cs;
+                    const int dxi = cand / 33, di = cand - dxi * 33;
+                    const int col = bxl * 16 + dxi;
+                    int wo = (byl * 16 + di + row) * RP + (col >> 2);
+                    asm volatile("" : "+v"(wo));
+                    lds_vu32p p = (lds_vu32p)(win + wo);
+                    const uint32_t sh = (uint32_t)(col & 3);
+                    const uint32_t q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4];
+                    uint32_t sad = __builtin_amdgcn_sad_u8(c0, __builtin_amdgcn_alignbyte(q1, q0, sh), 0u);
+                    sad = __builtin_amdgcn_sad_u8(c1, __builtin_amdgcn_alignbyte(q2, q1, sh), sad);
+                    sad = __builtin_amdgcn_sad_u8(c2, __builtin_amdgcn_alignbyte(q3, q2, sh), sad);
+                    sad = __builtin_amdgcn_sad_u8(c3, __builtin_amdgcn_alignbyte(q4, q3, sh), sad);
+                    sad = row_sum_u32(sad);
+                    const int dx = dxi - 16, dy = di - 16;
+                    const uint64_t key = me_key(sad, (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)),
+                                                (uint32_t)r, (uint32_t)cand);
+                    best = (act && key < best) ? key : best;
+                }
+            } else {
+                // one survivor per lane, 64 at a time
+#pragma unroll 1
+                for (uint32_t k0 = 0; k0 < nsur; k0 += 64) {
+                    const uint32_t idx = k0 + (uint32_t)lane;
+                    const int cand = idx < nsur ? (int)mylist[idx] : cs;
+                    const int dxi = cand / 33, di = cand - dxi * 33;
+                    const int col = bxl * 16 + dxi;
+                    const uint32_t sh = (uint32_t)(col & 3);
+                    uint32_t sad = 0;
+#pragma unroll
+                    for (int rr = 0; rr < 16; ++rr) {
+                        lds_vu32p p = (lds_vu32p)(win + (byl * 16 + di + rr) * RP + (col >> 2));
+                        const uint32_t q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4];
+                        const uint32_t* cr_ = curt + crow0 + rr * (CP / 4);
+                        sad = __builtin_amdgcn_sad_u8(cr_[0], __builtin_amdgcn_alignbyte(q1, q0, sh), sad);
+                        sad = __builtin_amdgcn_sad_u8(cr_[1], __builtin_amdgcn_alignbyte(q2, q1, sh), sad);
+                        sad = __builtin_amdgcn_sad_u8(cr_[2], __builtin_amdgcn_alignbyte(q3, q2, sh), sad);
+                        sad = __builtin_amdgcn_sad_u8(cr_[3], __builtin_amdgcn_alignbyte(q4, q3, sh), sad);
                     }
                     const int dx = dxi - 16, dy = di - 16;
                     const uint64_t key = me_key(sad, (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)),
@@ -1033,9 +1388,15 @@ int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, in
         const bool use_dense = impl && strcmp(impl, "dense") == 0;
         if (!use_fast && !use_dense && bs == 16 && out_sub == nullptr) {
             const dim3 sgrid(((nbx + SeaGeo::TBX - 1) / SeaGeo::TBX) * ((nrows + SeaGeo::TBY - 1) / SeaGeo::TBY));
-            hipLaunchKernelGGL(me_sea_kernel, sgrid, dim3(SeaGeo::NTHREADS), 0, st, cur, refs, nref, H, W, by0, by1,
-                               out_best);
-            return check_launch("me_sea_kernel");
+            const char* pr = getenv("SO_SEA_PROBE");   // timing probes only (tools/me_ab2.py)
+            if (impl && strcmp(impl, "sea1") == 0) {   // previous SEA kernel, A/B only
+                hipLaunchKernelGGL(me_sea_kernel, sgrid, dim3(SeaGeo::NTHREADS), 0, st, cur, refs, nref, H, W, by0,
+                                   by1, out_best, pr ? atoi(pr) : 0);
+                return check_launch("me_sea_kernel");
+            }
+            hipLaunchKernelGGL(me_sea2_kernel, sgrid, dim3(Sea2Geo::NTHREADS), 0, st, cur, refs, nref, H, W, by0, by1,
+                               out_best, pr ? atoi(pr) : 0);
+            return check_launch("me_sea2_kernel");
         }
         const int tb = bs == 16 ? MeGeo<16>::TB : MeGeo<8>::TB;
         const dim3 grid(((nbx + tb - 1) / tb) * ((nrows + tb - 1) / tb)), blk(MeGeo<16>::NTHREADS);
