@@ -236,24 +236,35 @@ SO_DEV void dequant_row(const int* q, int row, int qp, int* d) {
 
 // Token count of an N x N block (N lanes, lane l owns row l) = nnz + number of maximal
 // runs in anti-diagonal scan order (entropy_encoder_block emits one token per zero run,
-// one count token per non-zero run, and one token per non-zero value).
-// flags: N*N bytes of LDS owned by the group.
+// one count token per non-zero run, and one token per non-zero value), i.e.
+// nnz + 1 + (number of consecutive scan pairs whose zero/non-zero flags differ).
+// With M_i = the row-i non-zero bitmask, the 255 consecutive pairs are
+//   inside diagonals:  (i, j) -> (i+1, j-1), j >= 1, i <= N-2  -> M_i bits 1..N-1 against
+//                      M_{i+1} << 1, one XOR + popcount per lane (M_{i+1} by DPP row_shl:1);
+//   across diagonals:  end (k, 0) -> start (0, k+1) for k <= N-2 (lane k: M_k bit 0 vs
+//                      M_0 bit k+1) and end (N-1, k-N+1) -> start (k-N+2, N-1) for k >= N-1
+//                      (lane m = k-N+2 >= 1: M_{N-1} bit m-1 vs M_m bit N-1).
+// Registers only: no LDS, no barrier.  `flags` is unused (kept for the call sites).
 template <int N>
 SO_DEV int block_tokens(uint8_t* flags, int l, const int* q) {
+    (void)flags;
+    uint32_t m = 0;
 #pragma unroll
-    for (int c = 0; c < N; ++c) flags[scan_index(N, l, c)] = q[c] != 0;
-    wave_sync();
-    int nnz = 0, tr = 0;
-    int prev = flags[l == 0 ? 0 : l * N - 1];
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
-        const int f = flags[l * N + k];
-        nnz += f;
-        tr += (f != prev);
-        prev = f;
+    for (int c = 0; c < N; ++c) m |= (q[c] != 0 ? 1u : 0u) << c;
+    // M_{l+1}: DPP row_shl:1 (lane i reads lane i+1 of its 16-lane row; the value from
+    // the next group at the group's last lane is never used: i = N-1 has no pair)
+    const uint32_t mn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x101, 0xF, 0xF, false);
+    const int base = (threadIdx.x & 63) & ~(N - 1);
+    const uint32_t m0 = (uint32_t)__shfl((int)m, base, 64);
+    const uint32_t mlast = (uint32_t)__shfl((int)m, base + N - 1, 64);
+    constexpr uint32_t kInner = ((1u << N) - 1) & ~1u;
+    int tr = 0;
+    if (l <= N - 2) {
+        tr += __builtin_popcount((m ^ (mn << 1)) & kInner);
+        tr += (int)((m & 1u) ^ ((m0 >> (l + 1)) & 1u));
     }
-    wave_sync();
-    return group_sum<N>(nnz + tr) + 1;
+    if (l >= 1) tr += (int)(((mlast >> (l - 1)) & 1u) ^ ((m >> (N - 1)) & 1u));
+    return group_sum<N>(__builtin_popcount(m) + tr) + 1;
 }
 
 // Token counts of the four 8x8 sub-blocks (16 lanes, lane l owns sub j = l>>2, rows

@@ -2,7 +2,7 @@
 import csv, glob, os, sys
 from collections import defaultdict
 base, tag = sys.argv[1], sys.argv[2]
-for impl in ("sea", "dense", "wave", "tile", "fast"):
+for impl in ("sea", "sea2", "sea1", "dense", "wave", "tile", "fast"):
     c = defaultdict(list)
     for f in glob.glob(os.path.join(base, f"{tag}_{impl}_p*", "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
