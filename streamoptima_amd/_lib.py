@@ -75,7 +75,7 @@ def load(path: str | None = None):
     with _lock:
         if _lib is not None:
             return _lib
-        p = path or LIB_PATH
+        p = path or os.environ.get("SO_LIB_PATH") or LIB_PATH   # SO_LIB_PATH: A/B builds (tools/)
         if not os.path.exists(p):
             raise HipPathError(
                 f"{p} is missing: build it with `python -m streamoptima_amd.build` (hipcc, gfx950). "

@@ -377,6 +377,115 @@ intra_recon_kernel(int H, int W, int by0, const uint8_t* __restrict__ split, con
     }
 }
 
+// Sequential form of the same recurrence (default): value(p) = res(p) + (src(p) < x ?
+// value(src(p)) : 128), and src(p) >= x - sr, so walking a pixel row block by block left to
+// right needs only the last sr pixels.  BS lanes own one row (lane = column c of the
+// current block), a wave walks 64/BS rows side by side; a 128-entry LDS ring per row holds
+// the values already produced (sr <= 64, so x - src <= 64 + BS - 1 < 128 never aliases the
+// block being written).  nbx dependent steps of one LDS round trip each, instead of the
+// pointer-jumping kernel's log2(nbx) passes over the whole row with a barrier each.
+template <int BS, bool NEAR>
+__global__ void __launch_bounds__(256)
+intra_recon_seq_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict__ split, const int16_t* __restrict__ mv,
+                       const int32_t* __restrict__ idres, const uint8_t* __restrict__ cur,
+                       uint8_t* __restrict__ out_recon, int32_t* __restrict__ out_sse) {
+    constexpr int SB = BS / 2, RPW = 64 / BS, RING = 128;
+    __shared__ int ring[4 * RPW][RING];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int g = lane / BS, c = lane - g * BS;            // row group, column within the block
+    const int yl = (blockIdx.x * 4 + wv) * RPW + g;        // stripe-local pixel row
+    const bool act = yl < nrows_px;
+    const int ylc = act ? yl : nrows_px - 1;
+    const int yy = by0 * BS + ylc, byl = ylc / BS, i = ylc - byl * BS, nbx = W / BS;
+    int* rg = ring[wv * RPW + g];
+    const bool right = c >= SB, lower = i >= SB;
+    int sse = 0;
+    const uint8_t* crow = cur ? cur + (size_t)yy * W : nullptr;
+    uint8_t* orow = out_recon + (size_t)yy * W;
+    // the residuals and motion vectors of the next CH blocks are loaded while the current
+    // CH blocks walk the chain (their loads do not depend on it)
+    constexpr int CH = 8;
+    int resn[CH], dxn[CH], curn[CH];
+    auto fetch = [&](int bx0, int (&rs)[CH], int (&dv)[CH], int (&cv)[CH]) {
+#pragma unroll
+        for (int s = 0; s < CH; ++s) {
+            const int bx = bx0 + s < nbx ? bx0 + s : nbx - 1;
+            const int b = byl * nbx + bx;
+            rs[s] = idres[(size_t)b * BS * BS + i * BS + c];
+            cv[s] = crow ? (int)crow[bx * BS + c] : 0;
+            const uint2 m4 = *reinterpret_cast<const uint2*>(mv + (size_t)b * 4);
+            const int jj = split[b] ? (lower * 2 + right) : 0;
+            const uint32_t w = jj < 2 ? m4.x : m4.y;
+            dv[s] = (int)(int16_t)((jj & 1) ? (w >> 16) : (w & 0xFFFF));
+        }
+    };
+    fetch(0, resn, dxn, curn);
+    volatile int* vr = rg;   // one wave: LDS ops retire in order; volatile keeps their order
+    int pv = 0;              // NEAR: this lane's value in the previous block
+    for (int bx0 = 0; bx0 < nbx; bx0 += CH) {
+        int resc[CH], dxc[CH], curc[CH];
+#pragma unroll
+        for (int s = 0; s < CH; ++s) { resc[s] = resn[s]; dxc[s] = dxn[s]; curc[s] = curn[s]; }
+        if (bx0 + CH < nbx) fetch(bx0 + CH, resn, dxn, curn);
+#pragma unroll
+        for (int s = 0; s < CH; ++s) {
+            const int bx = bx0 + s;
+            if (bx < nbx) {                                    // wave-uniform
+                const int x = bx * BS;
+                int v = resc[s] + 128;
+                const int src = x + c + dxc[s];
+                if constexpr (NEAR) {
+                    // sr <= BS: every source is in the previous block, whose values the
+                    // group's lanes still hold -- one ds_bpermute, no LDS round trip
+                    const int idx = src - x + BS;        // in [0, BS) when src < x
+                    const int pvv = __shfl(pv, (lane & ~(BS - 1)) + (idx & (BS - 1)), 64);
+                    if (x != 0 && src < x) v = resc[s] + pvv;
+                    pv = v;
+                } else {
+                    if (x != 0 && src < x) v = resc[s] + vr[src & (RING - 1)];
+                    vr[(x + c) & (RING - 1)] = v;
+                }
+                const int o = v & 255;
+                if (act) {
+                    orow[x + c] = (uint8_t)o;
+                    const int d = curc[s] - o;
+                    sse += d * d;
+                }
+            }
+        }
+    }
+    if (out_sse) {
+#pragma unroll
+        for (int m = BS / 2; m >= 1; m >>= 1) sse += __shfl_xor(sse, m, 64);
+        if (act && c == 0) out_sse[yl] = sse;
+    }
+}
+
+// rows [0, nrows_px) of the stripe starting at block row by0: sequential kernel for sr <= 64
+static int intra_recon_rows(int W, int bs, int sr, int by0, int nrows_px, const uint8_t* split, const int16_t* mv,
+                            const int32_t* idres, const uint8_t* cur, uint8_t* out_recon, int32_t* out_sse, int H,
+                            hipStream_t st) {
+    if (nrows_px <= 0) return SO_OK;
+    if (sr <= 64) {
+        const int rows_per_blk = 4 * (64 / bs);
+        const dim3 grid((nrows_px + rows_per_blk - 1) / rows_per_blk);
+#define SO_IRS(B, N)                                                                                              \
+    hipLaunchKernelGGL((intra_recon_seq_kernel<B, N>), grid, dim3(256), 0, st, W, nrows_px, by0, split, mv, idres, \
+                       cur, out_recon, out_sse)
+        if (bs == 16) { if (sr <= 16) SO_IRS(16, true); else SO_IRS(16, false); }
+        else { if (sr <= 8) SO_IRS(8, true); else SO_IRS(8, false); }
+#undef SO_IRS
+        return check_launch("intra_recon_seq_kernel");
+    }
+    if (bs == 16)
+        hipLaunchKernelGGL((intra_recon_kernel<16>), dim3(nrows_px), dim3(256), 12 * (size_t)W, st, H, W, by0, split,
+                           mv, idres, cur, out_recon, out_sse);
+    else
+        hipLaunchKernelGGL((intra_recon_kernel<8>), dim3(nrows_px), dim3(256), 12 * (size_t)W, st, H, W, by0, split,
+                           mv, idres, cur, out_recon, out_sse);
+    return check_launch("intra_recon_kernel");
+}
+
 int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int by0, int by1, int qp_rd,
                         const int32_t* qp_row, const int32_t* qp_map, int vbs, double lam, uint8_t* out_split, int16_t* out_mv,
                         int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon,
@@ -400,13 +509,7 @@ int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int by
                            out_split, out_mv, out_qtc, out_tokens, out_mae, idres);
     int rc = check_launch("intra_tq_kernel");
     if (rc) return rc;
-    if (bs == 16)
-        hipLaunchKernelGGL((intra_recon_kernel<16>), dim3(nrows * bs), dim3(256), 12 * (size_t)W, st, H, W, by0, out_split,
-                           out_mv, idres, cur, out_recon, out_sse);
-    else
-        hipLaunchKernelGGL((intra_recon_kernel<8>), dim3(nrows * bs), dim3(256), 12 * (size_t)W, st, H, W, by0, out_split,
-                           out_mv, idres, cur, out_recon, out_sse);
-    return check_launch("intra_recon_kernel");
+    return intra_recon_rows(W, bs, sr, by0, nrows * bs, out_split, out_mv, idres, cur, out_recon, out_sse, H, st);
 }
 
 int intra_recon_launch(int H, int W, int bs, int sr, int qp, const int32_t* qp_row, const int32_t* qp_map,
@@ -424,13 +527,7 @@ int intra_recon_launch(int H, int W, int bs, int sr, int qp, const int32_t* qp_r
                            idres);
     int rc = check_launch("dequant_idct_kernel");
     if (rc) return rc;
-    if (bs == 16)
-        hipLaunchKernelGGL((intra_recon_kernel<16>), dim3(H), dim3(256), 12 * (size_t)W, st, H, W, 0, split, mv, idres,
-                           nullptr, out_recon, nullptr);
-    else
-        hipLaunchKernelGGL((intra_recon_kernel<8>), dim3(H), dim3(256), 12 * (size_t)W, st, H, W, 0, split, mv, idres,
-                           nullptr, out_recon, nullptr);
-    return check_launch("intra_recon_kernel");
+    return intra_recon_rows(W, bs, sr, 0, H, split, mv, idres, nullptr, out_recon, nullptr, H, st);
 }
 
 }  // namespace so

@@ -871,6 +871,9 @@ me_sea_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int
 //     ballot per candidate row -- the list order is irrelevant, the key decides;
 //   * more than CAP survivors: every valid candidate's SAD, one per lane (no dense kernel).
 // ---------------------------------------------------------------------------------------
+#ifndef SO_SEA2_WPE
+#define SO_SEA2_WPE 6
+#endif
 struct Sea2Geo {
     static constexpr int SR = 16, NT = 17;
     static constexpr int TBX = 8, TPY = 32, TBY = 2, TPX = 128;
@@ -891,7 +894,7 @@ SO_DEV uint32_t win_u32(const uint32_t* win, int row, int col) {
     return __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)(col & 3));
 }
 
-__global__ void __launch_bounds__(Sea2Geo::NTHREADS) __attribute__((amdgpu_waves_per_eu(6)))
+__global__ void __launch_bounds__(Sea2Geo::NTHREADS) __attribute__((amdgpu_waves_per_eu(SO_SEA2_WPE)))
 me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
                int32_t* __restrict__ out_best, int probe) {
     using G = Sea2Geo;
