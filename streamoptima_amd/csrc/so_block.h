@@ -164,8 +164,8 @@ SO_DEV void load_row_i16(const int16_t* __restrict__ p, int* v) {
 // ---- 2-D transforms through LDS --------------------------------------------------------------
 // N x N transform of one block by N lanes (lane l owns row l on input and output).
 // lds: N rows of pitch N+1 doubles owned by this lane group.
-template <int N, bool INVERSE>
-SO_DEV void xform2d_rows(double* lds, int l, const int* in_row, double* out_row) {
+template <int N, bool INVERSE, class T>
+SO_DEV void xform2d_rows(double* lds, int l, const T* in_row, double* out_row) {
     constexpr int P = N + 1;
 #pragma unroll
     for (int c = 0; c < N; ++c) lds[l * P + c] = (double)in_row[c];
@@ -187,8 +187,8 @@ SO_DEV void xform2d_rows(double* lds, int l, const int* in_row, double* out_row)
 
 // Four 8x8 sub-blocks by 16 lanes: lane l owns sub-block j = l >> 2 and rows
 // (l & 3), (l & 3) + 4 on input and output.  lds: 4 x 8 x 9 doubles.
-template <bool INVERSE>
-SO_DEV void xform2d_sub(double* lds, int l, const int (&in)[2][8], double (&out)[2][8]) {
+template <bool INVERSE, class T>
+SO_DEV void xform2d_sub(double* lds, int l, const T (&in)[2][8], double (&out)[2][8]) {
     const int j = l >> 2, r0 = l & 3;
     double* s = lds + j * 72;
 #pragma unroll
@@ -232,6 +232,48 @@ template <int N>
 SO_DEV void dequant_row(const int* q, int row, int qp, int* d) {
 #pragma unroll
     for (int c = 0; c < N; ++c) d[c] = q[c] * (1 << q_exp(row, c, N, qp));
+}
+
+// The same two steps on FP64 carriers, branch-free.  tcr = rint(DCT) (an integer-valued
+// double); ldexp by -k is exact and rint rounds half to even, so
+//   qd = rint(ldexp(tcr, -k)) == np.round(TC / 2^k)      (quantize_TC, Encoder.py:787-789)
+//   dq = ldexp(qd, k)          == QTC * Q                 (rescale_QTC, :820-821)
+// exactly, with k = qp + e(row + c) (generate_Q_matrix, :938-945) and
+// e(s) = med3(s - (N - 2), 0, 2): 0 above the anti-diagonal, 1 on it, 2 below.
+template <int N>
+SO_DEV int q_exp_fast(int row, int c, int qp) {
+    const int s = row + c - (N - 2);
+    return qp + (s < 0 ? 0 : (s > 2 ? 2 : s));
+}
+
+template <int N>
+SO_DEV void quant_row_d(const double* tcr, int row, int qp, double* qd, int* q) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) {
+        qd[c] = __builtin_rint(__builtin_amdgcn_ldexp(tcr[c], -q_exp_fast<N>(row, c, qp)));
+        q[c] = (int)qd[c];
+    }
+}
+
+template <int N>
+SO_DEV void dequant_row_d(const double* qd, int row, int qp, double* dq) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) dq[c] = __builtin_amdgcn_ldexp(qd[c], q_exp_fast<N>(row, c, qp));
+}
+
+// Integer-carrier forms (fewer live VGPRs where the state must survive the RD decision):
+// tc / q are exact int32 images of the integer-valued doubles.
+template <int N>
+SO_DEV void quant_row_i(const int* tc, int row, int qp, int* q) {
+#pragma unroll
+    for (int c = 0; c < N; ++c)
+        q[c] = (int)__builtin_rint(__builtin_amdgcn_ldexp((double)tc[c], -q_exp_fast<N>(row, c, qp)));
+}
+
+template <int N>
+SO_DEV void dequant_row_i(const int* q, int row, int qp, double* dq) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) dq[c] = __builtin_amdgcn_ldexp((double)q[c], q_exp_fast<N>(row, c, qp));
 }
 
 // Token count of an N x N block (N lanes, lane l owns row l) = nnz + number of maximal

@@ -50,12 +50,21 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, const uint8_t* __r
     load_cur_row<BS>(cur, W, x, y + l, crow);
 #pragma unroll
     for (int c = 0; c < BS; ++c) res[c] = crow[c] - pred[c];
-    double tcd[BS];
-    xform2d_rows<BS, false>(dl, l, res, tcd);
-    int tc[BS], q[BS];
+    double tcr[BS];
+    xform2d_rows<BS, false>(dl, l, res, tcr);
 #pragma unroll
-    for (int c = 0; c < BS; ++c) tc[c] = (int)__builtin_rint(tcd[c]);
-    quant_row<BS>(tc, l, qp_rd, q);
+    for (int c = 0; c < BS; ++c) tcr[c] = __builtin_rint(tcr[c]);
+    // Without VBS the RD QP is never used: quantise once at the block's final QP, FP64
+    // carriers throughout.  With VBS the state survives the RD decision as int32.
+    double qd[BS];
+    int q[BS], tc[BS];
+    if constexpr (VBS) {
+#pragma unroll
+        for (int c = 0; c < BS; ++c) tc[c] = (int)tcr[c];
+        quant_row_i<BS>(tc, l, qp_rd, q);
+    } else {
+        quant_row_d<BS>(tcr, l, qpr, qd, q);
+    }
 
     bool split = false;
     int mae_num = sad;
@@ -90,7 +99,7 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, const uint8_t* __r
             for (int h = 0; h < 2; ++h) {
 #pragma unroll
                 for (int c = 0; c < 8; ++c) stc[h][c] = (int)__builtin_rint(std_[h][c]);
-                quant_row<8>(stc[h], r0 + 4 * h, qpm1_rd, qs[h]);
+                quant_row_i<8>(stc[h], r0 + 4 * h, qpm1_rd, qs[h]);
             }
             const int tok_b = block_tokens<BS>(fl, l, q);
             const int tok_v = sub_tokens(fl, l, qs);
@@ -113,12 +122,13 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, const uint8_t* __r
 
     int tok, sse = 0;
     if (!split) {
-        if (qpr != qp_rd) quant_row<BS>(tc, l, qpr, q);
+        if (VBS && qpr != qp_rd) quant_row_i<BS>(tc, l, qpr, q);
         tok = block_tokens<BS>(fl, l, q);
         store_row_i16<BS>(out_qtc + (size_t)b * BS * BS + l * BS, q);
-        int dq[BS], rec[BS];
-        dequant_row<BS>(q, l, qpr, dq);
-        double rd[BS];
+        int rec[BS];
+        double dq[BS], rd[BS];
+        if constexpr (VBS) dequant_row_i<BS>(q, l, qpr, dq);
+        else dequant_row_d<BS>(qd, l, qpr, dq);
         xform2d_rows<BS, true>(dl, l, dq, rd);
 #pragma unroll
         for (int c = 0; c < BS; ++c) rec[c] = pred[c] + (int)__builtin_rint(rd[c]);
@@ -136,13 +146,13 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, const uint8_t* __r
             const int qpm1_rd = qp_rd > 0 ? qp_rd - 1 : qp_rd;
             if (qpm1 != qpm1_rd)
 #pragma unroll
-                for (int h = 0; h < 2; ++h) quant_row<8>(stc[h], r0 + 4 * h, qpm1, qs[h]);
+                for (int h = 0; h < 2; ++h) quant_row_i<8>(stc[h], r0 + 4 * h, qpm1, qs[h]);
             tok = sub_tokens(fl, l, qs);
-            int sdq[2][8];
+            double sdq[2][8];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 store_row_i16<8>(out_qtc + (size_t)b * BS * BS + j * 64 + (r0 + 4 * h) * 8, qs[h]);
-                dequant_row<8>(qs[h], r0 + 4 * h, qpm1, sdq[h]);
+                dequant_row_i<8>(qs[h], r0 + 4 * h, qpm1, sdq[h]);
             }
             double srd[2][8];
             xform2d_sub<true>(dl, l, sdq, srd);
