@@ -48,14 +48,18 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, out: str | None = None, defines: tuple = ()) -> str:
+    """Build the library in-tree.  `out` + `defines` make an A/B or instrumented variant
+    (tools/: e.g. -DSO_STAMPS) at another path; the product library is always LIB_PATH."""
+    target = out or LIB_PATH
+    if out is None and not defines and not force and not _stale():
         return LIB_PATH
     tlib = _torch_lib_dir()
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
+           *[f"-D{d}" for d in defines],
            "-I", os.path.join(os.path.dirname(PKG), "include"),
-           "-o", LIB_PATH + ".tmp", *sources(),
+           "-o", target + ".tmp", *sources(),
            f"-L{tlib}", "-lamdhip64", f"-Wl,-rpath,{tlib}"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
@@ -64,9 +68,15 @@ def build(force: bool = False, verbose: bool = False) -> str:
         raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-6000:]}")
     if verbose and r.stderr:
         print(r.stderr[-4000:], file=sys.stderr)
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+    os.replace(target + ".tmp", target)
+    return target
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--out", default=None, help="variant library path (A/B, instrumented)")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="extra preprocessor define")
+    a = ap.parse_args()
+    print(build(force=a.force, verbose=True, out=a.out, defines=tuple(a.defines)))

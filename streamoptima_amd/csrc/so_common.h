@@ -5,7 +5,9 @@
 
 #include "../../include/streamoptima.h"
 
+#ifndef SO_DEV
 #define SO_DEV __device__ __forceinline__
+#endif
 
 namespace so {
 

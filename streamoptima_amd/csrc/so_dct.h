@@ -171,10 +171,13 @@ SO_DEV void radb4(const double* cc, double* ch) {
     for (int k = 0; k < L1; k++) {
         double tr1, tr2;
         SO_PM(tr2, tr1, CC(0, 0, k), CC(IDO - 1, 3, k));
-        double tr3 = 2.0 * CC(IDO - 1, 1, k);
-        double tr4 = 2.0 * CC(0, 2, k);
-        SO_PM(CH(0, k, 0), CH(0, k, 2), tr2, tr3);
-        SO_PM(CH(0, k, 3), CH(0, k, 1), tr1, tr4);
+        // tr3 = 2 x, tr4 = 2 z and then tr2 +- tr3, tr1 +- tr4: 2x is exact, so
+        // fma(+-2, x, tr2) rounds once, exactly like tr2 +- fl(2x)
+        const double x = CC(IDO - 1, 1, k), z = CC(0, 2, k);
+        CH(0, k, 0) = __builtin_fma(2.0, x, tr2);
+        CH(0, k, 2) = __builtin_fma(-2.0, x, tr2);
+        CH(0, k, 3) = __builtin_fma(2.0, z, tr1);
+        CH(0, k, 1) = __builtin_fma(-2.0, z, tr1);
     }
     if constexpr ((IDO & 1) == 0) {
 #pragma unroll
@@ -264,13 +267,17 @@ SO_DEV void dct2(double* c) {
         c[k] += t;
     }
     Rfft<N>::backward(c);
+    // 0.5 (t1 +- t2) with the 0.5 folded into the twiddles: scaling by a power of two
+    // commutes with every rounding (no under/overflow at these magnitudes), so
+    // (0.5 w) a + (0.5 v) b == 0.5 (w a + v b) bit for bit
 #pragma unroll
     for (int k = 1; k < NS2; ++k) {
         const int kc = N - k;
-        double t1 = TW::dct(k - 1) * c[kc] + TW::dct(kc - 1) * c[k];
-        double t2 = TW::dct(k - 1) * c[k] - TW::dct(kc - 1) * c[kc];
-        c[k] = 0.5 * (t1 + t2);
-        c[kc] = 0.5 * (t1 - t2);
+        const double ha = 0.5 * TW::dct(k - 1), hb = 0.5 * TW::dct(kc - 1);
+        double t1 = ha * c[kc] + hb * c[k];
+        double t2 = ha * c[k] - hb * c[kc];
+        c[k] = t1 + t2;
+        c[kc] = t1 - t2;
     }
     c[NS2] *= TW::dct(NS2 - 1);
     c[0] *= kSqrt2 * 0.5;

@@ -894,6 +894,17 @@ SO_DEV uint32_t win_u32(const uint32_t* win, int row, int col) {
     return __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)(col & 3));
 }
 
+#ifdef SO_STAMPS
+// Instrumented builds only (tools/sea_stamps.py): per-workgroup phase time stamps.
+__device__ unsigned long long* g_sea_stamps = nullptr;
+#define SO_SEA_STAMP(i, v) do { if (tid == 0 && g_sea_stamps) g_sea_stamps[(size_t)blockIdx.x * 12 + (i)] = (v); } while (0)
+extern "C" int so_debug_set_sea_stamps(void* p) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_sea_stamps), &p, sizeof(p));
+}
+#else
+#define SO_SEA_STAMP(i, v) do { } while (0)
+#endif
+
 __global__ void __launch_bounds__(Sea2Geo::NTHREADS) __attribute__((amdgpu_waves_per_eu(SO_SEA2_WPE)))
 me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
                int32_t* __restrict__ out_best, int probe) {
@@ -916,6 +927,12 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
     const int x0 = bx0 * 16, y0 = byt0 * 16;
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifdef SO_STAMPS
+    __shared__ uint32_t st_fb, st_sur;
+    if (tid == 0) { st_fb = 0; st_sur = 0; }
+    SO_SEA_STAMP(0, __builtin_amdgcn_s_memrealtime());
+    SO_SEA_STAMP(1, __builtin_amdgcn_s_memtime());
+#endif
 
     for (int i = tid; i < G::NBLK; i += G::NTHREADS) keys[i] = kNoKey;
     {   // current tile (zero outside the frame / stripe)
@@ -945,6 +962,7 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
     for (int r = 0; r < nref; ++r) {
         const uint8_t* ref = refs.p[r];
         __syncthreads();
+        if (r == 0) SO_SEA_STAMP(2, __builtin_amdgcn_s_memtime());
         {   // window: all loads first, then the LDS stores
             constexpr int N = G::WR * RP, IT = (N + G::NTHREADS - 1) / G::NTHREADS;
             uint32_t v[IT];
@@ -962,6 +980,7 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
                 if (tid + k * G::NTHREADS < N) win[tid + k * G::NTHREADS] = v[k];
         }
         __syncthreads();
+        if (r == 0) SO_SEA_STAMP(3, __builtin_amdgcn_s_memtime());
         // 4x4 byte sums B4(row, c) = (sum of the 4x4 window block at (row, c)) >> 4, stored at
         // b4[row * B4P + (c & 3) * 40 + (c >> 2)] (a candidate's four sums of one 4x4 row --
         // columns c, c+4, c+8, c+12 -- are then consecutive bytes).  Thread = (dword column m:
@@ -994,6 +1013,7 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
             }
         }
         __syncthreads();
+        if (r == 0) SO_SEA_STAMP(4, __builtin_amdgcn_s_memtime());
         if (probe == 1) continue;   // timing probe (tools/me_ab2.py): staging + byte sums only
 #pragma unroll 1
         for (int u = wave; u < G::NBLK; u += G::NW) {
@@ -1085,6 +1105,9 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
             const uint32_t nmine = (uint32_t)__builtin_popcount(msk);
             const uint32_t nsur = wave_sum_u32(nmine);
             uint16_t* mylist = list + wave * CAP;
+#ifdef SO_STAMPS
+            if (lane == 0) { atomicAdd(&st_sur, nsur); if (nsur > (uint32_t)CAP) atomicAdd(&st_fb, 1u); }
+#endif
             if (nsur > (uint32_t)CAP) {
                 if (probe == 3) continue;
                 // fallback: the dense wave search on the single-copy window
@@ -1169,11 +1192,23 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
         }
     }
     __syncthreads();
+    SO_SEA_STAMP(5, __builtin_amdgcn_s_memtime());
     for (int i = tid; i < G::NBLK; i += G::NTHREADS) {
         const int gbx = bx0 + i % TBX, gby = byt0 + i / TBX;
         if (gbx >= nbx || gby >= by1) continue;
         decode_key(keys[i], SR, out_best + ((size_t)(gby - by0) * nbx + gbx) * 4);
     }
+#ifdef SO_STAMPS
+    if (tid == 0) {
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        SO_SEA_STAMP(6, __builtin_amdgcn_s_memtime());
+        SO_SEA_STAMP(7, __builtin_amdgcn_s_memrealtime());
+        SO_SEA_STAMP(8, ((unsigned long long)xcc << 32) | hw);
+        SO_SEA_STAMP(9, ((unsigned long long)st_fb << 32) | st_sur);
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------

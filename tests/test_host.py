@@ -180,3 +180,24 @@ def test_roi_rectangles_to_blocks():
     enc2 = Y_Video_codec(48, 64, 1, 16, 16, 4, 1, 0, 0.015, False, y_only_frame_arr=z,
                          roi=np.arange(12).reshape(3, 4))
     assert enc2.roi_block_offsets().tolist() == list(range(12))
+
+
+def test_device_dct_header_bitwise_vs_oracle(tmp_path):
+    """streamoptima_amd/csrc/so_dct.h (the kernels' FP64 DCT-II/III, with its exact
+    power-of-two folds) compiled for the host matches the oracle's pocketfft restatement
+    bit for bit on random, tie-heavy and dequantised vectors (tests/host/dct_host_check.cpp)."""
+    import shutil
+    import subprocess
+    from oracle import oracle as O
+    O.build()
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "dct_check")
+    libdir = os.path.dirname(O.LIB_PATH)
+    subprocess.run([gxx, "-O2", "-ffp-contract=off", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                    os.path.join(root, "tests", "host", "dct_host_check.cpp"), f"-L{libdir}", "-lso_oracle",
+                    f"-Wl,-rpath,{libdir}", "-o", exe], check=True, capture_output=True)
+    r = subprocess.run([exe, "300000"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
