@@ -113,6 +113,30 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
                      int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae_num,
                      uint8_t* out_recon, int32_t* out_sse, int32_t* scratch, void* stream);
 
+/*
+ * A run of consecutive P-frames (the GOP loop's P-frames between two I-frames,
+ * Encoder.py:1839-1867 with nRefFrames 1): frame i predicts from frame i-1's
+ * reconstruction (out_recon[i-1]), frame 0 from ref0.  Output is identical to
+ * so_encode_p_frame called per frame.  Covers bs 16 / sr 16 / no VBS with W a multiple
+ * of 128 (whole cache lines per tile row); anything else is SO_E_UNSUPPORTED (call
+ * so_encode_p_frame per frame).
+ *
+ * One persistent launch per 32 frames: workgroups take (frame, tile) tasks in frame-major
+ * raster order, and a tile of frame i starts once the tile rows of frame i-1 its +-16 px
+ * window reads are complete (device-scope counters in `workspace`; reconstructions are
+ * stored write-through), so consecutive frames overlap on the device with no host
+ * round trip.  curs / out_* are host arrays of nframes device pointers; out_sse may be
+ * NULL.  workspace: caller-owned uint32 [so_p_run_workspace_elems(H, W)], zeroed by the
+ * call (hipMemsetAsync on `stream`); word 1 is nonzero after the run if a dependency wait
+ * timed out (a bug; the tests check it).
+ */
+size_t so_p_run_workspace_elems(int H, int W);
+int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W,
+                    int bs, int sr, int qp_rd, const int32_t* qp_row, uint8_t* const* out_split,
+                    int16_t* const* out_mv, int16_t* const* out_qtc, int32_t* const* out_tokens,
+                    int32_t* const* out_mae_num, uint8_t* const* out_recon, int32_t* const* out_sse,
+                    uint32_t* workspace, void* stream);
+
 /* int32 elements of scratch so_encode_i_frame / so_intra_recon need: nb*(bs*bs) + nb*8 */
 size_t so_i_frame_scratch_elems(int H, int W, int bs);
 

@@ -392,7 +392,34 @@ class Y_Video_codec:
                 sym.extra["qp_map"] = qmap
             return sym
 
-        for i in range(nframes):
+        rc_switch = self.RCFlag is not None and self.RCFlag > 1 and (self.RCFlag == 2 or self.intra_thresh is not None)
+        # runs of P-frames with nothing per frame on the host go through one persistent launch
+        # (engine.encode_p_run): same symbols, frames overlapped on the device
+        pipelined = (not two_pass and roi_dev is None and not rc_switch and self.nRefFrames == 1
+                     and eng.pipelined_ok(1) and os.environ.get("SO_PIPELINE", "1") != "0")
+        i = 0
+        while i < nframes:
+            if pipelined and i % intra_dur != 0:
+                j = i
+                while j < nframes and j % intra_dur != 0:
+                    j += 1
+                self.set_Qp(self.const_init_Qp)
+                outs = []
+                for k in range(i, j):
+                    pre = symbols[k] if symbols is not None else None
+                    outs.append(pre if pre is not None and pre.frame_type == 1 else eng.new_symbols(1))
+                eng.encode_p_run([frames_dev[k] for k in range(i, j)], ref_frames[-1], self.Qp, outs,
+                                 qp_row=qp_sched, qp_row_dev=qp_sched_dev)
+                for sym in outs:
+                    out_syms.append(sym)
+                    ftypes.append(1)
+                    qp_rows.append(list(qp_sched) if rc_on else [])
+                if rc_on:
+                    self.set_Qp(qp_sched[-1])
+                ref_frames = [outs[-1].recon]
+                ref_float = [False]
+                i = j
+                continue
             cur = frames_dev[i]
             pre = symbols[i] if symbols is not None else None
             self.set_Qp(self.const_init_Qp)
@@ -420,6 +447,7 @@ class Y_Video_codec:
                     ref_float.pop(0)
                 ref_frames.append(sym.recon)
                 ref_float.append(False)
+            i += 1
         # per-block / per-row SSE came out of the encode kernels; one reduction per GOP
         sse = torch.stack([s.sse for s in out_syms]).sum(dim=1, dtype=torch.int64)
         return {"symbols": out_syms, "sse": sse, "frame_type": ftypes, "qp_rows": qp_rows}

@@ -3,6 +3,10 @@
 // synchronisation (every entry point is capturable into a hipGraph).
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
 
 #include "so_common.h"
 
@@ -26,6 +30,35 @@ int me_fme_launch(const uint8_t* cur, const uint8_t* planes, size_t pstride, int
 int fme_planes_launch(const uint8_t* ref, int H, int W, int wrap, uint8_t* out, size_t pstride, hipStream_t st);
 int me_fastpred_launch(const uint8_t* cur, const uint8_t* const* ptrs, int nptr, int nref, int H, int W, int bs,
                        int fme, int by0, int by1, int serial, int32_t* out_best, int32_t* out_sub, hipStream_t st);
+int p_tile_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int by0, int by1, int qp_rd,
+                  const int32_t* qp_row, const int32_t* qp_map, int32_t* out_best, uint8_t* out_split,
+                  int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon,
+                  int32_t* out_sse, hipStream_t st);
+
+struct PFrameOut {
+    uint8_t* split;
+    int16_t* mv;
+    int16_t* qtc;
+    int32_t* tokens;
+    int32_t* mae;
+    uint8_t* recon;
+    int32_t* sse;
+};
+size_t p_run_workspace_words(int H, int W);
+int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
+                 const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, hipStream_t st);
+
+// The fused search + transform tile kernel (so_me.hip p_tile_kernel) covers the headline
+// configuration: bs 16, sr 16, full search, no VBS / FME, one reference.  SO_FUSED=0 or an
+// SO_ME_IMPL A/B selection keeps the two-launch path (ME kernel + inter_tq_kernel).
+static bool use_fused(int bs, int sr, int vbs, int nref) {
+    if (bs != 16 || sr != 16 || vbs || nref != 1) return false;
+    const char* f = getenv("SO_FUSED");
+    if (f && strcmp(f, "0") == 0) return false;
+    const char* impl = getenv("SO_ME_IMPL");
+    return impl == nullptr || impl[0] == 0;
+}
+
 int inter_tq_launch(const uint8_t* cur, const RefSet& refs, const uint8_t* planes, size_t pstride, int H, int W,
                     int bs, int by0, int by1, const int32_t* best, const int32_t* sub, int qp_rd, const int32_t* qp_row,
                     const int32_t* qp_map, int vbs, double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
@@ -263,6 +296,9 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
     int32_t* best = scratch;
     int32_t* sub = vbs ? scratch + nbs * 4 : nullptr;
     hipStream_t st = (hipStream_t)stream;
+    if (use_fused(bs, sr, vbs, nref))
+        return p_tile_launch(cur, rs, H, W, by0, by1, qp_rd, qp_row, nullptr, best, out_split, out_mv, out_qtc,
+                             out_tokens, out_mae_num, out_recon, out_sse, st);
     SO_TRY(me_launch(cur, rs, nref, H, W, bs, sr, by0, by1, best, sub, st));
     return inter_tq_launch(cur, rs, nullptr, 0, H, W, bs, by0, by1, best, sub, qp_rd, qp_row, nullptr, vbs, lam, out_split,
                            out_mv, out_qtc, out_tokens, out_mae_num, out_recon, out_sse, st);
@@ -278,6 +314,42 @@ int so_encode_p_frame(const uint8_t* cur, const uint8_t* const* refs, int nref, 
     }
     return so_encode_p_rows(cur, refs, nref, H, W, bs, sr, 0, H / bs, qp_rd, qp_row, vbs, lam, out_split, out_mv,
                             out_qtc, out_tokens, out_mae_num, out_recon, out_sse, scratch, stream);
+}
+
+// ---- P-frame runs: one persistent launch (so_me.hip p_run_kernel) -----------------------
+size_t so_p_run_workspace_elems(int H, int W) {
+    if (H <= 0 || W <= 0) return 0;
+    return p_run_workspace_words(H, W);
+}
+
+int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int bs, int sr,
+                    int qp_rd, const int32_t* qp_row, uint8_t* const* out_split, int16_t* const* out_mv,
+                    int16_t* const* out_qtc, int32_t* const* out_tokens, int32_t* const* out_mae_num,
+                    uint8_t* const* out_recon, int32_t* const* out_sse, uint32_t* workspace, void* stream) {
+    const char* fn = "so_encode_p_run";
+    SO_TRY(check_geom(fn, H, W, bs, 0));
+    SO_TRY(check_sr(fn, sr));
+    SO_TRY(check_qp(fn, qp_rd));
+    if (bs != 16 || sr != 16 || W % 128 != 0) {
+        set_error("%s: covers bs 16 / sr 16 / W %% 128 == 0 (call so_encode_p_frame per frame)", fn);
+        return SO_E_UNSUPPORTED;
+    }
+    if (nframes <= 0) return SO_OK;
+    SO_NEED(curs, fn); SO_NEED(ref0, fn); SO_NEED(out_split, fn); SO_NEED(out_mv, fn); SO_NEED(out_qtc, fn);
+    SO_NEED(out_tokens, fn); SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn); SO_NEED(workspace, fn);
+    std::vector<PFrameOut> outs((size_t)nframes);
+    for (int i = 0; i < nframes; ++i) {
+        SO_NEED(curs[i], fn); SO_NEED(out_split[i], fn); SO_NEED(out_mv[i], fn); SO_NEED(out_qtc[i], fn);
+        SO_NEED(out_tokens[i], fn); SO_NEED(out_mae_num[i], fn); SO_NEED(out_recon[i], fn);
+        for (int j = -1; j < i; ++j)
+            if (out_recon[i] == (j < 0 ? ref0 : out_recon[j])) {
+                set_error("%s: out_recon[%d] aliases ref0 or another frame's reconstruction", fn, i);
+                return SO_E_INVALID;
+            }
+        outs[i] = PFrameOut{out_split[i], out_mv[i], out_qtc[i], out_tokens[i], out_mae_num[i], out_recon[i],
+                            out_sse ? out_sse[i] : nullptr};
+    }
+    return p_run_launch(curs, nframes, ref0, H, W, qp_rd, qp_row, outs.data(), workspace, (hipStream_t)stream);
 }
 
 size_t so_i_frame_scratch_elems(int H, int W, int bs) {
@@ -444,6 +516,9 @@ int so_encode_p_rows_ex(const uint8_t* cur, const uint8_t* const* refs, int nref
     if (flags & SO_REUSE_ME) {
         // pass 2 of two-pass RC: the ME records (and FME planes) of the previous call stay
         if (fme) SO_NEED(fme_planes, fn);
+    } else if (me_mode == SO_ME_FULL && !fme && use_fused(bs, sr, vbs, nref)) {
+        return p_tile_launch(cur, rs, H, W, by0, by1, qp_rd, qp_row, qp_map, best, out_split, out_mv, out_qtc,
+                             out_tokens, out_mae_num, out_recon, out_sse, st);
     } else {
         SO_TRY(me_ex(fn, cur, refs, nref, rs, H, W, bs, sr, by0, by1, me_mode, fme, fme_wrap, fme_planes, best, sub,
                      st));

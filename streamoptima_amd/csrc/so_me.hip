@@ -19,6 +19,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "so_block.h"
 #include "so_common.h"
 #include "so_dpp.h"
 
@@ -874,18 +875,24 @@ me_sea_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int
 #ifndef SO_SEA2_WPE
 #define SO_SEA2_WPE 6
 #endif
-struct Sea2Geo {
+// NW_ waves per workgroup: 8 (two blocks per wave; me_sea2_kernel) or 16 (one block per
+// wave; p_tile_kernel at 8 waves/SIMD)
+template <int NW_>
+struct Sea2GeoT {
     static constexpr int SR = 16, NT = 17;
     static constexpr int TBX = 8, TPY = 32, TBY = 2, TPX = 128;
     static constexpr int WR = TPY + 2 * SR;               // 64 window rows
     static constexpr int WD = (TPX + 2 * SR) / 4;         // 40 data dwords per row
     static constexpr int RP = WD + 1;                     // pitch 41
     static constexpr int B4R = WR - 3, B4C = TPX + 2 * SR - 3, B4P = 160;
-    static constexpr int B4BAND = 6, B4NB = (B4R + B4BAND - 1) / B4BAND;   // 11 bands of output rows
+    static constexpr int B4BAND = NW_ >= 16 ? 3 : 6;      // output rows per byte-sum thread
+    static constexpr int B4NB = (B4R + B4BAND - 1) / B4BAND;
     static constexpr int NBLK = TBX * TBY;
-    static constexpr int NW = 8, NTHREADS = NW * 64;
+    static constexpr int NW = NW_, NTHREADS = NW * 64;
     static constexpr int CAP = 192;
+    static_assert(WD * B4NB <= NTHREADS, "byte-sum threads");
 };
+using Sea2Geo = Sea2GeoT<8>;
 
 // 4 bytes of window row `row` starting at byte column `col` (single copy, pitch RP dwords)
 template <int RP>
@@ -905,30 +912,54 @@ extern "C" int so_debug_set_sea_stamps(void* p) {
 #define SO_SEA_STAMP(i, v) do { } while (0)
 #endif
 
-__global__ void __launch_bounds__(Sea2Geo::NTHREADS) __attribute__((amdgpu_waves_per_eu(SO_SEA2_WPE)))
-me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
-               int32_t* __restrict__ out_best, int probe) {
-    using G = Sea2Geo;
+// threadIdx.x behind an optimisation barrier: inside p_run_kernel's persistent loop the
+// tid-derived addresses are then recomputed per task instead of being hoisted out of the
+// loop and held in (spilled) registers across it.
+SO_DEV int opaque_tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
+// LDS of one SEA tile (me_sea2_kernel, p_tile_kernel).
+struct Sea2Lds {
+    uint32_t* win;             // [WR * RP + 4] reference window, single copy
+    uint32_t* b4w;             // [(B4R * B4P + 4) / 4] 4x4 byte sums of the window
+    uint32_t* curt;            // [TPY * TPX / 4] current tile, 32 rows x 128 B
+    uint32_t* a4;              // [NBLK * 4] per block: [j] = 4 byte sums (4x4 >> 4) of row j
+    uint16_t* list;            // [NW * CAP] survivor lists
+    uint32_t* lcount;          // [NW]
+    unsigned long long* keys;  // [NBLK] packed best key per block
+    uint32_t* st;              // [2] SO_STAMPS only: fallback blocks, survivors
+};
+
+// Exact SEA full search of tile `tile` (16 blocks of 16x16) over nref references.  On
+// return (after a barrier) keys[] holds every block's packed best key and win[] the last
+// reference's window (zero outside the frame).
+template <class G>
+SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cur, const RefSet& refs, int nref,
+                      int H, int W, int by0, int by1, int probe) {
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RP = G::RP, NT = G::NT;
     constexpr int B4P = G::B4P, CAP = G::CAP, CP = G::TPX;
-    __shared__ uint32_t win[G::WR * RP + 4];
-    __shared__ uint32_t b4w[(G::B4R * B4P + 4) / 4];
-    uint8_t* b4 = reinterpret_cast<uint8_t*>(b4w);
-    __shared__ uint32_t curt[G::TPY * CP / 4];      // current tile, 32 rows x 128 B
-    __shared__ uint32_t a4[G::NBLK * 4];           // per block: [j] = 4 byte sums (4x4 >> 4) of row j
-    __shared__ uint16_t list[G::NW * CAP];
-    __shared__ uint32_t lcount[G::NW];
-    __shared__ unsigned long long keys[G::NBLK];
+    uint32_t* const win = L.win;
+    uint32_t* const b4w = L.b4w;
+    uint8_t* const b4 = reinterpret_cast<uint8_t*>(b4w);
+    uint32_t* const curt = L.curt;
+    uint32_t* const a4 = L.a4;
+    uint16_t* const list = L.list;
+    uint32_t* const lcount = L.lcount;
+    unsigned long long* const keys = L.keys;
 
     const int nbx = W / 16;
     const int tiles_x = (nbx + TBX - 1) / TBX;
-    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    const int tx = tile % tiles_x, ty = tile / tiles_x;
     const int bx0 = tx * TBX, byt0 = by0 + ty * TBY;
     const int x0 = bx0 * 16, y0 = byt0 * 16;
-    const int tid = threadIdx.x;
+    const int tid = opaque_tid();
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 #ifdef SO_STAMPS
-    __shared__ uint32_t st_fb, st_sur;
+    uint32_t& st_fb = L.st[0];
+    uint32_t& st_sur = L.st[1];
     if (tid == 0) { st_fb = 0; st_sur = 0; }
     SO_SEA_STAMP(0, __builtin_amdgcn_s_memrealtime());
     SO_SEA_STAMP(1, __builtin_amdgcn_s_memtime());
@@ -1192,6 +1223,28 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
         }
     }
     __syncthreads();
+}
+
+__global__ void __launch_bounds__(Sea2Geo::NTHREADS) __attribute__((amdgpu_waves_per_eu(SO_SEA2_WPE)))
+me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
+               int32_t* __restrict__ out_best, int probe) {
+    using G = Sea2Geo;
+    constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RP = G::RP, B4P = G::B4P, CP = G::TPX;
+    __shared__ uint32_t win[G::WR * RP + 4];
+    __shared__ uint32_t b4w[(G::B4R * B4P + 4) / 4];
+    __shared__ uint32_t curt[G::TPY * CP / 4];
+    __shared__ uint32_t a4[G::NBLK * 4];
+    __shared__ uint16_t list[G::NW * G::CAP];
+    __shared__ uint32_t lcount[G::NW];
+    __shared__ unsigned long long keys[G::NBLK];
+    __shared__ uint32_t st[2];
+    const Sea2Lds L{win, b4w, curt, a4, list, lcount, keys, st};
+    sea2_tile<Sea2Geo>(L, blockIdx.x, cur, refs, nref, H, W, by0, by1, probe);
+
+    const int tid = threadIdx.x;
+    const int nbx = W / 16;
+    const int tiles_x = (nbx + TBX - 1) / TBX;
+    const int bx0 = (blockIdx.x % tiles_x) * TBX, byt0 = by0 + (blockIdx.x / tiles_x) * TBY;
     SO_SEA_STAMP(5, __builtin_amdgcn_s_memtime());
     for (int i = tid; i < G::NBLK; i += G::NTHREADS) {
         const int gbx = bx0 + i % TBX, gby = byt0 + i / TBX;
@@ -1206,9 +1259,322 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
         SO_SEA_STAMP(6, __builtin_amdgcn_s_memtime());
         SO_SEA_STAMP(7, __builtin_amdgcn_s_memrealtime());
         SO_SEA_STAMP(8, ((unsigned long long)xcc << 32) | hw);
-        SO_SEA_STAMP(9, ((unsigned long long)st_fb << 32) | st_sur);
+        SO_SEA_STAMP(9, ((unsigned long long)st[0] << 32) | st[1]);
     }
 #endif
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused P-frame tile (p_tile_kernel, the default for bs 16 / sr 16 / no VBS / one reference):
+// the SEA search of a 128x32 tile (sea2_tile) followed, in the same workgroup, by the
+// transform / quantisation / token / reconstruction of its 16 blocks -- the arithmetic of
+// inter_tq_kernel<16, false, false> (so_tq.hip), which replaces calculate_inter_frame_residual
+// (Encoder.py:432-460), apply_2d_dct (:779), quantize_TC (:787), len(entropy_encoder_block)
+// (:1086) and reconstruct_frame (:824-932).
+//   * One launch per frame (or stripe) instead of two: the ME launch's ramp / tail overlaps
+//     other workgroups' transform work and vice versa.
+//   * The prediction rows come from the LDS window the search used (it spans +-16 around the
+//     tile and is zero outside the frame, which is also handle_boundary_conditions' zero
+//     fill for the no-valid-candidate case), the current rows from the LDS tile: the
+//     transform phase reads nothing from HBM.
+//   * The transposes' FP64 scratch reuses the LDS of the byte sums and survivor lists.
+// Waves 0-3 run the transforms (16 lanes per block); the ME records are also written to
+// `out_best` when it is given (SO_REUSE_ME, the two-pass RC's second pass, reads them).
+//
+// p_run_kernel runs a whole run of P-frames (so_encode_p_run) as one persistent launch:
+// workgroups take (frame, tile) tasks from a queue in frame-major raster order, and a tile
+// of frame f starts once the three tile rows of frame f-1 its +-16 px window reads are
+// complete, so frame f's first rows overlap frame f-1's last ones and only the run's last
+// frame has a launch tail (a launch per frame leaves ~25% of the machine idle in its tail,
+// tools/sea_stamps.py).
+// ---------------------------------------------------------------------------------------
+template <class G>
+struct PTileGeo {
+    static constexpr int B4 = (G::B4R * G::B4P + 4) / 4;              // dwords
+    static constexpr int LIST = G::NW * G::CAP / 2;                   // dwords
+    static constexpr int TQD = G::NBLK * 16 * 17;                     // doubles
+    static constexpr int U64 = ((B4 + LIST + 1) / 2 > TQD) ? (B4 + LIST + 1) / 2 : TQD;
+};
+
+// 16 bytes of window row `row` from byte column `col`, as 4 dwords (5 aligned ds_read_b32
+// + v_alignbyte: misaligned wide DS reads are replayed on gfx950)
+SO_DEV void win_row16(const uint32_t* win, int row, int col, uint32_t (&w)[4]) {
+    constexpr int RP = Sea2Geo::RP;
+    lds_vu32p p = (lds_vu32p)(win + row * RP + (col >> 2));
+    const uint32_t sh = (uint32_t)(col & 3);
+    const uint32_t q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4];
+    w[0] = __builtin_amdgcn_alignbyte(q1, q0, sh);
+    w[1] = __builtin_amdgcn_alignbyte(q2, q1, sh);
+    w[2] = __builtin_amdgcn_alignbyte(q3, q2, sh);
+    w[3] = __builtin_amdgcn_alignbyte(q4, q3, sh);
+}
+
+typedef uint32_t so_v4u __attribute__((ext_vector_type(4)));
+
+// The LDS of one fused tile.
+template <class G>
+struct PTileLds {
+    uint32_t win[G::WR * G::RP + 4];
+    uint32_t curt[G::TPY * G::TPX / 4];
+    uint32_t a4[G::NBLK * 4];
+    uint32_t lcount[G::NW];
+    unsigned long long keys[G::NBLK];
+    uint32_t st[2];
+    int32_t mer[G::NBLK][4];               // decoded ME records (dx, dy, ref, sad)
+    double un[PTileGeo<G>::U64];           // byte sums + survivor lists | FP64 transposes
+};
+
+// Outputs of one frame (pointers relative to block row by0 of the launch).
+struct PFrameOut {
+    uint8_t* split;
+    int16_t* mv;
+    int16_t* qtc;
+    int32_t* tokens;
+    int32_t* mae;
+    uint8_t* recon;
+    int32_t* sse;
+};
+
+// Search + transforms of tile `tile` of one frame.  SC1: the reconstruction rows are stored
+// write-through (global_store sc1), so another XCD that later reads them (p_run_kernel's
+// next frame) gets them from memory without a release fence.  Ends with every wave's
+// stores retired (s_waitcnt vmcnt(0)) and a workgroup barrier.
+template <class G, bool SC1>
+SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur, const uint8_t* ref, int H, int W,
+                       int by0, int by1, int qp_rd, const int32_t* __restrict__ qp_row,
+                       const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best, const PFrameOut& o) {
+    constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, CP = G::TPX;
+    using P = PTileGeo<G>;
+    uint32_t* const b4w = reinterpret_cast<uint32_t*>(S.un);
+    uint16_t* const list = reinterpret_cast<uint16_t*>(b4w + P::B4);
+    const Sea2Lds L{S.win, b4w, S.curt, S.a4, list, S.lcount, S.keys, S.st};
+    RefSet refs{};
+    refs.p[0] = ref;
+    sea2_tile<G>(L, tile, cur, refs, 1, H, W, by0, by1, 0);   // ends with a barrier
+
+    const int tid = opaque_tid();
+    const int nbx = W / 16;
+    const int tiles_x = (nbx + TBX - 1) / TBX;
+    const int bx0 = (tile % tiles_x) * TBX, byt0 = by0 + (tile / tiles_x) * TBY;
+    for (int i = tid; i < G::NBLK; i += G::NTHREADS) {
+        decode_key(S.keys[i], SR, S.mer[i]);
+        const int gbx = bx0 + i % TBX, gby = byt0 + i / TBX;
+        if (out_best && gbx < nbx && gby < by1) {
+            int32_t* ob = out_best + ((size_t)(gby - by0) * nbx + gbx) * 4;
+            ob[0] = S.mer[i][0]; ob[1] = S.mer[i][1]; ob[2] = S.mer[i][2]; ob[3] = S.mer[i][3];
+        }
+    }
+    __syncthreads();
+    if (tid < G::NBLK * 16) {
+        const int g = tid >> 4, l = tid & 15;
+        const int bxl = g % TBX, byl = g / TBX;
+        const int gbx = bx0 + bxl, gby = byt0 + byl;
+        if (gbx < nbx && gby < by1) {   // uniform over the block's 16 lanes
+            const size_t b = (size_t)(gby - by0) * nbx + gbx;
+            const int x = gbx * 16, y = gby * 16;
+            const int qpr = qp_map ? qp_map[(size_t)gby * nbx + gbx] : (qp_row ? qp_row[gby] : qp_rd);
+            const int dx = S.mer[g][0], dy = S.mer[g][1], rf = S.mer[g][2], sad = S.mer[g][3];
+            const int prow = byl * 16 + SR + dy + l, pcol = bxl * 16 + SR + dx;   // window coordinates
+            const uint32_t* crow = S.curt + (byl * 16 + l) * (CP / 4) + bxl * 4;
+            double* dl = S.un + g * (16 * 17);
+            int res[16];
+            {
+                uint32_t pw[4];
+                win_row16(S.win, prow, pcol, pw);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t cw = crow[k];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        res[4 * k + e] = (int)((cw >> (8 * e)) & 255) - (int)((pw[k] >> (8 * e)) & 255);
+                }
+            }
+            double tcr[16];
+            xform2d_rows<16, false>(dl, l, res, tcr);
+            int q[16];
+#pragma unroll
+            for (int c = 0; c < 16; ++c)
+                q[c] = (int)__builtin_rint(__builtin_amdgcn_ldexp(__builtin_rint(tcr[c]), -q_exp_fast<16>(l, c, qpr)));
+            const int tok = block_tokens<16>(nullptr, l, q);
+            store_row_i16<16>(o.qtc + b * 256 + l * 16, q);
+            double dq[16], rd[16];
+            dequant_row_i<16>(q, l, qpr, dq);
+            xform2d_rows<16, true>(dl, l, dq, rd);
+            int rec[16];
+            {
+                uint32_t pw[4];
+                win_row16(S.win, prow, pcol, pw);
+#pragma unroll
+                for (int c = 0; c < 16; ++c) rec[c] = (int)((pw[c >> 2] >> (8 * (c & 3))) & 255) + (int)__builtin_rint(rd[c]);
+            }
+            if constexpr (SC1) {
+                so_v4u v;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    v[k] = (uint32_t)(rec[4 * k] & 255) | ((uint32_t)(rec[4 * k + 1] & 255) << 8) |
+                           ((uint32_t)(rec[4 * k + 2] & 255) << 16) | ((uint32_t)(rec[4 * k + 3] & 255) << 24);
+                uint8_t* rp = o.recon + (size_t)(y + l) * W + x;
+                asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(rp), "v"(v) : "memory");
+            } else {
+                store_row_u8<16>(o.recon, W, x, y + l, rec);
+            }
+            int sse = 0;
+            if (o.sse) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t cw = crow[k];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int d = (int)((cw >> (8 * e)) & 255) - (rec[4 * k + e] & 255);
+                        sse += d * d;
+                    }
+                }
+                sse = group_sum<16>(sse);
+            }
+            if (l < 12) o.mv[b * 12 + l] = (int16_t)(l == 0 ? dx : l == 1 ? dy : l == 2 ? rf : 0);
+            if (l == 0) {
+                o.split[b] = 0;
+                o.tokens[b] = tok;
+                o.mae[b] = sad;
+                if (o.sse) o.sse[b] = sse;
+            }
+        }
+    }
+    if constexpr (SC1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
+    __syncthreads();
+}
+
+#ifndef SO_PTILE_NW
+#define SO_PTILE_NW 8
+#endif
+template <int NW>
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? 8 : SO_SEA2_WPE)))
+p_tile_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W, int by0, int by1, int qp_rd,
+              const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best,
+              PFrameOut o) {
+    using G = Sea2GeoT<NW>;
+    __shared__ PTileLds<G> S;
+    ptile_body<G, false>(S, blockIdx.x, cur, refs.p[0], H, W, by0, by1, qp_rd, qp_row, qp_map, out_best, o);
+}
+
+int p_tile_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int by0, int by1, int qp_rd,
+                  const int32_t* qp_row, const int32_t* qp_map, int32_t* out_best, uint8_t* out_split,
+                  int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon,
+                  int32_t* out_sse, hipStream_t st) {
+    const int nbx = W / 16, nrows = by1 - by0;
+    if (nrows <= 0) return SO_OK;
+    const dim3 grid(((nbx + Sea2Geo::TBX - 1) / Sea2Geo::TBX) * ((nrows + Sea2Geo::TBY - 1) / Sea2Geo::TBY));
+    const PFrameOut o{out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon, out_sse};
+    hipLaunchKernelGGL(p_tile_kernel<SO_PTILE_NW>, grid, dim3(SO_PTILE_NW * 64), 0, st, cur, refs, H, W, by0, by1,
+                       qp_rd, qp_row, qp_map, out_best, o);
+    return check_launch("p_tile_kernel");
+}
+
+// ---- persistent run of P-frames ------------------------------------------------------------
+constexpr int kRunMax = 32;   // frames per launch (kernel-argument table)
+struct PRunArgs {
+    const uint8_t* cur[kRunMax];
+    PFrameOut out[kRunMax];
+};
+
+// Workspace words: [0] task counter, [1] timeout flag, [2 + f * ntr + r] tiles done in tile
+// row r of frame f.  Zeroed by the launcher before every launch.
+template <int NW>
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? 8 : SO_SEA2_WPE)))
+p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, int H, int W,
+             int qp_rd, const int32_t* __restrict__ qp_row, uint32_t* __restrict__ ws) {
+    using G = Sea2GeoT<NW>;
+    __shared__ PTileLds<G> S;
+    __shared__ int s_task;
+    const int tid = threadIdx.x;
+    const int nbx = W / 16, nby = H / 16;
+    const int tiles_x = (nbx + G::TBX - 1) / G::TBX, ntr = (nby + G::TBY - 1) / G::TBY;
+    const int ntiles = tiles_x * ntr, ntasks = ntiles * nframes;
+    uint32_t* const done = ws + 2;
+    // Every queue / counter access is made by ALL lanes of wave 0 under a wave-uniform
+    // branch (lane 0 adds 1, the others 0): a `tid == 0` branch ahead of a barrier inside
+    // this loop gets structurised into a divergent inner loop that never re-runs the
+    // dequeue (a hang; tools/ubench_rowdeps.cpp).
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t one = (tid & 63) == 0 ? 1u : 0u;
+    for (;;) {
+        if (wave == 0) {
+            const uint32_t v = __hip_atomic_fetch_add(&ws[0], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_task = (int)__builtin_amdgcn_readfirstlane(v);
+        }
+        __syncthreads();
+        const int task = __builtin_amdgcn_readfirstlane(s_task);
+        if (task >= ntasks) break;   // uniform: every wave leaves
+        const int f = task / ntiles, tile = task - f * ntiles, ty = tile / tiles_x;
+        if (f > 0 && wave == 0) {
+            // rows ty-1 .. ty+1 of frame f-1 (the window's +-16 px); every task they hold was
+            // dequeued before this one by a running workgroup, so the wait always ends.  It is
+            // bounded all the same (50 ms of s_memrealtime): a timeout flags the launch
+            // (Engine.run_timed_out, checked by the tests) and the tile proceeds.
+            const int r0 = ty > 0 ? ty - 1 : 0, r1 = ty + 1 < ntr ? ty + 1 : ntr - 1;
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            for (int r = r0; r <= r1; ++r) {
+                const uint32_t* c = done + (size_t)(f - 1) * ntr + r;
+                for (;;) {
+                    const uint32_t v = __builtin_amdgcn_readfirstlane(
+                        __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    if (v >= (uint32_t)tiles_x) break;
+                    __builtin_amdgcn_s_sleep(2);
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
+                        __hip_atomic_fetch_add(&ws[1], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+            }
+        }
+        __syncthreads();   // also: every wave has read s_task
+        ptile_body<G, true>(S, tile, a.cur[f], f ? a.out[f - 1].recon : ref0, H, W, 0, nby, qp_rd, qp_row, nullptr,
+                            nullptr, a.out[f]);
+        // ptile_body ended with every wave's write-through stores retired and a barrier
+        if (wave == 0)
+            __hip_atomic_fetch_add(done + (size_t)f * ntr + ty, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+size_t p_run_workspace_words(int H, int W) {
+    const int ntr = (H / 16 + Sea2Geo::TBY - 1) / Sea2Geo::TBY;
+    return 2 + (size_t)kRunMax * ntr;
+}
+
+int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
+                 const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, hipStream_t st) {
+    static int ncu = 0, per_cu = 0;
+    if (ncu == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+            ncu = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p_run_kernel<SO_PTILE_NW>, SO_PTILE_NW * 64, 0) !=
+                hipSuccess || per_cu <= 0)
+            per_cu = 1;
+    }
+    const int nbx = W / 16, nby = H / 16;
+    const long ntiles = (long)((nbx + Sea2Geo::TBX - 1) / Sea2Geo::TBX) * ((nby + Sea2Geo::TBY - 1) / Sea2Geo::TBY);
+    for (int f0 = 0; f0 < nframes; f0 += kRunMax) {
+        const int n = nframes - f0 < kRunMax ? nframes - f0 : kRunMax;
+        PRunArgs a{};
+        for (int i = 0; i < n; ++i) {
+            a.cur[i] = curs[f0 + i];
+            a.out[i] = outs[f0 + i];
+        }
+        const hipError_t e = hipMemsetAsync(ws, 0, p_run_workspace_words(H, W) * sizeof(uint32_t), st);
+        if (e != hipSuccess) {
+            set_error("p_run_kernel: hipMemsetAsync: %s", hipGetErrorString(e));
+            return (int)e;
+        }
+        long grid = (long)ncu * per_cu;
+        if (grid > ntiles * n) grid = ntiles * n;
+        hipLaunchKernelGGL(p_run_kernel<SO_PTILE_NW>, dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), 0, st, a, n,
+                           f0 ? outs[f0 - 1].recon : ref0, H, W, qp_rd, qp_row, ws);
+        const int rc = check_launch("p_run_kernel");
+        if (rc != SO_OK) return rc;
+    }
+    return SO_OK;
 }
 
 // ---------------------------------------------------------------------------------------

@@ -10,6 +10,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -180,6 +182,50 @@ class Engine:
         out.frame_type, out.qp_rd = 1, int(qp_rd)
         out.qp_row = None if qp_row is None else list(qp_row)
         return out
+
+    # ---- P-frame runs (one persistent launch) ----------------------------------------------
+    def pipelined_ok(self, nref: int = 1) -> bool:
+        """The configurations encode_p_run covers: the fused search + transform kernel
+        (bs 16, sr 16, full search, no VBS / FME, one reference) on whole 128-byte rows."""
+        return (self.bs == 16 and self.sr == 16 and self.me_mode == _lib.ME_FULL and not self.fme and not self.vbs
+                and nref == 1 and self.w % 128 == 0)
+
+    def encode_p_run(self, curs: list, ref0: torch.Tensor, qp_rd: int, outs: list, qp_row=None,
+                     qp_row_dev: torch.Tensor | None = None) -> list:
+        """so_encode_p_run: a run of consecutive P-frames (frame i predicts from frame i-1's
+        reconstruction, ref0 for the first) as one persistent launch whose workgroups start
+        a tile of frame i as soon as the rows of frame i-1 its window reads are done, so
+        only the run's last frame has a launch tail.  Symbols identical to per-frame
+        encode_p; asynchronous."""
+        if not self.pipelined_ok():
+            raise ValueError("encode_p_run covers bs 16 / sr 16 / full search / no VBS, FME / W % 128 == 0")
+        n = len(curs)
+        if n == 0:
+            return []
+        qrd = qp_row_dev if qp_row_dev is not None else self.qp_row_tensor(qp_row)
+        for t, name in [(ref0, "ref0")] + [(c, "cur") for c in curs]:
+            self._check_plane(t, name)
+        if getattr(self, "_run_ws", None) is None:
+            self._run_ws = torch.zeros(self.lib.so_p_run_workspace_elems(self.h, self.w), dtype=torch.int32,
+                                       device=self.device)
+
+        def arr(ts):
+            return (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
+        rc = self.lib.so_encode_p_run(
+            arr(curs), n, ref0.data_ptr(), self.h, self.w, self.bs, self.sr, int(qp_rd), _lib.ptr(qrd),
+            arr([o.split for o in outs]), arr([o.mv for o in outs]), arr([o.qtc for o in outs]),
+            arr([o.tokens for o in outs]), arr([o.mae_num for o in outs]), arr([o.recon for o in outs]),
+            arr([o.sse for o in outs]), self._run_ws.data_ptr(), _lib.stream_handle(self.device))
+        _lib.check(rc, "so_encode_p_run")
+        for o in outs:
+            o.frame_type, o.qp_rd = 1, int(qp_rd)
+            o.qp_row = None if qp_row is None else list(qp_row)
+        return outs
+
+    def run_timed_out(self) -> bool:
+        """True if the last encode_p_run's dependency wait timed out (never expected)."""
+        ws = getattr(self, "_run_ws", None)
+        return bool(ws is not None and int(ws[1].item()) != 0)
 
     def encode_i_rows(self, cur, by0: int, by1: int, qp_rd: int, out: FrameSymbols,
                       qp_row_dev: torch.Tensor | None = None, qp_map_dev: torch.Tensor | None = None,

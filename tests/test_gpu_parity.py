@@ -620,3 +620,34 @@ def test_two_pass_roi_bitstream_round_trip(gpu, tmp_path, monkeypatch):
     out = dec.decode_bitstream(files[0], files[1], qp_map_file=files[2])
     for i in range(f):
         assert (out[i] == enc._symbols[i].recon.cpu().numpy()).all(), i
+
+
+# ---------------------------------------------------------------- persistent P-frame runs
+@pytest.mark.parametrize("h,w,n,qp,seed", [(1088, 1920, 6, 4, 3), (2160, 3840, 4, 4, 0), (256, 384, 9, 2, 5),
+                                             (208, 256, 33, 4, 7)])
+def test_p_run_matches_per_frame(gpu, h, w, n, qp, seed):
+    """so_encode_p_run (one persistent launch; frame i+1's tiles start while frame i's last
+    rows finish) produces exactly the symbols of so_encode_p_frame called frame by frame,
+    incl. a run longer than one launch's 32 frames, and no dependency wait times out."""
+    from streamoptima_amd.engine import Engine, alloc_planes
+    from streamoptima_amd.synth import synth_sequence_torch
+    dev = gpu
+    fr = alloc_planes(n + 1, h, w, dev)
+    fr.copy_(synth_sequence_torch(n + 1, h, w, seed, dev))
+    eng = Engine(h, w, 16, 16, False, 0.015, dev)
+    i0 = eng.encode_i(fr[0], qp)
+    ref_syms = []
+    ref = i0.recon
+    for k in range(1, n + 1):
+        s = eng.encode_p(fr[k], [ref], qp)
+        ref_syms.append(s)
+        ref = s.recon
+    outs = [eng.new_symbols(1) for _ in range(n)]
+    eng.encode_p_run([fr[k] for k in range(1, n + 1)], i0.recon, qp, outs)
+    torch.cuda.synchronize()
+    assert not eng.run_timed_out()
+    for k in range(n):
+        a, b = _sym_host(outs[k]), _sym_host(ref_syms[k])
+        _assert_frame(a, b, keys=("split", "mv", "qtc", "tokens", "recon"))
+        assert torch.equal(outs[k].mae_num, ref_syms[k].mae_num)
+        assert torch.equal(outs[k].sse, ref_syms[k].sse)

@@ -33,9 +33,14 @@ def main():
     nb = (h // 16) * (w // 16)
     best = torch.empty((nb, 4), dtype=torch.int32, device=dev)
     refs = _lib.ref_array([p1.recon])
+    fused = os.environ.get("STAMP_FUSED", "0") == "1"    # p_tile_kernel (ME + transforms) instead
+    sp = eng.new_symbols(1)
     for _ in range(int(os.environ.get("REPS", 5))):
-        _lib.check(lib.so_me_full_search(fr[2].data_ptr(), refs, 1, h, w, 16, 16, best.data_ptr(), None,
-                                         _lib.stream_handle()), "me")
+        if fused:
+            eng.encode_p(fr[2], [p1.recon], 4, out=sp)
+        else:
+            _lib.check(lib.so_me_full_search(fr[2].data_ptr(), refs, 1, h, w, 16, 16, best.data_ptr(), None,
+                                             _lib.stream_handle()), "me")
     torch.cuda.synchronize()
     s = stamps.cpu().numpy().astype(np.int64)
     rt0, rt1 = s[:, 0], s[:, 7]
@@ -43,7 +48,7 @@ def main():
     span_rt = (rt1.max() - rt0.min()) * 10e-3          # us (100 MHz)
     ghz = (cyc / np.maximum((rt1 - rt0) * 10e-9, 1e-12)).mean() / 1e9
     print(f"tiles {ntiles}  kernel span (first start -> last end) {span_rt:.1f} us  shader clock ~{ghz:.2f} GHz")
-    names = ["cur+a4", "window", "b4 sums", "search", "epilogue"]
+    names = ["cur+a4", "window", "b4 sums", "search", "epilogue" + (" (records + transforms)" if fused else "")]
     for i, n in enumerate(names):
         d = s[:, i + 2] - s[:, i + 1]
         print(f"  {n:9s} cycles mean {d.mean():8.0f}  p50 {np.median(d):8.0f}  p90 {np.percentile(d, 90):8.0f}  "
