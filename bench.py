@@ -74,8 +74,8 @@ def parse():
     ap.add_argument("--me", choices=("full", "fme", "fast", "fastpar", "fast_fme"), default="full",
                     help="ME variant: full search (headline), FMEEnable, fast_me (serial chain), fast_me under "
                          "ParallelMode 2, fast_me + FMEEnable")
-    ap.add_argument("--no-graph", action="store_true",
-                    help="launch every frame from the host instead of replaying the GOP as one HIP graph")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the GOP as one captured HIP graph (measured slower than host launches here)")
     ap.add_argument("--pcie", action="store_true",
                     help="also time the PCIe-inclusive path (pinned host frames in, symbols out)")
     return ap.parse_args()
@@ -171,19 +171,30 @@ def kernel_roofline(codec, frames_dev, symbols, reps: int, me_variant: str = "fu
             else:
                 os.environ["SO_ME_IMPL"] = old
 
+    # the product path of a plain GOP: the P-frames as one persistent launch (p_run_kernel)
+    run_ok = (me_variant == "full" and eng.pipelined_ok(1) and codec.nRefFrames == 1
+              and os.environ.get("SO_PIPELINE", "1") != "0" and not getattr(codec, "_rc_on", lambda: False)())
+    run_outs = [eng.new_symbols(1) for _ in range(nf - 1)] if run_ok else None
+
+    def run():
+        eng.encode_p_run([frames_dev[i] for i in range(1, nf)], symbols[0].recon, 4, run_outs)
+
     todo = (("me", me), ("tq", tq), ("me_dense", me_dense)) if me_variant == "full" else (("me", me), ("tq", tq))
-    out = {"me_dense": float("nan")}
+    if run_ok:
+        todo = (("run", run),) + todo
+    out = {"me_dense": float("nan"), "run": None}
     for name, fn in todo:
         for _ in range(3):
             fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         e0.record()
-        for _ in range(reps):
+        n_rep = max(2, reps // 10) if name == "run" else reps
+        for _ in range(n_rep):
             fn()
         e1.record()
         torch.cuda.synchronize()
-        out[name] = e0.elapsed_time(e1) / reps / 1e3  # seconds per launch
+        out[name] = e0.elapsed_time(e1) / n_rep / 1e3  # seconds per launch
     nb = eng.nb
     d = 2 * sr + 1
     # algorithmic work of one ME launch:
@@ -198,8 +209,12 @@ def kernel_roofline(codec, frames_dev, symbols, reps: int, me_variant: str = "fu
     cands = int(vx.sum()) * int(vy.sum())
     me_bytes = 2 * h * w + 16 * nb
     tq_bytes = 5 * h * w + 8 * nb          # cur + pred + recon + QTC int16 + symbols
+    # one P-frame of the fused kernel: cur + ref read, recon + QTC int16 written (5 B/px), and
+    # per block split 1 + mv 12 x int16 + tokens, mae, sse int32 (37 B)
+    frame_bytes = 5 * h * w + 37 * nb
     return {"me_s": out["me"], "tq_s": out["tq"], "me_dense_s": out["me_dense"], "me_bytes": me_bytes, "tq_bytes": tq_bytes,
-            "sad_ops": cands * bs * bs, "cands": cands, "d": d}
+            "sad_ops": cands * bs * bs, "cands": cands, "d": d, "run_s": out["run"], "run_frames": nf - 1,
+            "run_bytes": (nf - 1) * frame_bytes, "frame_bytes": frame_bytes}
 
 
 def cpu_baseline(cfg, rows: int) -> dict:
@@ -312,11 +327,10 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # The GOP's launch sequence (kernel launches, cross-stream events of the pipelined P-frame
-    # runs) is captured once into a HIP graph and replayed: same kernels, same work per step,
-    # without the host issuing ~120 launches per GOP.  The stripe shard's RCCL all_gather
-    # stays on the host path.
-    graph = not args.no_graph and not stripe
+    # --graph: the GOP's launch sequence is captured once into a HIP graph and replayed (same
+    # kernels, same work per step).  Off by default: host launches measured faster here.  The
+    # stripe shard's RCCL all_gather stays on the host path.
+    graph = args.graph and not stripe
     if graph:
         g = torch.cuda.CUDAGraph()
         cap = torch.cuda.Stream(dev)
@@ -357,15 +371,57 @@ def main():
     units = 1 if stripe else world          # GOPs encoded per step across the job
     mpx = units * args.steps * f * h * w / elapsed / 1e6
     me_gbs = rl["me_bytes"] / rl["me_s"] / 1e9
-    traffic = None
+    traffic_doc = {}
     pmc = os.path.join(ROOT, "profiles", "pmc_me_traffic.json")
     if os.path.exists(pmc):
         try:
-            kern = json.load(open(pmc)).get(args.config + ("_vbs" if args.vbs else ""), {}).get("kernels", {})
-            hit = kern.get("so::" + me_kernel_name(args.vbs, args.me))
-            traffic = round(hit["hbm_bytes"]) if hit else None
+            traffic_doc = json.load(open(pmc)).get(args.config + ("_vbs" if args.vbs else ""), {}).get("kernels", {})
         except Exception:
-            traffic = None
+            traffic_doc = {}
+
+    def traffic_of(kernel):
+        hit = traffic_doc.get("so::" + kernel)
+        return round(hit["hbm_bytes"]) if hit else None
+
+    me_k = me_kernel_name(args.vbs, args.me)
+    me_part = {"kernel": me_k, "launch_us": round(rl["me_s"] * 1e6, 2), "achieved_gbs": round(me_gbs, 2),
+               "algorithmic_bytes": rl["me_bytes"], "traffic": traffic_of(me_k),
+               # dense-equivalent |diff| rate: the exhaustive search's candidates x 256 per
+               # launch time.  The SEA kernel prunes exactly, so it can exceed the
+               # v_sad_u8 issue peak; dense_me is the unpruned kernel on the same frame.
+               "valu_sad": {"dense_equivalent_ops": rl["sad_ops"] / rl["me_s"], "peak_ops": SAD_PEAK_OPS,
+                            "frac": round(rl["sad_ops"] / rl["me_s"] / SAD_PEAK_OPS, 4),
+                            "measured_peak_ops": SAD_MEASURED_OPS, "candidates": rl["cands"]},
+               "dense_me": {"kernel": "me_wave_kernel<16, %s>" % ("true" if args.vbs else "false"),
+                            "launch_us": round(rl["me_dense_s"] * 1e6, 2),
+                            "valu_sad_frac": round(rl["sad_ops"] / rl["me_dense_s"] / SAD_PEAK_OPS, 4)}}
+    tq_part = {"kernel": "inter_tq_kernel<16, %s, false>" % ("true" if args.vbs else "false"),
+               "launch_us": round(rl["tq_s"] * 1e6, 2),
+               "achieved_gbs": round(rl["tq_bytes"] / rl["tq_s"] / 1e9, 2)}
+    if args.me != "full":
+        # the SAD-op accounting is the integer full search's; the variants report time only
+        me_part["valu_sad"] = None
+        me_part["dense_me"] = None
+    if rl["run_s"]:
+        # the product path: the GOP's 29 P-frames as ONE persistent launch of the fused
+        # search + transform kernel (so_encode_p_run), timed with HIP events on its stream
+        run_k = "p_run_kernel<8>"
+        run_gbs = rl["run_bytes"] / rl["run_s"] / 1e9
+        n_launch = -(-rl["run_frames"] // 32)       # so_encode_p_run: <= 32 frames per launch
+        roofline = {"bound": "hbm", "kernel": run_k, "achieved": round(run_gbs, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(run_gbs / HBM_PEAK_GBS, 5), "traffic": traffic_of(run_k),
+                    "algorithmic_bytes": round(rl["run_bytes"] / n_launch),
+                    "launch_us": round(rl["run_s"] / n_launch * 1e6, 2),
+                    "frames_per_launch": round(rl["run_frames"] / n_launch, 2),
+                    "per_frame_us": round(rl["run_s"] / rl["run_frames"] * 1e6, 2),
+                    "note": "the fused kernel is VALU-bound (SEA search + FP64 pocketfft-exact DCT), not HBM-bound; "
+                            "components = the same work as separate launches",
+                    "components": {"me_search": me_part, "transform": tq_part}}
+    else:
+        roofline = {"bound": "hbm", "kernel": me_k, "achieved": round(me_gbs, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(me_gbs / HBM_PEAK_GBS, 5), "traffic": traffic_of(me_k),
+                    "algorithmic_bytes": rl["me_bytes"], "launch_us": round(rl["me_s"] * 1e6, 2),
+                    "valu_sad": me_part["valu_sad"], "dense_me": me_part["dense_me"], "tq_kernel": tq_part}
     line = {
         "metric": METRIC,
         "value": round(mpx, 2), "unit": "Mpx/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -376,30 +432,11 @@ def main():
                    "transform": "fp64 pocketfft-exact DCT",
                    "parallelism": f"stripe x{world} (all_gather recon per frame)" if stripe else f"gop-per-rank x{world}",
                    "launch": "hip-graph (one GOP per replay)" if graph else "host launches"},
-        "roofline": {"bound": "hbm", "kernel": me_kernel_name(args.vbs, args.me), "achieved": round(me_gbs, 2),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(me_gbs / HBM_PEAK_GBS, 5),
-                     "traffic": traffic, "algorithmic_bytes": rl["me_bytes"],
-                     "launch_us": round(rl["me_s"] * 1e6, 2),
-                     # dense-equivalent |diff| rate: the exhaustive search's candidates x 256 per
-                     # launch time.  me_sea_kernel prunes exactly, so it can exceed
-                     # the v_sad_u8 issue peak; dense_me is the unpruned kernel on the same frame.
-                     "valu_sad": {"dense_equivalent_ops": rl["sad_ops"] / rl["me_s"], "peak_ops": SAD_PEAK_OPS,
-                                  "frac": round(rl["sad_ops"] / rl["me_s"] / SAD_PEAK_OPS, 4),
-                                  "measured_peak_ops": SAD_MEASURED_OPS,
-                                  "candidates": rl["cands"]},
-                     "dense_me": {"kernel": "me_wave_kernel<16, %s>" % ("true" if args.vbs else "false"),
-                                  "launch_us": round(rl["me_dense_s"] * 1e6, 2),
-                                  "valu_sad_frac": round(rl["sad_ops"] / rl["me_dense_s"] / SAD_PEAK_OPS, 4)},
-                     "tq_kernel": {"launch_us": round(rl["tq_s"] * 1e6, 2),
-                                   "achieved_gbs": round(rl["tq_bytes"] / rl["tq_s"] / 1e9, 2)}},
+        "roofline": roofline,
         "cpu_baseline": cpu,
         "psnr_mean_db": round(psnr_mean, 4),
         "psnr_delta_vs_reference": delta,
     }
-    if args.me != "full":
-        # the SAD-op accounting above is the integer full search's; the variants report time only
-        line["roofline"]["valu_sad"] = None
-        line["roofline"]["dense_me"] = None
     if pcie:
         line.update(pcie)
     if cpu:

@@ -1166,56 +1166,63 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             uint64_t best = kNoKey;
-            if (nsur <= 8) {
-                // four survivors per pass: 16 lanes (one DPP row) per survivor, a row per lane
+            if (nsur <= 4) {
+                // one pass: 16 lanes (one DPP row) per survivor, a row per lane
                 const int sidx = lane >> 4, row = lane & 15;
                 const uint32_t* cr_ = curt + crow0 + row * (CP / 4);
                 const uint32_t c0 = cr_[0], c1 = cr_[1], c2 = cr_[2], c3 = cr_[3];
+                const bool act = (uint32_t)sidx < nsur;
+                const int cand = act ? (int)mylist[sidx] : cs;
+                const int dxi = cand / 33, di = cand - dxi * 33;
+                const int col = bxl * 16 + dxi;
+                int wo = (byl * 16 + di + row) * RP + (col >> 2);
+                asm volatile("" : "+v"(wo));
+                lds_vu32p p = (lds_vu32p)(win + wo);
+                const uint32_t sh = (uint32_t)(col & 3);
+                const uint32_t q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4];
+                uint32_t sad = __builtin_amdgcn_sad_u8(c0, __builtin_amdgcn_alignbyte(q1, q0, sh), 0u);
+                sad = __builtin_amdgcn_sad_u8(c1, __builtin_amdgcn_alignbyte(q2, q1, sh), sad);
+                sad = __builtin_amdgcn_sad_u8(c2, __builtin_amdgcn_alignbyte(q3, q2, sh), sad);
+                sad = __builtin_amdgcn_sad_u8(c3, __builtin_amdgcn_alignbyte(q4, q3, sh), sad);
+                sad = row_sum_u32(sad);
+                const int dx = dxi - 16, dy = di - 16;
+                const uint64_t key = me_key(sad, (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)),
+                                            (uint32_t)r, (uint32_t)cand);
+                best = (act && key < best) ? key : best;
+            } else {
+                // four lanes (one DPP quad) per survivor, rows 4q..4q+3 per lane: sixteen
+                // survivors per pass (one survivor per lane left 3/4 of the lanes idle at the
+                // typical 5..16 survivors)
+                const int sidx = lane >> 2, q = lane & 3;
+                uint32_t cr[4][4];
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) cr[rr][k] = curt[crow0 + (4 * q + rr) * (CP / 4) + k];
 #pragma unroll 1
-                for (uint32_t s0 = 0; s0 < nsur; s0 += 4) {
+                for (uint32_t s0 = 0; s0 < nsur; s0 += 16) {
                     const bool act = s0 + (uint32_t)sidx < nsur;
                     const int cand = act ? (int)mylist[s0 + sidx] : cs;
                     const int dxi = cand / 33, di = cand - dxi * 33;
                     const int col = bxl * 16 + dxi;
-                    int wo = (byl * 16 + di + row) * RP + (col >> 2);
-                    asm volatile("" : "+v"(wo));
-                    lds_vu32p p = (lds_vu32p)(win + wo);
                     const uint32_t sh = (uint32_t)(col & 3);
-                    const uint32_t q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4];
-                    uint32_t sad = __builtin_amdgcn_sad_u8(c0, __builtin_amdgcn_alignbyte(q1, q0, sh), 0u);
-                    sad = __builtin_amdgcn_sad_u8(c1, __builtin_amdgcn_alignbyte(q2, q1, sh), sad);
-                    sad = __builtin_amdgcn_sad_u8(c2, __builtin_amdgcn_alignbyte(q3, q2, sh), sad);
-                    sad = __builtin_amdgcn_sad_u8(c3, __builtin_amdgcn_alignbyte(q4, q3, sh), sad);
-                    sad = row_sum_u32(sad);
+                    int wo = (byl * 16 + di + 4 * q) * RP + (col >> 2);
+                    asm volatile("" : "+v"(wo));
+                    uint32_t sad = 0;
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) {
+                        lds_vu32p p = (lds_vu32p)(win + wo + rr * RP);
+                        const uint32_t q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4];
+                        sad = __builtin_amdgcn_sad_u8(cr[rr][0], __builtin_amdgcn_alignbyte(q1, q0, sh), sad);
+                        sad = __builtin_amdgcn_sad_u8(cr[rr][1], __builtin_amdgcn_alignbyte(q2, q1, sh), sad);
+                        sad = __builtin_amdgcn_sad_u8(cr[rr][2], __builtin_amdgcn_alignbyte(q3, q2, sh), sad);
+                        sad = __builtin_amdgcn_sad_u8(cr[rr][3], __builtin_amdgcn_alignbyte(q4, q3, sh), sad);
+                    }
+                    sad = quad_sum_u32(sad);
                     const int dx = dxi - 16, dy = di - 16;
                     const uint64_t key = me_key(sad, (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)),
                                                 (uint32_t)r, (uint32_t)cand);
                     best = (act && key < best) ? key : best;
-                }
-            } else {
-                // one survivor per lane, 64 at a time
-#pragma unroll 1
-                for (uint32_t k0 = 0; k0 < nsur; k0 += 64) {
-                    const uint32_t idx = k0 + (uint32_t)lane;
-                    const int cand = idx < nsur ? (int)mylist[idx] : cs;
-                    const int dxi = cand / 33, di = cand - dxi * 33;
-                    const int col = bxl * 16 + dxi;
-                    const uint32_t sh = (uint32_t)(col & 3);
-                    uint32_t sad = 0;
-#pragma unroll
-                    for (int rr = 0; rr < 16; ++rr) {
-                        lds_vu32p p = (lds_vu32p)(win + (byl * 16 + di + rr) * RP + (col >> 2));
-                        const uint32_t q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4];
-                        const uint32_t* cr_ = curt + crow0 + rr * (CP / 4);
-                        sad = __builtin_amdgcn_sad_u8(cr_[0], __builtin_amdgcn_alignbyte(q1, q0, sh), sad);
-                        sad = __builtin_amdgcn_sad_u8(cr_[1], __builtin_amdgcn_alignbyte(q2, q1, sh), sad);
-                        sad = __builtin_amdgcn_sad_u8(cr_[2], __builtin_amdgcn_alignbyte(q3, q2, sh), sad);
-                        sad = __builtin_amdgcn_sad_u8(cr_[3], __builtin_amdgcn_alignbyte(q4, q3, sh), sad);
-                    }
-                    const int dx = dxi - 16, dy = di - 16;
-                    const uint64_t key = me_key(sad, (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)),
-                                                (uint32_t)r, (uint32_t)cand);
-                    best = (idx < nsur && key < best) ? key : best;
                 }
             }
             best = wave_min_u64_dpp(best);
