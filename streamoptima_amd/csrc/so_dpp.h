@@ -12,21 +12,20 @@ namespace so {
 constexpr int kDppQuad1032 = 0xB1, kDppQuad2301 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
 constexpr int kDppBcast15 = 0x142, kDppBcast31 = 0x143;
 
+// (old = ~0u, the identity of min: the compiler folds each step into one v_min_u32_dpp)
 SO_DEV uint32_t row_min_u32(uint32_t v) {
-    uint32_t o;
-    o = __builtin_amdgcn_update_dpp(v, v, kDppQuad1032, 0xF, 0xF, false); v = o < v ? o : v;
-    o = __builtin_amdgcn_update_dpp(v, v, kDppQuad2301, 0xF, 0xF, false); v = o < v ? o : v;
-    o = __builtin_amdgcn_update_dpp(v, v, kDppHalfMirror, 0xF, 0xF, false); v = o < v ? o : v;
-    o = __builtin_amdgcn_update_dpp(v, v, kDppMirror, 0xF, 0xF, false); v = o < v ? o : v;
+    v = __builtin_elementwise_min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0u, v, kDppQuad1032, 0xF, 0xF, false));
+    v = __builtin_elementwise_min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0u, v, kDppQuad2301, 0xF, 0xF, false));
+    v = __builtin_elementwise_min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0u, v, kDppHalfMirror, 0xF, 0xF, false));
+    v = __builtin_elementwise_min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0u, v, kDppMirror, 0xF, 0xF, false));
     return v;
 }
 
 // wave-uniform minimum (SGPR)
 SO_DEV uint32_t wave_min_u32(uint32_t v) {
     v = row_min_u32(v);
-    uint32_t o;
-    o = __builtin_amdgcn_update_dpp(v, v, kDppBcast15, 0xA, 0xF, false); v = o < v ? o : v;
-    o = __builtin_amdgcn_update_dpp(v, v, kDppBcast31, 0xC, 0xF, false); v = o < v ? o : v;
+    v = __builtin_elementwise_min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0u, v, kDppBcast15, 0xA, 0xF, false));
+    v = __builtin_elementwise_min(v, (uint32_t)__builtin_amdgcn_update_dpp(~0u, v, kDppBcast31, 0xC, 0xF, false));
     return __builtin_amdgcn_readlane(v, 63);
 }
 
@@ -56,15 +55,11 @@ SO_DEV uint64_t dpp_min_step(uint64_t v) {
     return o < v ? o : v;
 }
 
-// wave-uniform 64-bit minimum
+// wave-uniform 64-bit minimum: the minimum high word, then the minimum low word among the
+// lanes holding it (two folded 32-bit DPP reductions instead of six 64-bit compare steps)
 SO_DEV uint64_t wave_min_u64_dpp(uint64_t v) {
-    v = dpp_min_step<kDppQuad1032, 0xF>(v);
-    v = dpp_min_step<kDppQuad2301, 0xF>(v);
-    v = dpp_min_step<kDppHalfMirror, 0xF>(v);
-    v = dpp_min_step<kDppMirror, 0xF>(v);
-    v = dpp_min_step<kDppBcast15, 0xA>(v);
-    v = dpp_min_step<kDppBcast31, 0xC>(v);
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, 63), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), 63);
+    const uint32_t hi = wave_min_u32((uint32_t)(v >> 32));
+    const uint32_t lo = wave_min_u32((uint32_t)(v >> 32) == hi ? (uint32_t)v : ~0u);
     return ((uint64_t)hi << 32) | lo;
 }
 

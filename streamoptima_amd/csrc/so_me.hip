@@ -884,12 +884,14 @@ struct Sea2GeoT {
     static constexpr int WR = TPY + 2 * SR;               // 64 window rows
     static constexpr int WD = (TPX + 2 * SR) / 4;         // 40 data dwords per row
     static constexpr int RP = WD + 1;                     // pitch 41
-    static constexpr int B4R = WR - 3, B4C = TPX + 2 * SR - 3, B4P = 160;
+    static constexpr int B4R = WR - 3, B4C = TPX + 2 * SR - 3, B4P = 164;   // 41 dwords: rows 16 apart land 16 banks apart
     static constexpr int B4BAND = NW_ >= 16 ? 3 : 6;      // output rows per byte-sum thread
     static constexpr int B4NB = (B4R + B4BAND - 1) / B4BAND;
     static constexpr int NBLK = TBX * TBY;
     static constexpr int NW = NW_, NTHREADS = NW * 64;
     static constexpr int CAP = 192;
+    static constexpr int CPD = TPX / 4 + 1;               // current-tile pitch in dwords: 16 rows of
+                                                          // one block column land on 16 banks
     static_assert(WD * B4NB <= NTHREADS, "byte-sum threads");
 };
 using Sea2Geo = Sea2GeoT<8>;
@@ -979,7 +981,10 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
         }
 #pragma unroll
         for (int k = 0; k < IT; ++k)
-            if (tid + k * G::NTHREADS < N) curt[tid + k * G::NTHREADS] = v[k];
+            if (tid + k * G::NTHREADS < N) {
+                const int i = tid + k * G::NTHREADS, rr = i / (CP / 4);
+                curt[i + rr] = v[k];   // pitch CP/4 + 1 (G::CPD)
+            }
     }
     __syncthreads();
     for (int i = tid; i < G::NBLK * 16; i += G::NTHREADS) {   // (block, j, ii) -> byte ii of a4[blk*4 + j]
@@ -987,7 +992,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
         const int rr = (blk / TBX) * 16 + 4 * j, m = (blk % TBX) * 4 + ii;
         uint32_t sum = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) sum = __builtin_amdgcn_sad_u8(curt[(rr + q) * (CP / 4) + m], 0u, sum);
+        for (int q = 0; q < 4; ++q) sum = __builtin_amdgcn_sad_u8(curt[(rr + q) * G::CPD + m], 0u, sum);
         reinterpret_cast<uint8_t*>(a4)[i] = (uint8_t)(sum >> 4);
     }
     for (int r = 0; r < nref; ++r) {
@@ -1068,11 +1073,20 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             uint32_t lb[NT];
 #pragma unroll
             for (int t = 0; t < NT; ++t) lb[t] = 0;
-            uint32_t n0 = p1[0], n1 = p1[1];
+            // byte-sum rows through a ring of PD rows in flight: the row used in step sr_ was
+            // loaded PD steps earlier, so LDS latency overlaps PD steps of v_sad_u8 work
+            // (one step ahead left every step waiting on its own loads)
+            constexpr int PD = 4;
+            uint32_t n0[PD], n1[PD];
+#pragma unroll
+            for (int k = 0; k < PD; ++k) { n0[k] = p1[k * (B4P / 4)]; n1[k] = p1[k * (B4P / 4) + 1]; }
 #pragma unroll
             for (int sr_ = 0; sr_ < NT + 12; ++sr_) {
-                const uint32_t w0 = n0, w1 = n1;
-                if (sr_ + 1 < NT + 12) { n0 = p1[(sr_ + 1) * (B4P / 4)]; n1 = p1[(sr_ + 1) * (B4P / 4) + 1]; }
+                const uint32_t w0 = n0[sr_ % PD], w1 = n1[sr_ % PD];
+                if (sr_ + PD < NT + 12) {
+                    n0[sr_ % PD] = p1[(sr_ + PD) * (B4P / 4)];
+                    n1[sr_ % PD] = p1[(sr_ + PD) * (B4P / 4) + 1];
+                }
                 const uint32_t P = __builtin_amdgcn_alignbyte(w1, w0, bsh);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -1116,12 +1130,12 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             const uint32_t kmin = wave_min_u32(kl);
             if (kmin == 0xFFFFFFFFu) continue;                 // no valid candidate: key stays none
             const int cs = (int)(kmin & 2047), cdx = cs / 33, cdi = cs - cdx * 33;
-            const int crow0 = byl * 16 * (CP / 4) + bxl * 4;   // current block in curt (dwords)
+            const int crow0 = byl * 16 * G::CPD + bxl * 4;   // current block in curt (dwords)
             uint32_t U;
             {
                 const int row = lane >> 2, kk = lane & 3;
                 const uint32_t w = win_u32<RP>(win, byl * 16 + cdi + row, bxl * 16 + cdx + 4 * kk);
-                U = wave_sum_u32(__builtin_amdgcn_sad_u8(curt[crow0 + row * (CP / 4) + kk], w, 0u));
+                U = wave_sum_u32(__builtin_amdgcn_sad_u8(curt[crow0 + row * G::CPD + kk], w, 0u));
             }
             if (probe == 2) {
                 if (lane == 0 && U < keys[u]) keys[u] = U;
@@ -1169,7 +1183,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             if (nsur <= 4) {
                 // one pass: 16 lanes (one DPP row) per survivor, a row per lane
                 const int sidx = lane >> 4, row = lane & 15;
-                const uint32_t* cr_ = curt + crow0 + row * (CP / 4);
+                const uint32_t* cr_ = curt + crow0 + row * G::CPD;
                 const uint32_t c0 = cr_[0], c1 = cr_[1], c2 = cr_[2], c3 = cr_[3];
                 const bool act = (uint32_t)sidx < nsur;
                 const int cand = act ? (int)mylist[sidx] : cs;
@@ -1198,7 +1212,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) cr[rr][k] = curt[crow0 + (4 * q + rr) * (CP / 4) + k];
+                    for (int k = 0; k < 4; ++k) cr[rr][k] = curt[crow0 + (4 * q + rr) * G::CPD + k];
 #pragma unroll 1
                 for (uint32_t s0 = 0; s0 < nsur; s0 += 16) {
                     const bool act = s0 + (uint32_t)sidx < nsur;
@@ -1239,7 +1253,7 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RP = G::RP, B4P = G::B4P, CP = G::TPX;
     __shared__ uint32_t win[G::WR * RP + 4];
     __shared__ uint32_t b4w[(G::B4R * B4P + 4) / 4];
-    __shared__ uint32_t curt[G::TPY * CP / 4];
+    __shared__ uint32_t curt[G::TPY * G::CPD];
     __shared__ uint32_t a4[G::NBLK * 4];
     __shared__ uint16_t list[G::NW * G::CAP];
     __shared__ uint32_t lcount[G::NW];
@@ -1322,7 +1336,7 @@ typedef uint32_t so_v4u __attribute__((ext_vector_type(4)));
 template <class G>
 struct PTileLds {
     uint32_t win[G::WR * G::RP + 4];
-    uint32_t curt[G::TPY * G::TPX / 4];
+    uint32_t curt[G::TPY * G::CPD];
     uint32_t a4[G::NBLK * 4];
     uint32_t lcount[G::NW];
     unsigned long long keys[G::NBLK];
@@ -1382,7 +1396,7 @@ SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur
             const int qpr = qp_map ? qp_map[(size_t)gby * nbx + gbx] : (qp_row ? qp_row[gby] : qp_rd);
             const int dx = S.mer[g][0], dy = S.mer[g][1], rf = S.mer[g][2], sad = S.mer[g][3];
             const int prow = byl * 16 + SR + dy + l, pcol = bxl * 16 + SR + dx;   // window coordinates
-            const uint32_t* crow = S.curt + (byl * 16 + l) * (CP / 4) + bxl * 4;
+            const uint32_t* crow = S.curt + (byl * 16 + l) * G::CPD + bxl * 4;
             double* dl = S.un + g * (16 * 17);
             int res[16];
             {
