@@ -887,6 +887,7 @@ struct Sea2GeoT {
     static constexpr int B4R = WR - 3, B4C = TPX + 2 * SR - 3, B4P = 164;   // 41 dwords: rows 16 apart land 16 banks apart
     static constexpr int B4BAND = NW_ >= 16 ? 3 : 6;      // output rows per byte-sum thread
     static constexpr int B4NB = (B4R + B4BAND - 1) / B4BAND;
+    static constexpr int B4RS = B4NB * B4BAND;            // stored rows: whole bands, no bounds tests
     static constexpr int NBLK = TBX * TBY;
     static constexpr int NW = NW_, NTHREADS = NW * 64;
     static constexpr int CAP = 192;
@@ -926,7 +927,7 @@ SO_DEV int opaque_tid() {
 // LDS of one SEA tile (me_sea2_kernel, p_tile_kernel).
 struct Sea2Lds {
     uint32_t* win;             // [WR * RP + 4] reference window, single copy
-    uint32_t* b4w;             // [(B4R * B4P + 4) / 4] 4x4 byte sums of the window
+    uint32_t* b4w;             // [(B4RS * B4P + 4) / 4] 4x4 byte sums of the window
     uint32_t* curt;            // [TPY * TPX / 4] current tile, 32 rows x 128 B
     uint32_t* a4;              // [NBLK * 4] per block: [j] = 4 byte sums (4x4 >> 4) of row j
     uint16_t* list;            // [NW * CAP] survivor lists
@@ -1036,17 +1037,14 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
                 h[i][2] = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w1, w0, 2), 0u, 0u);
                 h[i][3] = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w1, w0, 3), 0u, 0u);
             }
+            // whole bands, every column: rows >= B4R and columns >= B4C hold sums no valid
+            // candidate reads (the storage is B4RS rows), so the stores need no bounds tests
+            uint8_t* const ob = b4 + r0 * B4P + m;
 #pragma unroll
-            for (int i = 0; i < G::B4BAND; ++i) {
-                const int orow = r0 + i;
-                if (orow < G::B4R) {
+            for (int i = 0; i < G::B4BAND; ++i)
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        if (4 * m + k < G::B4C)
-                            b4[orow * B4P + k * 40 + m] = (uint8_t)((h[i][k] + h[i + 1][k] + h[i + 2][k] + h[i + 3][k]) >> 4);
-                    }
-                }
-            }
+                for (int k = 0; k < 4; ++k)
+                    ob[i * B4P + k * 40] = (uint8_t)((h[i][k] + h[i + 1][k] + h[i + 2][k] + h[i + 3][k]) >> 4);
         }
         __syncthreads();
         if (r == 0) SO_SEA_STAMP(4, __builtin_amdgcn_s_memtime());
@@ -1252,7 +1250,7 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
     using G = Sea2Geo;
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RP = G::RP, B4P = G::B4P, CP = G::TPX;
     __shared__ uint32_t win[G::WR * RP + 4];
-    __shared__ uint32_t b4w[(G::B4R * B4P + 4) / 4];
+    __shared__ uint32_t b4w[(G::B4RS * B4P + 4) / 4];
     __shared__ uint32_t curt[G::TPY * G::CPD];
     __shared__ uint32_t a4[G::NBLK * 4];
     __shared__ uint16_t list[G::NW * G::CAP];
@@ -1311,7 +1309,7 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
 // ---------------------------------------------------------------------------------------
 template <class G>
 struct PTileGeo {
-    static constexpr int B4 = (G::B4R * G::B4P + 4) / 4;              // dwords
+    static constexpr int B4 = (G::B4RS * G::B4P + 4) / 4;             // dwords
     static constexpr int LIST = G::NW * G::CAP / 2;                   // dwords
     static constexpr int TQD = G::NBLK * 16 * 17;                     // doubles
     static constexpr int U64 = ((B4 + LIST + 1) / 2 > TQD) ? (B4 + LIST + 1) / 2 : TQD;
