@@ -122,8 +122,8 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
  * so_encode_p_frame per frame).
  *
  * One persistent launch per 32 frames: workgroups take (frame, tile) tasks in frame-major
- * raster order, and a tile of frame i starts once the tile rows of frame i-1 its +-16 px
- * window reads are complete (device-scope counters in `workspace`; reconstructions are
+ * raster order, and a tile of frame i starts once the 3x3 tiles of frame i-1 its +-16 px
+ * window reads are done (device-scope flags in `workspace`; reconstructions are
  * stored write-through), so consecutive frames overlap on the device with no host
  * round trip.  curs / out_* are host arrays of nframes device pointers; out_sse may be
  * NULL.  workspace: caller-owned uint32 [so_p_run_workspace_elems(H, W)], zeroed by the

@@ -1302,10 +1302,11 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
 //
 // p_run_kernel runs a whole run of P-frames (so_encode_p_run) as one persistent launch:
 // workgroups take (frame, tile) tasks from a queue in frame-major raster order, and a tile
-// of frame f starts once the three tile rows of frame f-1 its +-16 px window reads are
-// complete, so frame f's first rows overlap frame f-1's last ones and only the run's last
-// frame has a launch tail (a launch per frame leaves ~25% of the machine idle in its tail,
-// tools/sea_stamps.py).
+// of frame f starts once the 3x3 tiles of frame f-1 its +-16 px window reads are done, so
+// frame f's first rows overlap frame f-1's last ones and only the run's last frame has a
+// launch tail (a launch per frame leaves ~25% of the machine idle in its tail,
+// tools/sea_stamps.py).  Per-tile flags (not per-row counters) matter at 1080p, where
+// fewer tiles than resident workgroups make the frame-to-frame latency the limit.
 // ---------------------------------------------------------------------------------------
 template <class G>
 struct PTileGeo {
@@ -1496,8 +1497,8 @@ struct PRunArgs {
     PFrameOut out[kRunMax];
 };
 
-// Workspace words: [0] task counter, [1] timeout flag, [2 + f * ntr + r] tiles done in tile
-// row r of frame f.  Zeroed by the launcher before every launch.
+// Workspace words: [0] task counter, [1] timeout flag, [2 + f * ntiles + t] = 1 once tile t of
+// frame f is done.  Zeroed by the launcher before every launch.
 template <int NW>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? 8 : SO_SEA2_WPE)))
 p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, int H, int W,
@@ -1510,12 +1511,13 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     const int tiles_x = (nbx + G::TBX - 1) / G::TBX, ntr = (nby + G::TBY - 1) / G::TBY;
     const int ntiles = tiles_x * ntr, ntasks = ntiles * nframes;
     uint32_t* const done = ws + 2;
-    // Every queue / counter access is made by ALL lanes of wave 0 under a wave-uniform
-    // branch (lane 0 adds 1, the others 0): a `tid == 0` branch ahead of a barrier inside
-    // this loop gets structurised into a divergent inner loop that never re-runs the
-    // dequeue (a hang; tools/ubench_rowdeps.cpp).
+    // Every queue / flag access is made by ALL lanes of wave 0 under a wave-uniform branch
+    // (lane 0 adds 1, the others 0): a `tid == 0` branch ahead of a barrier inside this loop
+    // gets structurised into a divergent inner loop that never re-runs the dequeue (a hang;
+    // tools/ubench_rowdeps.cpp).
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t one = (tid & 63) == 0 ? 1u : 0u;
+    const int lane = tid & 63;
+    const uint32_t one = lane == 0 ? 1u : 0u;
     for (;;) {
         if (wave == 0) {
             const uint32_t v = __hip_atomic_fetch_add(&ws[0], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1524,25 +1526,24 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
         __syncthreads();
         const int task = __builtin_amdgcn_readfirstlane(s_task);
         if (task >= ntasks) break;   // uniform: every wave leaves
-        const int f = task / ntiles, tile = task - f * ntiles, ty = tile / tiles_x;
+        const int f = task / ntiles, tile = task - f * ntiles, ty = tile / tiles_x, tx = tile - ty * tiles_x;
         if (f > 0 && wave == 0) {
-            // rows ty-1 .. ty+1 of frame f-1 (the window's +-16 px); every task they hold was
-            // dequeued before this one by a running workgroup, so the wait always ends.  It is
-            // bounded all the same (50 ms of s_memrealtime): a timeout flags the launch
+            // the 3x3 tiles of frame f-1 around this one (the window's +-16 px), one flag per
+            // lane, all polled in one round trip.  Every task they stand for was dequeued
+            // before this one by a running workgroup, so the wait always ends; it is bounded
+            // all the same (50 ms of s_memrealtime): a timeout flags the launch
             // (Engine.run_timed_out, checked by the tests) and the tile proceeds.
-            const int r0 = ty > 0 ? ty - 1 : 0, r1 = ty + 1 < ntr ? ty + 1 : ntr - 1;
+            const int nx = tx + lane % 3 - 1, ny = ty + lane / 3 - 1;
+            const bool need = lane < 9 && nx >= 0 && nx < tiles_x && ny >= 0 && ny < ntr;
+            const uint32_t* c = done + (size_t)(f - 1) * ntiles + (need ? ny * tiles_x + nx : 0);
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            for (int r = r0; r <= r1; ++r) {
-                const uint32_t* c = done + (size_t)(f - 1) * ntr + r;
-                for (;;) {
-                    const uint32_t v = __builtin_amdgcn_readfirstlane(
-                        __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                    if (v >= (uint32_t)tiles_x) break;
-                    __builtin_amdgcn_s_sleep(2);
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
-                        __hip_atomic_fetch_add(&ws[1], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        break;
-                    }
+            for (;;) {
+                const uint32_t v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (__builtin_amdgcn_ballot_w64(need && v == 0u) == 0) break;
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
+                    __hip_atomic_fetch_add(&ws[1], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
                 }
             }
         }
@@ -1551,13 +1552,13 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                             nullptr, a.out[f]);
         // ptile_body ended with every wave's write-through stores retired and a barrier
         if (wave == 0)
-            __hip_atomic_fetch_add(done + (size_t)f * ntr + ty, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(done + (size_t)f * ntiles + tile, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 size_t p_run_workspace_words(int H, int W) {
-    const int ntr = (H / 16 + Sea2Geo::TBY - 1) / Sea2Geo::TBY;
-    return 2 + (size_t)kRunMax * ntr;
+    const size_t ntiles = (size_t)((W / 16 + Sea2Geo::TBX - 1) / Sea2Geo::TBX) * ((H / 16 + Sea2Geo::TBY - 1) / Sea2Geo::TBY);
+    return 2 + (size_t)kRunMax * ntiles;
 }
 
 int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
