@@ -969,7 +969,19 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
 #endif
 
     for (int i = tid; i < G::NBLK; i += G::NTHREADS) keys[i] = kNoKey;
-    {   // current tile (zero outside the frame / stripe)
+    if (x0 + CP <= W && y0 + G::TPY <= H) {
+        // interior tile (uniform branch): thread = (row, column phase); the loads' and stores'
+        // per-dword offsets are immediates, so staging costs a few VALU per thread
+        constexpr int TPR = G::NTHREADS / G::TPY, NPT = (CP / 4) / TPR;   // threads per row, dwords per thread
+        static_assert(G::NTHREADS % G::TPY == 0 && (CP / 4) % TPR == 0, "current-tile staging");
+        const int rr = tid / TPR, c0 = tid - rr * TPR;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(cur + (size_t)(y0 + rr) * W + x0) + c0;
+        uint32_t v[NPT];
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) v[k] = src[k * TPR];
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) curt[rr * G::CPD + c0 + k * TPR] = v[k];
+    } else {   // current tile (zero outside the frame / stripe)
         constexpr int N = G::TPY * CP / 4, IT = (N + G::NTHREADS - 1) / G::NTHREADS;
         uint32_t v[IT];
 #pragma unroll
@@ -1000,7 +1012,21 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
         const uint8_t* ref = refs.p[r];
         __syncthreads();
         if (r == 0) SO_SEA_STAMP(2, __builtin_amdgcn_s_memtime());
-        {   // window: all loads first, then the LDS stores
+        if (x0 - SR >= 0 && x0 - SR + 4 * RP <= W && y0 - SR >= 0 && y0 - SR + G::WR <= H) {
+            // interior window (uniform branch): thread = (row, column phase) with immediate
+            // per-dword offsets; all loads first, then the LDS stores
+            constexpr int TPR = G::NTHREADS / G::WR, NPT = (RP + TPR - 1) / TPR;
+            static_assert(G::NTHREADS % G::WR == 0, "window staging");
+            const int wr = tid / TPR, c0 = tid - wr * TPR;
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(ref + (size_t)(y0 - SR + wr) * W + (x0 - SR)) + c0;
+            uint32_t v[NPT];
+#pragma unroll
+            for (int k = 0; k < NPT; ++k)
+                if (c0 + k * TPR < RP) v[k] = src[k * TPR];
+#pragma unroll
+            for (int k = 0; k < NPT; ++k)
+                if (c0 + k * TPR < RP) win[wr * RP + c0 + k * TPR] = v[k];
+        } else {   // window: all loads first, then the LDS stores (zero outside the frame)
             constexpr int N = G::WR * RP, IT = (N + G::NTHREADS - 1) / G::NTHREADS;
             uint32_t v[IT];
 #pragma unroll
