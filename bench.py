@@ -42,6 +42,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 # (4.39 cycles) = 1.434e14 |diffs|/s = 91% of this.
 SAD_PEAK_OPS = 1024 * 2.4e9 / 4 * 64 * 4
 SAD_MEASURED_OPS = 5.603e11 * 256
+VALU_PEAK_INSTR_S = 1024 * 2.4e9 / 4   # wave64 VALU instructions per second, all SIMDs
 METRIC = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "BASELINE.json")))["metric"]
 
 CONFIGS = {
@@ -383,6 +384,17 @@ def main():
         hit = traffic_doc.get("so::" + kernel)
         return round(hit["hbm_bytes"]) if hit else None
 
+    def valu_issue_of(kernel, launch_s):
+        # VALU issue roofline: SQ_INSTS_VALU per launch (PMC, profiles/pmc_me_traffic.json)
+        # against one wave64 VALU instruction per 4 cycles per SIMD, 1024 SIMDs at 2.4 GHz
+        hit = traffic_doc.get("so::" + kernel)
+        if not hit or "sq_insts_valu" not in hit:
+            return None
+        peak = VALU_PEAK_INSTR_S
+        achieved = hit["sq_insts_valu"] / launch_s
+        return {"valu_instrs": round(hit["sq_insts_valu"]), "achieved_instr_s": achieved, "peak_instr_s": peak,
+                "frac": round(achieved / peak, 4)}
+
     me_k = me_kernel_name(args.vbs, args.me)
     me_part = {"kernel": me_k, "launch_us": round(rl["me_s"] * 1e6, 2), "achieved_gbs": round(me_gbs, 2),
                "algorithmic_bytes": rl["me_bytes"], "traffic": traffic_of(me_k),
@@ -413,9 +425,10 @@ def main():
                     "algorithmic_bytes": round(rl["run_bytes"] / n_launch),
                     "launch_us": round(rl["run_s"] / n_launch * 1e6, 2),
                     "frames_per_launch": round(rl["run_frames"] / n_launch, 2),
+                    "valu_issue": valu_issue_of(run_k, rl["run_s"] / n_launch),
                     "per_frame_us": round(rl["run_s"] / rl["run_frames"] * 1e6, 2),
-                    "note": "the fused kernel is VALU-bound (SEA search + FP64 pocketfft-exact DCT), not HBM-bound; "
-                            "components = the same work as separate launches",
+                    "note": "the fused kernel is VALU-bound (SEA search + FP64 pocketfft-exact DCT), not HBM-bound: "
+                            "valu_issue is its roofline; components = the same work as separate launches",
                     "components": {"me_search": me_part, "transform": tq_part}}
     else:
         roofline = {"bound": "hbm", "kernel": me_k, "achieved": round(me_gbs, 2), "peak": HBM_PEAK_GBS,

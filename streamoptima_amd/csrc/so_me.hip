@@ -1100,7 +1100,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             // byte-sum rows through a ring of PD rows in flight: the row used in step sr_ was
             // loaded PD steps earlier, so LDS latency overlaps PD steps of v_sad_u8 work
             // (one step ahead left every step waiting on its own loads)
-            constexpr int PD = 4;
+            constexpr int PD = 2;
             uint32_t n0[PD], n1[PD];
 #pragma unroll
             for (int k = 0; k < PD; ++k) { n0[k] = p1[k * (B4P / 4)]; n1[k] = p1[k * (B4P / 4) + 1]; }
