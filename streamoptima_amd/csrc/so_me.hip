@@ -1168,12 +1168,24 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             // ---- 3. survivors: 16 LBq - 240 <= U, i.e. LBq < qU1 ------------------------------
             const uint32_t qU = (U + 240) >> 4;
             const uint32_t qU1 = xok ? qU + 1 : 0u;            // dx-invalid lanes: nothing passes
-            uint32_t msk = (ok2 && lb2 <= qU) ? (1u << NT) : 0u;
-#pragma unroll
-            for (int t = 0; t < NT; ++t) msk |= (lb[t] < qU1 ? 1u : 0u) << t;
-            const uint32_t nmine = (uint32_t)__builtin_popcount(msk);
-            const uint32_t nsur = wave_sum_u32(nmine);
+            // survivors by one wave ballot per candidate row t (t = NT: the dx = +16 column,
+            // lanes < 33): rows nobody passes cost one compare and a scalar branch; the others
+            // write their candidates at the running count + the lane's rank in the ballot (no
+            // per-lane bit loops, no LDS atomics).  Writes past CAP are dropped: that block
+            // takes the dense fallback below.
             uint16_t* mylist = list + wave * CAP;
+            const int cbase = xi * 33 + 16 * hh;
+            uint32_t nsur = 0;
+#pragma unroll
+            for (int t = 0; t <= NT; ++t) {
+                const bool pass = t < NT ? lb[t] < qU1 : (ok2 && lb2 <= qU);
+                const uint64_t bal = __builtin_amdgcn_ballot_w64(pass);
+                if (bal) {   // uniform
+                    const uint32_t pos = nsur + lane_prefix(bal);
+                    if (pass && pos < (uint32_t)CAP) mylist[pos] = (uint16_t)(t < NT ? cbase + t : 32 * 33 + d2);
+                    nsur += (uint32_t)__builtin_popcountll(bal);
+                }
+            }
 #ifdef SO_STAMPS
             if (lane == 0) { atomicAdd(&st_sur, nsur); if (nsur > (uint32_t)CAP) atomicAdd(&st_fb, 1u); }
 #endif
@@ -1185,21 +1197,6 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
                 continue;
             }
             if (probe == 4) continue;
-            // compaction: one LDS atomic per lane reserves its slots (the order is irrelevant:
-            // the packed key decides, ties included)
-            if (lane == 0) lcount[wave] = 0;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (nmine) {
-                uint32_t pos = atomicAdd(&lcount[wave], nmine);
-                uint32_t mm = msk;
-                while (mm) {
-                    const int t = __builtin_ctz(mm);
-                    mm &= mm - 1;
-                    mylist[pos++] = (uint16_t)(t < NT ? xi * 33 + 16 * hh + t : 32 * 33 + d2);
-                }
-            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
