@@ -53,9 +53,14 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int by0, int nrow
 
     // stage the original pixels left of the block (cols x-sr .. x-1, 0 where < 0)
     uint8_t* lrow = left + l * kIntraMaxSr;
-    for (int k = 0; k < sr; ++k) {
-        const int col = x - sr + k;
-        lrow[k] = col >= 0 ? cur[(size_t)(y + l) * W + col] : 0;
+    if (BS == 16 && sr == 16 && x != 0) {
+        // x >= 16: one aligned 16-byte row load and one ds_write_b128
+        *reinterpret_cast<uint4*>(lrow) = *reinterpret_cast<const uint4*>(cur + (size_t)(y + l) * W + x - 16);
+    } else {
+        for (int k = 0; k < sr; ++k) {
+            const int col = x - sr + k;
+            lrow[k] = col >= 0 ? cur[(size_t)(y + l) * W + col] : 0;
+        }
     }
     int crow[BS];
     load_cur_row<BS>(cur, W, x, y + l, crow);
