@@ -122,7 +122,7 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int by0, int nrow
     int tc[BS], q[BS];
 #pragma unroll
     for (int c = 0; c < BS; ++c) tc[c] = (int)__builtin_rint(tcd[c]);
-    quant_row<BS>(tc, l, qp_rd, q);
+    quant_row_i<BS>(tc, l, qp_rd, q);   // FP64 carriers, branch-free (so_block.h)
 
     bool split = false;
     int mae_num = sad;
@@ -225,11 +225,11 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int by0, int nrow
     int tok;
     int32_t* rb = idres + (size_t)b * BS * BS;
     if (!split) {
-        if (qpr != qp_rd) quant_row<BS>(tc, l, qpr, q);
+        if (qpr != qp_rd) quant_row_i<BS>(tc, l, qpr, q);
         tok = block_tokens<BS>(fl, l, q);
         store_row_i16<BS>(out_qtc + (size_t)b * BS * BS + l * BS, q);
-        int dq[BS];
-        dequant_row<BS>(q, l, qpr, dq);
+        double dq[BS];
+        dequant_row_i<BS>(q, l, qpr, dq);
         double rd[BS];
         xform2d_rows<BS, true>(dl, l, dq, rd);
 #pragma unroll

@@ -911,15 +911,6 @@ __device__ unsigned long long* g_sea_stamps = nullptr;
 extern "C" int so_debug_set_sea_stamps(void* p) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_sea_stamps), &p, sizeof(p));
 }
-__device__ unsigned long long g_tq_counts[2];   // MFMA transform path: blocks, blocks with a tie
-extern "C" int so_debug_tq_counts(unsigned long long* out, int reset) {
-    int rc = (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tq_counts), sizeof(g_tq_counts));
-    if (reset) {
-        const unsigned long long z[2] = {0, 0};
-        rc |= (int)hipMemcpyToSymbol(HIP_SYMBOL(g_tq_counts), z, sizeof(z));
-    }
-    return rc;
-}
 #else
 #define SO_SEA_STAMP(i, v) do { } while (0)
 #endif
@@ -1387,35 +1378,6 @@ struct PFrameOut {
     int32_t* sse;
 };
 
-#ifndef SO_TQ_MFMA
-#define SO_TQ_MFMA 0
-#endif
-// Orthonormal DCT-II matrix D[u][x] = c_u cos(pi (2x+1) u / 32), c_0 = 1/4, c_u = sqrt(2)/4
-// (the MFMA transform path; its results are only used where rint() is provably the same as
-// on the reference's pocketfft values, see ptile_body)
-__constant__ double kDct16[256] = {
-    0x1.0000000000000p-2, 0x1.0000000000000p-2, 0x1.0000000000000p-2, 0x1.0000000000000p-2, 0x1.0000000000000p-2, 0x1.0000000000000p-2, 0x1.0000000000000p-2, 0x1.0000000000000p-2, 0x1.0000000000000p-2, 0x1.0000000000000p-2, 0x1.0000000000000p-2, 0x1.0000000000000p-2, 0x1.0000000000000p-2, 0x1.0000000000000p-2, 0x1.0000000000000p-2, 0x1.0000000000000p-2,
-    0x1.684b9c80f1a8cp-2, 0x1.5a730c6c21c67p-2, 0x1.3f4a237187eafp-2, 0x1.17dc13dab2dd6p-2, 0x1.cb598cc4beea1p-3, 0x1.5553e3f5b5e5ap-3, 0x1.a4608aafa8526p-4, 0x1.1be35182fe5b3p-5, -0x1.1be35182fe5adp-5, -0x1.a4608aafa8522p-4, -0x1.5553e3f5b5e59p-3, -0x1.cb598cc4bee9fp-3, -0x1.17dc13dab2dd6p-2, -0x1.3f4a237187eaep-2, -0x1.5a730c6c21c67p-2, -0x1.684b9c80f1a8bp-2,
-    0x1.63150b15e8536p-2, 0x1.2d062ef88e31ap-2, 0x1.92469c0dcf32fp-3, 0x1.1a855dec071b7p-4, -0x1.1a855dec071b4p-4, -0x1.92469c0dcf32bp-3, -0x1.2d062ef88e31ap-2, -0x1.63150b15e8536p-2, -0x1.63150b15e8536p-2, -0x1.2d062ef88e31bp-2, -0x1.92469c0dcf32dp-3, -0x1.1a855dec071c0p-4, 0x1.1a855dec071b6p-4, 0x1.92469c0dcf329p-3, 0x1.2d062ef88e31ap-2, 0x1.63150b15e8535p-2,
-    0x1.5a730c6c21c67p-2, 0x1.cb598cc4beea1p-3, 0x1.1be35182fe5b3p-5, -0x1.5553e3f5b5e59p-3, -0x1.3f4a237187eaep-2, -0x1.684b9c80f1a8cp-2, -0x1.17dc13dab2dd5p-2, -0x1.a4608aafa853ep-4, 0x1.a4608aafa8536p-4, 0x1.17dc13dab2dd4p-2, 0x1.684b9c80f1a8cp-2, 0x1.3f4a237187eafp-2, 0x1.5553e3f5b5e5cp-3, -0x1.1be35182fe58ap-5, -0x1.cb598cc4bee98p-3, -0x1.5a730c6c21c65p-2,
-    0x1.4e7ae9144f0fcp-2, 0x1.1517a7bdb3896p-3, -0x1.1517a7bdb3895p-3, -0x1.4e7ae9144f0fcp-2, -0x1.4e7ae9144f0fdp-2, -0x1.1517a7bdb389cp-3, 0x1.1517a7bdb3898p-3, 0x1.4e7ae9144f0fbp-2, 0x1.4e7ae9144f0fcp-2, 0x1.1517a7bdb389ep-3, -0x1.1517a7bdb3897p-3, -0x1.4e7ae9144f0fap-2, -0x1.4e7ae9144f0fcp-2, -0x1.1517a7bdb389fp-3, 0x1.1517a7bdb3895p-3, 0x1.4e7ae9144f0fap-2,
-    0x1.3f4a237187eafp-2, 0x1.1be35182fe5b3p-5, -0x1.17dc13dab2dd6p-2, -0x1.5a730c6c21c68p-2, -0x1.a4608aafa8529p-4, 0x1.cb598cc4bee99p-3, 0x1.684b9c80f1a8bp-2, 0x1.5553e3f5b5e5cp-3, -0x1.5553e3f5b5e56p-3, -0x1.684b9c80f1a8cp-2, -0x1.cb598cc4bee9fp-3, 0x1.a4608aafa8504p-4, 0x1.5a730c6c21c69p-2, 0x1.17dc13dab2ddap-2, -0x1.1be35182fe5d8p-5, -0x1.3f4a237187eadp-2,
-    0x1.2d062ef88e31ap-2, -0x1.1a855dec071b4p-4, -0x1.63150b15e8536p-2, -0x1.92469c0dcf32dp-3, 0x1.92469c0dcf329p-3, 0x1.63150b15e8537p-2, 0x1.1a855dec071adp-4, -0x1.2d062ef88e313p-2, -0x1.2d062ef88e316p-2, 0x1.1a855dec0719ap-4, 0x1.63150b15e8536p-2, 0x1.92469c0dcf332p-3, -0x1.92469c0dcf325p-3, -0x1.63150b15e8537p-2, -0x1.1a855dec071e2p-4, 0x1.2d062ef88e312p-2,
-    0x1.17dc13dab2dd6p-2, -0x1.5553e3f5b5e59p-3, -0x1.5a730c6c21c68p-2, 0x1.1be35182fe591p-5, 0x1.684b9c80f1a8cp-2, 0x1.a4608aafa8541p-4, -0x1.3f4a237187eb3p-2, -0x1.cb598cc4beeb0p-3, 0x1.cb598cc4beea8p-3, 0x1.3f4a237187eb5p-2, -0x1.a4608aafa852cp-4, -0x1.684b9c80f1a8cp-2, -0x1.1be35182fe562p-5, 0x1.5a730c6c21c62p-2, 0x1.5553e3f5b5e62p-3, -0x1.17dc13dab2dcep-2,
-    0x1.0000000000001p-2, -0x1.0000000000000p-2, -0x1.0000000000001p-2, 0x1.ffffffffffffep-3, 0x1.0000000000001p-2, -0x1.ffffffffffff6p-3, -0x1.ffffffffffffcp-3, 0x1.ffffffffffff5p-3, 0x1.ffffffffffffdp-3, -0x1.ffffffffffff3p-3, -0x1.ffffffffffffep-3, 0x1.ffffffffffff2p-3, 0x1.0000000000000p-2, -0x1.ffffffffffff2p-3, -0x1.0000000000001p-2, 0x1.ffffffffffff0p-3,
-    0x1.cb598cc4beea1p-3, -0x1.3f4a237187eaep-2, -0x1.a4608aafa8529p-4, 0x1.684b9c80f1a8cp-2, -0x1.1be35182fe58ap-5, -0x1.5a730c6c21c6ap-2, 0x1.5553e3f5b5e54p-3, 0x1.17dc13dab2ddap-2, -0x1.17dc13dab2dd6p-2, -0x1.5553e3f5b5e60p-3, 0x1.5a730c6c21c68p-2, 0x1.1be35182fe61cp-5, -0x1.684b9c80f1a8dp-2, 0x1.a4608aafa8523p-4, 0x1.3f4a237187eacp-2, -0x1.cb598cc4bee91p-3,
-    0x1.92469c0dcf32fp-3, -0x1.63150b15e8536p-2, 0x1.1a855dec071b6p-4, 0x1.2d062ef88e31bp-2, -0x1.2d062ef88e319p-2, -0x1.1a855dec071dcp-4, 0x1.63150b15e8535p-2, -0x1.92469c0dcf325p-3, -0x1.92469c0dcf333p-3, 0x1.63150b15e8536p-2, -0x1.1a855dec071bdp-4, -0x1.2d062ef88e324p-2, 0x1.2d062ef88e31dp-2, 0x1.1a855dec071ebp-4, -0x1.63150b15e8534p-2, 0x1.92469c0dcf31fp-3,
-    0x1.5553e3f5b5e5ap-3, -0x1.684b9c80f1a8cp-2, 0x1.cb598cc4beea2p-3, 0x1.a4608aafa852cp-4, -0x1.5a730c6c21c67p-2, 0x1.17dc13dab2dcfp-2, 0x1.1be35182fe55cp-5, -0x1.3f4a237187eb6p-2, 0x1.3f4a237187eb2p-2, -0x1.1be35182fe517p-5, -0x1.17dc13dab2dd5p-2, 0x1.5a730c6c21c61p-2, -0x1.a4608aafa8520p-4, -0x1.cb598cc4beecap-3, 0x1.684b9c80f1a8bp-2, -0x1.5553e3f5b5e23p-3,
-    0x1.1517a7bdb3896p-3, -0x1.4e7ae9144f0fdp-2, 0x1.4e7ae9144f0fbp-2, -0x1.1517a7bdb3897p-3, -0x1.1517a7bdb389fp-3, 0x1.4e7ae9144f100p-2, -0x1.4e7ae9144f0fep-2, 0x1.1517a7bdb3869p-3, 0x1.1517a7bdb387ap-3, -0x1.4e7ae9144f102p-2, 0x1.4e7ae9144f0fdp-2, -0x1.1517a7bdb388ep-3, -0x1.1517a7bdb38a8p-3, 0x1.4e7ae9144f102p-2, -0x1.4e7ae9144f0f4p-2, 0x1.1517a7bdb385fp-3,
-    0x1.a4608aafa8526p-4, -0x1.17dc13dab2dd7p-2, 0x1.684b9c80f1a8cp-2, -0x1.3f4a237187eaep-2, 0x1.5553e3f5b5e54p-3, 0x1.1be35182fe610p-5, -0x1.cb598cc4beea2p-3, 0x1.5a730c6c21c6bp-2, -0x1.5a730c6c21c68p-2, 0x1.cb598cc4bee92p-3, -0x1.1be35182fe5bfp-5, -0x1.5553e3f5b5e66p-3, 0x1.3f4a237187eadp-2, -0x1.684b9c80f1a8bp-2, 0x1.17dc13dab2dcbp-2, -0x1.a4608aafa84bdp-4,
-    0x1.1a855dec071b7p-4, -0x1.92469c0dcf32dp-3, 0x1.2d062ef88e31bp-2, -0x1.63150b15e8537p-2, 0x1.63150b15e8536p-2, -0x1.2d062ef88e312p-2, 0x1.92469c0dcf34ap-3, -0x1.1a855dec07164p-4, -0x1.1a855dec07190p-4, 0x1.92469c0dcf35cp-3, -0x1.2d062ef88e318p-2, 0x1.63150b15e8539p-2, -0x1.63150b15e853ap-2, 0x1.2d062ef88e302p-2, -0x1.92469c0dcf31bp-3, 0x1.1a855dec0714fp-4,
-    0x1.1be35182fe5b3p-5, -0x1.a4608aafa8529p-4, 0x1.5553e3f5b5e5cp-3, -0x1.cb598cc4bee9fp-3, 0x1.17dc13dab2ddap-2, -0x1.3f4a237187eb6p-2, 0x1.5a730c6c21c65p-2, -0x1.684b9c80f1a8dp-2, 0x1.684b9c80f1a8bp-2, -0x1.5a730c6c21c61p-2, 0x1.3f4a237187eb1p-2, -0x1.17dc13dab2dbdp-2, 0x1.cb598cc4bee8dp-3, -0x1.5553e3f5b5e20p-3, 0x1.a4608aafa8511p-4, -0x1.1be35182fe4e6p-5,
-};
-
-// byte `col` of LDS row `row` (pitch in dwords)
-SO_DEV int lds_byte(const uint32_t* base, int pitch, int row, int col) {
-    return (int)((base[row * pitch + (col >> 2)] >> (8 * (col & 3))) & 255u);
-}
 
 // The exact transform path of one block: 16 lanes (l = row) run scipy.fftpack's pocketfft
 // DCT-II / DCT-III sequence in FP64 (so_dct.h) -- the arithmetic of inter_tq_kernel<16,
@@ -1529,178 +1491,9 @@ SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur
         }
     }
     __syncthreads();
-#if SO_TQ_MFMA
-    {
-        // Transforms on the matrix cores: each wave takes blocks g = wave, wave + NW.  The
-        // 2-D DCT is two FP64 GEMMs against the orthonormal DCT matrix D (v_mfma_f64_16x16x4:
-        // Y = D (X D^T), Z = D^T (DQ D)), the accumulator of the first being the B operand of
-        // the second as it stands.  The result equals the reference's pocketfft value to
-        // ~1e-10, so rint() agrees with it unless a value lies within 1e-7 of a half-integer:
-        // such a block (a tie) is redone by the exact VALU path.  Quantisation, tokens (row
-        // masks by ballot, transitions in SALU), stores and SSE work on the MFMA layout
-        // (lane: col = lane & 15, rows (lane >> 4) + 4 r).
-        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-        const int lc = lane & 15, lh = lane >> 4;
-        double* const wscr = S.un + wave * (16 * 17);   // per-wave LDS: DQ transpose / exact path
-        uint32_t ties = 0;   // blocks (bit g) whose values came within 1e-7 of a half-integer
-#pragma unroll 1
-        for (int g = wave; g < G::NBLK; g += G::NW) {
-            const int bxl = g % TBX, byl = g / TBX;
-            const int gbx = bx0 + bxl, gby = byt0 + byl;
-            if (gbx >= nbx || gby >= by1) continue;   // uniform
-            const size_t b = (size_t)(gby - by0) * nbx + gbx;
-            const int x = gbx * 16, y = gby * 16;
-            const int qpr = qp_map ? qp_map[(size_t)gby * nbx + gbx] : (qp_row ? qp_row[gby] : qp_rd);
-            const int dx = S.mer[g][0], dy = S.mer[g][1], rf = S.mer[g][2], sad = S.mer[g][3];
-            const int prow0 = byl * 16 + SR + dy, pcol0 = bxl * 16 + SR + dx;   // window coordinates
-            const int crow0 = byl * 16, ccol0 = bxl * 16;                       // current tile coordinates
-            // forward: U = X D^T (A = X in operand layout: row lc, col 4 s + lh), Y = D U
-            typedef double so_d4 __attribute__((ext_vector_type(4)));
-            // D fragments, loaded per block (cached): not held in registers across the loop
-            int di = lc * 16 + lh;
-            asm volatile("" : "+v"(di));
-            double dA[4];                              // D[lc][4s + lh]
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) dA[s4] = kDct16[di + 4 * s4];
-            so_d4 U = {0.0, 0.0, 0.0, 0.0}, Y = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-                const int j = 4 * s4 + lh;
-                const int cv = lds_byte(S.curt, G::CPD, crow0 + lc, ccol0 + j);
-                const int pv = lds_byte(S.win, G::RP, prow0 + lc, pcol0 + j);
-                U = __builtin_amdgcn_mfma_f64_16x16x4f64((double)(cv - pv), dA[s4], U, 0, 0, 0);
-            }
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) Y = __builtin_amdgcn_mfma_f64_16x16x4f64(dA[s4], U[s4], Y, 0, 0, 0);
-            bool tie = false;
-            double yr[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                yr[r] = __builtin_rint(Y[r]);
-                tie |= __builtin_fabs(Y[r] - yr[r]) > 0.5 - 1e-7;
-            }
-            int q[4];
-            so_d4 DQ;
-            so_d4 Z = {0.0, 0.0, 0.0, 0.0};
-            uint64_t nzb[4] = {0, 0, 0, 0};
-            if (!__builtin_amdgcn_ballot_w64(tie)) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = lh + 4 * r, k = q_exp_fast<16>(row, lc, qpr);
-                    const double qd = __builtin_rint(__builtin_amdgcn_ldexp(yr[r], -k));
-                    q[r] = (int)qd;
-                    DQ[r] = __builtin_amdgcn_ldexp(qd, k);
-                    nzb[r] = __builtin_amdgcn_ballot_w64(q[r] != 0);
-                }
-                // inverse: U' = DQ D (A = DQ transposed through LDS), Z = D^T U'
-                int dj = lh * 16 + lc;
-                asm volatile("" : "+v"(dj));
-                double dB[4];                          // D[4s + lh][lc]
-#pragma unroll
-                for (int s4 = 0; s4 < 4; ++s4) dB[s4] = kDct16[dj + 64 * s4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) wscr[(lh + 4 * r) * 17 + lc] = DQ[r];
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                so_d4 V = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int s4 = 0; s4 < 4; ++s4)
-                    V = __builtin_amdgcn_mfma_f64_16x16x4f64(wscr[lc * 17 + 4 * s4 + lh], dB[s4], V, 0, 0, 0);
-#pragma unroll
-                for (int s4 = 0; s4 < 4; ++s4) Z = __builtin_amdgcn_mfma_f64_16x16x4f64(dB[s4], V[s4], Z, 0, 0, 0);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-                for (int r = 0; r < 4; ++r) tie |= __builtin_fabs(Z[r] - __builtin_rint(Z[r])) > 0.5 - 1e-7;
-            }
-#ifdef SO_STAMPS
-            if (lane == 0) {
-                atomicAdd(&g_tq_counts[0], 1ull);
-                if (__builtin_amdgcn_ballot_w64(tie)) atomicAdd(&g_tq_counts[1], 1ull);
-            }
-#endif
-            if (__builtin_amdgcn_ballot_w64(tie)) {   // uniform: a tie -> the exact path, below
-                ties |= 1u << g;
-                continue;
-            }
-            // tokens: row masks M_i (bit = column) from the four ballots, transitions in SALU
-            // (ballot r holds row lh + 4 r of lane group lh at bits 16 lh .. 16 lh + 15)
-            uint32_t M[16];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) M[i] = (uint32_t)(nzb[i >> 2] >> (16 * (i & 3))) & 0xFFFFu;
-            int tok = 1;   // entropy_encoder_block length: nnz + runs, as block_tokens (so_block.h)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                tok += __builtin_popcount(M[i]);
-                if (i <= 14) {
-                    tok += __builtin_popcount((M[i] ^ (M[i + 1] << 1)) & 0xFFFEu);
-                    tok += (int)((M[i] & 1u) ^ ((M[0] >> (i + 1)) & 1u));
-                }
-                if (i >= 1) tok += (int)(((M[15] >> (i - 1)) & 1u) ^ ((M[i] >> 15) & 1u));
-            }
-            tok = __builtin_amdgcn_readfirstlane(tok);
-            // QTC (int16, 512 B) and the reconstruction (256 B) are staged in the wave's LDS
-            // and leave as whole 16-byte rows: element-wise 2- and 1-byte global stores (the
-            // write-through ones above all) cost a fabric transaction each
-            int16_t* const qs = reinterpret_cast<int16_t*>(wscr);
-            uint8_t* const rs = reinterpret_cast<uint8_t*>(wscr) + 512;
-            int sse = 0;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = lh + 4 * r;
-                qs[row * 16 + lc] = (int16_t)q[r];
-                const int pv = lds_byte(S.win, G::RP, prow0 + row, pcol0 + lc);
-                const int rec = (pv + (int)__builtin_rint(Z[r])) & 255;
-                rs[row * 16 + lc] = (uint8_t)rec;
-                const int d = lds_byte(S.curt, G::CPD, crow0 + row, ccol0 + lc) - rec;
-                sse += d * d;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (lane < 32) {
-                const uint4 v = reinterpret_cast<const uint4*>(qs)[lane];
-                reinterpret_cast<uint4*>(o.qtc + b * 256)[lane] = v;
-            } else if (lane < 48) {
-                const int row = lane - 32;
-                const uint4 v4 = reinterpret_cast<const uint4*>(rs)[row];
-                uint8_t* const rp = o.recon + (size_t)(y + row) * W + x;
-                if constexpr (SC1) {
-                    const so_v4u v = {v4.x, v4.y, v4.z, v4.w};
-                    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(rp), "v"(v) : "memory");
-                } else {
-                    *reinterpret_cast<uint4*>(rp) = v4;
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (o.sse) sse = (int)wave_sum_u32((uint32_t)sse);
-            if (lane < 12) o.mv[b * 12 + lane] = (int16_t)(lane == 0 ? dx : lane == 1 ? dy : lane == 2 ? rf : 0);
-            if (lane == 0) {
-                o.split[b] = 0;
-                o.tokens[b] = tok;
-                o.mae[b] = sad;
-                if (o.sse) o.sse[b] = sse;
-            }
-        }
-        // the exact VALU path for the blocks with a tie (nothing of the MFMA loop is live here)
-        ties = __builtin_amdgcn_readfirstlane(ties);
-#pragma unroll 1
-        while (ties) {
-            const int g = __builtin_ctz(ties);
-            ties &= ties - 1;
-            if (lane < 16)
-                tq16_exact<G, SC1>(S, g, lane, wscr, bx0, byt0, nbx, by0, by1, W, qp_rd, qp_row, qp_map, o);
-        }
-    }
-#else
     if (tid < G::NBLK * 16)
         tq16_exact<G, SC1>(S, tid >> 4, tid & 15, S.un + (tid >> 4) * (16 * 17), bx0, byt0, nbx, by0, by1, W, qp_rd,
                            qp_row, qp_map, o);
-#endif
     if constexpr (SC1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
     __syncthreads();
 }

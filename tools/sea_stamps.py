@@ -42,12 +42,6 @@ def main():
             _lib.check(lib.so_me_full_search(fr[2].data_ptr(), refs, 1, h, w, 16, 16, best.data_ptr(), None,
                                              _lib.stream_handle()), "me")
     torch.cuda.synchronize()
-    if hasattr(lib, "so_debug_tq_counts"):
-        cnt = (ctypes.c_ulonglong * 2)()
-        lib.so_debug_tq_counts.argtypes = [ctypes.c_void_p, ctypes.c_int]
-        lib.so_debug_tq_counts(ctypes.addressof(cnt), 1)
-        if cnt[0]:
-            print(f"MFMA transform path: {cnt[0]} blocks, {cnt[1]} with a tie ({cnt[1] / cnt[0] * 100:.2f}%)")
     s = stamps.cpu().numpy().astype(np.int64)
     rt0, rt1 = s[:, 0], s[:, 7]
     cyc = s[:, 6] - s[:, 1]
