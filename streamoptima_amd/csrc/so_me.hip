@@ -1479,6 +1479,7 @@ SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur
     sea2_tile<G>(L, tile, cur, refs, 1, H, W, by0, by1, 0);   // ends with a barrier
 
     const int tid = opaque_tid();
+    SO_SEA_STAMP(5, __builtin_amdgcn_s_memtime());
     const int nbx = W / 16;
     const int tiles_x = (nbx + TBX - 1) / TBX;
     const int bx0 = (tile % tiles_x) * TBX, byt0 = by0 + (tile / tiles_x) * TBY;
@@ -1509,6 +1510,18 @@ p_tile_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W, int by
     using G = Sea2GeoT<NW>;
     __shared__ PTileLds<G> S;
     ptile_body<G, false>(S, blockIdx.x, cur, refs.p[0], H, W, by0, by1, qp_rd, qp_row, qp_map, out_best, o);
+#ifdef SO_STAMPS
+    const int tid = threadIdx.x;
+    if (tid == 0) {   // tools/sea_stamps.py (STAMP_FUSED=1): epilogue = records + transforms
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        SO_SEA_STAMP(6, __builtin_amdgcn_s_memtime());
+        SO_SEA_STAMP(7, __builtin_amdgcn_s_memrealtime());
+        SO_SEA_STAMP(8, ((unsigned long long)xcc << 32) | hw);
+        SO_SEA_STAMP(9, ((unsigned long long)S.st[0] << 32) | S.st[1]);
+    }
+#endif
 }
 
 int p_tile_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int by0, int by1, int qp_rd,
