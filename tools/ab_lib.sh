@@ -1,6 +1,7 @@
 #!/bin/bash
 # bench A/B: the default library vs each tools/_ab/*.so (SO_LIB_PATH), 4K and 1080p.
 cd "$GRAFT_REPO_ROOT" || exit 1
+shopt -s nullglob
 for cfg in ${CFGS:-4k 1080p}; do
   for lib in "" tools/_ab/*.so; do
     SO_LIB_PATH=$lib timeout -k 10 200 python bench.py --no-cpu-baseline --config $cfg --kernel-reps 10 > gpurun_out/ab_$cfg.log 2>&1 || { tail -3 gpurun_out/ab_$cfg.log; exit 1; }
