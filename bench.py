@@ -82,15 +82,20 @@ def parse():
     return ap.parse_args()
 
 
-def dist_setup():
+def dist_setup(backend: str = "nccl"):
+    """One process per GPU (torchrun env).  backend "nccl" is RCCL on ROCm; the CPU tests
+    drive the same code with "gloo"."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    elif backend == "nccl":
         torch.cuda.set_device(0)
     return world, rank, local
 
@@ -105,7 +110,8 @@ def max_over_ranks(x: float, world: int) -> float:
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
