@@ -121,12 +121,9 @@ def me_kernel_name(vbs: bool, me: str = "full") -> str:
         f = "true" if "fme" in me else "false"
         s = "true" if vbs else "false"
         return {"fme": f"me_fme_kernel<{s}>"}.get(me, f"me_fastpred_kernel<{f}, {s}, 16>")
-    impl = os.environ.get("SO_ME_IMPL")
-    if impl == "fast":
-        return "me_fast_kernel"
-    if impl == "dense" or vbs:
+    if os.environ.get("SO_ME_IMPL") == "dense" or vbs:
         return "me_wave_kernel<16, %s>" % ("true" if vbs else "false")
-    return "me_sea2_kernel" if impl != "sea1" else "me_sea_kernel"
+    return "me_sea2_kernel"
 
 
 def kernel_roofline(codec, frames_dev, symbols, reps: int, me_variant: str = "full") -> dict:

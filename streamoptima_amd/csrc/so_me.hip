@@ -43,19 +43,6 @@ SO_DEV void decode_key(uint64_t k, int sr, int32_t* out) {
     out[3] = (int)(k >> 32);
 }
 
-// Geometry of the round-1 kernel (me_fast_kernel, kept for A/B).
-template <int BS>
-struct MeGeo {
-    static constexpr int SR = 16;
-    static constexpr int D = 2 * SR + 1;                  // 33 candidates per axis
-    static constexpr int TB = (BS == 16) ? 8 : 16;        // blocks per tile side
-    static constexpr int TPX = TB * BS;                   // 128 px
-    static constexpr int WP = TPX + 2 * SR;               // 160: window rows == pitch (bytes)
-    static constexpr int CP = TPX;                        // current tile pitch
-    static constexpr int NBLK = TB * TB;
-    static constexpr int NTHREADS = 704;                  // 11 waves
-};
-
 // ---------------------------------------------------------------------------------------
 // Wave path (default): one wavefront per block, current block in SGPRs, no v_alignbyte.
 //
@@ -235,7 +222,7 @@ SO_DEV uint64_t widen17_fme(uint32_t b32, uint32_t X, int hh, int xi, bool xok, 
 
 // Dense search of one block by one wavefront (phase 1 + phase 2 over the four shifted
 // window copies in `win`); merges the block key into keys[u] and, with VBS, the quadrant
-// keys into keys[nblk + 4u + j].  Shared by me_wave_kernel and me_sea_kernel's fallback.
+// keys into keys[nblk + 4u + j].  Used by me_wave_kernel.
 // ONE: the window is a single copy (me_sea2_kernel): the lane's 16 bytes at any column are
 // five ds_read_b32 + four v_alignbyte per row instead of four reads of its shifted copy.
 template <int BS, bool SUB, int RPD, int CS, bool FME = false, bool ONE = false>
@@ -574,303 +561,33 @@ int me_fme_launch(const uint8_t* cur, const uint8_t* planes, size_t pstride, int
 }
 
 // ---------------------------------------------------------------------------------------
-// SEA path (default for bs 16 without VBS): exact successive elimination.
+// SEA path (me_sea2_kernel and the fused tile kernels; the default for bs 16 without VBS):
+// exact successive elimination.
 //
 // With S = a 4x4 pixel sum (0..4080) and q = S >> 4 (a byte), write S = 16q + r, r < 16.
 // Then |S_cur - S_ref| >= 16|q_cur - q_ref| - 15, so for a candidate c
 //     SAD(c) >= sum_k |S_cur(k) - S_ref(c, k)| >= 16 * LBq(c) - 240,
 //     LBq(c) = sum over the 16 4x4 sub-blocks k of |q_cur(k) - q_ref(c, k)|
 // (triangle inequality).  Per block:
-//   1. LBq for all 1089 candidates: lane (xi, hh) as in the dense phase 1 (17 dy each, plus
-//      the dx = +16 column on lanes 0..32); a candidate's four byte sums of one 4x4 row are
-//      one dword, so LBq costs 4 v_sad_u8 per candidate instead of 64 for its SAD;
+//   1. LBq for all 1089 candidates; a candidate's four byte sums of one 4x4 row are one
+//      dword, so LBq costs 4 v_sad_u8 per candidate instead of 64 for its SAD;
 //   2. U = the full SAD of the valid candidate with the smallest LBq, so U >= min SAD;
 //   3. every valid candidate with 16 * LBq - 240 <= U gets its full SAD (survivors,
 //      compacted into an LDS list).  Any other candidate has SAD > U >= min SAD, so it can
 //      neither be the minimum nor tie it: the lexicographic key result is exactly the full
-//      search's.  More than CAP survivors (weak bounds: flat or noise-like content) falls
-//      back to the dense wave search of the block.
-// The reference's byte sums (B4) are built per tile in LDS from the shifted window copies
-// (one v_sad_u8 against 0 per row dword, sliding down each column), in a column layout
-// L(c) = (c&3)*40 + (c>>2) bytes that puts the sums at c, c+4, c+8, c+12 -- one 4x4 row of a
-// candidate -- in consecutive bytes.
-// ---------------------------------------------------------------------------------------
-struct SeaGeo {
-    static constexpr int BS = 16, SR = 16, NT = 17;
-    static constexpr int TBX = 8, TPY = 32, TBY = 2, TPX = 128;
-    static constexpr int WR = TPY + 2 * SR;               // 64 window rows
-    // copy row pitch: 40 dwords of window + 1 pad, so reads that walk down a column (dy
-    // lanes, survivor rows) hit 32 different banks (41 r mod 32) instead of 4 (40 r mod 32)
-    static constexpr int RPD = (TPX + 2 * SR) / 4 + 1;
-    static constexpr int CSTRIDE = WR * RPD + 8;           // = 8 (mod 32): see MeWGeo
-    static constexpr int B4R = WR - 3, B4C = TPX + 2 * SR - 3, B4P = 160;   // 61 x 157 byte sums (+4 pad)
-    static constexpr int NBLK = TBX * TBY;
-    static constexpr int NW = 8, NTHREADS = NW * 64;
-    static constexpr int CAP = 192;                       // survivors per block before fallback
-};
-
-
-
-__global__ void __launch_bounds__(SeaGeo::NTHREADS) __attribute__((amdgpu_waves_per_eu(4)))
-me_sea_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
-              int32_t* __restrict__ out_best, int probe) {
-    using G = SeaGeo;
-    constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RPD = G::RPD, CS = G::CSTRIDE, NT = G::NT;
-    constexpr int B4P = G::B4P, CAP = G::CAP, CP = G::TPX;
-    __shared__ uint32_t win[4 * CS];
-    __shared__ uint32_t b4w[(G::B4R * B4P + 4) / 4];
-    uint8_t* b4 = reinterpret_cast<uint8_t*>(b4w);
-    __shared__ uint32_t curt[G::TPY * CP / 4];      // current tile, 32 rows x 128 B
-    __shared__ uint32_t a4[G::NBLK * 4];           // per block: [j] = 4 byte sums (4x4 >> 4) of row j
-    __shared__ uint16_t list[G::NW * CAP];
-    __shared__ unsigned long long keys[G::NBLK];
-
-    const int nbx = W / 16;
-    const int tiles_x = (nbx + TBX - 1) / TBX;
-    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
-    const int bx0 = tx * TBX, byt0 = by0 + ty * TBY;
-    const int x0 = bx0 * 16, y0 = byt0 * 16;
-    const int tid = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-
-    for (int i = tid; i < G::NBLK; i += G::NTHREADS) keys[i] = kNoKey;
-    // current tile (zero outside the frame / stripe)
-    {
-        constexpr int N = G::TPY * CP / 4, IT = (N + G::NTHREADS - 1) / G::NTHREADS;
-        uint32_t v[IT];
-#pragma unroll
-        for (int k = 0; k < IT; ++k) {
-            const int i = tid + k * G::NTHREADS;
-            const int rr = i / (CP / 4), m = i - rr * (CP / 4);
-            const int gy = y0 + rr, gx = x0 + 4 * m;
-            v[k] = 0;
-            if (i < N && gy < H && gx + 4 <= W) v[k] = *reinterpret_cast<const uint32_t*>(cur + (size_t)gy * W + gx);
-        }
-#pragma unroll
-        for (int k = 0; k < IT; ++k)
-            if (tid + k * G::NTHREADS < N) curt[tid + k * G::NTHREADS] = v[k];
-    }
-    __syncthreads();
-    // current blocks' 4x4 byte sums: item (block, j, ii) -> byte ii of a4[blk*4 + j]
-    for (int i = tid; i < G::NBLK * 16; i += G::NTHREADS) {
-        const int blk = i >> 4, j = (i >> 2) & 3, ii = i & 3;
-        const int rr = (blk / TBX) * 16 + 4 * j, m = (blk % TBX) * 4 + ii;
-        uint32_t sum = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) sum = __builtin_amdgcn_sad_u8(curt[(rr + q) * (CP / 4) + m], 0u, sum);
-        reinterpret_cast<uint8_t*>(a4)[i] = (uint8_t)(sum >> 4);
-    }
-    for (int r = 0; r < nref; ++r) {
-        const uint8_t* ref = refs.p[r];
-        __syncthreads();
-        stage_window<G::WR, RPD, CS, G::NTHREADS>(win, ref, H, W, x0 - SR, y0 - SR, tid);
-        __syncthreads();
-        // B4(r, c): thread per (column, quarter of the rows) slides a 4-row sum of the
-        // horizontal 4-sums (one v_sad_u8 against 0 each) down its column
-        for (int i = tid; i < G::B4C * 4; i += G::NTHREADS) {
-            const int qtr = i / G::B4C, c = i - qtr * G::B4C;   // consecutive lanes: consecutive columns
-            const int r0 = qtr * 16, r1 = qtr == 3 ? G::B4R : r0 + 16;   // output rows [r0, r1)
-            const uint32_t* q = win + (c & 3) * CS + (c >> 2);
-            uint8_t* o = b4 + (c & 3) * 40 + (c >> 2);
-            uint32_t h0 = __builtin_amdgcn_sad_u8(q[r0 * RPD], 0u, 0u);
-            uint32_t h1 = __builtin_amdgcn_sad_u8(q[(r0 + 1) * RPD], 0u, 0u);
-            uint32_t h2 = __builtin_amdgcn_sad_u8(q[(r0 + 2) * RPD], 0u, 0u);
-            for (int rr = r0; rr < r1; ++rr) {
-                const uint32_t h3 = __builtin_amdgcn_sad_u8(q[(rr + 3) * RPD], 0u, 0u);
-                o[rr * B4P] = (uint8_t)((h0 + h1 + h2 + h3) >> 4);
-                h0 = h1; h1 = h2; h2 = h3;
-            }
-        }
-        __syncthreads();
-        if (probe == 1) continue;   // timing probe (tools/me_ab2.py): staging + byte sums only
-#pragma unroll 1
-        for (int u = wave; u < G::NBLK; u += G::NW) {
-            const int bxl = u % TBX, byl = u / TBX;
-            if (bx0 + bxl >= nbx || byt0 + byl >= by1) continue;   // wave-uniform
-            const int x = x0 + bxl * 16, y = y0 + byl * 16;
-            int lane = tid & 63;
-            asm volatile("" : "+v"(lane));
-            const int xi = lane & 31, hh = lane >> 5;
-            const int d2 = lane < 33 ? lane : 32;
-            uint32_t A[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) A[j] = a4[u * 4 + j];
-            // ---- 1. lower bounds ------------------------------------------------------------
-            const int cB = bxl * 16 + xi;
-            const int lb0 = (byl * 16 + 16 * hh) * B4P + (cB & 3) * 40 + (cB >> 2);   // byte offset
-            const uint32_t bsh = (uint32_t)lb0 & 3;
-            int lo1 = lb0 >> 2;
-            asm volatile("" : "+v"(lo1));
-            lds_vu32p p1 = (lds_vu32p)(b4w + lo1);
-            uint32_t lb[NT];
-#pragma unroll
-            for (int t = 0; t < NT; ++t) lb[t] = 0;
-            uint32_t n0 = p1[0], n1 = p1[1];
-#pragma unroll
-            for (int sr_ = 0; sr_ < NT + 12; ++sr_) {       // byte-sum rows of the lane's strip
-                const uint32_t w0 = n0, w1 = n1;
-                if (sr_ + 1 < NT + 12) { n0 = p1[(sr_ + 1) * (B4P / 4)]; n1 = p1[(sr_ + 1) * (B4P / 4) + 1]; }
-                const uint32_t P = __builtin_amdgcn_alignbyte(w1, w0, bsh);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int t = sr_ - 4 * j;
-                    if (t >= 0 && t < NT) lb[t] = __builtin_amdgcn_sad_u8(A[j], P, lb[t]);
-                }
-                acc_fence_n<NT>(lb);
-            }
-            uint32_t lb2 = 0;
-            {
-                // column c2 = bxl*16 + 32 = 0 (mod 4): its byte sums start dword-aligned
-                int lo2 = ((byl * 16 + d2) * B4P + ((bxl * 16 + 32) >> 2)) >> 2;
-                asm volatile("" : "+v"(lo2));
-                lds_vu32p p2 = (lds_vu32p)(b4w + lo2);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) lb2 = __builtin_amdgcn_sad_u8(A[j], p2[4 * j * (B4P / 4)], lb2);
-            }
-            // validity: dy index in [dlo, dhi], dx by lane.  Edge blocks (uniform) overwrite the
-            // bounds of out-of-frame dy with kBig once; everything below is mask-free.
-            constexpr uint32_t kBig = 0x07FFFFFFu;            // (kBig << 5) | t never wraps
-            int dlo = SR - y;              dlo = dlo < 0 ? 0 : dlo;
-            int dhi = H - 16 - y + SR - 1; dhi = dhi > 32 ? 32 : dhi;
-            const bool xok = (x + xi - 16 >= 0) && (x + xi - 16 < W - 16);
-            const bool ok2 = lane < 33 && (x + 16 < W - 16) && d2 >= dlo && d2 <= dhi;
-            if (dlo > 0 || dhi < 32) {
-                const int tlo = dlo - 16 * hh, thi = dhi - 16 * hh;
-#pragma unroll
-                for (int t = 0; t < NT; ++t) lb[t] = (t < tlo || t > thi) ? kBig : lb[t];
-            }
-            // ---- 2. U = SAD of the smallest-LB candidate ------------------------------------
-            uint32_t kt = 0xFFFFFFFFu;                         // (lb << 5 | t), lane-local
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                const uint32_t k = (lb[t] << 5) | (uint32_t)t;
-                kt = k < kt ? k : kt;
-            }
-            uint32_t kl = (xok && (kt >> 5) != kBig) ? ((kt >> 5) << 11) | (uint32_t)(xi * 33 + 16 * hh + (kt & 31))
-                                                      : 0xFFFFFFFFu;
-            {
-                const uint32_t k2 = (lb2 << 11) | (uint32_t)(32 * 33 + d2);
-                kl = (ok2 && k2 < kl) ? k2 : kl;
-            }
-            const uint32_t kmin = wave_min_u32(kl);
-            if (kmin == 0xFFFFFFFFu) continue;                 // no valid candidate: key stays none
-            const int cs = (int)(kmin & 2047), cdx = cs / 33, cdi = cs - cdx * 33;
-            const int crow0 = byl * 16 * (CP / 4) + bxl * 4;   // current block in curt (dwords)
-            uint32_t U;
-            {
-                const int row = lane >> 2, kk = lane & 3;
-                const int col = bxl * 16 + cdx;
-                const uint32_t w = ((lds_vu32p)win)[(col & 3) * CS + (byl * 16 + cdi + row) * RPD + (col >> 2) + kk];
-                const uint32_t c = curt[crow0 + row * (CP / 4) + kk];
-                U = wave_sum_u32(__builtin_amdgcn_sad_u8(c, w, 0u));
-            }
-            if (probe == 2) {          // timing probe: bounds + U, no survivor search
-                if (lane == 0 && U < keys[u]) keys[u] = U;
-                continue;
-            }
-            // ---- 3. survivors: 16 LBq - 240 <= U, i.e. LBq < qU1 (one v_cmp per t) -----------
-            const uint32_t qU = (U + 240) >> 4;
-            const uint32_t qU1 = xok ? qU + 1 : 0u;            // dx-invalid lanes: nothing passes
-            uint32_t nsur = 0;
-            uint16_t* mylist = list + wave * CAP;
-#pragma unroll
-            for (int t = 0; t <= NT; ++t) {
-                const bool sv = t < NT ? lb[t] < qU1 : (ok2 && lb2 <= qU);
-                const uint64_t bal = __ballot(sv);
-                if (bal) {                                     // wave-uniform, rare
-                    const int cand = t < NT ? xi * 33 + 16 * hh + t : 32 * 33 + d2;
-                    const uint32_t pos = nsur + lane_prefix(bal);
-                    if (sv && pos < (uint32_t)CAP) mylist[pos] = (uint16_t)cand;
-                    nsur += (uint32_t)__builtin_popcountll(bal);
-                }
-            }
-            if (nsur > (uint32_t)CAP) {
-                if (probe == 3) continue;   // timing probe: no dense fallback
-                wave_dense_block<16, false, RPD, CS>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u, tid, r);
-                continue;
-            }
-            if (probe == 4) continue;       // timing probe: bounds, U and the survivor list only
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            uint64_t best = kNoKey;
-            if (nsur <= 8) {
-                // few survivors: four per pass, 16 lanes (one DPP row) per survivor, one block
-                // row per lane
-                const int sidx = lane >> 4, row = lane & 15;
-                const uint32_t* cr_ = curt + crow0 + row * (CP / 4);
-                const uint32_t c0 = cr_[0], c1 = cr_[1], c2 = cr_[2], c3 = cr_[3];
-#pragma unroll 1
-                for (uint32_t s0 = 0; s0 < nsur; s0 += 4) {
-                    const bool act = s0 + (uint32_t)sidx < nsur;
-                    const int cand = act ? (int)mylist[s0 + sidx] : cs;
-                    const int dxi = cand / 33, di = cand - dxi * 33;
-                    const int col = bxl * 16 + dxi;
-                    int wo = (col & 3) * CS + (byl * 16 + di + row) * RPD + (col >> 2);
-                    asm volatile("" : "+v"(wo));
-                    lds_vu32p wr_ = (lds_vu32p)(win + wo);   // 4-byte aligned only: keep b32 reads
-                    uint32_t sad = __builtin_amdgcn_sad_u8(c0, wr_[0], 0u);
-                    sad = __builtin_amdgcn_sad_u8(c1, wr_[1], sad);
-                    sad = __builtin_amdgcn_sad_u8(c2, wr_[2], sad);
-                    sad = __builtin_amdgcn_sad_u8(c3, wr_[3], sad);
-                    sad = row_sum_u32(sad);                    // 16 lanes = one DPP row
-                    const int dx = dxi - 16, dy = di - 16;
-                    const uint64_t key = me_key(sad, (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)),
-                                                (uint32_t)r, (uint32_t)cand);
-                    best = (act && key < best) ? key : best;
-                }
-            } else {
-                // many: one survivor per lane, 64 at a time
-#pragma unroll 1
-                for (uint32_t k0 = 0; k0 < nsur; k0 += 64) {
-                    const uint32_t idx = k0 + (uint32_t)lane;
-                    const int cand = idx < nsur ? (int)mylist[idx] : cs;
-                    const int dxi = cand / 33, di = cand - dxi * 33;
-                    const int col = bxl * 16 + dxi;
-                    int wo = (col & 3) * CS + (byl * 16 + di) * RPD + (col >> 2);
-                    asm volatile("" : "+v"(wo));
-                    lds_vu32p wp = (lds_vu32p)(win + wo);
-                    uint32_t sad = 0;
-#pragma unroll
-                    for (int rr = 0; rr < 16; ++rr) {
-#pragma unroll
-                        for (int kk = 0; kk < 4; ++kk)
-                            sad = __builtin_amdgcn_sad_u8(curt[crow0 + rr * (CP / 4) + kk], wp[rr * RPD + kk], sad);
-                        asm volatile("" : "+v"(sad) : : "memory");
-                    }
-                    const int dx = dxi - 16, dy = di - 16;
-                    const uint64_t key = me_key(sad, (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)),
-                                                (uint32_t)r, (uint32_t)cand);
-                    best = (idx < nsur && key < best) ? key : best;
-                }
-            }
-            best = wave_min_u64_dpp(best);
-            if (lane == 0 && best < keys[u]) keys[u] = best;
-        }
-    }
-    __syncthreads();
-    for (int i = tid; i < G::NBLK; i += G::NTHREADS) {
-        const int gbx = bx0 + i % TBX, gby = byt0 + i / TBX;
-        if (gbx >= nbx || gby >= by1) continue;
-        decode_key(keys[i], SR, out_best + ((size_t)(gby - by0) * nbx + gbx) * 4);
-    }
-}
-
-// ---------------------------------------------------------------------------------------
-// SEA, single-copy window (me_sea2_kernel, the default for bs 16 without VBS).
-//
-// Same exact successive elimination as me_sea_kernel (bound, U, survivors, fallback), with
-// the per-block overheads cut -- the old kernel spent 23 of its 66 us per 4K P-frame
-// staging and 17 us compacting survivors (tools/me_ab2.py timing probes):
+//      search's.  More than CAP survivors (weak bounds: flat or noise-like content): every
+//      valid candidate's SAD, one per lane.
+// Layout and scheduling:
 //   * ONE copy of the window in LDS (pitch 41 dwords: column walks are conflict free); the
-//     byte-shifted reads the search needs are two ds_read_b32 + v_alignbyte.  LDS per
-//     workgroup drops from 59 KB to 28 KB, so three workgroups (6 waves/SIMD) share a CU;
+//     byte-shifted reads the search needs are two ds_read_b32 + v_alignbyte;
 //   * the window's loads are all issued before any LDS store;
-//   * the 4x4 byte sums are built by threads owning 4 adjacent columns and 6 output rows,
-//     all their LDS reads issued up front;
-//   * survivors are compacted with one LDS atomic per lane (its popcount) instead of a
-//     ballot per candidate row -- the list order is irrelevant, the key decides;
-//   * more than CAP survivors: every valid candidate's SAD, one per lane (no dense kernel).
+//   * the reference's 4x4 byte sums (B4) are built per tile in LDS by threads owning 4
+//     adjacent columns and a band of output rows, all their LDS reads issued up front;
+//   * survivors are compacted with one wave ballot per candidate row and the lane's rank in
+//     it (mbcnt) -- the list order is irrelevant, the key decides.
+// A first SEA kernel with four byte-shifted window copies (59 KB LDS per workgroup) took
+// 66-73 us per 4K P-frame, 23 us of it staging and 17 us compacting; it was retired once
+// this one replaced it.
 // ---------------------------------------------------------------------------------------
 #ifndef SO_SEA2_WPE
 #define SO_SEA2_WPE 6
@@ -1087,7 +804,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             uint32_t A[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) A[j] = a4[u * 4 + j];
-            // ---- 1. lower bounds (as me_sea_kernel) ------------------------------------------
+            // ---- 1. lower bounds --------------------------------------------------------------
             const int cB = bxl * 16 + xi;
             const int lb0 = (byl * 16 + 16 * hh) * B4P + (cB & 3) * 40 + (cB >> 2);   // byte offset
             const uint32_t bsh = (uint32_t)lb0 & 3;
@@ -1645,139 +1362,6 @@ int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, i
 }
 
 // ---------------------------------------------------------------------------------------
-// Round-1 kernel, kept for A/B (SO_ME_IMPL=fast): same tiling and tasks, but the current
-// block lives whole in VGPRs (168 VGPRs, 1 workgroup per CU), window rows are aligned
-// dword reads + v_alignbyte, and the argmin builds a 64-bit key per candidate.
-// ---------------------------------------------------------------------------------------
-template <int TBS, int SR>
-SO_DEV uint64_t me_task(const uint32_t* __restrict__ win, int wpd, const uint8_t* __restrict__ cur,
-                        int W, int H, int x, int y, int wrow0, int wcol0, int dxi, int ref) {
-    constexpr int D = 2 * SR + 1;
-    constexpr int NDW = TBS / 4;  // dwords per block row
-    uint32_t cr[TBS][NDW];
-#pragma unroll
-    for (int r = 0; r < TBS; ++r) {
-        const uint8_t* p = cur + (size_t)(y + r) * W + x;
-        if constexpr (TBS == 16) {
-            uint4 v = *reinterpret_cast<const uint4*>(p);
-            cr[r][0] = v.x; cr[r][1] = v.y; cr[r][2] = v.z; cr[r][3] = v.w;
-        } else {
-            uint2 v = *reinterpret_cast<const uint2*>(p);
-            cr[r][0] = v.x; cr[r][1] = v.y;
-        }
-    }
-    uint32_t acc[D];
-#pragma unroll
-    for (int i = 0; i < D; ++i) acc[i] = 0;
-
-    const int c = wcol0 + dxi;
-    const uint32_t sh = (uint32_t)(c & 3);
-    const uint32_t* rowp = win + wrow0 * wpd + (c >> 2);
-#pragma unroll
-    for (int j = 0; j < TBS + 2 * SR; ++j) {
-        uint32_t w[NDW + 1];
-#pragma unroll
-        for (int k = 0; k <= NDW; ++k) w[k] = rowp[j * wpd + k];
-        uint32_t rr[NDW];
-#pragma unroll
-        for (int k = 0; k < NDW; ++k) rr[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
-#pragma unroll
-        for (int r = 0; r < TBS; ++r) {
-            const int di = j - r;
-            if (di >= 0 && di < D) {
-#pragma unroll
-                for (int k = 0; k < NDW; ++k) acc[di] = __builtin_amdgcn_sad_u8(cr[r][k], rr[k], acc[di]);
-            }
-        }
-    }
-    const int dx = dxi - SR;
-    const bool xok = (x + dx >= 0) && (x + dx < W - TBS);
-    uint64_t best = kNoKey;
-    if (xok) {
-        const uint32_t adx = (uint32_t)(dx < 0 ? -dx : dx);
-#pragma unroll
-        for (int di = 0; di < D; ++di) {
-            const int dy = di - SR;
-            const bool ok = (y + dy >= 0) && (y + dy < H - TBS);
-            const uint64_t k = me_key(acc[di], adx + (uint32_t)(dy < 0 ? -dy : dy), (uint32_t)ref,
-                                      (uint32_t)(dxi * D + di));
-            best = (ok && k < best) ? k : best;
-        }
-    }
-    return best;
-}
-
-template <int BS, bool SUB>
-__global__ void __launch_bounds__(MeGeo<BS>::NTHREADS)
-me_fast_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
-               int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub) {
-    using G = MeGeo<BS>;
-    constexpr int SR = G::SR, D = G::D, TB = G::TB, SB = BS / 2;
-    constexpr int WPD = (G::WP + 16) / 4 + 1, WCD = G::WP / 4;
-    __shared__ uint32_t win[G::WP * WPD];
-    __shared__ unsigned long long keys[G::NBLK * (SUB ? 5 : 1)];
-
-    const int nbx = W / BS;
-    const int tiles_x = (nbx + TB - 1) / TB;
-    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
-    const int bx0 = tx * TB, byt0 = by0 + ty * TB;
-    const int x0 = bx0 * BS, y0 = byt0 * BS;
-    const int tid = threadIdx.x;
-
-    for (int i = tid; i < G::NBLK * (SUB ? 5 : 1); i += G::NTHREADS) keys[i] = kNoKey;
-
-    constexpr int NFULL = G::NBLK * D;
-    constexpr int NSUBT = SUB ? 4 * G::NBLK * D : 0;
-    constexpr int NTASK = NFULL + NSUBT;
-
-    for (int r = 0; r < nref; ++r) {
-        const uint8_t* ref = refs.p[r];
-        __syncthreads();
-        for (int i = tid; i < G::WP * WPD; i += G::NTHREADS) {
-            const int wr = i / WPD, wc = i % WPD;
-            const int gy = y0 - SR + wr, gx = x0 - SR + wc * 4;
-            uint32_t v = 0;
-            if (wc < WCD && gy >= 0 && gy < H && gx >= 0 && gx + 4 <= W)
-                v = *reinterpret_cast<const uint32_t*>(ref + (size_t)gy * W + gx);
-            win[i] = v;
-        }
-        __syncthreads();
-        for (int t0 = 0; t0 < NTASK; t0 += G::NTHREADS) {
-            const int t = t0 + tid;
-            if (t >= NTASK) break;
-            if (t < NFULL) {
-                const int blk = t / D, dxi = t % D;
-                const int bxl = blk % TB, byl = blk / TB;
-                if (bx0 + bxl < nbx && byt0 + byl < by1) {
-                    const uint64_t k = me_task<BS, SR>(win, WPD, cur, W, H, x0 + bxl * BS, y0 + byl * BS,
-                                                      byl * BS, bxl * BS, dxi, r);
-                    if (k != kNoKey) atomicMin(&keys[blk], (unsigned long long)k);
-                }
-            } else if constexpr (SUB) {
-                const int s = (t - NFULL) / D, dxi = (t - NFULL) % D;
-                const int blk = s >> 2, j = s & 3;
-                const int bxl = blk % TB, byl = blk / TB;
-                if (bx0 + bxl < nbx && byt0 + byl < by1) {
-                    const int ox = (j & 1) * SB, oy = (j >> 1) * SB;
-                    const uint64_t k = me_task<SB, SR>(win, WPD, cur, W, H, x0 + bxl * BS + ox,
-                                                      y0 + byl * BS + oy, byl * BS + oy, bxl * BS + ox, dxi, r);
-                    if (k != kNoKey) atomicMin(&keys[G::NBLK + s], (unsigned long long)k);
-                }
-            }
-        }
-    }
-    __syncthreads();
-    for (int i = tid; i < G::NBLK * (SUB ? 5 : 1); i += G::NTHREADS) {
-        const int blk = i < G::NBLK ? i : (i - G::NBLK) >> 2;
-        const int gbx = bx0 + blk % TB, gby = byt0 + blk / TB;
-        if (gbx >= nbx || gby >= by1) continue;
-        const size_t b = (size_t)(gby - by0) * nbx + gbx;
-        if (i < G::NBLK) decode_key(keys[i], SR, out_best + b * 4);
-        else decode_key(keys[i], SR, out_sub + (b * 4 + ((i - G::NBLK) & 3)) * 4);
-    }
-}
-
-// ---------------------------------------------------------------------------------------
 // Generic path: one thread per (block, ref, candidate); keys in global memory.
 // ---------------------------------------------------------------------------------------
 // The generic path keeps each unit's key in the first 8 bytes of its own 16-byte output
@@ -1852,54 +1436,31 @@ int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, in
     const int nbx = W / bs, nrows = by1 - by0;
     if (nrows <= 0) return SO_OK;
     if (sr == 16 && (bs == 16 || bs == 8) && (out_sub == nullptr || bs == 16)) {
-        // SO_ME_IMPL=fast (A/B only, tools/me_ab.py) selects the round-1 kernel
         // SO_ME_IMPL=dense selects the dense wave kernel where SEA would run (A/B, bench)
         const char* impl = getenv("SO_ME_IMPL");
-        const bool use_fast = impl && strcmp(impl, "fast") == 0;
         const bool use_dense = impl && strcmp(impl, "dense") == 0;
-        if (!use_fast && !use_dense && bs == 16 && out_sub == nullptr) {
-            const dim3 sgrid(((nbx + SeaGeo::TBX - 1) / SeaGeo::TBX) * ((nrows + SeaGeo::TBY - 1) / SeaGeo::TBY));
+        if (!use_dense && bs == 16 && out_sub == nullptr) {
+            const dim3 sgrid(((nbx + Sea2Geo::TBX - 1) / Sea2Geo::TBX) * ((nrows + Sea2Geo::TBY - 1) / Sea2Geo::TBY));
             const char* pr = getenv("SO_SEA_PROBE");   // timing probes only (tools/me_ab2.py)
-            if (impl && strcmp(impl, "sea1") == 0) {   // previous SEA kernel, A/B only
-                hipLaunchKernelGGL(me_sea_kernel, sgrid, dim3(SeaGeo::NTHREADS), 0, st, cur, refs, nref, H, W, by0,
-                                   by1, out_best, pr ? atoi(pr) : 0);
-                return check_launch("me_sea_kernel");
-            }
             hipLaunchKernelGGL(me_sea2_kernel, sgrid, dim3(Sea2Geo::NTHREADS), 0, st, cur, refs, nref, H, W, by0, by1,
                                out_best, pr ? atoi(pr) : 0);
             return check_launch("me_sea2_kernel");
         }
-        const int tb = bs == 16 ? MeGeo<16>::TB : MeGeo<8>::TB;
-        const dim3 grid(((nbx + tb - 1) / tb) * ((nrows + tb - 1) / tb)), blk(MeGeo<16>::NTHREADS);
-        if (!use_fast) {
-            const bool sub = out_sub != nullptr;
-            const int tbx = 128 / bs;
-            const int tby = (sub ? MeWGeo<16, true>::TPY : MeWGeo<16, false>::TPY) / bs;
-            const dim3 wgrid(((nbx + tbx - 1) / tbx) * ((nrows + tby - 1) / tby));
-            const dim3 wblk(sub ? MeWGeo<16, true>::NTHREADS : MeWGeo<16, false>::NTHREADS);
-            if (bs == 16 && out_sub)
-                hipLaunchKernelGGL((me_wave_kernel<16, true>), wgrid, wblk, 0, st, cur, refs, nref, H, W, by0, by1,
-                                   out_best, out_sub);
-            else if (bs == 16)
-                hipLaunchKernelGGL((me_wave_kernel<16, false>), wgrid, wblk, 0, st, cur, refs, nref, H, W, by0, by1,
-                                   out_best, out_sub);
-            else
-                hipLaunchKernelGGL((me_wave_kernel<8, false>), wgrid, wblk, 0, st, cur, refs, nref, H, W, by0, by1,
-                                   out_best, nullptr);
-            return check_launch("me_wave_kernel");
-        }
-        {
-            if (bs == 16 && out_sub)
-                hipLaunchKernelGGL((me_fast_kernel<16, true>), grid, blk, 0, st, cur, refs, nref, H, W, by0, by1,
-                                   out_best, out_sub);
-            else if (bs == 16)
-                hipLaunchKernelGGL((me_fast_kernel<16, false>), grid, blk, 0, st, cur, refs, nref, H, W, by0, by1,
-                                   out_best, out_sub);
-            else
-                hipLaunchKernelGGL((me_fast_kernel<8, false>), grid, blk, 0, st, cur, refs, nref, H, W, by0, by1,
-                                   out_best, nullptr);
-            return check_launch("me_fast_kernel");
-        }
+        const bool sub = out_sub != nullptr;
+        const int tbx = 128 / bs;
+        const int tby = (sub ? MeWGeo<16, true>::TPY : MeWGeo<16, false>::TPY) / bs;
+        const dim3 wgrid(((nbx + tbx - 1) / tbx) * ((nrows + tby - 1) / tby));
+        const dim3 wblk(sub ? MeWGeo<16, true>::NTHREADS : MeWGeo<16, false>::NTHREADS);
+        if (bs == 16 && out_sub)
+            hipLaunchKernelGGL((me_wave_kernel<16, true>), wgrid, wblk, 0, st, cur, refs, nref, H, W, by0, by1,
+                               out_best, out_sub);
+        else if (bs == 16)
+            hipLaunchKernelGGL((me_wave_kernel<16, false>), wgrid, wblk, 0, st, cur, refs, nref, H, W, by0, by1,
+                               out_best, out_sub);
+        else
+            hipLaunchKernelGGL((me_wave_kernel<8, false>), wgrid, wblk, 0, st, cur, refs, nref, H, W, by0, by1,
+                               out_best, nullptr);
+        return check_launch("me_wave_kernel");
     }
     return me_generic_launch(cur, refs, nullptr, 0, nref, H, W, bs, sr, by0, by1, out_best, out_sub, st);
 }

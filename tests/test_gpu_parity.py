@@ -340,8 +340,8 @@ def test_stripe_gop_encoder_single_rank(gpu):
 # ---------------------------------------------------------------- ME search paths (SEA / dense fallback)
 @pytest.mark.parametrize("kind", ["flat", "noise", "synth", "tie", "ramp"])
 def test_me_paths_vs_oracle(gpu, kind):
-    """The default bs-16 ME prunes candidates by 4x4-sum lower bounds (me_sea_kernel) and falls
-    back to the dense search when too many survive.  Flat frames make every candidate survive
+    """The default bs-16 ME prunes candidates by 4x4-sum lower bounds (me_sea2_kernel) and falls
+    back to every candidate's SAD when too many survive.  Flat frames make every candidate survive
     (fallback), noise gives weak bounds, tie-heavy and ramp content stress the tie-break.
     Every block's (dx, dy, ref, SAD) must equal the oracle's exhaustive search."""
     from oracle import oracle as O

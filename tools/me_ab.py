@@ -1,7 +1,7 @@
 """A/B of ME implementations in one process (interleaved rounds), 4K P-frame.
 
-Variants: me_sea_kernel (default for bs 16 without VBS; with VBS the dense wave kernel),
-me_wave_kernel (SO_ME_IMPL=dense) and the round-1 me_fast_kernel (SO_ME_IMPL=fast).  Checks every variant's output equals
+Variants: me_sea2_kernel (default for bs 16 without VBS; with VBS the dense wave kernel) and
+me_wave_kernel (SO_ME_IMPL=dense).  Checks every variant's output equals
 the first one's, then prints us/launch per variant."""
 import os, sys
 import torch
@@ -10,7 +10,7 @@ from streamoptima_amd import _lib
 from streamoptima_amd.engine import alloc_planes
 from streamoptima_amd.synth import synth_sequence_torch
 
-VARIANTS = {"sea": {}, "dense": {"SO_ME_IMPL": "dense"}, "fast": {"SO_ME_IMPL": "fast"}}
+VARIANTS = {"sea": {}, "dense": {"SO_ME_IMPL": "dense"}}
 
 
 def main():

@@ -12,7 +12,7 @@ from streamoptima_amd import _lib  # noqa: E402
 from streamoptima_amd.engine import Engine, alloc_planes  # noqa: E402
 from streamoptima_amd.synth import synth_sequence_torch  # noqa: E402
 
-VARIANTS = {"sea": {}, "sea1": {"SO_ME_IMPL": "sea1"}, "dense": {"SO_ME_IMPL": "dense"}, "probe_stage": {"SO_SEA_PROBE": "1"},
+VARIANTS = {"sea": {}, "dense": {"SO_ME_IMPL": "dense"}, "probe_stage": {"SO_SEA_PROBE": "1"},
             "probe_bounds": {"SO_SEA_PROBE": "2"}, "probe_nofallback": {"SO_SEA_PROBE": "3"},
             "probe_list": {"SO_SEA_PROBE": "4"}}
 

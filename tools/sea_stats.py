@@ -1,4 +1,4 @@
-"""Offline survivor statistics of the exact SEA pruning in me_sea_kernel (so_me.hip) on the
+"""Offline survivor statistics of the exact SEA pruning in me_sea2_kernel (so_me.hip) on the
 bench content: per block, count the candidates whose 4x4-sum lower bound does not exceed the
 SAD of the smallest-bound candidate.  Uses the C oracle for the I-frame reconstruction."""
 import numpy as np, sys
