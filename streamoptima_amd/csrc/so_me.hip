@@ -592,6 +592,9 @@ int me_fme_launch(const uint8_t* cur, const uint8_t* planes, size_t pstride, int
 #ifndef SO_SEA2_WPE
 #define SO_SEA2_WPE 6
 #endif
+#ifndef SO_PTILE_WPE16   // waves per SIMD of the 16-wave fused tile kernels (A/B builds only)
+#define SO_PTILE_WPE16 8
+#endif
 // NW_ waves per workgroup: 8 (two blocks per wave; me_sea2_kernel) or 16 (one block per
 // wave; p_tile_kernel at 8 waves/SIMD)
 template <int NW_>
@@ -656,9 +659,15 @@ struct Sea2Lds {
 // Exact SEA full search of tile `tile` (16 blocks of 16x16) over nref references.  On
 // return (after a barrier) keys[] holds every block's packed best key and win[] the last
 // reference's window (zero outside the frame).
-template <class G>
+struct NoPre {
+    SO_DEV void operator()() const {}
+};
+// `pre` runs (on every wave) after the current tile is staged and before the first
+// reference's window is read: p_run_kernel waits there for the reference's tiles, so the
+// current-tile staging overlaps that wait.
+template <class G, class Pre = NoPre>
 SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cur, const RefSet& refs, int nref,
-                      int H, int W, int by0, int by1, int probe) {
+                      int H, int W, int by0, int by1, int probe, const Pre& pre = Pre()) {
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RP = G::RP, NT = G::NT;
     constexpr int B4P = G::B4P, CAP = G::CAP, CP = G::TPX;
     uint32_t* const win = L.win;
@@ -686,6 +695,11 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
 #endif
 
     for (int i = tid; i < G::NBLK; i += G::NTHREADS) keys[i] = kNoKey;
+    // interior window (uniform): thread = (row, column phase) with immediate per-dword offsets
+    constexpr int WTPR = G::NTHREADS / G::WR, WNPT = (RP + WTPR - 1) / WTPR;
+    static_assert(G::NTHREADS % G::WR == 0, "window staging");
+    const int wwr = tid / WTPR, wc0 = tid - wwr * WTPR;
+    const bool win_int = x0 - SR >= 0 && x0 - SR + 4 * RP <= W && y0 - SR >= 0 && y0 - SR + G::WR <= H;
     if (x0 + CP <= W && y0 + G::TPY <= H) {
         // interior tile (uniform branch): thread = (row, column phase); the loads' and stores'
         // per-dword offsets are immediates, so staging costs a few VALU per thread
@@ -727,22 +741,18 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
     }
     for (int r = 0; r < nref; ++r) {
         const uint8_t* ref = refs.p[r];
+        if (r == 0) pre();
         __syncthreads();
         if (r == 0) SO_SEA_STAMP(2, __builtin_amdgcn_s_memtime());
-        if (x0 - SR >= 0 && x0 - SR + 4 * RP <= W && y0 - SR >= 0 && y0 - SR + G::WR <= H) {
-            // interior window (uniform branch): thread = (row, column phase) with immediate
-            // per-dword offsets; all loads first, then the LDS stores
-            constexpr int TPR = G::NTHREADS / G::WR, NPT = (RP + TPR - 1) / TPR;
-            static_assert(G::NTHREADS % G::WR == 0, "window staging");
-            const int wr = tid / TPR, c0 = tid - wr * TPR;
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(ref + (size_t)(y0 - SR + wr) * W + (x0 - SR)) + c0;
-            uint32_t v[NPT];
+        if (win_int) {   // all loads first, then the LDS stores
+            uint32_t wv0[WNPT];
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(ref + (size_t)(y0 - SR + wwr) * W + (x0 - SR)) + wc0;
 #pragma unroll
-            for (int k = 0; k < NPT; ++k)
-                if (c0 + k * TPR < RP) v[k] = src[k * TPR];
+            for (int k = 0; k < WNPT; ++k)
+                if (wc0 + k * WTPR < RP) wv0[k] = src[k * WTPR];
 #pragma unroll
-            for (int k = 0; k < NPT; ++k)
-                if (c0 + k * TPR < RP) win[wr * RP + c0 + k * TPR] = v[k];
+            for (int k = 0; k < WNPT; ++k)
+                if (wc0 + k * WTPR < RP) win[wwr * RP + wc0 + k * WTPR] = wv0[k];
         } else {   // window: all loads first, then the LDS stores (zero outside the frame)
             constexpr int N = G::WR * RP, IT = (N + G::NTHREADS - 1) / G::NTHREADS;
             uint32_t v[IT];
@@ -1181,11 +1191,12 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
 // Search + transforms of tile `tile` of one frame.  SC1: the reconstruction rows are stored
 // write-through (global_store sc1), so another XCD that later reads them (p_run_kernel's
 // next frame) gets them from memory without a release fence.  Ends with every wave's
-// stores retired (s_waitcnt vmcnt(0)) and a workgroup barrier.
-template <class G, bool SC1>
+// stores retired (s_waitcnt vmcnt(0)) and a workgroup barrier.  `pre`: as sea2_tile's.
+template <class G, bool SC1, class Pre = NoPre>
 SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur, const uint8_t* ref, int H, int W,
                        int by0, int by1, int qp_rd, const int32_t* __restrict__ qp_row,
-                       const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best, const PFrameOut& o) {
+                       const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best, const PFrameOut& o,
+                       const Pre& pre = Pre()) {
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, CP = G::TPX;
     using P = PTileGeo<G>;
     uint32_t* const b4w = reinterpret_cast<uint32_t*>(S.un);
@@ -1193,7 +1204,7 @@ SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur
     const Sea2Lds L{S.win, b4w, S.curt, S.a4, list, S.lcount, S.keys, S.st};
     RefSet refs{};
     refs.p[0] = ref;
-    sea2_tile<G>(L, tile, cur, refs, 1, H, W, by0, by1, 0);   // ends with a barrier
+    sea2_tile<G>(L, tile, cur, refs, 1, H, W, by0, by1, 0, pre);   // ends with a barrier
 
     const int tid = opaque_tid();
     SO_SEA_STAMP(5, __builtin_amdgcn_s_memtime());
@@ -1220,7 +1231,7 @@ SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur
 #define SO_PTILE_NW 8
 #endif
 template <int NW>
-__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? 8 : SO_SEA2_WPE)))
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE)))
 p_tile_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W, int by0, int by1, int qp_rd,
               const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best,
               PFrameOut o) {
@@ -1264,7 +1275,7 @@ struct PRunArgs {
 // Workspace words: [0] task counter, [1] timeout flag, [2 + f * ntiles + t] = 1 once tile t of
 // frame f is done.  Zeroed by the launcher before every launch.
 template <int NW>
-__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? 8 : SO_SEA2_WPE)))
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE)))
 p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, int H, int W,
              int qp_rd, const int32_t* __restrict__ qp_row, uint32_t* __restrict__ ws) {
     using G = Sea2GeoT<NW>;
@@ -1291,12 +1302,14 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
         const int task = __builtin_amdgcn_readfirstlane(s_task);
         if (task >= ntasks) break;   // uniform: every wave leaves
         const int f = task / ntiles, tile = task - f * ntiles, ty = tile / tiles_x, tx = tile - ty * tiles_x;
-        if (f > 0 && wave == 0) {
-            // the 3x3 tiles of frame f-1 around this one (the window's +-16 px), one flag per
-            // lane, all polled in one round trip.  Every task they stand for was dequeued
-            // before this one by a running workgroup, so the wait always ends; it is bounded
-            // all the same (50 ms of s_memrealtime): a timeout flags the launch
-            // (Engine.run_timed_out, checked by the tests) and the tile proceeds.
+        // the 3x3 tiles of frame f-1 around this one (the window's +-16 px), one flag per lane,
+        // all polled in one round trip by wave 0 once the current tile is staged (ptile_body's
+        // `pre`; the barrier after it releases the other waves).  Every task they stand for was
+        // dequeued before this one by a running workgroup, so the wait always ends; it is
+        // bounded all the same (50 ms of s_memrealtime): a timeout flags the launch
+        // (Engine.run_timed_out, checked by the tests) and the tile proceeds.
+        const auto wait_ref = [&]() {
+            if (f == 0 || wave != 0) return;
             const int nx = tx + lane % 3 - 1, ny = ty + lane / 3 - 1;
             const bool need = lane < 9 && nx >= 0 && nx < tiles_x && ny >= 0 && ny < ntr;
             const uint32_t* c = done + (size_t)(f - 1) * ntiles + (need ? ny * tiles_x + nx : 0);
@@ -1310,10 +1323,9 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                     break;
                 }
             }
-        }
-        __syncthreads();   // also: every wave has read s_task
+        };
         ptile_body<G, true>(S, tile, a.cur[f], f ? a.out[f - 1].recon : ref0, H, W, 0, nby, qp_rd, qp_row, nullptr,
-                            nullptr, a.out[f]);
+                            nullptr, a.out[f], wait_ref);
         // ptile_body ended with every wave's write-through stores retired and a barrier
         if (wave == 0)
             __hip_atomic_fetch_add(done + (size_t)f * ntiles + tile, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

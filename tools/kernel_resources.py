@@ -4,7 +4,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 srcs = sys.argv[1:] or sorted(glob.glob(os.path.join(ROOT, "streamoptima_amd/csrc/*.hip")))
 for src in srcs:
     r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-                        "-I", os.path.join(ROOT, "include"), "-c", src, "-o", "/tmp/_kr.o",
+                        "-I", os.path.join(ROOT, "include"), *os.environ.get("KR_DEFINES", "").split(), "-c", src, "-o", "/tmp/_kr.o",
                         "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True)
     cur = None; rows = []
     for line in r.stderr.splitlines():

@@ -40,6 +40,28 @@ KERNEL(k_add3_vvv, asm volatile("v_add3_u32 %0, %1, %2, %0" : "+v"(acc[i]) : "v"
 KERNEL(k_add_vv, acc[i] = acc[i] + a[i])
 KERNEL(k_align_vvs, acc[i] = __builtin_amdgcn_alignbyte(a[i], acc[i], s0))
 
+// FP64 VALU (the pocketfft-exact transforms): is a wave64 v_add/mul/fma_f64 4 cycles?
+#define KERNELD(NAME, BODY)                                                                   \
+    __global__ void NAME(const uint32_t* in, uint32_t* out, int n_iter, uint32_t s0, uint32_t s1, \
+                         uint32_t s2, uint32_t s3) {                                         \
+        double a[NACC], b[NACC], acc[NACC];                                                  \
+        _Pragma("unroll") for (int i = 0; i < NACC; ++i) {                                   \
+            a[i] = 1.0 + 1e-9 * in[threadIdx.x + i + 1];                                     \
+            b[i] = 1e-9 * in[threadIdx.x + 2 * i + 3];                                       \
+            acc[i] = i;                                                                      \
+        }                                                                                    \
+        for (int it = 0; it < n_iter; ++it) {                                                \
+            _Pragma("unroll") for (int i = 0; i < NACC; ++i) { BODY; }                       \
+        }                                                                                    \
+        double s = 0;                                                                        \
+        _Pragma("unroll") for (int i = 0; i < NACC; ++i) s += acc[i];                        \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s;                            \
+    }
+KERNELD(k_add_f64, acc[i] = acc[i] + a[i])
+KERNELD(k_mul_f64, acc[i] = acc[i] * a[i])
+KERNELD(k_fma_f64, acc[i] = __builtin_fma(acc[i], a[i], b[i]))
+KERNELD(k_rndne_f64, acc[i] = __builtin_rint(acc[i] + b[i]))
+
 template <typename K>
 static void run(K kern, const char* name, int blocks, int threads, uint32_t* din, uint32_t* dout) {
     hipEvent_t e0, e1;
@@ -74,6 +96,10 @@ int main() {
         run(k_add3_vvv, "add3_vvv", blocks, threads, din, dout);
         run(k_add_vv, "add_vv", blocks, threads, din, dout);
         run(k_align_vvs, "align_vvs", blocks, threads, din, dout);
+        run(k_add_f64, "add_f64", blocks, threads, din, dout);
+        run(k_mul_f64, "mul_f64", blocks, threads, din, dout);
+        run(k_fma_f64, "fma_f64", blocks, threads, din, dout);
+        run(k_rndne_f64, "add+rndne", blocks, threads, din, dout);
     }
     return 0;
 }
