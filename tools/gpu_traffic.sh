@@ -2,7 +2,8 @@
 # HBM traffic of every kernel in the bench command (MI355X_MICROARCH.md HBM section):
 # FETCH_SIZE and WRITE_SIZE in separate --pmc passes over a short bench run (and one pass of
 # SQ instruction counts), then
-# tools/traffic_json.py writes profiles/pmc_me_traffic.json (bench.py roofline.traffic).
+# tools/traffic_json.py writes profiles/pmc_me_traffic.json (bench.py roofline.traffic).  Run it
+# HERE on the merged gpurun_out/traffic: a profiles/ file written on the GPU box does not come back.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out/traffic
