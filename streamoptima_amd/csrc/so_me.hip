@@ -592,6 +592,9 @@ int me_fme_launch(const uint8_t* cur, const uint8_t* planes, size_t pstride, int
 #ifndef SO_SEA2_WPE
 #define SO_SEA2_WPE 6
 #endif
+#ifndef SO_SEA_CAP   // survivors per block evaluated from the list; more take the dense fallback
+#define SO_SEA_CAP 192
+#endif
 #ifndef SO_PTILE_WPE16   // waves per SIMD of the 16-wave fused tile kernels (A/B builds only)
 #define SO_PTILE_WPE16 8
 #endif
@@ -610,7 +613,7 @@ struct Sea2GeoT {
     static constexpr int B4RS = B4NB * B4BAND;            // stored rows: whole bands, no bounds tests
     static constexpr int NBLK = TBX * TBY;
     static constexpr int NW = NW_, NTHREADS = NW * 64;
-    static constexpr int CAP = 192;
+    static constexpr int CAP = SO_SEA_CAP;
     static constexpr int CPD = TPX / 4 + 1;               // current-tile pitch in dwords: 16 rows of
                                                           // one block column land on 16 banks
     static_assert(WD * B4NB <= NTHREADS, "byte-sum threads");
@@ -1363,7 +1366,17 @@ int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, i
             set_error("p_run_kernel: hipMemsetAsync: %s", hipGetErrorString(e));
             return (int)e;
         }
-        long grid = (long)ncu * per_cu;
+        // A frame with fewer tiles than resident slots (1080p: 510 tiles, 768 slots) gets
+        // ceil(ntiles / ncu) workgroups per CU: every CU then runs its share of a frame's tiles
+        // side by side, instead of some CUs running three (slower) while the next frame's tiles
+        // wait on others -- a frame's time is its slowest tile's (1080p: 30 vs 33 us/frame).
+        int pcu = (int)((ntiles + ncu - 1) / ncu);
+        if (pcu > per_cu) pcu = per_cu;
+        if (const char* e = getenv("SO_RUN_PER_CU")) {   // A/B only: resident workgroups per CU
+            const int v = atoi(e);
+            if (v > 0 && v < per_cu) pcu = v;
+        }
+        long grid = (long)ncu * pcu;
         if (grid > ntiles * n) grid = ntiles * n;
         hipLaunchKernelGGL(p_run_kernel<SO_PTILE_NW>, dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), 0, st, a, n,
                            f0 ? outs[f0 - 1].recon : ref0, H, W, qp_rd, qp_row, ws);

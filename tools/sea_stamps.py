@@ -18,7 +18,7 @@ from streamoptima_amd.synth import synth_sequence_torch  # noqa: E402
 
 
 def main():
-    h, w = 2160, 3840
+    h, w = int(os.environ.get("STAMP_H", 2160)), int(os.environ.get("STAMP_W", 3840))
     dev = torch.device("cuda:0")
     lib = _lib.load()
     fr = alloc_planes(3, h, w, dev)
