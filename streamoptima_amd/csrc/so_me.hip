@@ -782,25 +782,35 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             const int m = tid % G::WD, band = tid / G::WD;
             const int r0 = band * G::B4BAND;
             constexpr int NR = G::B4BAND + 3;
-            uint32_t h[NR][4];
+            // row sums of 4 bytes at byte shifts k = 0..3, two per dword as 16-bit halves
+            // (v_sad_hi_u8 adds its sum << 16): h[i][0] = (k 0 | k 2 << 16), h[i][1] = (k 1 | k 3
+            // << 16).  A 4x4 sum is <= 4080, so the column sums below never carry across halves
+            // The last band reads up to 5 rows past the window (the next LDS fields, or 0 past
+            // the allocation): those rows only feed sums >= B4R, which no valid candidate reads.
+            uint32_t h[NR][2];
+            lds_vu32p p = (lds_vu32p)(win + r0 * RP + m);
 #pragma unroll
             for (int i = 0; i < NR; ++i) {
-                const int row = r0 + i < G::WR ? r0 + i : G::WR - 1;
-                lds_vu32p p = (lds_vu32p)(win + row * RP + m);
-                const uint32_t w0 = p[0], w1 = p[1];
-                h[i][0] = __builtin_amdgcn_sad_u8(w0, 0u, 0u);
-                h[i][1] = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w1, w0, 1), 0u, 0u);
-                h[i][2] = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w1, w0, 2), 0u, 0u);
-                h[i][3] = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w1, w0, 3), 0u, 0u);
+                const uint32_t w0 = p[i * RP], w1 = p[i * RP + 1];
+                h[i][0] = __builtin_amdgcn_sad_hi_u8(__builtin_amdgcn_alignbyte(w1, w0, 2), 0u,
+                                                     __builtin_amdgcn_sad_u8(w0, 0u, 0u));
+                h[i][1] = __builtin_amdgcn_sad_hi_u8(__builtin_amdgcn_alignbyte(w1, w0, 3), 0u,
+                                                     __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(w1, w0, 1), 0u, 0u));
             }
             // whole bands, every column: rows >= B4R and columns >= B4C hold sums no valid
-            // candidate reads (the storage is B4RS rows), so the stores need no bounds tests
+            // candidate reads (the storage is B4RS rows), so the stores need no bounds tests.
+            // One packed shift per two sums; the high byte goes out by ds_write_b8_d16_hi.
+            typedef unsigned short so_v2u16 __attribute__((ext_vector_type(2)));
             uint8_t* const ob = b4 + r0 * B4P + m;
 #pragma unroll
             for (int i = 0; i < G::B4BAND; ++i)
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    ob[i * B4P + k * 40] = (uint8_t)((h[i][k] + h[i + 1][k] + h[i + 2][k] + h[i + 3][k]) >> 4);
+                for (int j = 0; j < 2; ++j) {
+                    const uint32_t sum = h[i][j] + h[i + 1][j] + h[i + 2][j] + h[i + 3][j];
+                    const uint32_t q = __builtin_bit_cast(uint32_t, __builtin_bit_cast(so_v2u16, sum) >> (so_v2u16){4, 4});
+                    ob[i * B4P + j * 40] = (uint8_t)q;
+                    ob[i * B4P + (j + 2) * 40] = (uint8_t)(q >> 16);
+                }
         }
         __syncthreads();
         if (r == 0) SO_SEA_STAMP(4, __builtin_amdgcn_s_memtime());
