@@ -905,9 +905,13 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
                 if (lane == 0 && U < keys[u]) keys[u] = U;
                 continue;
             }
-            // ---- 3. survivors: 16 LBq - 240 <= U, i.e. LBq < qU1 ------------------------------
+            // ---- 3. survivors: 16 LBq - 240 <= U, i.e. LBq <= qU = (U + 240) >> 4 ------------
             const uint32_t qU = (U + 240) >> 4;
-            const uint32_t qU1 = xok ? qU + 1 : 0u;            // dx-invalid lanes: nothing passes
+            // per-lane threshold (dx-invalid lanes: -1, nothing passes), opaque so that the
+            // compare stays a plain v_cmp whose mask IS the ballot (folded back into
+            // `xok && lb <= qU` it costs a 0/1 select and a second compare per row)
+            int thr = xok ? (int)qU : -1;
+            asm volatile("" : "+v"(thr));
             // survivors by one wave ballot per candidate row t (t = NT: the dx = +16 column,
             // lanes < 33): rows nobody passes cost one compare and a scalar branch; the others
             // write their candidates at the running count + the lane's rank in the ballot (no
@@ -918,7 +922,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             uint32_t nsur = 0;
 #pragma unroll
             for (int t = 0; t <= NT; ++t) {
-                const bool pass = t < NT ? lb[t] < qU1 : (ok2 && lb2 <= qU);
+                const bool pass = t < NT ? (int)lb[t] <= thr : (ok2 && lb2 <= qU);
                 const uint64_t bal = __builtin_amdgcn_ballot_w64(pass);
                 if (bal) {   // uniform
                     const uint32_t pos = nsur + lane_prefix(bal);
