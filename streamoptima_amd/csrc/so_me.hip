@@ -834,9 +834,12 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             int lo1 = lb0 >> 2;
             asm volatile("" : "+v"(lo1));
             lds_vu32p p1 = (lds_vu32p)(b4w + lo1);
+            // lb[t] = (LBq << 16) | t: v_sad_hi_u8 accumulates each sum << 16 onto the initial t
+            // (an inline constant), so the smallest-bound key below needs no shifts or ORs
+            // (LBq <= 16 * 255 < 2^16)
             uint32_t lb[NT];
 #pragma unroll
-            for (int t = 0; t < NT; ++t) lb[t] = 0;
+            for (int t = 0; t < NT; ++t) lb[t] = (uint32_t)t;
             // byte-sum rows through a ring of PD rows in flight: the row used in step sr_ was
             // loaded PD steps earlier, so LDS latency overlaps PD steps of v_sad_u8 work
             // (one step ahead left every step waiting on its own loads)
@@ -855,9 +858,13 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int t = sr_ - 4 * j;
-                    if (t >= 0 && t < NT) lb[t] = __builtin_amdgcn_sad_u8(A[j], P, lb[t]);
+                    if (t >= 0 && t < NT) lb[t] = __builtin_amdgcn_sad_hi_u8(A[j], P, lb[t]);
                 }
-                acc_fence_n<NT>(lb);
+                // fence the started accumulators only: a not yet started one stays the inline
+                // constant t that its first v_sad_hi_u8 takes directly
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+                    if (t <= sr_) asm volatile("" : "+v"(lb[t]) : : "memory");
             }
             uint32_t lb2 = 0;
             {
@@ -867,7 +874,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
 #pragma unroll
                 for (int j = 0; j < 4; ++j) lb2 = __builtin_amdgcn_sad_u8(A[j], p2[4 * j * (B4P / 4)], lb2);
             }
-            constexpr uint32_t kBig = 0x07FFFFFFu;
+            constexpr uint32_t kBig = 0x7FFFFFFFu;   // a masked row: above every (LBq << 16) | t
             int dlo = SR - y;              dlo = dlo < 0 ? 0 : dlo;
             int dhi = H - 16 - y + SR - 1; dhi = dhi > 32 ? 32 : dhi;
             const bool xok = (x + xi - 16 >= 0) && (x + xi - 16 < W - 16);
@@ -879,14 +886,11 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
                 for (int t = 0; t < NT; ++t) lb[t] = (t < tlo || t > thi) ? kBig : lb[t];
             }
             // ---- 2. U = SAD of the smallest-bound candidate ----------------------------------
-            uint32_t kt = 0xFFFFFFFFu;
+            uint32_t kt = lb[0];
 #pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                const uint32_t k = (lb[t] << 5) | (uint32_t)t;
-                kt = k < kt ? k : kt;
-            }
-            uint32_t kl = (xok && (kt >> 5) != kBig) ? ((kt >> 5) << 11) | (uint32_t)(xi * 33 + 16 * hh + (kt & 31))
-                                                      : 0xFFFFFFFFu;
+            for (int t = 1; t < NT; ++t) kt = lb[t] < kt ? lb[t] : kt;
+            uint32_t kl = (xok && kt != kBig) ? ((kt >> 16) << 11) | (uint32_t)(xi * 33 + 16 * hh + (kt & 31))
+                                              : 0xFFFFFFFFu;
             {
                 const uint32_t k2 = (lb2 << 11) | (uint32_t)(32 * 33 + d2);
                 kl = (ok2 && k2 < kl) ? k2 : kl;
@@ -910,7 +914,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             // per-lane threshold (dx-invalid lanes: -1, nothing passes), opaque so that the
             // compare stays a plain v_cmp whose mask IS the ballot (folded back into
             // `xok && lb <= qU` it costs a 0/1 select and a second compare per row)
-            int thr = xok ? (int)qU : -1;
+            int thr = xok ? (int)((qU << 16) | 0xFFFFu) : -1;
             asm volatile("" : "+v"(thr));
             // survivors by one wave ballot per candidate row t (t = NT: the dx = +16 column,
             // lanes < 33): rows nobody passes cost one compare and a scalar branch; the others
