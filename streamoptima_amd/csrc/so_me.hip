@@ -1159,10 +1159,15 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
         }
         double tcr[16];
         xform2d_rows<16, false>(dl, l, res, tcr);
+        // np.round to int by the 1.5 * 2^52 shift (|values| < 2^51): x + kRne rounds x to an
+        // integer half-to-even, held in the low mantissa dword as two's complement -- one
+        // v_add_f64 instead of v_rndne + v_cvt_i32
+        constexpr double kRne = 0x1.8p52;
         int q[16];
 #pragma unroll
         for (int c = 0; c < 16; ++c)
-            q[c] = (int)__builtin_rint(__builtin_amdgcn_ldexp(__builtin_rint(tcr[c]), -q_exp_fast<16>(l, c, qpr)));
+            q[c] = (int)(uint32_t)__builtin_bit_cast(
+                uint64_t, __builtin_amdgcn_ldexp(__builtin_rint(tcr[c]), -q_exp_fast<16>(l, c, qpr)) + kRne);
         const int tok = block_tokens<16>(nullptr, l, q);
         store_row_i16<16>(o.qtc + b * 256 + l * 16, q);
         double dq[16], rd[16];
@@ -1173,7 +1178,9 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
             uint32_t pw[4];
             win_row16(S.win, prow, pcol, pw);
 #pragma unroll
-            for (int c = 0; c < 16; ++c) rec[c] = (int)((pw[c >> 2] >> (8 * (c & 3))) & 255) + (int)__builtin_rint(rd[c]);
+            for (int c = 0; c < 16; ++c)
+                rec[c] = (int)((pw[c >> 2] >> (8 * (c & 3))) & 255) +
+                         (int)(uint32_t)__builtin_bit_cast(uint64_t, rd[c] + kRne);
         }
         if constexpr (SC1) {
             so_v4u v;
