@@ -126,10 +126,15 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
  * window reads are done (device-scope flags in `workspace`; reconstructions are
  * stored write-through), so consecutive frames overlap on the device with no host
  * round trip.  curs / out_* are host arrays of nframes device pointers; out_sse may be
- * NULL.  workspace: caller-owned uint32 [so_p_run_workspace_elems(H, W)], zeroed by the
- * call (hipMemsetAsync on `stream`); word 1 is nonzero after the run if a dependency wait
- * timed out (a bug; the tests check it).
+ * NULL.  workspace: caller-owned uint32 [so_p_run_workspace_elems(H, W)]; the call zeroes
+ * its task counter and done flags (hipMemsetAsync on `stream`) but NOT word 32
+ * (SO_P_RUN_TIMEOUT_WORD), the timeout count: the caller zeroes it once and reads it after
+ * the run (or after a whole GOP of runs).
+ * Nonzero means a dependency wait passed 50 ms and the run's symbols may be wrong; the
+ * facade raises (Engine.check_run).  Consumers poll the flags and then take an agent-scope
+ * acquire before reading the reference rows.
  */
+#define SO_P_RUN_TIMEOUT_WORD 32
 size_t so_p_run_workspace_elems(int H, int W);
 int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W,
                     int bs, int sr, int qp_rd, const int32_t* qp_row, uint8_t* const* out_split,

@@ -29,10 +29,13 @@ def bitrate_per_row(target, frame_rate, h, bs):
 
 def encode_gop(frames, qp, intra_dur, bs=16, sr=16, vbs=False, lam=0.015, nref=1, rc=None,
                target=None, tables=None, intra_thresh=None, frame_rate=30, fast_me=False, fme=False,
-               parallel_mode=0, roi=None, qp_clamp=(0, 12)):
+               parallel_mode=0, roi=None, qp_clamp=(0, 12), on_frame=None):
     """encode() (Encoder.py:1790-1898) over the C oracle.  Build extensions restated from
     streamoptima_amd/Encoder.py: rc = 3 is two-pass RC (pass-1 tokens -> oc_qp_map -> pass
-    2), roi = flat per-block QP offsets (or None); r["qp_map"] holds the per-block QPs."""
+    2), roi = flat per-block QP offsets (or None); r["qp_map"] holds the per-block QPs.
+    on_frame(i, r): called per frame; the large fixtures digest each frame there and the
+    returned list then keeps only the frame types and PSNRs (4K x 120 frames of symbols would
+    be ~3.6 GB)."""
     f, h, w = frames.shape
     # the start reference is float64 all-128 (Encoder.py:1798): it matters only to the
     # frac frame's uint8 wrap (oracle.fme_upsample)
@@ -77,11 +80,14 @@ def encode_gop(frames, qp, intra_dur, bs=16, sr=16, vbs=False, lam=0.015, nref=1
         r["qp_row"] = list(qp_sched) if qp_sched else []
         sse = O.sse(cur, r["recon"])
         r["psnr"] = float("inf") if sse == 0 else float(10 * np.log10((255 ** 2) / (sse / (h * w))))
-        out.append(r)
         if i < f - 1:
             if len(ref_frames) >= nref:
                 ref_frames.pop(0)
                 ref_float.pop(0)
             ref_frames.append(r["recon"])
             ref_float.append(False)
+        if on_frame is not None:
+            on_frame(i, r)
+            r = {"frame_type": ft, "psnr": r["psnr"], "tokens_sum": int(r["tokens"].sum())}
+        out.append(r)
     return out

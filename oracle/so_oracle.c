@@ -463,8 +463,28 @@ EXPORT void oc_fme_upsample(const uint8_t *ref, int H, int W, int wrap, uint8_t 
  * the block is sampled every other row/column, Encoder.py:699-700). */
 typedef struct { const uint8_t *const *p; int H, W, step; } om_planes;
 
+/* Integer SAD of a bs x bs block on a step-1 plane.  Same value as the generic loop below;
+ * written over uint8 rows with an int accumulator so gcc vectorises it (psadbw): the large
+ * parity fixtures (tests/golden/make_large_fixtures.py, 4K x 120 frames) need it. */
+static long plane_sad1(const uint8_t *restrict cur, int cstride, const uint8_t *restrict pl, size_t PW, int bs) {
+    int sad = 0;
+    if (bs == 16) {
+        for (int i = 0; i < 16; ++i) {
+            const uint8_t *a = cur + (size_t)i * cstride, *b = pl + (size_t)i * PW;
+            for (int j = 0; j < 16; ++j) sad += abs((int)a[j] - (int)b[j]);
+        }
+        return (long)sad;
+    }
+    for (int i = 0; i < bs; ++i) {
+        const uint8_t *a = cur + (size_t)i * cstride, *b = pl + (size_t)i * PW;
+        for (int j = 0; j < bs; ++j) sad += abs((int)a[j] - (int)b[j]);
+    }
+    return (long)sad;
+}
+
 static long plane_sad(const uint8_t *cur, int cstride, const uint8_t *pl, int PW, int X, int Y, int bs,
                       int step) {
+    if (step == 1) return plane_sad1(cur, cstride, pl + (size_t)Y * PW + X, (size_t)PW, bs);
     long sad = 0;
     for (int i = 0; i < bs; ++i)
         for (int j = 0; j < bs; ++j)

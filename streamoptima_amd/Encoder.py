@@ -112,19 +112,8 @@ class Y_Video_codec:
 
     def roi_block_offsets(self):
         """ROI as int32 [nb] per-block QP offsets (raster order), or None."""
-        if self.roi is None:
-            return None
-        bs = self.block_size
-        nby, nbx = math.ceil(self.h_pixels / bs), math.ceil(self.w_pixels / bs)
-        a = np.asarray(self.roi)
-        if a.ndim == 2 and a.shape == (nby, nbx):
-            return a.astype(np.int32).reshape(-1)
-        out = np.zeros((nby, nbx), np.int32)
-        cy = np.arange(nby)[:, None] * bs + bs / 2
-        cx = np.arange(nbx)[None, :] * bs + bs / 2
-        for x0, y0, x1, y1, off in self.roi:
-            out[(cy >= y0) & (cy < y1) & (cx >= x0) & (cx < x1)] = int(off)
-        return out.reshape(-1)
+        from .workloads import roi_offsets
+        return roi_offsets(self.roi, self.h_pixels, self.w_pixels, self.block_size)
 
     # ---- host helpers with the reference's semantics ---------------------------------------
     def set_target_bitrate(self, targetBR):
@@ -350,9 +339,12 @@ class Y_Video_codec:
         self.inter0.append(time.time() - t0)
         return psnr_per_frame
 
-    def encode_device(self, frames_dev: torch.Tensor, intra_dur: int, symbols=None):
-        """The GOP loop on device-resident frames [F, Hp, Wp]; no host sync unless
-        RCFlag > 1 needs residual_size.  Returns symbols per frame and a device SSE array."""
+    def encode_device(self, frames_dev: torch.Tensor, intra_dur: int, symbols=None, check: bool = True):
+        """The GOP loop on device-resident frames [F, Hp, Wp].  Returns symbols per frame and
+        a device SSE array.  check=True ends with one host read of the persistent runs'
+        timeout count (Engine.check_run: raises if a dependency wait timed out); a caller
+        that times back-to-back GOPs passes False and calls engine().check_run() after them.
+        Otherwise no host sync unless RCFlag > 1 needs residual_size."""
         eng = self.engine()
         nframes = frames_dev.shape[0]
         ref_frames = [alloc_planes(1, eng.h, eng.w, self.device, fill=128)[0]]
@@ -450,6 +442,8 @@ class Y_Video_codec:
             i += 1
         # per-block / per-row SSE came out of the encode kernels; one reduction per GOP
         sse = torch.stack([s.sse for s in out_syms]).sum(dim=1, dtype=torch.int64)
+        if check and pipelined:
+            eng.check_run()
         return {"symbols": out_syms, "sse": sse, "frame_type": ftypes, "qp_rows": qp_rows}
 
     def _save_recon(self, syms):

@@ -1300,8 +1300,25 @@ struct PRunArgs {
     PFrameOut out[kRunMax];
 };
 
-// Workspace words: [0] task counter, [1] timeout flag, [2 + f * ntiles + t] = 1 once tile t of
-// frame f is done.  Zeroed by the launcher before every launch.
+// Workspace words: [0] task counter, [32] timeout count, [64 + f * ntiles + t] = 1 once tile t
+// of frame f is done.  The launcher zeroes [0, 32) and the done flags before every launch;
+// [32] is the CALLER's: it accumulates over launches and calls until the caller reads and
+// clears it (Engine.check_run), so a timeout in any launch of a GOP is seen.
+#ifndef SO_RUN_ACQUIRE
+#define SO_RUN_ACQUIRE 1
+#endif
+#ifndef SO_RUN_ABORT_CHECK
+#define SO_RUN_ABORT_CHECK 1
+#endif
+#ifndef SO_RUN_TIMEOUT_WORD
+#define SO_RUN_TIMEOUT_WORD 32
+#endif
+#ifndef SO_RUN_DONE_BASE
+#define SO_RUN_DONE_BASE 64
+#endif
+// the task counter (hammered by every workgroup's dequeue), the timeout count and the done
+// flags live on separate 128-byte lines
+constexpr int kRunTimeoutWord = SO_RUN_TIMEOUT_WORD, kRunDoneBase = SO_RUN_DONE_BASE;
 template <int NW>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE)))
 p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, int H, int W,
@@ -1313,7 +1330,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     const int nbx = W / 16, nby = H / 16;
     const int tiles_x = (nbx + G::TBX - 1) / G::TBX, ntr = (nby + G::TBY - 1) / G::TBY;
     const int ntiles = tiles_x * ntr, ntasks = ntiles * nframes;
-    uint32_t* const done = ws + 2;
+    uint32_t* const done = ws + kRunDoneBase;
     // Every queue / flag access is made by ALL lanes of wave 0 under a wave-uniform branch
     // (lane 0 adds 1, the others 0): a `tid == 0` branch ahead of a barrier inside this loop
     // gets structurised into a divergent inner loop that never re-runs the dequeue (a hang;
@@ -1340,6 +1357,13 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             if (f == 0 || wave != 0) return;
             const int nx = tx + lane % 3 - 1, ny = ty + lane / 3 - 1;
             const bool need = lane < 9 && nx >= 0 && nx < tiles_x && ny >= 0 && ny < ntr;
+            // the timeout count, read once per tile: after one timeout the later tiles of the
+            // run skip their waits (the run is already flagged wrong), so a lost flag cannot
+            // stall the launch for 50 ms per remaining tile.  (Polling it in the loop put
+            // every waiting workgroup on one word: +70 % per frame.)
+#if SO_RUN_ABORT_CHECK
+            if (__hip_atomic_load(ws + kRunTimeoutWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
+#endif
             const uint32_t* c = done + (size_t)(f - 1) * ntiles + (need ? ny * tiles_x + nx : 0);
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
             for (;;) {
@@ -1347,10 +1371,17 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 if (__builtin_amdgcn_ballot_w64(need && v == 0u) == 0) break;
                 __builtin_amdgcn_s_sleep(1);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
-                    __hip_atomic_fetch_add(&ws[1], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(&ws[kRunTimeoutWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
             }
+#if SO_RUN_ACQUIRE
+            // consumer side of the hand-off (MI355X_MICROARCH.md, "Valid forms"): one relaxed
+            // poll, ONE agent-scope acquire (invalidates this CU's L1), its completion awaited
+            // before the barrier that releases the other waves to the window loads
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
         };
         ptile_body<G, true>(S, tile, a.cur[f], f ? a.out[f - 1].recon : ref0, H, W, 0, nby, qp_rd, qp_row, nullptr,
                             nullptr, a.out[f], wait_ref);
@@ -1362,7 +1393,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 
 size_t p_run_workspace_words(int H, int W) {
     const size_t ntiles = (size_t)((W / 16 + Sea2Geo::TBX - 1) / Sea2Geo::TBX) * ((H / 16 + Sea2Geo::TBY - 1) / Sea2Geo::TBY);
-    return 2 + (size_t)kRunMax * ntiles;
+    return (size_t)kRunDoneBase + (size_t)kRunMax * ntiles;
 }
 
 int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
@@ -1386,7 +1417,10 @@ int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, i
             a.cur[i] = curs[f0 + i];
             a.out[i] = outs[f0 + i];
         }
-        const hipError_t e = hipMemsetAsync(ws, 0, p_run_workspace_words(H, W) * sizeof(uint32_t), st);
+        // the task counter and the done flags; never the timeout count (the caller's)
+        hipError_t e = hipMemsetAsync(ws, 0, kRunTimeoutWord * sizeof(uint32_t), st);
+        if (e == hipSuccess)
+            e = hipMemsetAsync(ws + kRunDoneBase, 0, (p_run_workspace_words(H, W) - kRunDoneBase) * sizeof(uint32_t), st);
         if (e != hipSuccess) {
             set_error("p_run_kernel: hipMemsetAsync: %s", hipGetErrorString(e));
             return (int)e;

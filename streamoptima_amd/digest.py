@@ -1,0 +1,49 @@
+"""Canonical per-frame digests of the encoder's symbols.
+
+One sha256 per frame over the frame's symbols in a fixed byte layout, so the HIP path's
+output at the benchmarked sizes (4K x 120 frames: ~3 GB of symbols) can be compared with
+the C oracle's through a small committed fixture (tests/golden/large_gops.json):
+
+    frame_type u8 | split u8[nb] | mv int16 [nb,4,3] (P) or [nb,4] (I) |
+    qtc int16 [nb, bs*bs] | tokens int32 [nb] | mae_num int64 [nb] (MAE * bs^2, -1 = inf) |
+    recon u8 [Hp, Wp] | qp_map int32 [nb] (ROI / two-pass RC only)
+
+all little-endian, in that order.  The same function digests numpy arrays from the oracle
+and arrays copied back from the GPU.
+"""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+
+_LAYOUT = (("split", np.uint8), ("mv", "<i2"), ("qtc", "<i2"), ("tokens", "<i4"), ("mae_num", "<i8"),
+           ("recon", np.uint8))
+
+
+def frame_digest(frame_type: int, arrays: dict) -> str:
+    """sha256 hex of one frame's symbols; `arrays` maps the names above to array-likes."""
+    h = hashlib.sha256(bytes([int(frame_type) & 255]))
+    for name, dt in _LAYOUT:
+        h.update(np.ascontiguousarray(np.asarray(arrays[name]), dtype=dt).tobytes())
+    qm = arrays.get("qp_map")
+    if qm is not None:
+        h.update(np.ascontiguousarray(np.asarray(qm), dtype="<i4").tobytes())
+    return h.hexdigest()
+
+
+def gop_digest(frame_digests) -> str:
+    """sha256 of the concatenated per-frame digests (the whole GOP in one value)."""
+    h = hashlib.sha256()
+    for d in frame_digests:
+        h.update(bytes.fromhex(d))
+    return h.hexdigest()
+
+
+def symbols_digest(sym) -> str:
+    """frame_digest of a streamoptima_amd.engine.FrameSymbols (copies it to the host)."""
+    arrs = {k: getattr(sym, k).cpu().numpy() for k in ("split", "mv", "qtc", "tokens", "mae_num", "recon")}
+    qm = sym.extra.get("qp_map") if sym.extra else None
+    if qm is not None:
+        arrs["qp_map"] = qm.cpu().numpy()
+    return frame_digest(sym.frame_type, arrs)

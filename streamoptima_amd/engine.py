@@ -17,6 +17,7 @@ import torch
 from . import _lib
 
 SLACK = 64  # bytes readable past every plane (kernels read aligned words at row ends)
+RUN_TIMEOUT_WORD = 32   # so_encode_p_run workspace: the timeout count (include/streamoptima.h)
 
 
 def alloc_planes(n: int, h: int, w: int, device, fill: int | None = None) -> torch.Tensor:
@@ -206,6 +207,7 @@ class Engine:
         for t, name in [(ref0, "ref0")] + [(c, "cur") for c in curs]:
             self._check_plane(t, name)
         if getattr(self, "_run_ws", None) is None:
+            # the timeout count (RUN_TIMEOUT_WORD) is zeroed here once and then only by check_run
             self._run_ws = torch.zeros(self.lib.so_p_run_workspace_elems(self.h, self.w), dtype=torch.int32,
                                        device=self.device)
 
@@ -223,9 +225,21 @@ class Engine:
         return outs
 
     def run_timed_out(self) -> bool:
-        """True if the last encode_p_run's dependency wait timed out (never expected)."""
+        """True if a dependency wait of any encode_p_run since the last check_run timed out
+        (never expected: the run's symbols would then be unreliable).  Synchronises."""
         ws = getattr(self, "_run_ws", None)
-        return bool(ws is not None and int(ws[1].item()) != 0)
+        return bool(ws is not None and int(ws[RUN_TIMEOUT_WORD].item()) != 0)
+
+    def check_run(self) -> None:
+        """Raise if any encode_p_run since the last check timed out, then clear the count.
+        Encoder.encode()/encode_device(check=True) and bench.py call it once per GOP."""
+        ws = getattr(self, "_run_ws", None)
+        if ws is None:
+            return
+        n = int(ws[RUN_TIMEOUT_WORD].item())
+        if n:
+            ws[RUN_TIMEOUT_WORD].zero_()
+            raise RuntimeError(f"p_run_kernel: {n} dependency wait(s) timed out; the GOP's symbols are unreliable")
 
     def encode_i_rows(self, cur, by0: int, by1: int, qp_rd: int, out: FrameSymbols,
                       qp_row_dev: torch.Tensor | None = None, qp_map_dev: torch.Tensor | None = None,

@@ -346,6 +346,105 @@ def gen_inter_me_variants(Encoder, out):
     np.savez_compressed(os.path.join(out, "inter_me_variants.npz"), **res)
 
 
+def canon_residuals(res_list, bs):
+    """inter/intra_prediction's residual_per_block [(0, r bs x bs) | (1, [r x 4])] as
+    int16 [nb][bs*bs] (split: the 4 sub-blocks' (bs/2)^2 values in Z order)."""
+    out = np.zeros((len(res_list), bs * bs), np.int16)
+    for i, (s, r) in enumerate(res_list):
+        if s == 0:
+            out[i] = np.asarray(r).reshape(-1)
+        else:
+            q = bs * bs // 4
+            for j in range(4):
+                out[i, j * q:(j + 1) * q] = np.asarray(r[j]).reshape(-1)
+    return out
+
+
+def gen_blockapi(Encoder, out):
+    """The reference's per-block / per-frame public methods, called directly:
+    inter_prediction (Encoder.py:462-585), intra_prediction (:1238-1347), find_best_match
+    with FMEEnable on frac frames (:678-717), reconstruct_block (:824-827) and
+    calculate_RD_cost (:1133-1158)."""
+    res = {}
+    rng = np.random.default_rng(4321)
+    # inter_prediction, CIF, VBS on and off (mvs, average MAE, unquantised residuals)
+    seq = synth_sequence(2, 288, 352, seed=0)
+    for vbs in (False, True):
+        enc = make_codec(Encoder, seq, 4, vbs=vbs)
+        enc.set_Qp(4)
+        cur = enc.pad_hw(seq[1], 16, 128)
+        with quiet():
+            mvs, avg, resid = enc.inter_prediction(cur, [seq[0]], 16, 16)
+        split, mv, _ = canon_inter(mvs, [(m[0], np.zeros((16, 16)) if m[0] == 0 else [np.zeros((8, 8))] * 4)
+                                         for m in mvs], 16)
+        k = f"inter_vbs{int(vbs)}"
+        res[k + "_split"], res[k + "_mv"] = split, mv
+        res[k + "_avg_mae"] = np.float64(avg)
+        res[k + "_resid"] = canon_residuals(resid, 16)
+    res["inter_cur"], res["inter_ref"] = seq[1], seq[0]
+    # inter_prediction with FMEEnable: complete_inter_flow's call (frac frames, 2 sr; :1647-1651)
+    sq = synth_sequence(2, 64, 96, seed=4)
+    enc = make_codec(Encoder, sq, 4, vbs=True, fme=True)
+    enc.set_Qp(4)
+    cur = enc.pad_hw(sq[1], 16, 128)
+    frac = enc.frac_me_reference_frame([sq[0]], 16)
+    with quiet():
+        mvs, avg, resid = enc.inter_prediction(cur, frac, 16, 32)
+    split, mv, _ = canon_inter(mvs, [(m[0], np.zeros((16, 16)) if m[0] == 0 else [np.zeros((8, 8))] * 4)
+                                     for m in mvs], 16)
+    res["fme_split"], res["fme_mv"], res["fme_avg_mae"] = split, mv, np.float64(avg)
+    res["fme_resid"] = canon_residuals(resid, 16)
+    res["fme_cur"], res["fme_ref"] = sq[1], sq[0]
+    # find_best_match on the frac frame (FMEEnable), full blocks and 8x8 sub-blocks
+    fbm = []
+    for by in range(4):
+        for bx in range(6):
+            for bs_, off in ((16, (0, 0)), (8, (8, 8))):
+                x, y = bx * 16 + off[0], by * 16 + off[1]
+                (dx, dy, r), mae = enc.find_best_match(cur[y:y + bs_, x:x + bs_], frac, 2 * x, 2 * y, bs_, 32)
+                fbm.append((x, y, bs_, dx, dy, r, int(mae * bs_ * bs_) if np.isfinite(mae) else -1))
+    res["fme_fbm"] = np.array(fbm, np.int32)
+    # intra_prediction, CIF, VBS on (canvas 288x352 is the frame here)
+    sq = synth_sequence(1, 288, 352, seed=0)
+    enc = make_codec(Encoder, sq, 6, vbs=True)
+    enc.set_Qp(6)
+    cur = enc.pad_hw(sq[0], 16, 128)
+    with quiet():
+        mvs, avg, resid, canvas = enc.intra_prediction(cur, 0, 16, 16)
+    split, mv, _ = canon_intra(mvs, [(m[0], np.zeros((16, 16)) if m[0] == 0 else [np.zeros((8, 8))] * 4)
+                                     for m in mvs], 16)
+    res["intra_cur"], res["intra_split"], res["intra_mv"] = sq[0], split, mv
+    res["intra_avg_mae"] = np.float64(avg)
+    res["intra_resid"] = canon_residuals(resid, 16)
+    res["intra_canvas"] = np.asarray(canvas, np.float64)
+    # reconstruct_block: predicted uint8 + dequantised IDCT of QTC, Q of QP 0..6, both sizes
+    enc = make_codec(Encoder, np.zeros((1, 32, 32), np.uint8), 4)
+    for n in (16, 8):
+        kb = 300
+        pred = rng.integers(0, 256, size=(kb, n, n)).astype(np.uint8)
+        qtc = (rng.integers(-6, 7, size=(kb, n, n)) * (rng.random((kb, n, n)) < 0.3)).astype(np.int64)
+        qp = rng.integers(0, 7, size=kb)
+        rec = np.stack([enc.reconstruct_block(pred[i], qtc[i], enc.generate_Q_matrix(n, int(qp[i])))
+                        for i in range(kb)])
+        res[f"rb{n}_pred"], res[f"rb{n}_qtc"], res[f"rb{n}_qp"] = pred, qtc.astype(np.int16), qp.astype(np.int8)
+        res[f"rb{n}_out"] = rec.astype(np.uint8)
+    # calculate_RD_cost: (frame_type, split) x residual blocks x QP, float64 costs
+    cost, cin = [], []
+    for i in range(200):
+        ft, sp = int(rng.integers(0, 2)), int(rng.integers(0, 2))
+        qp = int(rng.integers(0, 7))
+        mae = float(rng.integers(0, 40 * 256)) / 256.0
+        enc.set_Qp(qp)
+        r16 = rng.integers(-60, 61, size=(16, 16)).astype(np.float64)
+        resid = r16 if sp == 0 else [r16[:8, :8], r16[:8, 8:], r16[8:, :8], r16[8:, 8:]]
+        cost.append(enc.calculate_RD_cost(ft, sp, mae, resid, 16, 8, 0.015))
+        cin.append((ft, sp, qp, mae))
+        res[f"rd_res{i}"] = r16.astype(np.int16)
+    res["rd_in"] = np.array(cin, np.float64)
+    res["rd_cost"] = np.array(cost, np.float64)
+    np.savez_compressed(os.path.join(out, "blockapi.npz"), **res)
+
+
 def gen_rc(Encoder, out):
     """Golden vector 6: the per-row QP schedule (Encoder.py:78-88, 1576-1609)."""
     tables = [[9000, 6000, 4000, 2600, 1700, 1100, 700, 450, 300, 200],
@@ -458,6 +557,9 @@ def main():
         gen_gop(Encoder, out, "gop_fast_fme", frames=3, intra_dur=3, qp=4, vbs=False, h=64, w=96, seed=8,
                 fast_me=True, fme=True)
         print("gop fme/fast done", flush=True)
+    if "blockapi" in todo:
+        gen_blockapi(Encoder, out)
+        print("blockapi done", flush=True)
     if args.large:
         gen_large(Encoder, out)
 

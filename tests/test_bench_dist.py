@@ -48,3 +48,29 @@ def test_bench_single_rank_defaults():
         os.environ.pop(k, None)
     assert bench.dist_setup(backend="gloo") == (1, 0, 0)
     assert bench.max_over_ranks(3.5, 1) == 3.5
+
+
+def test_bench_gpus_flag_launches_ranks_cpu_plumbing():
+    """`bench.py --gpus 2` with no torchrun environment re-launches itself as 2 ranks
+    (torch.distributed.run) and rank 0 prints n_gpus 2 for configs[3] (one 4K GOP sharded
+    over the ranks, strong scaling).  --cpu-plumbing swaps the HIP engine for a trivial CPU
+    stand-in (gloo), so this runs without a GPU; --frames keeps it short."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-plumbing", "--gpus", "2",
+                          "--frames", "3", "--steps", "1", "--warmup", "1"], env=env, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["config"]["name"] == "4k120" and "configs[3]" in line["config"]["workload"]
+    assert line["config"]["parallelism"].startswith("stripe x2")
+
+
+def test_bench_gpus_mismatch_is_an_error():
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-plumbing", "--gpus", "2"], env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "WORLD_SIZE 1" in out.stderr

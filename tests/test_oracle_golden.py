@@ -103,11 +103,14 @@ def test_inter_recon_equals_encoder_recon():
     assert (rec == g["recon"]).all()
 
 
-def test_large_1088p_hash():
-    """2-frame 1920x1088 I+P encode vs the reference's sha256 (the reference took ~90 s)."""
+@pytest.mark.parametrize("key,h,w", [("1920x1088", 1088, 1920), ("3840x2160", 2160, 3840)])
+def test_large_hash(key, h, w):
+    """2-frame I+P encodes at 1920x1088 and 4K vs the reference's sha256 (the reference took
+    ~90 s and ~340 s): the pin of the oracle at the benchmarked sizes, which
+    tests/golden/make_large_fixtures.py then runs over the whole benchmarked GOPs."""
     from streamoptima_amd.synth import synth_sequence
-    exp = json.load(open(os.path.join(GOLDEN, "large_hashes.json")))["1920x1088"]
-    seq = synth_sequence(2, 1088, 1920, seed=0)
+    exp = json.load(open(os.path.join(GOLDEN, "large_hashes.json")))[key]
+    seq = synth_sequence(2, h, w, seed=0)
     out = encode_gop(seq, 4, 2)
     sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()  # noqa: E731
     for i in range(2):
@@ -172,3 +175,28 @@ def test_gop_me_variants(name, cfg):
         assert (o["recon"] == g["recon"][i]).all()
         assert o["psnr"] == pytest.approx(float(g["psnr"][i]), abs=1e-9)
     assert (g["decoded"] == g["recon"]).all()
+
+
+@pytest.mark.parametrize("name,n", [("1080p", 3), ("4k", 2), ("4k120", 2), ("4k_rc2pass", 2)])
+def test_large_gop_fixture_head_reproduces(name, n):
+    """tests/golden/large_gops.json (the digests the -m gpu tests and bench.py check the HIP
+    path against) is reproducible: the oracle's first frames of each benchmarked workload
+    digest to the committed values (the full GOPs: tests/golden/make_large_fixtures.py)."""
+    from streamoptima_amd.digest import frame_digest
+    from streamoptima_amd.synth import synth_sequence
+    from streamoptima_amd.workloads import RC_TABLES, WORKLOADS, padded, roi_offsets
+    fx = json.load(open(os.path.join(GOLDEN, "large_gops.json")))[name]
+    cfg = WORKLOADS[name]
+    assert len(fx["frame_sha256"]) == cfg["frames"] and fx["config"]["seed"] == cfg["seed"]
+    h, w = cfg["h"], cfg["w"]
+    fr = np.full((n, padded(h), padded(w)), 128, np.uint8)
+    fr[:, :h, :w] = synth_sequence(n, h, w, seed=cfg["seed"])
+    rc = cfg.get("rc")
+    out = encode_gop(fr, cfg["qp"], cfg["intra_dur"], rc=rc, target=cfg.get("target"), tables=RC_TABLES if rc else None,
+                     roi=roi_offsets(cfg.get("roi"), h, w, 16))
+    for i, r in enumerate(out):
+        arrs = {k: r[k] for k in ("split", "mv", "qtc", "tokens", "mae_num", "recon")}
+        if r.get("qp_map") is not None:
+            arrs["qp_map"] = r["qp_map"]
+        assert frame_digest(r["frame_type"], arrs) == fx["frame_sha256"][i], (name, i)
+        assert r["psnr"] == pytest.approx(fx["psnr"][i], abs=1e-9)
