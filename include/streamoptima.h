@@ -272,6 +272,21 @@ int so_intra_recon(int H, int W, int bs, int qp, const int32_t* qp_row,
                    uint8_t* out_recon, int32_t* scratch, void* stream);
 
 /*
+ * Batched per-block transforms for the reference's per-block public methods (the drop-in
+ * surface): n blocks of N x N doubles (N = 16 or 8), row-major [n][N][N].
+ *   inverse 0: out_tc = np.round(DCT-II 2-D)     -- apply_2d_dct (Encoder.py:779-784)
+ *              with qp >= 0 also out_q = np.round(TC / Q(N, qp)) -- quantize_TC (:787-789)
+ *              and out_tokens[n] = len(entropy_encoder_block(QTC)) (:1086-1131), the
+ *              per-block terms of calculate_RD_cost (:1133-1158)
+ *   inverse 1: out_tc = np.round(DCT-III 2-D)    -- apply_2d_idct (:810-817), the transform
+ *              inside reconstruct_block (:824-827); out_q / out_tokens must be NULL
+ * Outputs are device int32 [n][N][N] / [n] (each may be NULL).  Same FP64 operation order as
+ * the frame kernels (pocketfft replica, bitwise equal to scipy.fftpack).
+ */
+int so_block_xform(const double* in, int n, int N, int inverse, int qp, int32_t* out_tc,
+                   int32_t* out_q, int32_t* out_tokens, void* stream);
+
+/*
  * Sum of squared differences of two uint8 planes of n pixels, ADDED into *out_sse
  * (device uint64; zero it first).  PSNR per frame (calculate_metrics, Encoder.py:934)
  * is 10*log10(255^2 / (sse / n)) on the host.

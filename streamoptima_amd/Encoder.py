@@ -30,6 +30,7 @@ import torch
 
 from . import decoder as _decoder_mod
 from .engine import Engine, FrameSymbols, alloc_planes
+from .blockapi import BlockAPI
 from .bitstream import (differential_encoder_frame as _diff_enc, entropy_encoder_block as _ent_blk,
                         entropy_encoder_frame as _ent_frame)
 from .package import LazyPackage, frame_mvs, frame_residuals, symbols_to_host
@@ -43,8 +44,9 @@ def _psnr_from_sse(sse: int, n: int) -> float:
     return float(10 * np.log10((255 ** 2) / mse))
 
 
-class Y_Video_codec:
-    """See Encoder.py:24 of the reference for the argument meanings."""
+class Y_Video_codec(BlockAPI):
+    """See Encoder.py:24 of the reference for the argument meanings.  The per-block public
+    methods (find_best_match, inter_prediction, apply_2d_dct, ...) come from BlockAPI."""
 
     def __init__(self, h_pixels, w_pixels, frames, block_size, search_range, Qp, intra_dur, intra_mode,
                  lam=None, VBSEnable=False, nRefFrames=1, yuv_file=None, y_only_frame_arr=None,
@@ -298,10 +300,11 @@ class Y_Video_codec:
             return mvs, avg_mae, qblocks, qp_row, recon, resid_frame, rsize, row_pct
         return mvs, avg_mae, qblocks, qp_row, recon, rsize, row_pct
 
-    def _avg_mae(self, mae_num: np.ndarray) -> float:
+    def _avg_mae(self, mae_num: np.ndarray, bs: int | None = None) -> float:
         if (mae_num < 0).any():
             return float("inf")
-        bb = self.block_size * self.block_size
+        bs = self.block_size if bs is None else bs
+        bb = bs * bs
         return (int(mae_num.astype(np.int64).sum()) / bb) / len(mae_num)
 
     # ---- GOP driver ------------------------------------------------------------------------

@@ -48,6 +48,7 @@ _SIGS = {
     "so_inter_recon": ([_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "so_intra_recon": ([_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "so_sse_u8": ([_vp, _vp, ctypes.c_int64, _vp, _vp], _i),
+    "so_block_xform": ([_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp], _i),
     "so_fme_plane_stride": ([_i, _i], _sz),
     "so_fme_workspace_bytes": ([_i, _i, _i], _sz),
     "so_fme_planes": ([_vp, _i, _i, _i, _vp, _vp], _i),

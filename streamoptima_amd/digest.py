@@ -2,13 +2,13 @@
 
 One sha256 per frame over the frame's symbols in a fixed byte layout, so the HIP path's
 output at the benchmarked sizes (4K x 120 frames: ~3 GB of symbols) can be compared with
-the C oracle's through a small committed fixture (tests/golden/large_gops.json):
+the CPU checker's through a small committed fixture (tests/golden/large_gops.json):
 
     frame_type u8 | split u8[nb] | mv int16 [nb,4,3] (P) or [nb,4] (I) |
     qtc int16 [nb, bs*bs] | tokens int32 [nb] | mae_num int64 [nb] (MAE * bs^2, -1 = inf) |
     recon u8 [Hp, Wp] | qp_map int32 [nb] (ROI / two-pass RC only)
 
-all little-endian, in that order.  The same function digests numpy arrays from the oracle
+all little-endian, in that order.  The same function digests numpy arrays from the CPU checker
 and arrays copied back from the GPU.
 """
 from __future__ import annotations

@@ -118,3 +118,17 @@ def synth_sequence_torch(frames: int, height: int, width: int, seed: int = 0, de
         tn = _t_umod(_t_h(xs, ys, seed ^ (0xA5A5 + t)), 5)
         out[t] = (moved + tn - 2).clamp_(0, 255).to(torch.uint8)
     return out
+
+
+def write_synth_yuv420(path: str, frames: int, height: int, width: int, seed: int = 0) -> None:
+    """A raw planar 4:2:0 file (Y | U | V per frame, the reference's input format,
+    video_manager.py:53-77): Y = synth_sequence, U / V = synth_sequence at half size with
+    seeds + 1 / + 2."""
+    y = synth_sequence(frames, height, width, seed)
+    u = synth_sequence(frames, height // 2, width // 2, seed + 1)
+    v = synth_sequence(frames, height // 2, width // 2, seed + 2)
+    with open(path, "wb") as f:
+        for t in range(frames):
+            f.write(y[t].tobytes())
+            f.write(u[t].tobytes())
+            f.write(v[t].tobytes())

@@ -1,6 +1,6 @@
 """The benchmarked workloads (BASELINE.json `configs`), in one place.
 
-bench.py times them, tests/golden/make_large_fixtures.py runs the C oracle over them to
+bench.py times them, tests/golden/make_large_fixtures.py runs the CPU checker over them to
 produce the committed per-frame digests (tests/golden/large_gops.json), and the `-m gpu`
 tests and bench.py check the HIP path's output against those digests.
 

@@ -445,6 +445,31 @@ def gen_blockapi(Encoder, out):
     np.savez_compressed(os.path.join(out, "blockapi.npz"), **res)
 
 
+def gen_yuv(Encoder, out):
+    """YUV file I/O (video_manager.py:4-241, Encoder.read_yuv :110-126): the reference's
+    Video_Manager on a 21-frame CIF 4:2:0 file (its constructor always reads 21 frames) and
+    read_yuv on the same file; sha256 of each output (the file is regenerated by the tests
+    from streamoptima_amd/synth.py:write_synth_yuv420)."""
+    import video_manager as vmod
+    from streamoptima_amd.synth import write_synth_yuv420
+    path = os.path.join(os.getcwd(), "cif.yuv")
+    write_synth_yuv420(path, 21, 288, 352, seed=12)
+    vm = vmod.Video_Manager(path, 288, 352, 21, "yuv_420")
+    up = vm.upscale_yuv420_to_yuv444()
+    rgb = vm.convert_yuv444_to_rgb()
+    y = vm.extract_y_only()
+    ry = Encoder.Y_Video_codec.read_yuv(path, 288, 352, 21)
+    rec = {"frames": 21, "h": 288, "w": 352, "seed": 12,
+           "yuv420_shape": list(vm.vid_frames_yuv420.shape), "yuv420_sha": sha(vm.vid_frames_yuv420),
+           "upscale_shape": list(up.shape), "upscale_sha": sha(up),
+           "yuv444_shape": list(vm.vid_frames_yuv444.shape), "yuv444_sha": sha(vm.vid_frames_yuv444),
+           "rgb_shape": list(rgb.shape), "rgb_sha": sha(rgb), "rgb_dtype": str(rgb.dtype),
+           "y_shape": list(y.shape), "y_sha": sha(y), "read_yuv_sha": sha(np.asarray(ry)),
+           "read_yuv_dtype": str(np.asarray(ry).dtype)}
+    with open(os.path.join(out, "yuv_io.json"), "w") as f:
+        json.dump(rec, f, indent=1)
+
+
 def gen_rc(Encoder, out):
     """Golden vector 6: the per-row QP schedule (Encoder.py:78-88, 1576-1609)."""
     tables = [[9000, 6000, 4000, 2600, 1700, 1100, 700, 450, 300, 200],
@@ -557,6 +582,9 @@ def main():
         gen_gop(Encoder, out, "gop_fast_fme", frames=3, intra_dur=3, qp=4, vbs=False, h=64, w=96, seed=8,
                 fast_me=True, fme=True)
         print("gop fme/fast done", flush=True)
+    if "yuv" in todo:
+        gen_yuv(Encoder, out)
+        print("yuv done", flush=True)
     if "blockapi" in todo:
         gen_blockapi(Encoder, out)
         print("blockapi done", flush=True)

@@ -1,9 +1,10 @@
 #!/bin/bash
-# GPU parity suite (no -x: report every failure); stops the call on a crash code.
+# The -m gpu suite in one process, with a per-test time limit and a whole-run limit.
 cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -q -m gpu -p no:cacheprovider "$@" > gpurun_out/pytest_gpu.log 2>&1
-rc=$?
-echo "pytest rc=$rc"
-grep -E "passed|failed|error|FAILED|ERROR" gpurun_out/pytest_gpu.log | tail -40
+T=${TAG:-tests}
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider ${PYTEST_ARGS} \
+    > gpurun_out/pytest_gpu_$T.log 2>&1
+rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|FAILED|ERROR|Error" gpurun_out/pytest_gpu_$T.log | tail -15
 exit $rc
