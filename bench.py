@@ -78,6 +78,9 @@ def parse(argv=None):
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-pcie", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=20)
+    ap.add_argument("--exchange", choices=("p2p", "allgather"), default="p2p",
+                    help="stripe hand-off: inside the persistent launch over xGMI (p2p, self-checked against "
+                         "allgather before timing) or an RCCL all_gather of every reconstruction (allgather)")
     ap.add_argument("--shard", choices=("stripe", "gop"), default="stripe",
                     help="N>1: block-row stripes of ONE GOP (strong, configs[3]) or a GOP per rank (weak)")
     ap.add_argument("--me", choices=("full", "fme", "fast", "fastpar", "fast_fme"), default="full",
@@ -85,6 +88,9 @@ def parse(argv=None):
                          "ParallelMode 2, fast_me + FMEEnable")
     ap.add_argument("--graph", action="store_true",
                     help="replay the GOP as one captured HIP graph (measured slower than host launches here)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal on a one-GPU host: every rank on cuda:0, gloo collectives, each rank's persistent "
+                         "grid capped to a 1/(2N) share of the GPU (numbers are not a scaling measurement)")
     ap.add_argument("--cpu-plumbing", action="store_true",
                     help="test mode: gloo + a trivial CPU stand-in engine (no encode, no GPU) to exercise the "
                          "rank launch, sharding, timing and JSON line on a CPU-only host")
@@ -483,6 +489,41 @@ def record_1080p(args, dev) -> dict:
     return rec
 
 
+# ---- multi-GPU hand-off -------------------------------------------------------------------------
+def p2p_encoder(eng, frames, cfg, senc, world, max_wg=0):
+    """The in-launch stripe hand-off (streamoptima_amd/pipeline.py), self-checked before
+    timing: the first 4 frames of the workload through it and through the RCCL all_gather
+    path must give identical symbols on every rank, with no dependency wait timed out.
+    Anything else (IPC unavailable, a lost flag, a mismatch) falls back to all_gather."""
+    import torch.distributed as dist
+    from streamoptima_amd.digest import frame_digest
+    from streamoptima_amd.pipeline import PipelinedStripeGOPEncoder
+    ok, penc, why = 1, None, ""
+    try:
+        penc = PipelinedStripeGOPEncoder(eng, cfg["frames"], max_wg=max_wg)
+    except Exception as e:   # noqa: BLE001 -- any failure to set up the peer mapping
+        ok, why = 0, f"setup: {e}"
+    flag = torch.tensor([ok], dtype=torch.int32, device=eng.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 0:
+        return None, "all_gather (RCCL) per frame; p2p hand-off unavailable" + (f" ({why})" if why else "")
+    k = min(4, cfg["frames"])
+    a = penc.encode(frames[:k], cfg["intra_dur"], cfg["qp"])
+    b = senc.encode(frames[:k], cfg["intra_dur"], cfg["qp"])
+    torch.cuda.synchronize()
+    good = not penc.r.timed_out()
+    for i in range(k):
+        ga, gb = penc.gather_symbols(a["symbols"][i], i), senc.gather_symbols(b["symbols"][i])
+        da = frame_digest(ga["frame_type"], {n: (v.cpu().numpy() if torch.is_tensor(v) else v) for n, v in ga.items()})
+        db = frame_digest(gb["frame_type"], {n: (v.cpu().numpy() if torch.is_tensor(v) else v) for n, v in gb.items()})
+        good = good and da == db
+    flag = torch.tensor([1 if good else 0], dtype=torch.int32, device=eng.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 0:
+        return None, "all_gather (RCCL) per frame; p2p self-check failed"
+    return penc, "in-launch p2p over xGMI (uncached landing planes, IPC), self-checked"
+
+
 # ---- CPU plumbing stand-in (--cpu-plumbing) ---------------------------------------------------------
 class _PlumbingEngine:
     """A trivial CPU stand-in with the Engine stripe methods StripeGOPEncoder calls: symbols
@@ -521,7 +562,10 @@ def main(argv=None):
     args = parse(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
-    world, rank, local = dist_setup("gloo" if args.cpu_plumbing else "nccl")
+    world, rank, local = dist_setup("gloo" if (args.cpu_plumbing or args.share_gpu) else "nccl")
+    if args.share_gpu:
+        local = 0
+        torch.cuda.set_device(0)
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}")
     from streamoptima_amd.workloads import WORKLOADS
@@ -535,6 +579,8 @@ def main(argv=None):
     dev = torch.device("cpu") if args.cpu_plumbing else torch.device("cuda", local)
     h, w, f = cfg["h"], cfg["w"], cfg["frames"]
 
+    exchange_note = "all_gather per frame"
+    penc = None
     if args.cpu_plumbing:
         from streamoptima_amd.dist import StripeGOPEncoder
         from streamoptima_amd.synth import synth_sequence
@@ -554,11 +600,22 @@ def main(argv=None):
         frames = make_frames(cfg, dev, cfg["seed"])
         senc = StripeGOPEncoder(eng)
         rc = cfg.get("rc")
+        penc = None
+        if args.exchange == "p2p" and not rc and args.me == "full" and not args.vbs and eng.pipelined_ok(1):
+            penc, exchange_note = p2p_encoder(eng, frames, cfg, senc, world,
+                                              max_wg=768 // (2 * world) if args.share_gpu else 0)
+        else:
+            exchange_note = "all_gather (RCCL) per frame" + (": RC/ROI GOP" if rc else "")
+        if penc is not None:
+            pre_s = [penc.r.new_symbols(0 if i % cfg["intra_dur"] == 0 else 1) for i in range(f)]
 
-        def step():
-            return senc.encode(frames, cfg["intra_dur"], cfg["qp"],
-                               qp_sched=codec.row_qp_schedule(eng.nby) if rc else None, rc_flag=rc,
-                               intra_thresh=None, roi=codec.roi_block_offsets())
+            def step():
+                return penc.encode(frames, cfg["intra_dur"], cfg["qp"], symbols=pre_s)
+        else:
+            def step():
+                return senc.encode(frames, cfg["intra_dur"], cfg["qp"],
+                                   qp_sched=codec.row_qp_schedule(eng.nby) if rc else None, rc_flag=rc,
+                                   intra_thresh=None, roi=codec.roi_block_offsets())
     else:
         codec, frames, pre, step = run_single(cfg, args, dev, parity_ok)
         if world > 1 and rank > 0:   # --shard gop: an independent GOP per rank (seed + rank)
@@ -567,12 +624,30 @@ def main(argv=None):
     elapsed, res = time_steps(step, world, args.steps, args.warmup, dev)
     if codec is not None and not stripe:
         codec.engine().check_run()
+    if penc is not None:
+        # a lost hand-off anywhere voids the timed run: time the all_gather path instead
+        import torch.distributed as dist
+        lost = torch.tensor([1 if penc.r.timed_out() else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(lost, op=dist.ReduceOp.MAX)
+        if int(lost.item()):
+            penc.r._ws[32].zero_()
+            penc = None
+            exchange_note = "all_gather (RCCL) per frame; the p2p run timed out a hand-off and was discarded"
+            rc = cfg.get("rc")
+
+            def step():  # noqa: F811
+                return senc.encode(frames, cfg["intra_dur"], cfg["qp"])
+            elapsed, res = time_steps(step, world, args.steps, args.warmup, dev)
 
     # ---- after timing: parity of the timed output ----
     parity = None
     if parity_ok and not args.cpu_plumbing:
         if stripe:
-            full = [senc.gather_symbols(s) for s in res["symbols"]]
+            if penc is not None:
+                penc.check()
+                full = [penc.gather_symbols(s, i) for i, s in enumerate(res["symbols"])]
+            else:
+                full = [senc.gather_symbols(s) for s in res["symbols"]]
             if rank == 0:
                 hosts = [{k: (v.cpu().numpy() if torch.is_tensor(v) else v) for k, v in g.items()} for g in full]
                 parity = parity_of(hosts, name, cfg) if not cfg.get("rc") else {
@@ -596,8 +671,10 @@ def main(argv=None):
     rl = None
     if rank == 0 and not args.cpu_plumbing and args.me == "full" and codec.engine().pipelined_ok(1) \
             and not cfg.get("rc") and not args.vbs:
-        # (stripe mode: every frame's recon plane is the gathered full frame)
-        rl = kernel_roofline(codec, frames, res["symbols"], args.kernel_reps)
+        # stripe mode: the kernel is timed on rank 0's GPU alone over the full frame (a
+        # one-GPU GOP supplies the reference reconstructions it replays)
+        syms = res["symbols"] if not stripe else codec.encode_device(frames, cfg["intra_dur"])["symbols"]
+        rl = kernel_roofline(codec, frames, syms, args.kernel_reps)
     records = None
     if rank == 0 and world == 1 and not args.cpu_plumbing and not args.no_records and name == "4k" \
             and args.me == "full" and not args.vbs:
@@ -626,7 +703,7 @@ def main(argv=None):
                    "intra_dur": cfg["intra_dur"], "block_size": 16, "search_range": 16, "qp": cfg["qp"],
                    "seed": cfg["seed"], "vbs": bool(args.vbs), "nRefFrames": 1, "me": args.me,
                    "transform": "fp64 pocketfft-exact DCT",
-                   "parallelism": (f"stripe x{world} (block rows of one GOP, all_gather recon per frame)" if stripe
+                   "parallelism": (f"stripe x{world} (block rows of one GOP; hand-off: {exchange_note})" if stripe
                                    else f"gop-per-rank x{world}"),
                    "launch": "hip-graph (one GOP per replay)" if args.graph else "host launches"},
         "parity": parity,

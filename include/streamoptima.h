@@ -142,6 +142,58 @@ int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0
                     int32_t* const* out_mae_num, uint8_t* const* out_recon, int32_t* const* out_sse,
                     uint32_t* workspace, void* stream);
 
+/*
+ * ONE GOP across the GPUs of a node (BASELINE configs[3]): rank r encodes the block rows
+ * [by0, by1) of every P-frame of a run with the persistent kernel of so_encode_p_run, and the
+ * stripes hand their boundary rows to each other inside the launch -- the reference's frame
+ * dependency (Encoder.py:1864-1867, P(i) searches recon(i-1)) extended across GPUs:
+ *   * each rank's reconstruction planes live in UNCACHED device memory (so_alloc_uncached),
+ *     addressed by "virtual" full-frame bases (row y of frame gf at base_gf + y * W; the
+ *     allocation holds rows [16 by0 - 16, 16 by1 + 32));
+ *   * a tile of the stripe's first (last) tile row also stores its top (bottom) 16 rows into
+ *     the up (down) neighbour's plane of the frame -- peer memory mapped with so_ipc_open,
+ *     reached over xGMI -- with system-scope write-through stores and, once they have drained,
+ *     sets the neighbour's flag [gf * tiles_x + tx] (tiles_x = W / 128) to `epoch`;
+ *   * a first- (last-) row tile waits, besides its own 3x3 tiles of the frame before, for
+ *     my_up_flags (my_dn_flags) [(gf - 1) * tiles_x + tx - 1 .. tx + 1] == epoch.
+ * curs: the frames (full H x W planes, only the stripe rows are read); out_recon[i]: virtual
+ * bases of the stripe's planes; ref0: the virtual base of frame gbase - 1; symbol outputs are
+ * stripe-local as in so_encode_p_rows.  peer_up0 / peer_dn0: the neighbours' virtual bases
+ * of frame 0 as mapped here (frame gf at + gf * stride); any of the four neighbour pointers
+ * NULL = no neighbour on that side.  epoch: a per-GOP value the flags are compared with
+ * (they are never reset).  max_wg > 0 caps the resident grid (ranks sharing one GPU).
+ * gbase >= 1 (frame 0 is the GOP's I-frame).
+ */
+int so_encode_p_run_stripe(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W,
+                           int bs, int sr, int by0, int by1, int qp_rd, const int32_t* qp_row,
+                           uint8_t* const* out_split, int16_t* const* out_mv, int16_t* const* out_qtc,
+                           int32_t* const* out_tokens, int32_t* const* out_mae_num,
+                           uint8_t* const* out_recon, int32_t* const* out_sse, uint32_t* workspace,
+                           int gbase, uint8_t* peer_up0, uint8_t* peer_dn0, long long stride,
+                           const uint32_t* my_up_flags, const uint32_t* my_dn_flags,
+                           uint32_t* peer_up_flags, uint32_t* peer_dn_flags, uint32_t epoch, int max_wg,
+                           void* stream);
+
+/* The I-frame's hand-off: rows [16 by0, 16 by0 + 16) of `plane` (a virtual base) to peer_up,
+ * rows [16 by1 - 16, 16 by1) to peer_dn (the neighbours' virtual bases of frame gf), then
+ * their flags [gf * tiles_x + tx] = epoch.  NULL peer = no neighbour on that side. */
+int so_stripe_halo_push(const uint8_t* plane, int H, int W, int by0, int by1, int gf, uint8_t* peer_up,
+                        uint8_t* peer_dn, uint32_t* peer_up_flags, uint32_t* peer_dn_flags,
+                        uint32_t epoch, void* stream);
+
+/* Device memory the ranks share.  The one exception to "the library never allocates": the
+ * landing planes and flags of the cross-GPU hand-off must be uncached
+ * (hipExtMallocWithFlags(hipDeviceMallocUncached)), which PyTorch cannot allocate. */
+#define SO_IPC_HANDLE_BYTES 64
+int so_alloc_uncached(size_t bytes, void** out);
+int so_free_device(void* p);
+int so_ipc_export(void* p, uint8_t* out_handle);            /* hipIpcGetMemHandle */
+int so_ipc_open(const uint8_t* handle, void** out);         /* hipIpcOpenMemHandle */
+int so_ipc_close(void* p);
+/* stream-ordered copies / fills of such memory (torch cannot wrap it) */
+int so_copy_d2d(void* dst, const void* src, size_t bytes, void* stream);
+int so_memset_d8(void* dst, int value, size_t bytes, void* stream);
+
 /* int32 elements of scratch so_encode_i_frame / so_intra_recon need: nb*(bs*bs) + nb*8 */
 size_t so_i_frame_scratch_elems(int H, int W, int bs);
 

@@ -49,6 +49,16 @@ _SIGS = {
     "so_intra_recon": ([_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "so_sse_u8": ([_vp, _vp, ctypes.c_int64, _vp, _vp], _i),
     "so_block_xform": ([_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp], _i),
+    "so_encode_p_run_stripe": ([_vp, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                _i, _vp, _vp, ctypes.c_longlong, _vp, _vp, _vp, _vp, ctypes.c_uint32, _i, _vp], _i),
+    "so_stripe_halo_push": ([_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, ctypes.c_uint32, _vp], _i),
+    "so_alloc_uncached": ([_sz, ctypes.POINTER(ctypes.c_void_p)], _i),
+    "so_free_device": ([_vp], _i),
+    "so_ipc_export": ([_vp, _vp], _i),
+    "so_ipc_open": ([_vp, ctypes.POINTER(ctypes.c_void_p)], _i),
+    "so_ipc_close": ([_vp], _i),
+    "so_copy_d2d": ([_vp, _vp, _sz, _vp], _i),
+    "so_memset_d8": ([_vp, _i, _sz, _vp], _i),
     "so_fme_plane_stride": ([_i, _i], _sz),
     "so_fme_workspace_bytes": ([_i, _i, _i], _sz),
     "so_fme_planes": ([_vp, _i, _i, _i, _vp, _vp], _i),

@@ -8,6 +8,8 @@
 
 #include <vector>
 
+#include <hip/hip_ext.h>
+
 #include "so_common.h"
 
 namespace so {
@@ -47,6 +49,23 @@ struct PFrameOut {
 size_t p_run_workspace_words(int H, int W);
 int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                  const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, hipStream_t st);
+struct PRunStripe {
+    int by0, by1;
+    uint8_t* peer_up0;
+    uint8_t* peer_dn0;
+    long long stride;
+    const uint32_t* my_up_flags;
+    const uint32_t* my_dn_flags;
+    uint32_t* peer_up_flags;
+    uint32_t* peer_dn_flags;
+    uint32_t epoch;
+    int gbase;
+};
+int p_run_stripe_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
+                        const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg,
+                        hipStream_t st);
+int stripe_halo_push_launch(const uint8_t* plane, int W, int by0, int by1, uint8_t* up, uint8_t* dn,
+                            uint32_t* up_flags, uint32_t* dn_flags, int gf, uint32_t epoch, hipStream_t st);
 
 // The fused search + transform tile kernel (so_me.hip p_tile_kernel) covers the headline
 // configuration: bs 16, sr 16, full search, no VBS / FME, one reference.  SO_FUSED=0 or an
@@ -350,6 +369,153 @@ int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0
                             out_sse ? out_sse[i] : nullptr};
     }
     return p_run_launch(curs, nframes, ref0, H, W, qp_rd, qp_row, outs.data(), workspace, (hipStream_t)stream);
+}
+
+// ---- one GOP across GPUs: a rank's stripe of every frame (so_me.hip PRunStripe) -------------
+int so_encode_p_run_stripe(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int bs, int sr,
+                           int by0, int by1, int qp_rd, const int32_t* qp_row, uint8_t* const* out_split,
+                           int16_t* const* out_mv, int16_t* const* out_qtc, int32_t* const* out_tokens,
+                           int32_t* const* out_mae_num, uint8_t* const* out_recon, int32_t* const* out_sse,
+                           uint32_t* workspace, int gbase, uint8_t* peer_up0, uint8_t* peer_dn0, long long stride,
+                           const uint32_t* my_up_flags, const uint32_t* my_dn_flags, uint32_t* peer_up_flags,
+                           uint32_t* peer_dn_flags, uint32_t epoch, int max_wg, void* stream) {
+    const char* fn = "so_encode_p_run_stripe";
+    SO_TRY(check_geom(fn, H, W, bs, 0));
+    SO_TRY(check_sr(fn, sr));
+    SO_TRY(check_qp(fn, qp_rd));
+    if (bs != 16 || sr != 16 || W % 128 != 0) {
+        set_error("%s: covers bs 16 / sr 16 / W %% 128 == 0", fn);
+        return SO_E_UNSUPPORTED;
+    }
+    if (by0 < 0 || by1 > H / 16 || by1 <= by0 || gbase < 1) {
+        set_error("%s: bad stripe [%d, %d) of %d block rows or gbase %d", fn, by0, by1, H / 16, gbase);
+        return SO_E_INVALID;
+    }
+    if ((peer_up0 != nullptr) != (peer_up_flags != nullptr) || (peer_dn0 != nullptr) != (peer_dn_flags != nullptr) ||
+        (peer_up0 != nullptr) != (my_up_flags != nullptr) || (peer_dn0 != nullptr) != (my_dn_flags != nullptr) ||
+        (peer_up0 && by0 == 0) || (peer_dn0 && by1 == H / 16)) {
+        set_error("%s: a neighbour needs its plane, its flags and mine, and none past the frame edge", fn);
+        return SO_E_INVALID;
+    }
+    if (nframes <= 0) return SO_OK;
+    SO_NEED(curs, fn); SO_NEED(ref0, fn); SO_NEED(out_split, fn); SO_NEED(out_mv, fn); SO_NEED(out_qtc, fn);
+    SO_NEED(out_tokens, fn); SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn); SO_NEED(workspace, fn);
+    std::vector<PFrameOut> outs((size_t)nframes);
+    for (int i = 0; i < nframes; ++i) {
+        SO_NEED(curs[i], fn); SO_NEED(out_split[i], fn); SO_NEED(out_mv[i], fn); SO_NEED(out_qtc[i], fn);
+        SO_NEED(out_tokens[i], fn); SO_NEED(out_mae_num[i], fn); SO_NEED(out_recon[i], fn);
+        outs[i] = PFrameOut{out_split[i], out_mv[i], out_qtc[i], out_tokens[i], out_mae_num[i], out_recon[i],
+                            out_sse ? out_sse[i] : nullptr};
+    }
+    PRunStripe sp{by0, by1, peer_up0, peer_dn0, stride, my_up_flags, my_dn_flags, peer_up_flags, peer_dn_flags,
+                  epoch, gbase};
+    return p_run_stripe_launch(curs, nframes, ref0, H, W, qp_rd, qp_row, outs.data(), workspace, sp, max_wg,
+                               (hipStream_t)stream);
+}
+
+int so_stripe_halo_push(const uint8_t* plane, int H, int W, int by0, int by1, int gf, uint8_t* peer_up,
+                        uint8_t* peer_dn, uint32_t* peer_up_flags, uint32_t* peer_dn_flags, uint32_t epoch,
+                        void* stream) {
+    const char* fn = "so_stripe_halo_push";
+    SO_TRY(check_geom(fn, H, W, 16, 0));
+    if (W % 128 != 0 || by0 < 0 || by1 > H / 16 || by1 <= by0 || gf < 0 || by1 - by0 < 1) {
+        set_error("%s: bad stripe [%d, %d) / frame %d", fn, by0, by1, gf);
+        return SO_E_INVALID;
+    }
+    if ((peer_up != nullptr) != (peer_up_flags != nullptr) || (peer_dn != nullptr) != (peer_dn_flags != nullptr)) {
+        set_error("%s: a neighbour plane needs its flags", fn);
+        return SO_E_INVALID;
+    }
+    SO_NEED(plane, fn);
+    if (!peer_up && !peer_dn) return SO_OK;
+    return stripe_halo_push_launch(plane, W, by0, by1, peer_up, peer_dn, peer_up_flags, peer_dn_flags, gf, epoch,
+                                   (hipStream_t)stream);
+}
+
+// ---- memory the ranks share (uncached landing planes, IPC) ----------------------------------
+int so_alloc_uncached(size_t bytes, void** out) {
+    if (!out || bytes == 0) {
+        set_error("so_alloc_uncached: bad arguments");
+        return SO_E_INVALID;
+    }
+    const hipError_t e = hipExtMallocWithFlags(out, bytes, hipDeviceMallocUncached);
+    if (e != hipSuccess) {
+        set_error("so_alloc_uncached(%zu): %s", bytes, hipGetErrorString(e));
+        return (int)e;
+    }
+    return SO_OK;
+}
+
+int so_free_device(void* p) {
+    const hipError_t e = hipFree(p);
+    if (e != hipSuccess) {
+        set_error("so_free_device: %s", hipGetErrorString(e));
+        return (int)e;
+    }
+    return SO_OK;
+}
+
+int so_ipc_export(void* p, uint8_t* out_handle) {
+    static_assert(sizeof(hipIpcMemHandle_t) <= SO_IPC_HANDLE_BYTES, "IPC handle size");
+    if (!p || !out_handle) {
+        set_error("so_ipc_export: bad arguments");
+        return SO_E_INVALID;
+    }
+    hipIpcMemHandle_t h;
+    const hipError_t e = hipIpcGetMemHandle(&h, p);
+    if (e != hipSuccess) {
+        set_error("so_ipc_export: %s", hipGetErrorString(e));
+        return (int)e;
+    }
+    memset(out_handle, 0, SO_IPC_HANDLE_BYTES);
+    memcpy(out_handle, &h, sizeof(h));
+    return SO_OK;
+}
+
+int so_ipc_open(const uint8_t* handle, void** out) {
+    if (!handle || !out) {
+        set_error("so_ipc_open: bad arguments");
+        return SO_E_INVALID;
+    }
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, sizeof(h));
+    const hipError_t e = hipIpcOpenMemHandle(out, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+        set_error("so_ipc_open: %s", hipGetErrorString(e));
+        return (int)e;
+    }
+    return SO_OK;
+}
+
+int so_copy_d2d(void* dst, const void* src, size_t bytes, void* stream) {
+    if ((!dst || !src) && bytes) {
+        set_error("so_copy_d2d: bad arguments");
+        return SO_E_INVALID;
+    }
+    const hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+    if (e != hipSuccess) {
+        set_error("so_copy_d2d: %s", hipGetErrorString(e));
+        return (int)e;
+    }
+    return SO_OK;
+}
+
+int so_memset_d8(void* dst, int value, size_t bytes, void* stream) {
+    const hipError_t e = hipMemsetAsync(dst, value, bytes, (hipStream_t)stream);
+    if (e != hipSuccess) {
+        set_error("so_memset_d8: %s", hipGetErrorString(e));
+        return (int)e;
+    }
+    return SO_OK;
+}
+
+int so_ipc_close(void* p) {
+    const hipError_t e = hipIpcCloseMemHandle(p);
+    if (e != hipSuccess) {
+        set_error("so_ipc_close: %s", hipGetErrorString(e));
+        return (int)e;
+    }
+    return SO_OK;
 }
 
 size_t so_i_frame_scratch_elems(int H, int W, int bs) {

@@ -628,13 +628,21 @@ SO_DEV uint32_t win_u32(const uint32_t* win, int row, int col) {
 }
 
 #ifdef SO_STAMPS
-// Instrumented builds only (tools/sea_stamps.py): per-workgroup phase time stamps.
+// Instrumented builds only (tools/sea_stamps.py, tools/run_stamps.py): per-workgroup (per-task
+// in p_run_kernel) phase time stamps.  s_stamp_rec is the workgroup's current record.
 __device__ unsigned long long* g_sea_stamps = nullptr;
-#define SO_SEA_STAMP(i, v) do { if (tid == 0 && g_sea_stamps) g_sea_stamps[(size_t)blockIdx.x * 12 + (i)] = (v); } while (0)
+__device__ unsigned long long* g_run_stamps = nullptr;
+__shared__ unsigned long long* s_stamp_rec;
+#define SO_SEA_STAMP(i, v) do { if (tid == 0 && s_stamp_rec) s_stamp_rec[(i)] = (v); } while (0)
+#define SO_STAMP_REC_SET(p) do { if (threadIdx.x == 0) s_stamp_rec = (p); } while (0)
 extern "C" int so_debug_set_sea_stamps(void* p) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_sea_stamps), &p, sizeof(p));
 }
+extern "C" int so_debug_set_run_stamps(void* p) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_run_stamps), &p, sizeof(p));
+}
 #else
+#define SO_STAMP_REC_SET(p) do { } while (0)
 #define SO_SEA_STAMP(i, v) do { } while (0)
 #endif
 
@@ -1029,6 +1037,7 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
     __shared__ unsigned long long keys[G::NBLK];
     __shared__ uint32_t st[2];
     const Sea2Lds L{win, b4w, curt, a4, list, lcount, keys, st};
+    SO_STAMP_REC_SET(g_sea_stamps ? g_sea_stamps + (size_t)blockIdx.x * 12 : nullptr);
     sea2_tile<Sea2Geo>(L, blockIdx.x, cur, refs, nref, H, W, by0, by1, probe);
 
     const int tid = threadIdx.x;
@@ -1127,13 +1136,23 @@ struct PFrameOut {
 };
 
 
+// Boundary rows of a rank's stripe that the neighbouring ranks read (so_encode_p_run_stripe):
+// rows [y0s, up_end) are also stored into the up neighbour's landing plane of the frame, rows
+// [dn_begin, y1s) into the down neighbour's ("virtual" full-frame bases: row y of the frame is
+// at base + y * W).  Null = no such neighbour.
+struct PHalo {
+    uint8_t* up;
+    uint8_t* dn;
+    int up_end, dn_begin;
+};
+
 // The exact transform path of one block: 16 lanes (l = row) run scipy.fftpack's pocketfft
 // DCT-II / DCT-III sequence in FP64 (so_dct.h) -- the arithmetic of inter_tq_kernel<16,
 // false, false>.  `scratch` = 16 x 17 doubles of LDS owned by the calling lanes.
-template <class G, bool SC1>
+template <class G, bool SC1, bool HALO = false>
 SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, int byt0, int nbx, int by0, int by1,
                        int W, int qp_rd, const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map,
-                       const PFrameOut& o) {
+                       const PFrameOut& o, const PHalo& hl = PHalo{}) {
     constexpr int SR = G::SR, TBX = G::TBX;
     const int bxl = g % TBX, byl = g / TBX;
     const int gbx = bx0 + bxl, gby = byt0 + byl;
@@ -1190,6 +1209,18 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
                        ((uint32_t)(rec[4 * k + 2] & 255) << 16) | ((uint32_t)(rec[4 * k + 3] & 255) << 24);
             uint8_t* rp = o.recon + (size_t)(y + l) * W + x;
             asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(rp), "v"(v) : "memory");
+            if constexpr (HALO) {
+                // the rows a neighbouring rank's window reads: system-scope write-through
+                // stores into its uncached landing plane (peer memory over xGMI)
+                if (hl.up && y + l < hl.up_end) {
+                    uint8_t* q = hl.up + (size_t)(y + l) * W + x;
+                    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(q), "v"(v) : "memory");
+                }
+                if (hl.dn && y + l >= hl.dn_begin) {
+                    uint8_t* q = hl.dn + (size_t)(y + l) * W + x;
+                    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(q), "v"(v) : "memory");
+                }
+            }
         } else {
             store_row_u8<16>(o.recon, W, x, y + l, rec);
         }
@@ -1220,11 +1251,11 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
 // write-through (global_store sc1), so another XCD that later reads them (p_run_kernel's
 // next frame) gets them from memory without a release fence.  Ends with every wave's
 // stores retired (s_waitcnt vmcnt(0)) and a workgroup barrier.  `pre`: as sea2_tile's.
-template <class G, bool SC1, class Pre = NoPre>
+template <class G, bool SC1, class Pre = NoPre, bool HALO = false>
 SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur, const uint8_t* ref, int H, int W,
                        int by0, int by1, int qp_rd, const int32_t* __restrict__ qp_row,
                        const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best, const PFrameOut& o,
-                       const Pre& pre = Pre()) {
+                       const Pre& pre = Pre(), const PHalo& hl = PHalo{}) {
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, CP = G::TPX;
     using P = PTileGeo<G>;
     uint32_t* const b4w = reinterpret_cast<uint32_t*>(S.un);
@@ -1249,8 +1280,8 @@ SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur
     }
     __syncthreads();
     if (tid < G::NBLK * 16)
-        tq16_exact<G, SC1>(S, tid >> 4, tid & 15, S.un + (tid >> 4) * (16 * 17), bx0, byt0, nbx, by0, by1, W, qp_rd,
-                           qp_row, qp_map, o);
+        tq16_exact<G, SC1, HALO>(S, tid >> 4, tid & 15, S.un + (tid >> 4) * (16 * 17), bx0, byt0, nbx, by0, by1, W,
+                                 qp_rd, qp_row, qp_map, o, hl);
     if constexpr (SC1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
     __syncthreads();
 }
@@ -1265,6 +1296,7 @@ p_tile_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W, int by
               PFrameOut o) {
     using G = Sea2GeoT<NW>;
     __shared__ PTileLds<G> S;
+    SO_STAMP_REC_SET(g_sea_stamps ? g_sea_stamps + (size_t)blockIdx.x * 12 : nullptr);
     ptile_body<G, false>(S, blockIdx.x, cur, refs.p[0], H, W, by0, by1, qp_rd, qp_row, qp_map, out_best, o);
 #ifdef SO_STAMPS
     const int tid = threadIdx.x;
@@ -1319,16 +1351,44 @@ struct PRunArgs {
 // the task counter (hammered by every workgroup's dequeue), the timeout count and the done
 // flags live on separate 128-byte lines
 constexpr int kRunTimeoutWord = SO_RUN_TIMEOUT_WORD, kRunDoneBase = SO_RUN_DONE_BASE;
-template <int NW>
+// A rank's stripe of a frame shared across GPUs (so_encode_p_run_stripe): block rows [by0, by1)
+// of every frame, the reconstruction planes in uncached memory addressed by "virtual" full-frame
+// bases (row y at base + y * W; the allocation holds rows [16 * by0 - 16, 16 * by1 + 32)), and
+// the hand-off with the neighbouring ranks:
+//   * a tile in the stripe's first (last) tile row also stores its top (bottom) 16 recon rows
+//     into the up (down) neighbour's plane of the frame (PHalo: system-scope write-through
+//     stores over xGMI) and, once every storing wave has drained, sets that neighbour's flag
+//     dn_flags[gf * tiles_x + tx] (up_flags[...]) to `epoch` (system scope);
+//   * a tile in the first (last) tile row additionally waits for my_up (my_dn) flags
+//     [(gf - 1) * tiles_x + tx - 1 .. tx + 1] == epoch: the rows its window reads from the
+//     neighbour's stripe.  Epochs (one per GOP) mean the flag arrays are never reset, so a fast
+//     neighbour can never have its flag erased by a slow rank's reset.
+// peer planes of global frame gf: peer_*0 + gf * stride.  All-null peers / flags: one GPU.
+struct PRunStripe {
+    int by0, by1;
+    uint8_t* peer_up0;
+    uint8_t* peer_dn0;
+    long long stride;
+    const uint32_t* my_up_flags;
+    const uint32_t* my_dn_flags;
+    uint32_t* peer_up_flags;   // the up neighbour's my_dn_flags, mapped here
+    uint32_t* peer_dn_flags;   // the down neighbour's my_up_flags
+    uint32_t epoch;
+    int gbase;                 // global frame index of the launch's first frame
+};
+
+template <int NW, bool STRIPE>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE)))
 p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, int H, int W,
-             int qp_rd, const int32_t* __restrict__ qp_row, uint32_t* __restrict__ ws) {
+             int qp_rd, const int32_t* __restrict__ qp_row, uint32_t* __restrict__ ws, int ws_stamp_base,
+             const PRunStripe sp) {
     using G = Sea2GeoT<NW>;
     __shared__ PTileLds<G> S;
     __shared__ int s_task;
     const int tid = threadIdx.x;
-    const int nbx = W / 16, nby = H / 16;
-    const int tiles_x = (nbx + G::TBX - 1) / G::TBX, ntr = (nby + G::TBY - 1) / G::TBY;
+    const int nbx = W / 16;
+    const int by0 = STRIPE ? sp.by0 : 0, by1 = STRIPE ? sp.by1 : H / 16;
+    const int tiles_x = (nbx + G::TBX - 1) / G::TBX, ntr = (by1 - by0 + G::TBY - 1) / G::TBY;
     const int ntiles = tiles_x * ntr, ntasks = ntiles * nframes;
     uint32_t* const done = ws + kRunDoneBase;
     // Every queue / flag access is made by ALL lanes of wave 0 under a wave-uniform branch
@@ -1346,17 +1406,31 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
         __syncthreads();
         const int task = __builtin_amdgcn_readfirstlane(s_task);
         if (task >= ntasks) break;   // uniform: every wave leaves
+#ifdef SO_STAMPS
+        unsigned long long* const rec = g_run_stamps ? g_run_stamps + (size_t)(ws_stamp_base + task) * 16 : nullptr;
+        SO_STAMP_REC_SET(rec);
+        if (tid == 0 && rec) rec[8] = __builtin_amdgcn_s_memrealtime();
+#endif
         const int f = task / ntiles, tile = task - f * ntiles, ty = tile / tiles_x, tx = tile - ty * tiles_x;
+        const bool first_row = ty == 0, last_row = ty == ntr - 1;
         // the 3x3 tiles of frame f-1 around this one (the window's +-16 px), one flag per lane,
         // all polled in one round trip by wave 0 once the current tile is staged (ptile_body's
-        // `pre`; the barrier after it releases the other waves).  Every task they stand for was
-        // dequeued before this one by a running workgroup, so the wait always ends; it is
-        // bounded all the same (50 ms of s_memrealtime): a timeout flags the launch
-        // (Engine.run_timed_out, checked by the tests) and the tile proceeds.
+        // `pre`; the barrier after it releases the other waves).  Stripe: lanes 9-11 (12-14)
+        // poll the up (down) neighbour's hand-off flags of the frame before.  Every task they
+        // stand for was dequeued before this one by a running workgroup (here or on the
+        // neighbour), so the wait always ends; it is bounded all the same (50 ms of
+        // s_memrealtime): a timeout flags the run (Engine.check_run raises) and the tile proceeds.
         const auto wait_ref = [&]() {
-            if (f == 0 || wave != 0) return;
+            if (wave != 0) return;
+            const int gprev = (STRIPE ? sp.gbase : 0) + f - 1;   // global index of the reference frame
+            const bool remote = STRIPE && (first_row ? sp.my_up_flags != nullptr : false);
+            const bool remote_dn = STRIPE && (last_row ? sp.my_dn_flags != nullptr : false);
+            if (f == 0 && !remote && !remote_dn) return;
+#ifdef SO_STAMPS
+            if (lane == 0 && rec) rec[9] = __builtin_amdgcn_s_memrealtime();
+#endif
             const int nx = tx + lane % 3 - 1, ny = ty + lane / 3 - 1;
-            const bool need = lane < 9 && nx >= 0 && nx < tiles_x && ny >= 0 && ny < ntr;
+            const bool need = f > 0 && lane < 9 && nx >= 0 && nx < tiles_x && ny >= 0 && ny < ntr;
             // the timeout count, read once per tile: after one timeout the later tiles of the
             // run skip their waits (the run is already flagged wrong), so a lost flag cannot
             // stall the launch for 50 ms per remaining tile.  (Polling it in the loop put
@@ -1364,30 +1438,87 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 #if SO_RUN_ABORT_CHECK
             if (__hip_atomic_load(ws + kRunTimeoutWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
 #endif
-            const uint32_t* c = done + (size_t)(f - 1) * ntiles + (need ? ny * tiles_x + nx : 0);
+            const uint32_t* c = done + (size_t)(f > 0 ? f - 1 : 0) * ntiles + (need ? ny * tiles_x + nx : 0);
+            bool rneed = false;
+            if constexpr (STRIPE) {
+                const int rx = tx + (lane - 9) % 3 - 1;
+                if (lane >= 9 && lane < 12 && remote && rx >= 0 && rx < tiles_x) {
+                    c = sp.my_up_flags + (size_t)gprev * tiles_x + rx;
+                    rneed = true;
+                } else if (lane >= 12 && lane < 15 && remote_dn && rx >= 0 && rx < tiles_x) {
+                    c = sp.my_dn_flags + (size_t)gprev * tiles_x + rx;
+                    rneed = true;
+                }
+            }
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
             for (;;) {
-                const uint32_t v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (__builtin_amdgcn_ballot_w64(need && v == 0u) == 0) break;
+                uint32_t v;
+                if (STRIPE && rneed)
+                    v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == sp.epoch ? 1u : 0u;
+                else
+                    v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (__builtin_amdgcn_ballot_w64((need || rneed) && v == 0u) == 0) break;
                 __builtin_amdgcn_s_sleep(1);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
                     __hip_atomic_fetch_add(&ws[kRunTimeoutWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
             }
+#ifdef SO_STAMPS
+            if (lane == 0 && rec) rec[10] = __builtin_amdgcn_s_memrealtime();
+#endif
 #if SO_RUN_ACQUIRE
             // consumer side of the hand-off (MI355X_MICROARCH.md, "Valid forms"): one relaxed
             // poll, ONE agent-scope acquire (invalidates this CU's L1), its completion awaited
-            // before the barrier that releases the other waves to the window loads
+            // before the barrier that releases the other waves to the window loads.  (A
+            // stripe's planes are uncached: the neighbour's rows come from memory either way.)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
         };
-        ptile_body<G, true>(S, tile, a.cur[f], f ? a.out[f - 1].recon : ref0, H, W, 0, nby, qp_rd, qp_row, nullptr,
-                            nullptr, a.out[f], wait_ref);
-        // ptile_body ended with every wave's write-through stores retired and a barrier
-        if (wave == 0)
-            __hip_atomic_fetch_add(done + (size_t)f * ntiles + tile, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint8_t* ref = f ? a.out[f - 1].recon : ref0;
+        if constexpr (STRIPE) {
+            const int gf = sp.gbase + f;
+            PHalo hl{};
+            if (first_row && sp.peer_up0) {
+                hl.up = sp.peer_up0 + (long long)gf * sp.stride;
+                hl.up_end = by0 * 16 + 16;
+            }
+            if (last_row && sp.peer_dn0) {
+                hl.dn = sp.peer_dn0 + (long long)gf * sp.stride;
+                hl.dn_begin = by1 * 16 - 16;
+            }
+            ptile_body<G, true, decltype(wait_ref), true>(S, tile, a.cur[f], ref, H, W, by0, by1, qp_rd, qp_row,
+                                                          nullptr, nullptr, a.out[f], wait_ref, hl);
+            // ptile_body ended with every wave's stores (local and remote) retired and a barrier
+            if (wave == 0) {
+                __hip_atomic_fetch_add(done + (size_t)f * ntiles + tile, one, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0 && hl.up)
+                    __hip_atomic_store(sp.peer_up_flags + (size_t)gf * tiles_x + tx, sp.epoch, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                if (lane == 1 && hl.dn)
+                    __hip_atomic_store(sp.peer_dn_flags + (size_t)gf * tiles_x + tx, sp.epoch, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        } else {
+            ptile_body<G, true>(S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd, qp_row, nullptr, nullptr, a.out[f],
+                                wait_ref);
+            // ptile_body ended with every wave's write-through stores retired and a barrier
+            if (wave == 0)
+                __hip_atomic_fetch_add(done + (size_t)f * ntiles + tile, one, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        }
+#ifdef SO_STAMPS
+        if (tid == 0 && rec) {
+            uint32_t hw, xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            rec[11] = __builtin_amdgcn_s_memrealtime();
+            rec[12] = ((unsigned long long)xcc << 32) | hw;
+            rec[13] = __builtin_amdgcn_s_memtime();
+        }
+#endif
     }
 }
 
@@ -1396,20 +1527,25 @@ size_t p_run_workspace_words(int H, int W) {
     return (size_t)kRunDoneBase + (size_t)kRunMax * ntiles;
 }
 
-int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
-                 const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, hipStream_t st) {
+// Launch the run in <= kRunMax-frame launches.  max_wg > 0 caps the resident grid (several
+// ranks sharing one GPU in the tests).
+template <bool STRIPE>
+static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
+                          const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp0,
+                          int max_wg, hipStream_t st) {
     static int ncu = 0, per_cu = 0;
     if (ncu == 0) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
             ncu = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p_run_kernel<SO_PTILE_NW>, SO_PTILE_NW * 64, 0) !=
-                hipSuccess || per_cu <= 0)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p_run_kernel<SO_PTILE_NW, STRIPE>, SO_PTILE_NW * 64,
+                                                         0) != hipSuccess || per_cu <= 0)
             per_cu = 1;
     }
-    const int nbx = W / 16, nby = H / 16;
-    const long ntiles = (long)((nbx + Sea2Geo::TBX - 1) / Sea2Geo::TBX) * ((nby + Sea2Geo::TBY - 1) / Sea2Geo::TBY);
+    const int nbx = W / 16;
+    const int rows = STRIPE ? sp0.by1 - sp0.by0 : H / 16;
+    const long ntiles = (long)((nbx + Sea2Geo::TBX - 1) / Sea2Geo::TBX) * ((rows + Sea2Geo::TBY - 1) / Sea2Geo::TBY);
     for (int f0 = 0; f0 < nframes; f0 += kRunMax) {
         const int n = nframes - f0 < kRunMax ? nframes - f0 : kRunMax;
         PRunArgs a{};
@@ -1437,12 +1573,62 @@ int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, i
         }
         long grid = (long)ncu * pcu;
         if (grid > ntiles * n) grid = ntiles * n;
-        hipLaunchKernelGGL(p_run_kernel<SO_PTILE_NW>, dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), 0, st, a, n,
-                           f0 ? outs[f0 - 1].recon : ref0, H, W, qp_rd, qp_row, ws);
+        if (max_wg > 0 && grid > max_wg) grid = max_wg;
+        PRunStripe sp = sp0;
+        sp.gbase = sp0.gbase + f0;
+        hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, STRIPE>), dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), 0, st, a, n,
+                           f0 ? outs[f0 - 1].recon : ref0, H, W, qp_rd, qp_row, ws, (int)(f0 * ntiles), sp);
         const int rc = check_launch("p_run_kernel");
         if (rc != SO_OK) return rc;
     }
     return SO_OK;
+}
+
+int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
+                 const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, hipStream_t st) {
+    PRunStripe sp{};
+    sp.by0 = 0;
+    sp.by1 = H / 16;
+    return p_run_launch_t<false>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, 0, st);
+}
+
+int p_run_stripe_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
+                        const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg,
+                        hipStream_t st) {
+    return p_run_launch_t<true>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st);
+}
+
+// The I-frame's hand-off (the P-frame run's frame 0 reads its boundary rows): copy the
+// stripe's top 16 rows into the up neighbour's plane and its bottom 16 rows into the down
+// neighbour's, then set their flags [gf * tiles_x + tx] = epoch.  One workgroup per (tile
+// column, direction): 16 rows x 128 bytes, one dwordx4 per thread, system-scope write-through.
+__global__ void __launch_bounds__(128) stripe_halo_push_kernel(const uint8_t* __restrict__ plane, int W, int y0, int y1,
+                                                               uint8_t* up, uint8_t* dn, uint32_t* up_flags,
+                                                               uint32_t* dn_flags, int gf, int tiles_x,
+                                                               uint32_t epoch) {
+    const int tx = blockIdx.x % tiles_x, dir = blockIdx.x / tiles_x;   // 0 up, 1 down
+    uint8_t* dst = dir == 0 ? up : dn;
+    if (dst == nullptr) return;   // uniform
+    const int r = threadIdx.x >> 3, c = (threadIdx.x & 7) * 16;       // 16 rows x 8 dwordx4
+    const int y = (dir == 0 ? y0 : y1 - 16) + r, x = tx * 128 + c;
+    if (x < W && y >= y0 && y < y1) {
+        const so_v4u v = *reinterpret_cast<const so_v4u*>(plane + (size_t)y * W + x);
+        uint8_t* q = dst + (size_t)y * W + x;
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(q), "v"(v) : "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store((dir == 0 ? up_flags : dn_flags) + (size_t)gf * tiles_x + tx, epoch, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+int stripe_halo_push_launch(const uint8_t* plane, int W, int by0, int by1, uint8_t* up, uint8_t* dn,
+                            uint32_t* up_flags, uint32_t* dn_flags, int gf, uint32_t epoch, hipStream_t st) {
+    const int tiles_x = (W / 16 + Sea2Geo::TBX - 1) / Sea2Geo::TBX;
+    hipLaunchKernelGGL(stripe_halo_push_kernel, dim3(2 * tiles_x), dim3(128), 0, st, plane, W, by0 * 16, by1 * 16, up,
+                       dn, up_flags, dn_flags, gf, tiles_x, epoch);
+    return check_launch("stripe_halo_push_kernel");
 }
 
 // ---------------------------------------------------------------------------------------

@@ -1,0 +1,292 @@
+"""ONE GOP across the GPUs of a node with the hand-off inside the persistent launch
+(BASELINE configs[3]).
+
+Encoder.encode() (reference Encoder.py:1790-1898) is sequential over frames: P(i) searches
+the reconstruction of frame i-1 (:1864-1867).  Its blocks are independent given that
+reference, and a block's +-16 px search window reaches only the neighbouring block rows, so:
+
+  * rank r of N owns the block rows [by0, by1) of every frame (dist.stripe_rows);
+  * one persistent launch per <= 32 P-frames runs the rank's stripe of consecutive frames
+    (so_encode_p_run_stripe): a tile of frame f starts once the tiles of frame f-1 its
+    window reads are done -- its own rank's 3x3 neighbourhood, and for the stripe's first /
+    last tile row also the neighbour rank's three tiles across the boundary;
+  * those neighbour tiles store their 16 boundary rows straight into this rank's uncached
+    landing plane of the frame (peer memory over xGMI, mapped by IPC) and raise a flag there,
+    so frames pipeline across the ranks exactly as they do across the workgroups of one GPU:
+    no host round trip and no collective per frame;
+  * the I-frame's stripe (intra mode 0 needs no halo) is followed by one small push of its
+    boundary rows (so_stripe_halo_push).
+
+The symbols are the rank-order concatenation of the stripes, bit-identical to one GPU.  The
+per-row RC schedule is content-independent (:1599-1609) but this path runs the plain GOP
+(configs[3]); RC / ROI / two-pass GOPs use dist.StripeGOPEncoder.
+
+`StripeRunRank` holds one rank's buffers and launches; `connect()` takes the neighbours'
+buffers as mapped in this process (IPC handles across processes, plain pointers when several
+ranks share one GPU in the tests).  `PipelinedStripeGOPEncoder` is the torch.distributed
+front end (handles exchanged with all_gather_object; SSE summed with one all_reduce).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .dist import stripe_rows
+from .engine import FrameSymbols
+
+HALO_TOP, HALO_BOT = 16, 32       # landing-plane rows above / below the stripe
+
+
+class StripeRunRank:
+    """Buffers and launches of one rank of a GOP split into block-row stripes."""
+
+    def __init__(self, engine, world: int, rank: int, max_frames: int, stream=None, max_wg: int = 0):
+        e = engine
+        if not e.pipelined_ok(1):
+            raise ValueError("the stripe run covers bs 16 / sr 16 / full search / no VBS, FME / W % 128 == 0")
+        self.eng, self.world, self.rank = e, world, rank
+        self.by0, self.by1, self.rps = stripe_rows(e.nby, world, rank)
+        if self.by1 <= self.by0:
+            raise ValueError(f"rank {rank} of {world} has no block rows ({e.nby} rows)")
+        self.max_frames = max_frames
+        self.stream = stream
+        self.max_wg = max_wg
+        self.tiles_x = e.w // 128
+        lib = self.lib = _lib.load()
+        w = e.w
+        self.ext_rows = self.rps * 16 + HALO_TOP + HALO_BOT
+        self.stride = -(-self.ext_rows * w // 256) * 256
+        self._planes = ctypes.c_void_p()
+        _lib.check(lib.so_alloc_uncached(max_frames * self.stride + 256, ctypes.byref(self._planes)), "so_alloc_uncached")
+        self._flags = ctypes.c_void_p()
+        self.flag_words = 2 * max_frames * self.tiles_x
+        _lib.check(lib.so_alloc_uncached(self.flag_words * 4, ctypes.byref(self._flags)), "so_alloc_uncached")
+        _lib.check(lib.so_memset_d8(self._flags, 0, self.flag_words * 4, self._st()), "so_memset_d8")
+        _lib.check(lib.so_memset_d8(self._planes, 0, max_frames * self.stride + 256, self._st()), "so_memset_d8")
+        self.epoch = 0
+        self.peer_up = self.peer_dn = None      # (virtual base of frame 0, flags array to set)
+        self._opened = []
+        self._ws = torch.zeros(lib.so_p_run_workspace_elems(e.h, e.w), dtype=torch.int32, device=e.device)
+
+    # ---- addressing -----------------------------------------------------------------------
+    def _st(self):
+        return self.stream.cuda_stream if self.stream is not None else _lib.stream_handle(self.eng.device)
+
+    @property
+    def planes(self) -> int:
+        return self._planes.value
+
+    @property
+    def flags(self) -> int:
+        return self._flags.value
+
+    def up_flags(self) -> int:       # set by the up neighbour (its bottom rows arrived)
+        return self.flags
+
+    def dn_flags(self) -> int:       # set by the down neighbour
+        return self.flags + self.max_frames * self.tiles_x * 4
+
+    def virt(self, gf: int, planes: int | None = None, by0: int | None = None) -> int:
+        """Virtual full-frame base of frame gf's landing plane (row y at base + y * W)."""
+        planes = self.planes if planes is None else planes
+        by0 = self.by0 if by0 is None else by0
+        return planes + gf * self.stride - (by0 * 16 - HALO_TOP) * self.eng.w
+
+    def info(self) -> dict:
+        """What a neighbour needs to reach this rank (pointers valid in THIS process)."""
+        return {"planes": self.planes, "flags": self.flags, "by0": self.by0, "rank": self.rank}
+
+    def export(self) -> dict:
+        """IPC handles of this rank's planes and flags (for another process)."""
+        hp = (ctypes.c_uint8 * 64)()
+        hf = (ctypes.c_uint8 * 64)()
+        _lib.check(self.lib.so_ipc_export(self._planes, hp), "so_ipc_export")
+        _lib.check(self.lib.so_ipc_export(self._flags, hf), "so_ipc_export")
+        return {"planes_h": bytes(hp), "flags_h": bytes(hf), "by0": self.by0, "rank": self.rank}
+
+    def open(self, exported: dict) -> dict:
+        """Map a neighbour's exported buffers into this process."""
+        out = {"by0": exported["by0"], "rank": exported["rank"]}
+        for k in ("planes", "flags"):
+            p = ctypes.c_void_p()
+            h = (ctypes.c_uint8 * 64).from_buffer_copy(exported[k + "_h"])
+            _lib.check(self.lib.so_ipc_open(h, ctypes.byref(p)), "so_ipc_open")
+            self._opened.append(p)
+            out[k] = p.value
+        return out
+
+    def connect(self, up: dict | None, dn: dict | None) -> None:
+        """up / dn: the neighbours' info() as mapped in this process (None at the frame edge)."""
+        mf, tx = self.max_frames, self.tiles_x
+        if up is not None:
+            # my top rows land in the up neighbour's plane below ITS stripe; its dn flags
+            self.peer_up = (self.virt(0, up["planes"], up["by0"]), up["flags"] + mf * tx * 4)
+        if dn is not None:
+            self.peer_dn = (self.virt(0, dn["planes"], dn["by0"]), dn["flags"])
+
+    def close(self) -> None:
+        for p in self._opened:
+            self.lib.so_ipc_close(p)
+        self._opened = []
+        for p in (self._planes, self._flags):
+            if p.value:
+                self.lib.so_free_device(p)
+        self._planes = ctypes.c_void_p()
+        self._flags = ctypes.c_void_p()
+
+    # ---- one GOP ---------------------------------------------------------------------------
+    def new_symbols(self, frame_type: int) -> FrameSymbols:
+        e, bs = self.eng, self.eng.bs
+        d = e.device
+        nbs = e.nbx * (self.by1 - self.by0)
+        mv_shape = (nbs, 4, 3) if frame_type == 1 else (nbs, 4)
+        return FrameSymbols(frame_type=frame_type,
+                            split=torch.empty(nbs, dtype=torch.uint8, device=d),
+                            mv=torch.empty(mv_shape, dtype=torch.int16, device=d),
+                            qtc=torch.empty((nbs, bs * bs), dtype=torch.int16, device=d),
+                            tokens=torch.empty(nbs, dtype=torch.int32, device=d),
+                            mae_num=torch.empty(nbs, dtype=torch.int32, device=d),
+                            recon=None,
+                            sse=torch.zeros(max(nbs, (self.by1 - self.by0) * bs), dtype=torch.int32, device=d),
+                            extra={"by0": self.by0, "by1": self.by1})
+
+    def encode(self, frames: torch.Tensor, intra_dur: int, qp: int, out=None) -> list:
+        """The stripe's symbols of every frame (stripe-local; recon stays in the landing
+        planes: stripe_recon(gf)).  Asynchronous on the rank's stream; no host sync."""
+        e, lib = self.eng, self.lib
+        nf = frames.shape[0]
+        if nf > self.max_frames:
+            raise ValueError(f"{nf} frames > max_frames {self.max_frames}")
+        self.epoch += 1
+        ep = self.epoch
+        st = self._st()
+        syms = out if out is not None else [self.new_symbols(0 if i % intra_dur == 0 else 1) for i in range(nf)]
+        up_v, up_f = self.peer_up if self.peer_up else (None, None)
+        dn_v, dn_f = self.peer_dn if self.peer_dn else (None, None)
+        my_up = self.up_flags() if self.peer_up else None
+        my_dn = self.dn_flags() if self.peer_dn else None
+        i = 0
+        while i < nf:
+            if i % intra_dur == 0:
+                s = syms[i]
+                _lib.check(lib.so_encode_i_rows_ex(
+                    frames[i].data_ptr(), e.h, e.w, e.bs, e.sr, self.by0, self.by1, int(qp), None, None, 0, 0.0,
+                    s.split.data_ptr(), s.mv.data_ptr(), s.qtc.data_ptr(), s.tokens.data_ptr(), s.mae_num.data_ptr(),
+                    self.virt(i), s.sse.data_ptr(), e.scratch.data_ptr(), st), "so_encode_i_rows_ex")
+                s.frame_type, s.qp_rd = 0, int(qp)
+                _lib.check(lib.so_stripe_halo_push(
+                    self.virt(i), e.h, e.w, self.by0, self.by1, i,
+                    None if up_v is None else up_v + i * self.stride, None if dn_v is None else dn_v + i * self.stride,
+                    up_f, dn_f, ep, st), "so_stripe_halo_push")
+                i += 1
+                continue
+            j = i
+            while j < nf and j % intra_dur != 0:
+                j += 1
+            n = j - i
+            arr = lambda xs: (ctypes.c_void_p * n)(*xs)  # noqa: E731
+            ss = syms[i:j]
+            _lib.check(lib.so_encode_p_run_stripe(
+                arr([frames[k].data_ptr() for k in range(i, j)]), n, self.virt(i - 1), e.h, e.w, e.bs, e.sr,
+                self.by0, self.by1, int(qp), None,
+                arr([s.split.data_ptr() for s in ss]), arr([s.mv.data_ptr() for s in ss]),
+                arr([s.qtc.data_ptr() for s in ss]), arr([s.tokens.data_ptr() for s in ss]),
+                arr([s.mae_num.data_ptr() for s in ss]), arr([self.virt(k) for k in range(i, j)]),
+                arr([s.sse.data_ptr() for s in ss]), self._ws.data_ptr(), i,
+                up_v, dn_v, self.stride, my_up, my_dn, up_f, dn_f, ep, int(self.max_wg), st), "so_encode_p_run_stripe")
+            for s in ss:
+                s.frame_type, s.qp_rd = 1, int(qp)
+            i = j
+        return syms
+
+    def stripe_recon(self, gf: int) -> torch.Tensor:
+        """The stripe's rows of frame gf's reconstruction, copied into a tensor."""
+        e = self.eng
+        rows = (self.by1 - self.by0) * 16
+        out = torch.empty((rows, e.w), dtype=torch.uint8, device=e.device)
+        src = self.virt(gf) + self.by0 * 16 * e.w
+        # on the caller's stream (which `out` belongs to), after everything on the rank's
+        cur = torch.cuda.current_stream(e.device)
+        if self.stream is not None:
+            cur.wait_stream(self.stream)
+        _lib.check(self.lib.so_copy_d2d(out.data_ptr(), src, rows * e.w, cur.cuda_stream), "so_copy_d2d")
+        return out
+
+    def timed_out(self) -> bool:
+        return int(self._ws[32].item()) != 0
+
+    def check(self) -> None:
+        n = int(self._ws[32].item())
+        if n:
+            self._ws[32].zero_()
+            raise RuntimeError(f"p_run stripe: {n} dependency wait(s) timed out (lost hand-off); symbols unreliable")
+
+
+class PipelinedStripeGOPEncoder:
+    """torch.distributed front end of StripeRunRank: one rank per GPU, neighbours' buffers
+    mapped by IPC (handles exchanged with all_gather_object over the process group)."""
+
+    def __init__(self, engine, max_frames: int, group=None, max_wg: int = 0):
+        import torch.distributed as dist
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.eng = engine
+        self.r = StripeRunRank(engine, self.world, self.rank, max_frames, max_wg=max_wg)
+        torch.cuda.synchronize(engine.device)
+        if self.world > 1:
+            mine = self.r.export()
+            alls = [None] * self.world
+            dist.all_gather_object(alls, mine, group=group)
+            # ranks past the last block row own nothing (never happens for world <= nby)
+            up = self.r.open(alls[self.rank - 1]) if self.rank > 0 else None
+            dn = self.r.open(alls[self.rank + 1]) if self.rank < self.world - 1 else None
+            self.r.connect(up, dn)
+            dist.barrier(group=group)
+        self.by0, self.by1, self.rps = self.r.by0, self.r.by1, self.r.rps
+
+    def encode(self, frames, intra_dur: int, qp: int, symbols=None) -> dict:
+        syms = self.r.encode(frames, intra_dur, qp, out=symbols)
+        sse = torch.stack([s.sse for s in syms]).sum(dim=1, dtype=torch.int64)
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(sse, group=self.group)
+        return {"symbols": syms, "frame_type": [s.frame_type for s in syms], "sse": sse}
+
+    def check(self) -> None:
+        self.r.check()
+
+    def gather_symbols(self, sym, gf: int) -> dict:
+        """Whole-frame symbols of frame gf (rank-order concatenation) on every rank."""
+        import torch.distributed as dist
+        e = self.eng
+        nbx, rows = e.nbx, self.rps * 16
+        out = {}
+        for name in ("split", "mv", "qtc", "tokens", "mae_num"):
+            t = getattr(sym, name)
+            rec = tuple(t.shape[1:])
+            pad = torch.zeros((self.rps * nbx,) + rec, dtype=t.dtype, device=t.device)
+            pad[: t.shape[0]].copy_(t)
+            full = torch.empty((self.world * self.rps * nbx,) + rec, dtype=t.dtype, device=t.device)
+            if self.world > 1:
+                dist.all_gather_into_tensor(full.view(-1).view(torch.uint8), pad.view(-1).view(torch.uint8),
+                                            group=self.group)
+            else:
+                full.copy_(pad)
+            out[name] = full[: e.nby * nbx]
+        rec = torch.zeros((rows, e.w), dtype=torch.uint8, device=e.device)
+        mine = self.r.stripe_recon(gf)
+        rec[: mine.shape[0]].copy_(mine)
+        full = torch.empty((self.world * rows, e.w), dtype=torch.uint8, device=e.device)
+        if self.world > 1:
+            dist.all_gather_into_tensor(full.view(-1), rec.view(-1), group=self.group)
+        else:
+            full.copy_(rec)
+        out["recon"] = full[: e.h]
+        out["frame_type"] = sym.frame_type
+        return out
+
+    def close(self) -> None:
+        self.r.close()

@@ -1,0 +1,140 @@
+"""ONE GOP split into block-row stripes with the hand-off inside the persistent launch
+(streamoptima_amd/pipeline.py, so_encode_p_run_stripe): the concatenated stripes must be
+bit-identical to the one-GPU GOP, i.e. to the C oracle's digests of the benchmarked
+workloads (tests/golden/large_gops.json).
+
+On a one-GPU box the ranks share the GPU: in one process on separate streams (peers'
+buffers as plain pointers), and as two processes whose buffers are mapped by IPC
+(hipIpcGetMemHandle / hipIpcOpenMemHandle, the path the ranks of an 8-GPU node take over
+xGMI).  Each rank's persistent grid is capped (half the machine for all of them) so that all
+ranks are resident together and the I-frame kernels of a slower rank still find CUs, and
+at most 3 ranks share the GPU in one process: a process has 4 hardware queues
+(GPU_MAX_HW_QUEUES), and two ranks' streams on one queue would serialise the ranks' persistent
+kernels (each waiting on the other's hand-off until the 50 ms timeout flags the run)."""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+FIX = json.load(open(os.path.join(GOLDEN, "large_gops.json")))
+
+
+def _frames(name, dev, nframes=None):
+    from streamoptima_amd.engine import alloc_planes
+    from streamoptima_amd.synth import synth_sequence_torch
+    from streamoptima_amd.workloads import WORKLOADS, padded
+    cfg = dict(WORKLOADS[name])
+    if nframes:
+        cfg["frames"] = nframes
+    h, w, f = cfg["h"], cfg["w"], cfg["frames"]
+    fr = alloc_planes(f, padded(h), padded(w), dev, fill=128)
+    fr[:, :h, :w].copy_(synth_sequence_torch(f, h, w, seed=cfg["seed"], device=dev))
+    return cfg, fr
+
+
+def _digest_concat(ranks, syms_per_rank, nframes):
+    from streamoptima_amd.digest import frame_digest
+    out = []
+    for i in range(nframes):
+        parts = [s[i] for s in syms_per_rank]
+        arr = {k: np.concatenate([getattr(p, k).cpu().numpy() for p in parts]) for k in
+               ("split", "mv", "qtc", "tokens", "mae_num")}
+        arr["recon"] = np.concatenate([r.stripe_recon(i).cpu().numpy() for r in ranks])
+        out.append(frame_digest(parts[0].frame_type, arr))
+    return out
+
+
+_STREAMS = []
+
+
+def _streams(dev):
+    """Three streams created once per process: each test's ranks then sit on distinct hardware
+    queues (new streams per test would cycle through the 4 queues and could put two ranks of
+    one test on one queue)."""
+    while len(_STREAMS) < 3:
+        _STREAMS.append(torch.cuda.Stream(dev))
+    return _STREAMS
+
+
+@pytest.mark.parametrize("name,world,nframes", [("1080p", 2, 30), ("4k", 3, 12), ("4k", 2, 30)])
+def test_stripe_run_in_process_matches_one_gpu(gpu, name, world, nframes):
+    from streamoptima_amd.engine import Engine
+    from streamoptima_amd.pipeline import StripeRunRank
+    cfg, fr = _frames(name, gpu, nframes)
+    h, w = fr.shape[1:]
+    engines = [Engine(h, w, 16, 16, False, 0.015, gpu) for _ in range(world)]
+    streams = _streams(gpu)[:world]
+    cap = 768 // (2 * world)     # half the machine for the persistent grids: the other ranks'
+    ranks = [StripeRunRank(engines[r], world, r, nframes, stream=streams[r], max_wg=cap) for r in range(world)]
+    torch.cuda.synchronize()
+    for r in range(world):
+        ranks[r].connect(ranks[r - 1].info() if r > 0 else None, ranks[r + 1].info() if r < world - 1 else None)
+    for rep in range(2):     # twice: the second GOP runs on epoch 2 over the first GOP's planes and flags
+        syms = []
+        for r in range(world):
+            with torch.cuda.stream(streams[r]):
+                syms.append(ranks[r].encode(fr, cfg["intra_dur"], cfg["qp"]))
+        torch.cuda.synchronize()
+        for r in ranks:
+            r.check()
+        got = _digest_concat(ranks, syms, nframes)
+        exp = FIX[name]["frame_sha256"][:nframes]
+        bad = [i for i, (a, b) in enumerate(zip(got, exp)) if a != b]
+        assert not bad, f"rep {rep}: frames {bad[:10]} differ from the one-GPU GOP"
+    for r in ranks:
+        r.close()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _ipc_worker(rank, world, port, name, nframes, outdir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from streamoptima_amd.engine import Engine
+        from streamoptima_amd.pipeline import PipelinedStripeGOPEncoder
+        dev = torch.device("cuda:0")
+        cfg, fr = _frames(name, dev, nframes)
+        eng = Engine(fr.shape[1], fr.shape[2], 16, 16, False, 0.015, dev)
+        enc = PipelinedStripeGOPEncoder(eng, nframes, max_wg=768 // (2 * world))
+        res = enc.encode(fr, cfg["intra_dur"], cfg["qp"])
+        torch.cuda.synchronize()
+        enc.check()
+        from streamoptima_amd.digest import frame_digest
+        digs = []
+        for i, s in enumerate(res["symbols"]):
+            g = enc.gather_symbols(s, i)
+            digs.append(frame_digest(g["frame_type"], {k: (v.cpu().numpy() if torch.is_tensor(v) else v)
+                                                        for k, v in g.items()}))
+        if rank == 0:
+            with open(os.path.join(outdir, "digests.json"), "w") as fh:
+                json.dump({"digests": digs, "sse": res["sse"].cpu().tolist()}, fh)
+        dist.barrier()
+        enc.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_stripe_run_two_processes_ipc(gpu, tmp_path):
+    """Two ranks as two processes (one GPU, buffers mapped by IPC), 1080p GOP head."""
+    import torch.multiprocessing as mp
+    n = 10
+    mp.start_processes(_ipc_worker, args=(2, _free_port(), "1080p", n, str(tmp_path)), nprocs=2,
+                       start_method="spawn")
+    got = json.load(open(tmp_path / "digests.json"))
+    assert got["digests"] == FIX["1080p"]["frame_sha256"][:n]
+    hp, w = 1088, 1920
+    psnr = [10 * np.log10(255 ** 2 / (s / (hp * w))) for s in got["sse"]]
+    np.testing.assert_allclose(psnr, FIX["1080p"]["psnr"][:n], rtol=0, atol=1e-9)
