@@ -256,9 +256,13 @@ def pmc_record(config: str):
     if not os.path.exists(p):
         return {}
     try:
-        return json.load(open(p)).get(config, {}).get("kernels", {}).get("so::p_run_kernel<8>", {})
+        ks = json.load(open(p)).get(config, {}).get("kernels", {})
     except (ValueError, OSError):
         return {}
+    for k, v in ks.items():
+        if k.startswith("so::p_run_kernel<8"):      # p_run_kernel<8, false> (one GPU, full frame)
+            return v
+    return {}
 
 
 def roofline_of(rl: dict, config: str) -> dict:
@@ -270,16 +274,22 @@ def roofline_of(rl: dict, config: str) -> dict:
     traffic = round(pm["hbm_bytes"]) if pm.get("hbm_bytes") else None
     valu = None
     if pm.get("sq_active_inst_valu") and pm.get("grbm_gui_active"):
-        # SQ_ACTIVE_INST_VALU counts quad-cycles summed over waves; GRBM_GUI_ACTIVE is summed
-        # over the 8 XCDs (MI355X_MICROARCH.md): busy = 4 * active / (cycles per XCD * SIMDs)
+        # SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES count quad-cycles summed over waves and
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md): the VALU busy
+        # fraction = 4 * active / (kernel cycles per XCD * 1024 SIMDs)
         cyc = pm["grbm_gui_active"] / 8
         valu = {"valu_busy_frac": round(4 * pm["sq_active_inst_valu"] / (cyc * N_SIMD), 4),
                 "sq_insts_valu": round(pm.get("sq_insts_valu", 0)),
-                "kernel_cycles": round(cyc), "effective_clock_ghz": round(cyc / (pm.get("pmc_launch_s") or launch_s) / 1e9, 3)
-                if pm.get("pmc_launch_s") else None,
-                "source": "profiles/pmc_me_traffic.json (rocprofv3 --pmc SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE ...)"}
-    return {"bound": "hbm", "kernel": "p_run_kernel<8>", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
+                "cycles_per_valu_instr": round(4 * pm["sq_active_inst_valu"] / pm["sq_insts_valu"], 2)
+                if pm.get("sq_insts_valu") else None,
+                "waves_per_simd": round(4 * pm["sq_wave_cycles"] / (cyc * N_SIMD), 2) if pm.get("sq_wave_cycles") else None,
+                "kernel_cycles": round(cyc), "effective_clock_ghz": round(cyc / launch_s / 1e9, 3),
+                "source": "profiles/pmc_me_traffic.json (rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES "
+                          "GRBM_GUI_ACTIVE ..., tools/gpu_traffic.sh)"}
+    return {"bound": "hbm", "kernel": "p_run_kernel<8, false>", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "traffic_note": "HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE x 2, the "
+                            "factor measured for 4-B and 16-B coalesced reads (tools/ubench_fetch.cpp)",
             "algorithmic_bytes": round(alg), "launch_us": round(launch_s * 1e6, 2),
             "frames_per_launch": round(rl["run_frames"] / n_launch, 2),
             "per_frame_us": round(rl["run_s"] / rl["run_frames"] * 1e6, 2),

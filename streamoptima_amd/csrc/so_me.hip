@@ -1279,10 +1279,13 @@ SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur
         }
     }
     __syncthreads();
+    SO_SEA_STAMP(6, __builtin_amdgcn_s_memtime());
     if (tid < G::NBLK * 16)
         tq16_exact<G, SC1, HALO>(S, tid >> 4, tid & 15, S.un + (tid >> 4) * (16 * 17), bx0, byt0, nbx, by0, by1, W,
                                  qp_rd, qp_row, qp_map, o, hl);
+    SO_SEA_STAMP(7, __builtin_amdgcn_s_memtime());
     if constexpr (SC1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
+    SO_SEA_STAMP(14, __builtin_amdgcn_s_memtime());
     __syncthreads();
 }
 

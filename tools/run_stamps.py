@@ -56,6 +56,8 @@ def analyse(rec, nframes, tiles_x, ntr):
     out["cycles_p50"] = {
         "stage_cur_wait": float(np.median(cyc(1, 2))), "window": float(np.median(cyc(2, 3))),
         "b4": float(np.median(cyc(3, 4))), "search": float(np.median(cyc(4, 5))),
+        "decode": float(np.median(cyc(5, 6))), "tq_wave0": float(np.median(cyc(6, 7))),
+        "store_drain_wave0": float(np.median(cyc(7, 14))), "barrier_flag": float(np.median(cyc(14, 13))),
         "tq_store_flag": float(np.median(cyc(5, 13)))}
     return out
 
