@@ -346,6 +346,28 @@ int so_block_xform(const double* in, int n, int N, int inverse, int qp, int32_t*
 int so_sse_u8(const uint8_t* a, const uint8_t* b, int64_t n, uint64_t* out_sse,
               void* stream);
 
+/*
+ * Packed symbol stream: the content of the reference's two text lines per frame
+ * (differential_encoder_frame's MVs before differencing, Encoder.py:1419-1520, and
+ * entropy_encoder_block's RLE token lists, :1086-1131 / :1522-1542) as zigzag LEB128
+ * varints, per block in raster order:  split | mv values | token lists of its (sub-)blocks.
+ * Replaces downloading the dense int16 QTC (2 B/px) when symbols leave the GPU
+ * (transmit_bitstream, :1544-1580).  Format: so_pack.hip; host decoder: bitstream.unpack_frame.
+ *
+ * so_pack_bound: the worst-case bytes of a frame of nb blocks (a capacity that never
+ *   overflows).
+ * so_pack_frames: for frame i (frame_types: a HOST array, 0 = intra, 1 = inter; split / mv /
+ *   qtc: device arrays in the canonical symbol layout) writes offs[i][0..nb) = each block's byte offset, offs[i][nb] =
+ *   the frame's total, and the stream into out[i][0..total).  Blocks that would pass `cap`
+ *   bytes are not written: the caller checks offs[i][nb] <= cap before using out[i].
+ *   Stream-ordered, no host synchronisation.
+ */
+size_t so_pack_bound(int nb, int block_size);
+int so_pack_frames(int nframes, const int32_t* frame_types, const uint8_t* const* split,
+                   const int16_t* const* mv, const int16_t* const* qtc, int nb, int block_size,
+                   uint32_t* const* offs, uint8_t* const* out, unsigned long long cap,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

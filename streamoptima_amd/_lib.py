@@ -59,6 +59,8 @@ _SIGS = {
     "so_ipc_close": ([_vp], _i),
     "so_copy_d2d": ([_vp, _vp, _sz, _vp], _i),
     "so_memset_d8": ([_vp, _i, _sz, _vp], _i),
+    "so_pack_bound": ([_i, _i], _sz),
+    "so_pack_frames": ([_i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, ctypes.c_ulonglong, _vp], _i),
     "so_fme_plane_stride": ([_i, _i], _sz),
     "so_fme_workspace_bytes": ([_i, _i, _i], _sz),
     "so_fme_planes": ([_vp, _i, _i, _i, _vp, _vp], _i),

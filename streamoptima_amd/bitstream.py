@@ -8,6 +8,8 @@
   * differential_encoder_frame — Encoder.py:1419-1520 (MV / QP differential line,
                               including the reference's split-under-RC intra quirk).
   * entropy_encoder_frame   — Encoder.py:1522-1542.
+  * varints / unpack_frame  — host decoder of the packed symbol stream the GPU writes
+                              (so_pack_frames, include/streamoptima.h; format in so_pack.hip).
 """
 from __future__ import annotations
 
@@ -214,6 +216,65 @@ def entropy_decoder_frame(line: str, block_size) -> list:
         else:
             out.append((1, [np.array(entropy_decoder_block(sb, block_size // 2)) for sb in v]))
     return out
+
+
+# ---- packed symbol stream (so_pack_frames) -----------------------------------------------------
+def varints(buf) -> np.ndarray:
+    """Zigzag LEB128 varints -> int64 values (vectorised over the whole stream)."""
+    b = np.asarray(buf, dtype=np.uint8).reshape(-1)
+    if b.size == 0:
+        return np.zeros(0, dtype=np.int64)
+    ends = np.flatnonzero((b & 0x80) == 0)
+    if ends.size == 0 or ends[-1] != b.size - 1:
+        raise ValueError("packed stream ends inside a varint")
+    starts = np.concatenate(([0], ends[:-1] + 1))
+    lens = ends - starts + 1
+    z = np.zeros(ends.size, dtype=np.int64)
+    for k in range(int(lens.max())):
+        m = lens > k
+        z[m] |= (b[starts[m] + k].astype(np.int64) & 0x7F) << (7 * k)
+    return (z >> 1) ^ -(z & 1)
+
+
+def unpack_frame(buf, nb: int, bs: int, frame_type: int) -> dict:
+    """One frame's packed stream -> {"split", "mv", "qtc"} in the canonical symbol layout
+    (mv entries past the first of an unsplit block stay 0)."""
+    v = varints(buf).tolist()
+    inter = frame_type == 1
+    split = np.zeros(nb, dtype=np.uint8)
+    mv = np.zeros((nb, 4, 3) if inter else (nb, 4), dtype=np.int16)
+    qtc = np.zeros((nb, bs * bs), dtype=np.int16)
+    sb = bs // 2
+    p = 0
+    try:
+        for b in range(nb):
+            sp = v[p]
+            p += 1
+            split[b] = sp
+            for j in range(4 if sp else 1):
+                if inter:
+                    mv[b, j] = v[p:p + 3]
+                    p += 3
+                else:
+                    mv[b, j] = v[p]
+                    p += 1
+            for n, off in ([(sb, j * sb * sb) for j in range(4)] if sp else [(bs, 0)]):
+                order, k = scan_order(n), 0
+                while k < n * n:
+                    t = v[p]
+                    p += 1
+                    if t < 0:
+                        qtc[b, off + order[k:k - t]] = v[p:p - t]
+                        p, k = p - t, k - t
+                    elif t == 0:
+                        break
+                    else:
+                        k += t
+    except IndexError:
+        raise ValueError(f"packed stream ends inside block {b}") from None
+    if p != len(v):
+        raise ValueError(f"{len(v) - p} values after the last block")
+    return {"split": split, "mv": mv, "qtc": qtc}
 
 
 # ---- per-block QP map line (build extension: ROI / two-pass RC) --------------------------------

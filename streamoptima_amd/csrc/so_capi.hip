@@ -64,6 +64,16 @@ struct PRunStripe {
 int p_run_stripe_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                         const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg,
                         hipStream_t st);
+struct PackFrame {
+    const uint8_t* split;
+    const int16_t* mv;
+    const int16_t* qtc;
+    uint32_t* offs;
+    uint8_t* out;
+    int frame_type;
+};
+size_t pack_block_bound(int bs);
+int pack_frames_launch(const PackFrame* frames, int nframes, int nb, int bs, unsigned long long cap, hipStream_t st);
 int stripe_halo_push_launch(const uint8_t* plane, int W, int by0, int by1, uint8_t* up, uint8_t* dn,
                             uint32_t* up_flags, uint32_t* dn_flags, int gf, uint32_t epoch, hipStream_t st);
 
@@ -777,6 +787,38 @@ int so_sse_u8(const uint8_t* a, const uint8_t* b, int64_t n, uint64_t* out_sse, 
     hipLaunchKernelGGL(sse_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a, b, n,
                        reinterpret_cast<unsigned long long*>(out_sse));
     return check_launch("sse_kernel");
+}
+
+// ---- packed symbol stream (so_pack.hip) -----------------------------------------------------
+size_t so_pack_bound(int nb, int bs) {
+    if (nb <= 0 || (bs != 16 && bs != 8)) return 0;
+    return (size_t)nb * pack_block_bound(bs);
+}
+
+int so_pack_frames(int nframes, const int32_t* frame_types, const uint8_t* const* split, const int16_t* const* mv,
+                   const int16_t* const* qtc, int nb, int bs, uint32_t* const* offs, uint8_t* const* out,
+                   unsigned long long cap, void* stream) {
+    const char* fn = "so_pack_frames";
+    if (bs != 16 && bs != 8) {
+        set_error("%s: block_size %d not built", fn, bs);
+        return SO_E_UNSUPPORTED;
+    }
+    if (nb <= 0 || nframes < 0) {
+        set_error("%s: nb %d / nframes %d", fn, nb, nframes);
+        return SO_E_INVALID;
+    }
+    if (nframes == 0) return SO_OK;
+    SO_NEED(frame_types, fn); SO_NEED(split, fn); SO_NEED(mv, fn); SO_NEED(qtc, fn); SO_NEED(offs, fn); SO_NEED(out, fn);
+    std::vector<PackFrame> fr((size_t)nframes);
+    for (int i = 0; i < nframes; ++i) {
+        SO_NEED(split[i], fn); SO_NEED(mv[i], fn); SO_NEED(qtc[i], fn); SO_NEED(offs[i], fn); SO_NEED(out[i], fn);
+        if (frame_types[i] != 0 && frame_types[i] != 1) {
+            set_error("%s: frame_types[%d] = %d", fn, i, frame_types[i]);
+            return SO_E_INVALID;
+        }
+        fr[i] = PackFrame{split[i], mv[i], qtc[i], offs[i], out[i], frame_types[i]};
+    }
+    return pack_frames_launch(fr.data(), nframes, nb, bs, cap, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -687,7 +687,6 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
     uint32_t* const curt = L.curt;
     uint32_t* const a4 = L.a4;
     uint16_t* const list = L.list;
-    uint32_t* const lcount = L.lcount;
     unsigned long long* const keys = L.keys;
 
     const int nbx = W / 16;
@@ -1027,7 +1026,7 @@ __global__ void __launch_bounds__(Sea2Geo::NTHREADS) __attribute__((amdgpu_waves
 me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
                int32_t* __restrict__ out_best, int probe) {
     using G = Sea2Geo;
-    constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RP = G::RP, B4P = G::B4P, CP = G::TPX;
+    constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RP = G::RP, B4P = G::B4P;
     __shared__ uint32_t win[G::WR * RP + 4];
     __shared__ uint32_t b4w[(G::B4RS * B4P + 4) / 4];
     __shared__ uint32_t curt[G::TPY * G::CPD];
@@ -1256,7 +1255,7 @@ SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur
                        int by0, int by1, int qp_rd, const int32_t* __restrict__ qp_row,
                        const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best, const PFrameOut& o,
                        const Pre& pre = Pre(), const PHalo& hl = PHalo{}) {
-    constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, CP = G::TPX;
+    constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY;
     using P = PTileGeo<G>;
     uint32_t* const b4w = reinterpret_cast<uint32_t*>(S.un);
     uint16_t* const list = reinterpret_cast<uint16_t*>(b4w + P::B4);

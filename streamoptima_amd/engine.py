@@ -279,6 +279,36 @@ class Engine:
         _lib.check(rc, "so_intra_recon_ex")
         return out
 
+    # ---- packed symbol stream (so_pack_frames) --------------------------------------------
+    def pack_bound(self, nb: int | None = None) -> int:
+        return int(self.lib.so_pack_bound(int(self.nb if nb is None else nb), self.bs))
+
+    def pack_symbols(self, syms: list, offs: torch.Tensor | None = None, out: torch.Tensor | None = None):
+        """Each frame's symbols as one packed byte stream on the device (include/streamoptima.h
+        so_pack_frames); asynchronous.  Returns (offs int32 [n, nb + 1], out uint8 [n, cap]):
+        frame i's stream is out[i, :offs[i, nb]], block b starts at offs[i, b]
+        (bitstream.unpack_frame decodes it).  The default capacity never overflows."""
+        n = len(syms)
+        if n == 0:
+            raise ValueError("pack_symbols: no frames")
+        nb = syms[0].split.numel()
+        if any(s.split.numel() != nb for s in syms):
+            raise ValueError("pack_symbols: frames with different block counts")
+        cap = self.pack_bound(nb) if out is None else out.shape[1]
+        offs = torch.empty((n, nb + 1), dtype=torch.int32, device=self.device) if offs is None else offs
+        out = torch.empty((n, cap), dtype=torch.uint8, device=self.device) if out is None else out
+        if offs.shape != (n, nb + 1) or offs.dtype != torch.int32 or out.shape[0] != n or out.dtype != torch.uint8:
+            raise ValueError("pack_symbols: offs must be int32 [n, nb + 1] and out uint8 [n, cap]")
+
+        def arr(ts):
+            return (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
+        types = (ctypes.c_int32 * n)(*[int(s.frame_type) for s in syms])
+        rc = self.lib.so_pack_frames(n, types, arr([s.split for s in syms]), arr([s.mv for s in syms]),
+                                     arr([s.qtc for s in syms]), nb, self.bs, arr(list(offs)), arr(list(out)),
+                                     int(cap), _lib.stream_handle(self.device))
+        _lib.check(rc, "so_pack_frames")
+        return offs, out
+
     # ---- metrics ---------------------------------------------------------------------------
     def sse_into(self, a: torch.Tensor, b: torch.Tensor, acc: torch.Tensor) -> None:
         """acc (uint64 view of an int64 device scalar) += sum((a-b)^2)."""
