@@ -342,12 +342,20 @@ class Y_Video_codec(BlockAPI):
         self.inter0.append(time.time() - t0)
         return psnr_per_frame
 
-    def encode_device(self, frames_dev: torch.Tensor, intra_dur: int, symbols=None, check: bool = True):
+    def encode_device(self, frames_dev: torch.Tensor, intra_dur: int, symbols=None, check: bool = True,
+                      chunk: int | None = None, wait_input=None, on_output=None):
         """The GOP loop on device-resident frames [F, Hp, Wp].  Returns symbols per frame and
         a device SSE array.  check=True ends with one host read of the persistent runs'
         timeout count (Engine.check_run: raises if a dependency wait timed out); a caller
         that times back-to-back GOPs passes False and calls engine().check_run() after them.
-        Otherwise no host sync unless RCFlag > 1 needs residual_size."""
+        Otherwise no host sync unless RCFlag > 1 needs residual_size.
+
+        Streaming hooks (hoststream.HostStreamEncoder): a persistent P-run covers at most
+        `chunk` frames per launch; wait_input(k0, k1) is called before the work reading frames
+        [k0, k1) is enqueued (to make the stream wait for their upload) and on_output(k0, k1,
+        syms) after the work producing their symbols is enqueued.  Symbols are identical."""
+        wait_input = wait_input or (lambda k0, k1: None)
+        on_output = on_output or (lambda k0, k1, syms: None)
         eng = self.engine()
         nframes = frames_dev.shape[0]
         ref_frames = [alloc_planes(1, eng.h, eng.w, self.device, fill=128)[0]]
@@ -396,8 +404,9 @@ class Y_Video_codec(BlockAPI):
         while i < nframes:
             if pipelined and i % intra_dur != 0:
                 j = i
-                while j < nframes and j % intra_dur != 0:
+                while j < nframes and j % intra_dur != 0 and (chunk is None or j - i < chunk):
                     j += 1
+                wait_input(i, j)
                 self.set_Qp(self.const_init_Qp)
                 outs = []
                 for k in range(i, j):
@@ -413,8 +422,10 @@ class Y_Video_codec(BlockAPI):
                     self.set_Qp(qp_sched[-1])
                 ref_frames = [outs[-1].recon]
                 ref_float = [False]
+                on_output(i, j, outs)
                 i = j
                 continue
+            wait_input(i, i + 1)
             cur = frames_dev[i]
             pre = symbols[i] if symbols is not None else None
             self.set_Qp(self.const_init_Qp)
@@ -436,6 +447,7 @@ class Y_Video_codec(BlockAPI):
             out_syms.append(sym)
             ftypes.append(sym.frame_type)
             qp_rows.append(list(qp_sched) if rc_on else [])
+            on_output(i, i + 1, [sym])
             if i < nframes - 1:
                 if len(ref_frames) >= self.nRefFrames:
                     ref_frames.pop(0)

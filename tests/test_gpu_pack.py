@@ -85,3 +85,29 @@ def test_pack_capacity_guard(gpu):
     o2 = out2[0].cpu().numpy()
     assert o2[:fit].tobytes() == out[0, :fit].cpu().numpy().tobytes()
     assert (o2[cap:] == 0xAB).all()
+
+
+@pytest.mark.parametrize("h,w,frames,intra_dur,chunk", [(288, 384, 7, 7, 2), (2160, 3840, 8, 4, 3)])
+def test_host_stream_matches_resident_encode(gpu, h, w, frames, intra_dur, chunk):
+    """hoststream.HostStreamEncoder (overlapped H2D / encode+pack / D2H, P-runs in chunks):
+    the downloaded packed streams equal so_pack_frames of encode_device's symbols, and the
+    SSE matches; two GOPs back to back reuse the buffers."""
+    from streamoptima_amd.Encoder import Y_Video_codec
+    from streamoptima_amd.hoststream import HostStreamEncoder
+    from streamoptima_amd.synth import synth_sequence_torch
+    from streamoptima_amd.engine import alloc_planes
+    c = Y_Video_codec(h, w, frames, 16, 16, 4, intra_dur, 0, 0.015, False, device=gpu)
+    fr = alloc_planes(frames, h, w, gpu)
+    fr.copy_(synth_sequence_torch(frames, h, w, seed=5, device=gpu))
+    res = c.encode_device(fr, intra_dur)
+    offs, out = c.engine().pack_symbols(res["symbols"])
+    want = [out[i, :int(offs[i, -1])].cpu() for i in range(frames)]
+    sse = res["sse"].cpu()
+    hs = HostStreamEncoder(c, frames, chunk=chunk)
+    host = fr.cpu().pin_memory()
+    for _ in range(2):
+        got = hs.encode(host, intra_dur)
+        assert got["frame_type"] == res["frame_type"]
+        assert torch.equal(got["sse"], sse)
+        for i in range(frames):
+            assert torch.equal(got["packed"][i], want[i]), i
