@@ -181,6 +181,33 @@ int so_stripe_halo_push(const uint8_t* plane, int H, int W, int by0, int by1, in
                         uint8_t* peer_dn, uint32_t* peer_up_flags, uint32_t* peer_dn_flags,
                         uint32_t epoch, void* stream);
 
+/*
+ * One GOP across GPUs, consecutive frames on consecutive ranks (the frame pipeline of
+ * DESIGN.md §6; north_star "frames within a GOP shard across the GPUs").  Rank g of N encodes
+ * the frames k = g + N*j; frame k predicts from frame k-1, encoded by rank g-1 (mod N).  Each
+ * rank owns uncached landing planes (so_alloc_uncached; slot j at land0 + j * stride, at least
+ * H*W bytes + 16) with one flag word per 128x32 tile (land_flags + j * ntiles, ntiles =
+ * (W/128) * ceil(H/32)): slot j holds the reconstruction of frame k-1 for its frame j, flagged
+ * tile by tile == epoch as it arrives.  The persistent run of the rank's frames [slot0,
+ * slot0 + nframes) waits per tile for the 3x3 arrived tiles of its reference, and stores every
+ * tile's reconstruction both into out_recon[i] (local) and, system-scope write-through over
+ * xGMI, into the next rank's plane peer_land0 + (slot + peer_slot_off) * stride (peer_slot_off
+ * = 1 on rank N-1, whose frames feed rank 0's next slot; 0 otherwise) before setting that
+ * rank's flag to epoch.  Epochs are never reset (a new GOP uses a new epoch).  The symbols
+ * are those of so_encode_p_run over the same frames.  so_frame_push sends a finished frame
+ * (the I-frame) the same way.  workspace: so_p_run_workspace_elems(H, W), as so_encode_p_run.
+ */
+int so_encode_p_run_fpipe(const uint8_t* const* curs, int nframes, int H, int W, int bs, int sr,
+                          int qp_rd, const int32_t* qp_row, uint8_t* const* out_split,
+                          int16_t* const* out_mv, int16_t* const* out_qtc, int32_t* const* out_tokens,
+                          int32_t* const* out_mae_num, uint8_t* const* out_recon,
+                          int32_t* const* out_sse, uint32_t* workspace, const uint8_t* land0,
+                          const uint32_t* land_flags, int slot0, uint8_t* peer_land0,
+                          uint32_t* peer_flags, int peer_slot_off, long long stride, uint32_t epoch,
+                          int max_wg, void* stream);
+int so_frame_push(const uint8_t* plane, int H, int W, uint8_t* peer_plane, uint32_t* peer_flags,
+                  uint32_t epoch, void* stream);
+
 /* Device memory the ranks share.  The one exception to "the library never allocates": the
  * landing planes and flags of the cross-GPU hand-off must be uncached
  * (hipExtMallocWithFlags(hipDeviceMallocUncached)), which PyTorch cannot allocate. */

@@ -60,6 +60,9 @@ _SIGS = {
     "so_copy_d2d": ([_vp, _vp, _sz, _vp], _i),
     "so_memset_d8": ([_vp, _i, _sz, _vp], _i),
     "so_pack_bound": ([_i, _i], _sz),
+    "so_encode_p_run_fpipe": ([_vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                               _vp, _vp, _i, _vp, _vp, _i, ctypes.c_longlong, ctypes.c_uint32, _i, _vp], _i),
+    "so_frame_push": ([_vp, _i, _i, _vp, _vp, ctypes.c_uint32, _vp], _i),
     "so_pack_frames": ([_i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, ctypes.c_ulonglong, _vp], _i),
     "so_fme_plane_stride": ([_i, _i], _sz),
     "so_fme_workspace_bytes": ([_i, _i, _i], _sz),

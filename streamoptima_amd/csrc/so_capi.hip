@@ -60,6 +60,8 @@ struct PRunStripe {
     uint32_t* peer_dn_flags;
     uint32_t epoch;
     int gbase;
+    const uint8_t* land0;
+    int peer_slot_off;
 };
 int p_run_stripe_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                         const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg,
@@ -76,6 +78,10 @@ size_t pack_block_bound(int bs);
 int pack_frames_launch(const PackFrame* frames, int nframes, int nb, int bs, unsigned long long cap, hipStream_t st);
 int stripe_halo_push_launch(const uint8_t* plane, int W, int by0, int by1, uint8_t* up, uint8_t* dn,
                             uint32_t* up_flags, uint32_t* dn_flags, int gf, uint32_t epoch, hipStream_t st);
+int p_run_fpipe_launch(const uint8_t* const* curs, int nframes, int H, int W, int qp_rd, const int32_t* qp_row,
+                       const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg, hipStream_t st);
+int frame_push_launch(const uint8_t* plane, int H, int W, uint8_t* dst, uint32_t* flags, uint32_t epoch,
+                      hipStream_t st);
 
 // The fused search + transform tile kernel (so_me.hip p_tile_kernel) covers the headline
 // configuration: bs 16, sr 16, full search, no VBS / FME, one reference.  SO_FUSED=0 or an
@@ -418,7 +424,7 @@ int so_encode_p_run_stripe(const uint8_t* const* curs, int nframes, const uint8_
                             out_sse ? out_sse[i] : nullptr};
     }
     PRunStripe sp{by0, by1, peer_up0, peer_dn0, stride, my_up_flags, my_dn_flags, peer_up_flags, peer_dn_flags,
-                  epoch, gbase};
+                  epoch, gbase, nullptr, 0};
     return p_run_stripe_launch(curs, nframes, ref0, H, W, qp_rd, qp_row, outs.data(), workspace, sp, max_wg,
                                (hipStream_t)stream);
 }
@@ -440,6 +446,60 @@ int so_stripe_halo_push(const uint8_t* plane, int H, int W, int by0, int by1, in
     if (!peer_up && !peer_dn) return SO_OK;
     return stripe_halo_push_launch(plane, W, by0, by1, peer_up, peer_dn, peer_up_flags, peer_dn_flags, gf, epoch,
                                    (hipStream_t)stream);
+}
+
+// ---- one GOP across GPUs: consecutive frames on consecutive ranks (so_me.hip kRunFPipe) -----
+int so_encode_p_run_fpipe(const uint8_t* const* curs, int nframes, int H, int W, int bs, int sr, int qp_rd,
+                          const int32_t* qp_row, uint8_t* const* out_split, int16_t* const* out_mv,
+                          int16_t* const* out_qtc, int32_t* const* out_tokens, int32_t* const* out_mae_num,
+                          uint8_t* const* out_recon, int32_t* const* out_sse, uint32_t* workspace,
+                          const uint8_t* land0, const uint32_t* land_flags, int slot0, uint8_t* peer_land0,
+                          uint32_t* peer_flags, int peer_slot_off, long long stride, uint32_t epoch, int max_wg,
+                          void* stream) {
+    const char* fn = "so_encode_p_run_fpipe";
+    SO_TRY(check_geom(fn, H, W, bs, 0));
+    SO_TRY(check_sr(fn, sr));
+    SO_TRY(check_qp(fn, qp_rd));
+    if (bs != 16 || sr != 16 || W % 128 != 0) {
+        set_error("%s: covers bs 16 / sr 16 / W %% 128 == 0", fn);
+        return SO_E_UNSUPPORTED;
+    }
+    if (slot0 < 0 || peer_slot_off < 0 || peer_slot_off > 1 || stride < (long long)H * W) {
+        set_error("%s: slot0 %d / peer_slot_off %d / stride %lld", fn, slot0, peer_slot_off, stride);
+        return SO_E_INVALID;
+    }
+    if (nframes <= 0) return SO_OK;
+    SO_NEED(curs, fn); SO_NEED(out_split, fn); SO_NEED(out_mv, fn); SO_NEED(out_qtc, fn); SO_NEED(out_tokens, fn);
+    SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn); SO_NEED(workspace, fn); SO_NEED(land0, fn);
+    SO_NEED(land_flags, fn); SO_NEED(peer_land0, fn); SO_NEED(peer_flags, fn);
+    std::vector<PFrameOut> outs((size_t)nframes);
+    const uint8_t* land_end = land0 + (long long)(slot0 + nframes) * stride;
+    for (int i = 0; i < nframes; ++i) {
+        SO_NEED(curs[i], fn); SO_NEED(out_split[i], fn); SO_NEED(out_mv[i], fn); SO_NEED(out_qtc[i], fn);
+        SO_NEED(out_tokens[i], fn); SO_NEED(out_mae_num[i], fn); SO_NEED(out_recon[i], fn);
+        if (out_recon[i] >= land0 && out_recon[i] < land_end) {
+            set_error("%s: out_recon[%d] lies in the landing planes", fn, i);
+            return SO_E_INVALID;
+        }
+        outs[i] = PFrameOut{out_split[i], out_mv[i], out_qtc[i], out_tokens[i], out_mae_num[i], out_recon[i],
+                            out_sse ? out_sse[i] : nullptr};
+    }
+    PRunStripe sp{0, H / 16, nullptr, peer_land0, stride, nullptr, land_flags, nullptr, peer_flags,
+                  epoch, slot0, land0, peer_slot_off};
+    return p_run_fpipe_launch(curs, nframes, H, W, qp_rd, qp_row, outs.data(), workspace, sp, max_wg,
+                              (hipStream_t)stream);
+}
+
+int so_frame_push(const uint8_t* plane, int H, int W, uint8_t* peer_plane, uint32_t* peer_flags, uint32_t epoch,
+                  void* stream) {
+    const char* fn = "so_frame_push";
+    SO_TRY(check_geom(fn, H, W, 16, 0));
+    if (W % 128 != 0) {
+        set_error("%s: W %% 128 != 0", fn);
+        return SO_E_UNSUPPORTED;
+    }
+    SO_NEED(plane, fn); SO_NEED(peer_plane, fn); SO_NEED(peer_flags, fn);
+    return frame_push_launch(plane, H, W, peer_plane, peer_flags, epoch, (hipStream_t)stream);
 }
 
 // ---- memory the ranks share (uncached landing planes, IPC) ----------------------------------

@@ -1377,9 +1377,17 @@ struct PRunStripe {
     uint32_t* peer_dn_flags;   // the down neighbour's my_up_flags
     uint32_t epoch;
     int gbase;                 // global frame index of the launch's first frame
+    // frame pipeline (kRunFPipe): frame j of this rank's run (its slot) predicts from the
+    // reconstruction the previous rank pushed into land0 + j * stride, with my_dn_flags
+    // [j * ntiles + tile] == epoch once that tile arrived; every tile of frame j is pushed
+    // into the next rank's plane peer_dn0 + (j + peer_slot_off) * stride and flagged in
+    // peer_dn_flags[(j + peer_slot_off) * ntiles + tile].  gbase = slot of the launch's first frame.
+    const uint8_t* land0;
+    int peer_slot_off;
 };
+constexpr int kRunSingle = 0, kRunStripe = 1, kRunFPipe = 2;
 
-template <int NW, bool STRIPE>
+template <int NW, int MODE>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE)))
 p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, int H, int W,
              int qp_rd, const int32_t* __restrict__ qp_row, uint32_t* __restrict__ ws, int ws_stamp_base,
@@ -1389,6 +1397,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     __shared__ int s_task;
     const int tid = threadIdx.x;
     const int nbx = W / 16;
+    constexpr bool STRIPE = MODE == kRunStripe, FPIPE = MODE == kRunFPipe;
     const int by0 = STRIPE ? sp.by0 : 0, by1 = STRIPE ? sp.by1 : H / 16;
     const int tiles_x = (nbx + G::TBX - 1) / G::TBX, ntr = (by1 - by0 + G::TBY - 1) / G::TBY;
     const int ntiles = tiles_x * ntr, ntasks = ntiles * nframes;
@@ -1427,12 +1436,12 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             const int gprev = (STRIPE ? sp.gbase : 0) + f - 1;   // global index of the reference frame
             const bool remote = STRIPE && (first_row ? sp.my_up_flags != nullptr : false);
             const bool remote_dn = STRIPE && (last_row ? sp.my_dn_flags != nullptr : false);
-            if (f == 0 && !remote && !remote_dn) return;
+            if (!FPIPE && f == 0 && !remote && !remote_dn) return;
 #ifdef SO_STAMPS
             if (lane == 0 && rec) rec[9] = __builtin_amdgcn_s_memrealtime();
 #endif
             const int nx = tx + lane % 3 - 1, ny = ty + lane / 3 - 1;
-            const bool need = f > 0 && lane < 9 && nx >= 0 && nx < tiles_x && ny >= 0 && ny < ntr;
+            const bool need = (FPIPE || f > 0) && lane < 9 && nx >= 0 && nx < tiles_x && ny >= 0 && ny < ntr;
             // the timeout count, read once per tile: after one timeout the later tiles of the
             // run skip their waits (the run is already flagged wrong), so a lost flag cannot
             // stall the launch for 50 ms per remaining tile.  (Polling it in the loop put
@@ -1442,6 +1451,10 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 #endif
             const uint32_t* c = done + (size_t)(f > 0 ? f - 1 : 0) * ntiles + (need ? ny * tiles_x + nx : 0);
             bool rneed = false;
+            if constexpr (FPIPE) {   // the previous frame's tiles arrive from the previous rank
+                c = sp.my_dn_flags + (size_t)(sp.gbase + f) * ntiles + (need ? ny * tiles_x + nx : 0);
+                rneed = need;
+            }
             if constexpr (STRIPE) {
                 const int rx = tx + (lane - 9) % 3 - 1;
                 if (lane >= 9 && lane < 12 && remote && rx >= 0 && rx < tiles_x) {
@@ -1455,7 +1468,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
             for (;;) {
                 uint32_t v;
-                if (STRIPE && rneed)
+                if ((STRIPE || FPIPE) && rneed)
                     v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == sp.epoch ? 1u : 0u;
                 else
                     v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1478,8 +1491,23 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
         };
-        const uint8_t* ref = f ? a.out[f - 1].recon : ref0;
-        if constexpr (STRIPE) {
+        const uint8_t* ref = FPIPE ? sp.land0 + (long long)(sp.gbase + f) * sp.stride : (f ? a.out[f - 1].recon : ref0);
+        if constexpr (FPIPE) {
+            const int slot = sp.gbase + f + sp.peer_slot_off;   // the next rank's slot of this frame
+            PHalo hl{};
+            hl.dn = sp.peer_dn0 + (long long)slot * sp.stride;   // every row of the tile
+            hl.dn_begin = 0;
+            ptile_body<G, true, decltype(wait_ref), true>(S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd, qp_row,
+                                                          nullptr, nullptr, a.out[f], wait_ref, hl);
+            // ptile_body ended with every wave's stores (local and remote) retired and a barrier
+            if (wave == 0) {
+                __hip_atomic_fetch_add(done + (size_t)f * ntiles + tile, one, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0)
+                    __hip_atomic_store(sp.peer_dn_flags + (size_t)slot * ntiles + tile, sp.epoch, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        } else if constexpr (STRIPE) {
             const int gf = sp.gbase + f;
             PHalo hl{};
             if (first_row && sp.peer_up0) {
@@ -1531,7 +1559,7 @@ size_t p_run_workspace_words(int H, int W) {
 
 // Launch the run in <= kRunMax-frame launches.  max_wg > 0 caps the resident grid (several
 // ranks sharing one GPU in the tests).
-template <bool STRIPE>
+template <int MODE>
 static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                           const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp0,
                           int max_wg, hipStream_t st) {
@@ -1541,12 +1569,12 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
             ncu = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p_run_kernel<SO_PTILE_NW, STRIPE>, SO_PTILE_NW * 64,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p_run_kernel<SO_PTILE_NW, MODE>, SO_PTILE_NW * 64,
                                                          0) != hipSuccess || per_cu <= 0)
             per_cu = 1;
     }
     const int nbx = W / 16;
-    const int rows = STRIPE ? sp0.by1 - sp0.by0 : H / 16;
+    const int rows = MODE == kRunStripe ? sp0.by1 - sp0.by0 : H / 16;
     const long ntiles = (long)((nbx + Sea2Geo::TBX - 1) / Sea2Geo::TBX) * ((rows + Sea2Geo::TBY - 1) / Sea2Geo::TBY);
     for (int f0 = 0; f0 < nframes; f0 += kRunMax) {
         const int n = nframes - f0 < kRunMax ? nframes - f0 : kRunMax;
@@ -1578,7 +1606,7 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
         if (max_wg > 0 && grid > max_wg) grid = max_wg;
         PRunStripe sp = sp0;
         sp.gbase = sp0.gbase + f0;
-        hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, STRIPE>), dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), 0, st, a, n,
+        hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, MODE>), dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), 0, st, a, n,
                            f0 ? outs[f0 - 1].recon : ref0, H, W, qp_rd, qp_row, ws, (int)(f0 * ntiles), sp);
         const int rc = check_launch("p_run_kernel");
         if (rc != SO_OK) return rc;
@@ -1591,13 +1619,18 @@ int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, i
     PRunStripe sp{};
     sp.by0 = 0;
     sp.by1 = H / 16;
-    return p_run_launch_t<false>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, 0, st);
+    return p_run_launch_t<kRunSingle>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, 0, st);
 }
 
 int p_run_stripe_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                         const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg,
                         hipStream_t st) {
-    return p_run_launch_t<true>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st);
+    return p_run_launch_t<kRunStripe>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st);
+}
+
+int p_run_fpipe_launch(const uint8_t* const* curs, int nframes, int H, int W, int qp_rd, const int32_t* qp_row,
+                       const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg, hipStream_t st) {
+    return p_run_launch_t<kRunFPipe>(curs, nframes, nullptr, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st);
 }
 
 // The I-frame's hand-off (the P-frame run's frame 0 reads its boundary rows): copy the
@@ -1631,6 +1664,33 @@ int stripe_halo_push_launch(const uint8_t* plane, int W, int by0, int by1, uint8
     hipLaunchKernelGGL(stripe_halo_push_kernel, dim3(2 * tiles_x), dim3(128), 0, st, plane, W, by0 * 16, by1 * 16, up,
                        dn, up_flags, dn_flags, gf, tiles_x, epoch);
     return check_launch("stripe_halo_push_kernel");
+}
+
+// The I-frame's hand-off in the frame pipeline (kRunFPipe): the whole reconstruction into
+// the next rank's landing plane `dst`, tile by tile (128 x 32 px: one dwordx4 per thread,
+// system-scope write-through), each tile's flag flags[t] = epoch once its stores drained.
+__global__ void __launch_bounds__(256) frame_push_kernel(const uint8_t* __restrict__ plane, int H, int W,
+                                                         uint8_t* dst, uint32_t* flags, int tiles_x, uint32_t epoch) {
+    const int t = blockIdx.x, tx = t % tiles_x, ty = t / tiles_x;
+    const int r = threadIdx.x >> 3, c = (threadIdx.x & 7) * 16;       // 32 rows x 8 dwordx4
+    const int y = ty * 32 + r, x = tx * 128 + c;
+    if (x < W && y < H) {
+        const so_v4u v = *reinterpret_cast<const so_v4u*>(plane + (size_t)y * W + x);
+        uint8_t* q = dst + (size_t)y * W + x;
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(q), "v"(v) : "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flags + t, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+int frame_push_launch(const uint8_t* plane, int H, int W, uint8_t* dst, uint32_t* flags, uint32_t epoch,
+                      hipStream_t st) {
+    const int tiles_x = (W / 16 + Sea2Geo::TBX - 1) / Sea2Geo::TBX;
+    const int ntr = (H / 16 + Sea2Geo::TBY - 1) / Sea2Geo::TBY;
+    hipLaunchKernelGGL(frame_push_kernel, dim3(tiles_x * ntr), dim3(256), 0, st, plane, H, W, dst, flags, tiles_x,
+                       epoch);
+    return check_launch("frame_push_kernel");
 }
 
 // ---------------------------------------------------------------------------------------

@@ -290,3 +290,179 @@ class PipelinedStripeGOPEncoder:
 
     def close(self) -> None:
         self.r.close()
+
+
+# ---- frame pipeline: consecutive frames on consecutive ranks -----------------------------------
+class FramePipeRank:
+    """One rank of a GOP whose frames are dealt round-robin over the ranks:
+    rank g encodes frames k = g + N*j (rank 0's frame 0 is the I-frame) with ONE persistent
+    launch (so_encode_p_run_fpipe); frame k's reference, frame k-1, arrives tile by tile from
+    rank g-1 into this rank's uncached landing plane of slot j, and every tile of frame k is
+    pushed on into rank g+1's plane as it completes.  Each rank encodes whole frames at full
+    chip throughput while the frames of the other ranks run a couple of tile rows behind or
+    ahead, so N ranks encode N frames at once; the only traffic is each reconstruction,
+    once, over the xGMI link to the next rank."""
+
+    def __init__(self, engine, world: int, rank: int, max_frames: int, stream=None, max_wg: int = 0):
+        e = engine
+        if world < 2:
+            raise ValueError("the frame pipeline needs at least 2 ranks")
+        if not e.pipelined_ok(1):
+            raise ValueError("the frame pipeline covers bs 16 / sr 16 / full search / no VBS, FME / W % 128 == 0")
+        self.eng, self.world, self.rank, self.max_frames = e, world, rank, max_frames
+        self.stream, self.max_wg = stream, max_wg
+        lib = self.lib = _lib.load()
+        self.tiles_x, self.ntr = e.w // 128, -(-e.nby // 2)
+        self.ntiles = self.tiles_x * self.ntr
+        self.nslots = -(-max_frames // world) + 1
+        self.stride = -(-(e.h * e.w + 256) // 256) * 256
+        self._planes, self._flags = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(lib.so_alloc_uncached(self.nslots * self.stride, ctypes.byref(self._planes)), "so_alloc_uncached")
+        _lib.check(lib.so_alloc_uncached(self.nslots * self.ntiles * 4, ctypes.byref(self._flags)), "so_alloc_uncached")
+        _lib.check(lib.so_memset_d8(self._planes, 0, self.nslots * self.stride, self._st()), "so_memset_d8")
+        _lib.check(lib.so_memset_d8(self._flags, 0, self.nslots * self.ntiles * 4, self._st()), "so_memset_d8")
+        self.epoch = 0
+        self.peer = None
+        self._opened = []
+        self._ws = torch.zeros(lib.so_p_run_workspace_elems(e.h, e.w), dtype=torch.int32, device=e.device)
+        self._syms = None
+
+    def _st(self):
+        return self.stream.cuda_stream if self.stream is not None else _lib.stream_handle(self.eng.device)
+
+    def frames_of(self, nframes: int) -> list:
+        """Global indices of this rank's frames, in order (slot j <-> frame rank + N*j)."""
+        return [k for k in range(self.rank, nframes, self.world)]
+
+    def info(self) -> dict:
+        return {"planes": self._planes.value, "flags": self._flags.value, "rank": self.rank}
+
+    def export(self) -> dict:
+        hp, hf = (ctypes.c_uint8 * 64)(), (ctypes.c_uint8 * 64)()
+        _lib.check(self.lib.so_ipc_export(self._planes, hp), "so_ipc_export")
+        _lib.check(self.lib.so_ipc_export(self._flags, hf), "so_ipc_export")
+        return {"planes_h": bytes(hp), "flags_h": bytes(hf), "rank": self.rank}
+
+    def open(self, exported: dict) -> dict:
+        out = {"rank": exported["rank"]}
+        for k in ("planes", "flags"):
+            p = ctypes.c_void_p()
+            h = (ctypes.c_uint8 * 64).from_buffer_copy(exported[k + "_h"])
+            _lib.check(self.lib.so_ipc_open(h, ctypes.byref(p)), "so_ipc_open")
+            self._opened.append(p)
+            out[k] = p.value
+        return out
+
+    def connect(self, nxt: dict) -> None:
+        """nxt: the next rank's info() as mapped in this process."""
+        if nxt["rank"] != (self.rank + 1) % self.world:
+            raise ValueError("connect() takes the next rank")
+        self.peer = (nxt["planes"], nxt["flags"])
+
+    def close(self) -> None:
+        for p in self._opened:
+            self.lib.so_ipc_close(p)
+        self._opened = []
+        for p in (self._planes, self._flags):
+            if p.value:
+                self.lib.so_free_device(p)
+        self._planes, self._flags = ctypes.c_void_p(), ctypes.c_void_p()
+
+    def encode(self, frames: torch.Tensor, intra_dur: int, qp: int) -> dict:
+        """This rank's frames of the GOP {global index: FrameSymbols} (whole-frame symbols,
+        local reconstructions).  Asynchronous on the rank's stream."""
+        e, lib = self.eng, self.lib
+        nf = frames.shape[0]
+        if nf > self.max_frames or intra_dur < nf:
+            raise ValueError("the frame pipeline runs one GOP of <= max_frames frames with its only I-frame first")
+        if self.peer is None:
+            raise RuntimeError("connect() first")
+        self.epoch += 1
+        ep, st = self.epoch, self._st()
+        mine = self.frames_of(nf)
+        if self._syms is None or len(self._syms) != len(mine):
+            self._syms = {k: e.new_symbols(0 if k == 0 else 1) for k in mine}
+        syms = self._syms
+        pplanes, pflags = self.peer
+        ks = mine
+        if self.rank == 0:
+            s0 = syms[0]
+            _lib.check(lib.so_encode_i_rows_ex(
+                frames[0].data_ptr(), e.h, e.w, e.bs, e.sr, 0, e.nby, int(qp), None, None, 0, 0.0,
+                s0.split.data_ptr(), s0.mv.data_ptr(), s0.qtc.data_ptr(), s0.tokens.data_ptr(), s0.mae_num.data_ptr(),
+                s0.recon.data_ptr(), s0.sse.data_ptr(), e.scratch.data_ptr(), st), "so_encode_i_rows_ex")
+            s0.frame_type, s0.qp_rd = 0, int(qp)
+            if nf > 1:   # frame 1 is rank 1's slot 0
+                _lib.check(lib.so_frame_push(s0.recon.data_ptr(), e.h, e.w, pplanes, pflags, ep, st), "so_frame_push")
+            ks = mine[1:]
+        if ks:
+            n = len(ks)
+            slot0 = (ks[0] - self.rank) // self.world
+            arr = lambda xs: (ctypes.c_void_p * n)(*xs)  # noqa: E731
+            ss = [syms[k] for k in ks]
+            _lib.check(lib.so_encode_p_run_fpipe(
+                arr([frames[k].data_ptr() for k in ks]), n, e.h, e.w, e.bs, e.sr, int(qp), None,
+                arr([s.split.data_ptr() for s in ss]), arr([s.mv.data_ptr() for s in ss]),
+                arr([s.qtc.data_ptr() for s in ss]), arr([s.tokens.data_ptr() for s in ss]),
+                arr([s.mae_num.data_ptr() for s in ss]), arr([s.recon.data_ptr() for s in ss]),
+                arr([s.sse.data_ptr() for s in ss]), self._ws.data_ptr(), self._planes.value, self._flags.value,
+                slot0, pplanes, pflags, 1 if self.rank == self.world - 1 else 0, self.stride, ep,
+                int(self.max_wg), st), "so_encode_p_run_fpipe")
+            for s in ss:
+                s.frame_type, s.qp_rd = 1, int(qp)
+        return syms
+
+    def timed_out(self) -> bool:
+        return int(self._ws[32].item()) != 0
+
+    def check(self) -> None:
+        n = int(self._ws[32].item())
+        if n:
+            self._ws[32].zero_()
+            raise RuntimeError(f"p_run frame pipeline: {n} dependency wait(s) timed out; symbols unreliable")
+
+
+class FramePipelineGOPEncoder:
+    """torch.distributed front end of FramePipeRank (one rank per GPU; the next rank's
+    landing planes mapped by IPC, handles exchanged with all_gather_object)."""
+
+    def __init__(self, engine, max_frames: int, group=None, max_wg: int = 0):
+        import torch.distributed as dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.eng = engine
+        self.r = FramePipeRank(engine, self.world, self.rank, max_frames, max_wg=max_wg)
+        torch.cuda.synchronize(engine.device)
+        alls = [None] * self.world
+        dist.all_gather_object(alls, self.r.export(), group=group)
+        self.r.connect(self.r.open(alls[(self.rank + 1) % self.world]))
+        dist.barrier(group=group)
+
+    def encode(self, frames, intra_dur: int, qp: int) -> dict:
+        import torch.distributed as dist
+        syms = self.r.encode(frames, intra_dur, qp)
+        nf = frames.shape[0]
+        sse = torch.zeros(nf, dtype=torch.int64, device=self.eng.device)
+        for k, s in syms.items():
+            sse[k] = s.sse.sum(dtype=torch.int64)
+        dist.all_reduce(sse, group=self.group)
+        return {"symbols": syms, "sse": sse, "frame_type": [0 if k == 0 else 1 for k in range(nf)]}
+
+    def check(self) -> None:
+        self.r.check()
+
+    def digests(self, syms: dict, nframes: int) -> list:
+        """Per-frame digests (digest.symbols_digest) of the whole GOP, on every rank."""
+        import torch.distributed as dist
+        from .digest import symbols_digest
+        mine = {k: symbols_digest(s) for k, s in syms.items()}
+        alls = [None] * self.world
+        dist.all_gather_object(alls, mine, group=self.group)
+        out = {}
+        for d in alls:
+            out.update(d)
+        return [out[k] for k in range(nframes)]
+
+    def close(self) -> None:
+        self.r.close()

@@ -138,3 +138,72 @@ def test_stripe_run_two_processes_ipc(gpu, tmp_path):
     hp, w = 1088, 1920
     psnr = [10 * np.log10(255 ** 2 / (s / (hp * w))) for s in got["sse"]]
     np.testing.assert_allclose(psnr, FIX["1080p"]["psnr"][:n], rtol=0, atol=1e-9)
+
+
+# ---- frame pipeline (consecutive frames on consecutive ranks, so_encode_p_run_fpipe) -------------
+@pytest.mark.parametrize("name,world,nframes", [("4k", 2, 12), ("4k", 3, 13), ("1080p", 2, 30)])
+def test_frame_pipeline_in_process_matches_one_gpu(gpu, name, world, nframes):
+    """Rank g encodes frames g, g+N, ...; each frame's reference arrives tile by tile from the
+    previous rank.  Whole-frame symbols and local reconstructions of every frame must equal
+    the one-GPU GOP (oracle digests), twice in a row (epoch 2 over epoch 1's planes)."""
+    from streamoptima_amd.digest import symbols_digest
+    from streamoptima_amd.engine import Engine
+    from streamoptima_amd.pipeline import FramePipeRank
+    cfg, fr = _frames(name, gpu, nframes)
+    h, w = fr.shape[1:]
+    engines = [Engine(h, w, 16, 16, False, 0.015, gpu) for _ in range(world)]
+    streams = _streams(gpu)[:world]
+    cap = 768 // (2 * world)
+    ranks = [FramePipeRank(engines[r], world, r, nframes, stream=streams[r], max_wg=cap) for r in range(world)]
+    torch.cuda.synchronize()
+    for r in range(world):
+        ranks[r].connect(ranks[(r + 1) % world].info())
+    for rep in range(2):
+        syms = {}
+        for r in range(world):
+            with torch.cuda.stream(streams[r]):
+                syms.update(ranks[r].encode(fr, nframes, cfg["qp"]))
+        torch.cuda.synchronize()
+        for r in ranks:
+            r.check()
+        got = [symbols_digest(syms[k]) for k in range(nframes)]
+        exp = FIX[name]["frame_sha256"][:nframes]
+        bad = [i for i, (a, b) in enumerate(zip(got, exp)) if a != b]
+        assert not bad, f"rep {rep}: frames {bad[:10]} differ from the one-GPU GOP"
+    for r in ranks:
+        r.close()
+
+
+def _fpipe_worker(rank, world, port, name, nframes, outdir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from streamoptima_amd.engine import Engine
+        from streamoptima_amd.pipeline import FramePipelineGOPEncoder
+        dev = torch.device("cuda:0")
+        cfg, fr = _frames(name, dev, nframes)
+        eng = Engine(fr.shape[1], fr.shape[2], 16, 16, False, 0.015, dev)
+        enc = FramePipelineGOPEncoder(eng, nframes, max_wg=768 // (2 * world))
+        res = enc.encode(fr, nframes, cfg["qp"])
+        torch.cuda.synchronize()
+        enc.check()
+        digs = enc.digests(res["symbols"], nframes)
+        if rank == 0:
+            with open(os.path.join(outdir, "digests.json"), "w") as fh:
+                json.dump({"digests": digs, "sse": res["sse"].cpu().tolist()}, fh)
+        dist.barrier()
+        enc.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_frame_pipeline_two_processes_ipc(gpu, tmp_path):
+    """Two ranks as two processes (one GPU, landing planes mapped by IPC), 4K GOP head."""
+    import torch.multiprocessing as mp
+    n = 8
+    mp.start_processes(_fpipe_worker, args=(2, _free_port(), "4k", n, str(tmp_path)), nprocs=2, start_method="spawn")
+    got = json.load(open(tmp_path / "digests.json"))
+    assert got["digests"] == FIX["4k"]["frame_sha256"][:n]
+    psnr = [10 * np.log10(255 ** 2 / (s / (2160 * 3840))) for s in got["sse"]]
+    np.testing.assert_allclose(psnr, FIX["4k"]["psnr"][:n], rtol=0, atol=1e-9)
