@@ -10,8 +10,11 @@ VBS off):
         carries a `records.1080p` entry for configs[1] (1920x1080 padded to 1088 rows),
         measured the same way in the same run.
   N > 1 (default --config 4k120): configs[3], ONE 4K 120-frame GOP per step, sharded over
-        the N ranks (streamoptima_amd/dist.py; strong scaling).  --shard gop is the opt-in
-        weak-scaling mode (an independent GOP per rank).
+        the N ranks (strong scaling): by default the frame pipeline (rank g encodes frames
+        g, g+N, ..., each reference arriving tile by tile from the previous rank over xGMI;
+        streamoptima_amd/pipeline.py FramePipelineGOPEncoder), self-checked before timing,
+        else block-row stripes (--shard stripe; dist.py / pipeline.py).  --shard gop is the
+        opt-in weak-scaling mode (an independent GOP per rank).
 One step = one GOP through Y_Video_codec.encode_device(): every frame's ME, residual,
 DCT/Q/IDCT, token count, reconstruction and per-block SSE.  It is encode()'s GPU work minus
 the closed-loop decoder re-run (Encoder.py:1873, whose output the reference discards) and
@@ -81,8 +84,9 @@ def parse(argv=None):
     ap.add_argument("--exchange", choices=("p2p", "allgather"), default="p2p",
                     help="stripe hand-off: inside the persistent launch over xGMI (p2p, self-checked against "
                          "allgather before timing) or an RCCL all_gather of every reconstruction (allgather)")
-    ap.add_argument("--shard", choices=("stripe", "gop"), default="stripe",
-                    help="N>1: block-row stripes of ONE GOP (strong, configs[3]) or a GOP per rank (weak)")
+    ap.add_argument("--shard", choices=("fpipe", "stripe", "gop"), default="fpipe",
+                    help="N>1: ONE GOP (strong, configs[3]) as a frame pipeline over the ranks (fpipe; falls back to "
+                         "stripes if its self-check fails) or as block-row stripes, or a GOP per rank (weak)")
     ap.add_argument("--me", choices=("full", "fme", "fast", "fastpar", "fast_fme"), default="full",
                     help="ME variant: full search (headline), FMEEnable, fast_me (serial chain), fast_me under "
                          "ParallelMode 2, fast_me + FMEEnable")
@@ -568,6 +572,40 @@ def p2p_encoder(eng, frames, cfg, senc, world, max_wg=0):
     return penc, "in-launch p2p over xGMI (uncached landing planes, IPC), self-checked"
 
 
+def fpipe_encoder(codec, frames, cfg, world, max_wg=0):
+    """The frame pipeline (streamoptima_amd/pipeline.py FramePipelineGOPEncoder), self-checked
+    before timing: the first 2N+1 frames through it must give, on every rank, the digests of
+    a one-GPU encode of the same frames, with no hand-off wait timed out.  (None, why) else."""
+    import torch.distributed as dist
+    from streamoptima_amd.digest import symbols_digest
+    from streamoptima_amd.pipeline import FramePipelineGOPEncoder
+    eng = codec.engine()
+    ok, penc, why = 1, None, ""
+    if cfg["intra_dur"] < cfg["frames"] or not eng.pipelined_ok(1):
+        ok, why = 0, "needs one I-frame per GOP and the persistent-run configuration"
+    else:
+        try:
+            penc = FramePipelineGOPEncoder(eng, cfg["frames"], max_wg=max_wg)
+        except Exception as e:   # noqa: BLE001 -- any failure to set up the peer mapping
+            ok, why = 0, f"setup: {e}"
+    flag = torch.tensor([ok], dtype=torch.int32, device=eng.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 0:
+        return None, why or "unavailable on another rank"
+    k = min(2 * world + 1, cfg["frames"])
+    a = penc.encode(frames[:k], k, cfg["qp"])
+    torch.cuda.synchronize()
+    got = penc.digests(a["symbols"], k)
+    ref = [symbols_digest(s) for s in codec.encode_device(frames[:k], k)["symbols"]]
+    good = not penc.r.timed_out() and got == ref
+    flag = torch.tensor([1 if good else 0], dtype=torch.int32, device=eng.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 0:
+        penc.r._ws[32].zero_()
+        return None, "self-check failed"
+    return penc, "frame pipeline over xGMI (IPC-mapped uncached landing planes), self-checked"
+
+
 # ---- CPU plumbing stand-in (--cpu-plumbing) ---------------------------------------------------------
 class _PlumbingEngine:
     """A trivial CPU stand-in with the Engine stripe methods StripeGOPEncoder calls: symbols
@@ -619,12 +657,13 @@ def main(argv=None):
         cfg["frames"] = args.frames
         cfg["intra_dur"] = min(cfg["intra_dur"], args.frames)
     parity_ok = not (args.no_parity or args.frames or args.vbs or args.me != "full")
-    stripe = world > 1 and args.shard == "stripe"
+    stripe = world > 1 and args.shard in ("stripe", "fpipe")    # one GOP over the ranks
     dev = torch.device("cpu") if args.cpu_plumbing else torch.device("cuda", local)
     h, w, f = cfg["h"], cfg["w"], cfg["frames"]
 
     exchange_note = "all_gather per frame"
-    penc = None
+    penc = fenc = None
+    mode_note = f"stripe x{world} (block rows of one GOP; hand-off: {{}})"
     if args.cpu_plumbing:
         from streamoptima_amd.dist import StripeGOPEncoder
         from streamoptima_amd.synth import synth_sequence
@@ -644,22 +683,34 @@ def main(argv=None):
         frames = make_frames(cfg, dev, cfg["seed"])
         senc = StripeGOPEncoder(eng)
         rc = cfg.get("rc")
-        penc = None
-        if args.exchange == "p2p" and not rc and args.me == "full" and not args.vbs and eng.pipelined_ok(1):
-            penc, exchange_note = p2p_encoder(eng, frames, cfg, senc, world,
-                                              max_wg=768 // (2 * world) if args.share_gpu else 0)
-        else:
-            exchange_note = "all_gather (RCCL) per frame" + (": RC/ROI GOP" if rc else "")
-        if penc is not None:
-            pre_s = [penc.r.new_symbols(0 if i % cfg["intra_dur"] == 0 else 1) for i in range(f)]
+        cap = 768 // (2 * world) if args.share_gpu else 0
+        plain = not rc and args.me == "full" and not args.vbs and eng.pipelined_ok(1)
+        fpipe_note = ""
+        if args.shard == "fpipe" and plain:
+            fenc, fpipe_note = fpipe_encoder(codec, frames, cfg, world, max_wg=cap)
+        if fenc is not None:
+            mode_note = f"frame pipeline x{world} (rank g encodes frames g, g+N, ...; {{}})"
+            exchange_note = fpipe_note
 
             def step():
-                return penc.encode(frames, cfg["intra_dur"], cfg["qp"], symbols=pre_s)
+                return fenc.encode(frames, cfg["intra_dur"], cfg["qp"])
         else:
-            def step():
-                return senc.encode(frames, cfg["intra_dur"], cfg["qp"],
-                                   qp_sched=codec.row_qp_schedule(eng.nby) if rc else None, rc_flag=rc,
-                                   intra_thresh=None, roi=codec.roi_block_offsets())
+            if args.exchange == "p2p" and plain:
+                penc, exchange_note = p2p_encoder(eng, frames, cfg, senc, world, max_wg=cap)
+            else:
+                exchange_note = "all_gather (RCCL) per frame" + (": RC/ROI GOP" if rc else "")
+            if fpipe_note:
+                exchange_note += f"; frame pipeline not used: {fpipe_note}"
+            if penc is not None:
+                pre_s = [penc.r.new_symbols(0 if i % cfg["intra_dur"] == 0 else 1) for i in range(f)]
+
+                def step():
+                    return penc.encode(frames, cfg["intra_dur"], cfg["qp"], symbols=pre_s)
+            else:
+                def step():
+                    return senc.encode(frames, cfg["intra_dur"], cfg["qp"],
+                                       qp_sched=codec.row_qp_schedule(eng.nby) if rc else None, rc_flag=rc,
+                                       intra_thresh=None, roi=codec.roi_block_offsets())
     else:
         codec, frames, pre, step = run_single(cfg, args, dev, parity_ok)
         if world > 1 and rank > 0:   # --shard gop: an independent GOP per rank (seed + rank)
@@ -668,16 +719,17 @@ def main(argv=None):
     elapsed, res = time_steps(step, world, args.steps, args.warmup, dev)
     if codec is not None and not stripe:
         codec.engine().check_run()
-    if penc is not None:
+    if penc is not None or fenc is not None:
         # a lost hand-off anywhere voids the timed run: time the all_gather path instead
         import torch.distributed as dist
-        lost = torch.tensor([1 if penc.r.timed_out() else 0], dtype=torch.int32, device=dev)
+        r_ = (penc or fenc).r
+        lost = torch.tensor([1 if r_.timed_out() else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(lost, op=dist.ReduceOp.MAX)
         if int(lost.item()):
-            penc.r._ws[32].zero_()
-            penc = None
+            r_._ws[32].zero_()
+            penc = fenc = None
+            mode_note = f"stripe x{world} (block rows of one GOP; hand-off: {{}})"
             exchange_note = "all_gather (RCCL) per frame; the p2p run timed out a hand-off and was discarded"
-            rc = cfg.get("rc")
 
             def step():  # noqa: F811
                 return senc.encode(frames, cfg["intra_dur"], cfg["qp"])
@@ -695,7 +747,15 @@ def main(argv=None):
     # ---- after timing: parity of the timed output ----
     parity = None
     if parity_ok and not args.cpu_plumbing:
-        if stripe:
+        if fenc is not None:
+            fenc.check()
+            got = fenc.digests(res["symbols"], f)
+            if rank == 0:
+                fx = load_fixture(name)
+                parity = compare_digests(got, fx) if fx else {"bit_exact": None, "note": "no fixture"}
+                if fx:
+                    parity["fixture"] = "tests/golden/large_gops.json (C oracle, tests/golden/make_large_fixtures.py)"
+        elif stripe:
             if penc is not None:
                 penc.check()
                 full = [penc.gather_symbols(s, i) for i, s in enumerate(res["symbols"])]
@@ -749,8 +809,7 @@ def main(argv=None):
                    "intra_dur": cfg["intra_dur"], "block_size": 16, "search_range": 16, "qp": cfg["qp"],
                    "seed": cfg["seed"], "vbs": bool(args.vbs), "nRefFrames": 1, "me": args.me,
                    "transform": "fp64 pocketfft-exact DCT",
-                   "parallelism": (f"stripe x{world} (block rows of one GOP; hand-off: {exchange_note})" if stripe
-                                   else f"gop-per-rank x{world}"),
+                   "parallelism": (mode_note.format(exchange_note) if stripe else f"gop-per-rank x{world}"),
                    "launch": "hip-graph (one GOP per replay)" if args.graph else "host launches"},
         "parity": parity,
         "roofline": roofline_of(rl, name) if rl else None,
