@@ -374,7 +374,7 @@ def cpu_baseline(cfg, rows: int, pool_rows: int) -> dict:
 
 
 # ---- PCIe-inclusive --------------------------------------------------------------------------------
-def pcie_inclusive(codec, cfg, frames_dev, reps: int = 2) -> dict:
+def pcie_inclusive(codec, cfg, frames_dev, reps: int = 6) -> dict:
     """BASELINE.md §4's timed region: pinned host Y planes -> HBM, the GOP encode, and the
     symbols back to pinned host memory -- as the dense arrays (split, mv, qtc, tokens), and as
     the packed stream (so_pack_frames: varint MVs + RLE token lists, plus per-frame SSE)."""
@@ -401,16 +401,18 @@ def pcie_inclusive(codec, cfg, frames_dev, reps: int = 2) -> dict:
         got.update(hs.encode(host, cfg["intra_dur"]))
         return sum(got["bytes"]) + 8 * f
 
+    med = {}
+
     def timed(fn):
-        best, nbytes = None, None
-        for _ in range(reps + 1):
+        ts, nbytes = [], None
+        for _ in range(reps + 1):      # the first call warms the path (allocations, first copies)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             nbytes = fn()
             torch.cuda.synchronize()
-            dt = time.perf_counter() - t0
-            best = dt if best is None else min(best, dt)
-        return best, nbytes
+            ts.append(time.perf_counter() - t0)
+        med[fn.__name__] = float(np.median(ts[1:]))
+        return min(ts[1:]), nbytes
 
     def dense_timed():
         frames_dev.copy_(host, non_blocking=True)
@@ -424,6 +426,7 @@ def pcie_inclusive(codec, cfg, frames_dev, reps: int = 2) -> dict:
     same = all(torch.equal(got["packed"][i], packed[i, :int(offs[i, -1])].cpu()) for i in range(f))
     px = f * cfg["h"] * cfg["w"]
     return {"mpx_s": round(px / best_p / 1e6, 2), "ms_per_gop": round(best_p * 1e3, 3),
+            "ms_per_gop_median": round(med["packed_run"] * 1e3, 3), "reps": reps,
             "h2d_bytes": int(host.numel()), "d2h_bytes": int(d2h_p), "packed_equals_resident_symbols": bool(same),
             "note": "streamoptima_amd/hoststream.py: per-frame H2D on one copy stream, P-runs of 2 frames + "
                     "so_pack_frames on the compute stream, packed symbol stream + per-frame SSE D2H on a second "

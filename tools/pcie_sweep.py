@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--chunks", default="2,3,4,6,10,29")
-    ap.add_argument("--reps", type=int, default=4)
+    ap.add_argument("--reps", type=int, default=8)
     a = ap.parse_args()
     from streamoptima_amd.Encoder import Y_Video_codec
     from streamoptima_amd.engine import alloc_planes
@@ -38,14 +38,13 @@ def main():
     out = {"h2d_only_ms": round(up * 1e3, 3), "h2d_gbs": round(host.numel() / up / 1e9, 2)}
     for ch in [int(x) for x in a.chunks.split(",")]:
         hs = HostStreamEncoder(c, f, chunk=ch)
-        best = None
+        ts = []
         for _ in range(a.reps):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             r = hs.encode(host, f)
-            dt = time.perf_counter() - t0
-            best = dt if best is None else min(best, dt)
-        out[f"chunk_{ch}_ms"] = round(best * 1e3, 3)
+            ts.append(round((time.perf_counter() - t0) * 1e3, 3))
+        out[f"chunk_{ch}_ms"] = ts
         print(json.dumps(out), flush=True)
         del hs
     out["packed_bytes"] = sum(r["bytes"])
