@@ -293,6 +293,19 @@ class PipelinedStripeGOPEncoder:
 
 
 # ---- frame pipeline: consecutive frames on consecutive ranks -----------------------------------
+def fpipe_plan(world: int, rank: int, nframes: int) -> dict:
+    """Which frames rank `rank` of `world` encodes and where its references land.
+    frames: its global frame indices (k = rank + world * slot); run: the P-frames of its
+    persistent launch (rank 0's frame 0 is the I-frame); slot0: the slot of run[0] (its
+    reference, frame run[0] - 1, arrives in that landing slot); peer_slot_off: frame k of this
+    rank is the reference of frame k + 1, slot (k + 1 - next) / world on the next rank, i.e.
+    this rank's slot + peer_slot_off (1 on the last rank, whose next is rank 0)."""
+    frames = list(range(rank, nframes, world))
+    run = [k for k in frames if k > 0]
+    return {"frames": frames, "run": run, "slot0": (run[0] - rank) // world if run else 0,
+            "peer_slot_off": 1 if rank == world - 1 else 0, "nslots": -(-nframes // world) + 1}
+
+
 class FramePipeRank:
     """One rank of a GOP whose frames are dealt round-robin over the ranks:
     rank g encodes frames k = g + N*j (rank 0's frame 0 is the I-frame) with ONE persistent
@@ -314,7 +327,7 @@ class FramePipeRank:
         lib = self.lib = _lib.load()
         self.tiles_x, self.ntr = e.w // 128, -(-e.nby // 2)
         self.ntiles = self.tiles_x * self.ntr
-        self.nslots = -(-max_frames // world) + 1
+        self.nslots = fpipe_plan(world, rank, max_frames)["nslots"]
         self.stride = -(-(e.h * e.w + 256) // 256) * 256
         self._planes, self._flags = ctypes.c_void_p(), ctypes.c_void_p()
         _lib.check(lib.so_alloc_uncached(self.nslots * self.stride, ctypes.byref(self._planes)), "so_alloc_uncached")
@@ -332,7 +345,7 @@ class FramePipeRank:
 
     def frames_of(self, nframes: int) -> list:
         """Global indices of this rank's frames, in order (slot j <-> frame rank + N*j)."""
-        return [k for k in range(self.rank, nframes, self.world)]
+        return fpipe_plan(self.world, self.rank, nframes)["frames"]
 
     def info(self) -> dict:
         return {"planes": self._planes.value, "flags": self._flags.value, "rank": self.rank}
@@ -395,9 +408,10 @@ class FramePipeRank:
             if nf > 1:   # frame 1 is rank 1's slot 0
                 _lib.check(lib.so_frame_push(s0.recon.data_ptr(), e.h, e.w, pplanes, pflags, ep, st), "so_frame_push")
             ks = mine[1:]
+        plan = fpipe_plan(self.world, self.rank, nf)
         if ks:
             n = len(ks)
-            slot0 = (ks[0] - self.rank) // self.world
+            slot0 = plan["slot0"]
             arr = lambda xs: (ctypes.c_void_p * n)(*xs)  # noqa: E731
             ss = [syms[k] for k in ks]
             _lib.check(lib.so_encode_p_run_fpipe(
@@ -406,7 +420,7 @@ class FramePipeRank:
                 arr([s.qtc.data_ptr() for s in ss]), arr([s.tokens.data_ptr() for s in ss]),
                 arr([s.mae_num.data_ptr() for s in ss]), arr([s.recon.data_ptr() for s in ss]),
                 arr([s.sse.data_ptr() for s in ss]), self._ws.data_ptr(), self._planes.value, self._flags.value,
-                slot0, pplanes, pflags, 1 if self.rank == self.world - 1 else 0, self.stride, ep,
+                slot0, pplanes, pflags, plan["peer_slot_off"], self.stride, ep,
                 int(self.max_wg), st), "so_encode_p_run_fpipe")
             for s in ss:
                 s.frame_type, s.qp_rd = 1, int(qp)
