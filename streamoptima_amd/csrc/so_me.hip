@@ -600,14 +600,19 @@ int me_fme_launch(const uint8_t* cur, const uint8_t* planes, size_t pstride, int
 #endif
 // NW_ waves per workgroup: 8 (two blocks per wave; me_sea2_kernel) or 16 (one block per
 // wave; p_tile_kernel at 8 waves/SIMD)
-template <int NW_>
+// TPX_: tile width, 128 (16 blocks; the default) or 64 (8 blocks: p_run_kernel when a frame
+// has fewer 128-wide tiles than resident workgroups, where a tile's latency sets the frame time)
+template <int NW_, int TPX_ = 128>
 struct Sea2GeoT {
     static constexpr int SR = 16, NT = 17;
-    static constexpr int TBX = 8, TPY = 32, TBY = 2, TPX = 128;
+    static constexpr int TPX = TPX_, TBX = TPX / 16, TPY = 32, TBY = 2;
     static constexpr int WR = TPY + 2 * SR;               // 64 window rows
-    static constexpr int WD = (TPX + 2 * SR) / 4;         // 40 data dwords per row
-    static constexpr int RP = WD + 1;                     // pitch 41
-    static constexpr int B4R = WR - 3, B4C = TPX + 2 * SR - 3, B4P = 164;   // 41 dwords: rows 16 apart land 16 banks apart
+    static constexpr int WD = (TPX + 2 * SR) / 4;         // 40 (24) data dwords per row
+    static constexpr int RP = WD + 1;                     // pitch 41 (25)
+    static constexpr int B4R = WR - 3, B4C = TPX + 2 * SR - 3, B4P = 4 * RP;   // 41 dwords: rows 16 apart land 16 banks apart
+    // transform phase: blocks per wave (16 lanes each); 4 (waves 0-3 for 16 blocks) or 2
+    // (waves 0-3 for 8 blocks: half the per-wave latency)
+    static constexpr int TQ_BPW = TPX == 128 ? 4 : 2;
     static constexpr int B4BAND = NW_ >= 16 ? 3 : 6;      // output rows per byte-sum thread
     static constexpr int B4NB = (B4R + B4BAND - 1) / B4BAND;
     static constexpr int B4RS = B4NB * B4BAND;            // stored rows: whole bands, no bounds tests
@@ -782,7 +787,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
         __syncthreads();
         if (r == 0) SO_SEA_STAMP(3, __builtin_amdgcn_s_memtime());
         // 4x4 byte sums B4(row, c) = (sum of the 4x4 window block at (row, c)) >> 4, stored at
-        // b4[row * B4P + (c & 3) * 40 + (c >> 2)] (a candidate's four sums of one 4x4 row --
+        // b4[row * B4P + (c & 3) * WD + (c >> 2)] (a candidate's four sums of one 4x4 row --
         // columns c, c+4, c+8, c+12 -- are then consecutive bytes).  Thread = (dword column m:
         // columns 4m..4m+3, band of B4BAND output rows).
         if (tid < G::WD * G::B4NB) {
@@ -815,8 +820,8 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
                 for (int j = 0; j < 2; ++j) {
                     const uint32_t sum = h[i][j] + h[i + 1][j] + h[i + 2][j] + h[i + 3][j];
                     const uint32_t q = __builtin_bit_cast(uint32_t, __builtin_bit_cast(so_v2u16, sum) >> (so_v2u16){4, 4});
-                    ob[i * B4P + j * 40] = (uint8_t)q;
-                    ob[i * B4P + (j + 2) * 40] = (uint8_t)(q >> 16);
+                    ob[i * B4P + j * G::WD] = (uint8_t)q;
+                    ob[i * B4P + (j + 2) * G::WD] = (uint8_t)(q >> 16);
                 }
         }
         __syncthreads();
@@ -836,7 +841,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             for (int j = 0; j < 4; ++j) A[j] = a4[u * 4 + j];
             // ---- 1. lower bounds --------------------------------------------------------------
             const int cB = bxl * 16 + xi;
-            const int lb0 = (byl * 16 + 16 * hh) * B4P + (cB & 3) * 40 + (cB >> 2);   // byte offset
+            const int lb0 = (byl * 16 + 16 * hh) * B4P + (cB & 3) * G::WD + (cB >> 2);   // byte offset
             const uint32_t bsh = (uint32_t)lb0 & 3;
             int lo1 = lb0 >> 2;
             asm volatile("" : "+v"(lo1));
@@ -1097,8 +1102,8 @@ struct PTileGeo {
 
 // 16 bytes of window row `row` from byte column `col`, as 4 dwords (5 aligned ds_read_b32
 // + v_alignbyte: misaligned wide DS reads are replayed on gfx950)
+template <int RP>
 SO_DEV void win_row16(const uint32_t* win, int row, int col, uint32_t (&w)[4]) {
-    constexpr int RP = Sea2Geo::RP;
     lds_vu32p p = (lds_vu32p)(win + row * RP + (col >> 2));
     const uint32_t sh = (uint32_t)(col & 3);
     const uint32_t q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4];
@@ -1166,7 +1171,7 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
         int res[16];
         {
             uint32_t pw[4];
-            win_row16(S.win, prow, pcol, pw);
+            win_row16<G::RP>(S.win, prow, pcol, pw);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const uint32_t cw = crow[k];
@@ -1194,7 +1199,7 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
         int rec[16];
         {
             uint32_t pw[4];
-            win_row16(S.win, prow, pcol, pw);
+            win_row16<G::RP>(S.win, prow, pcol, pw);
 #pragma unroll
             for (int c = 0; c < 16; ++c)
                 rec[c] = (int)((pw[c >> 2] >> (8 * (c & 3))) & 255) +
@@ -1279,9 +1284,12 @@ SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur
     }
     __syncthreads();
     SO_SEA_STAMP(6, __builtin_amdgcn_s_memtime());
-    if (tid < G::NBLK * 16)
-        tq16_exact<G, SC1, HALO>(S, tid >> 4, tid & 15, S.un + (tid >> 4) * (16 * 17), bx0, byt0, nbx, by0, by1, W,
-                                 qp_rd, qp_row, qp_map, o, hl);
+    {   // block g = wave * TQ_BPW + (lane >> 4) on lanes [0, 16 * TQ_BPW) of waves 0..NBLK/TQ_BPW-1
+        const int ln = tid & 63, gq = (tid >> 6) * G::TQ_BPW + (ln >> 4);
+        if (ln < 16 * G::TQ_BPW && gq < G::NBLK)
+            tq16_exact<G, SC1, HALO>(S, gq, ln & 15, S.un + gq * (16 * 17), bx0, byt0, nbx, by0, by1, W, qp_rd, qp_row,
+                                     qp_map, o, hl);
+    }
     SO_SEA_STAMP(7, __builtin_amdgcn_s_memtime());
     if constexpr (SC1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
     SO_SEA_STAMP(14, __builtin_amdgcn_s_memtime());
@@ -1387,12 +1395,12 @@ struct PRunStripe {
 };
 constexpr int kRunSingle = 0, kRunStripe = 1, kRunFPipe = 2;
 
-template <int NW, int MODE>
+template <int NW, int MODE, int TPX = 128>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE)))
 p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, int H, int W,
              int qp_rd, const int32_t* __restrict__ qp_row, uint32_t* __restrict__ ws, int ws_stamp_base,
              const PRunStripe sp) {
-    using G = Sea2GeoT<NW>;
+    using G = Sea2GeoT<NW, TPX>;
     __shared__ PTileLds<G> S;
     __shared__ int s_task;
     const int tid = threadIdx.x;
@@ -1553,29 +1561,35 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 }
 
 size_t p_run_workspace_words(int H, int W) {
-    const size_t ntiles = (size_t)((W / 16 + Sea2Geo::TBX - 1) / Sea2Geo::TBX) * ((H / 16 + Sea2Geo::TBY - 1) / Sea2Geo::TBY);
+    using G64 = Sea2GeoT<8, 64>;   // the narrower tiles: the larger tile count
+    const size_t ntiles = (size_t)((W / 16 + G64::TBX - 1) / G64::TBX) * ((H / 16 + G64::TBY - 1) / G64::TBY);
     return (size_t)kRunDoneBase + (size_t)kRunMax * ntiles;
 }
 
 // Launch the run in <= kRunMax-frame launches.  max_wg > 0 caps the resident grid (several
 // ranks sharing one GPU in the tests).
-template <int MODE>
+static void device_shape(int* ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || *ncu <= 0)
+        *ncu = 256;
+}
+
+template <int MODE, int TPX>
 static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                           const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp0,
                           int max_wg, hipStream_t st) {
+    using G = Sea2GeoT<SO_PTILE_NW, TPX>;
     static int ncu = 0, per_cu = 0;
     if (ncu == 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-            ncu = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p_run_kernel<SO_PTILE_NW, MODE>, SO_PTILE_NW * 64,
-                                                         0) != hipSuccess || per_cu <= 0)
+        device_shape(&ncu);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p_run_kernel<SO_PTILE_NW, MODE, TPX>,
+                                                         SO_PTILE_NW * 64, 0) != hipSuccess || per_cu <= 0)
             per_cu = 1;
     }
     const int nbx = W / 16;
     const int rows = MODE == kRunStripe ? sp0.by1 - sp0.by0 : H / 16;
-    const long ntiles = (long)((nbx + Sea2Geo::TBX - 1) / Sea2Geo::TBX) * ((rows + Sea2Geo::TBY - 1) / Sea2Geo::TBY);
+    const long ntiles = (long)((nbx + G::TBX - 1) / G::TBX) * ((rows + G::TBY - 1) / G::TBY);
     for (int f0 = 0; f0 < nframes; f0 += kRunMax) {
         const int n = nframes - f0 < kRunMax ? nframes - f0 : kRunMax;
         PRunArgs a{};
@@ -1606,7 +1620,7 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
         if (max_wg > 0 && grid > max_wg) grid = max_wg;
         PRunStripe sp = sp0;
         sp.gbase = sp0.gbase + f0;
-        hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, MODE>), dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), 0, st, a, n,
+        hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, MODE, TPX>), dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), 0, st, a, n,
                            f0 ? outs[f0 - 1].recon : ref0, H, W, qp_rd, qp_row, ws, (int)(f0 * ntiles), sp);
         const int rc = check_launch("p_run_kernel");
         if (rc != SO_OK) return rc;
@@ -1614,23 +1628,30 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
     return SO_OK;
 }
 
+// One GPU: 128-px tiles.  SO_RUN_TPX=64 runs the 64-px variant (8 blocks per tile: one per
+// wave in the search, two per wave in the transforms) -- measured no faster where a frame has
+// fewer tiles than resident workgroups (1088p 29.5 vs 28.3 us per frame, 3840x272 24.2 vs
+// 25.3) and 1.56x slower at 4K (tools/tpx_ab.py), so it is an A/B option only.
 int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                  const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, hipStream_t st) {
     PRunStripe sp{};
     sp.by0 = 0;
     sp.by1 = H / 16;
-    return p_run_launch_t<kRunSingle>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, 0, st);
+    const char* e = getenv("SO_RUN_TPX");
+    if (e && atoi(e) == 64)
+        return p_run_launch_t<kRunSingle, 64>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, 0, st);
+    return p_run_launch_t<kRunSingle, 128>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, 0, st);
 }
 
 int p_run_stripe_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                         const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg,
                         hipStream_t st) {
-    return p_run_launch_t<kRunStripe>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st);
+    return p_run_launch_t<kRunStripe, 128>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st);
 }
 
 int p_run_fpipe_launch(const uint8_t* const* curs, int nframes, int H, int W, int qp_rd, const int32_t* qp_row,
                        const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg, hipStream_t st) {
-    return p_run_launch_t<kRunFPipe>(curs, nframes, nullptr, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st);
+    return p_run_launch_t<kRunFPipe, 128>(curs, nframes, nullptr, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st);
 }
 
 // The I-frame's hand-off (the P-frame run's frame 0 reads its boundary rows): copy the
