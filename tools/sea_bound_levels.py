@@ -1,0 +1,58 @@
+"""Offline: how many candidates a successive-elimination lower bound leaves for a full SAD,
+per cell size, on the bench content (synthetic frames, the C oracle's I-frame reconstruction
+as the reference).  For each block: U = the SAD of the candidate with the smallest bound (as
+sea2_tile does; for 8x8 also the best SAD of the k smallest bounds), survivors = candidates
+whose bound <= U.  4x4 uses the kernel's quantised bytes (16 * sum|q_c - q_r| - 240);
+8x8 bytes: 64 * sum|q_c - q_r| - 252.   python tools/sea_bound_levels.py"""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from oracle import oracle as O  # noqa: E402
+from streamoptima_amd.synth import synth_sequence  # noqa: E402
+
+
+def boxsum(a, k):
+    c = np.zeros((a.shape[0] + 1, a.shape[1] + 1), np.int64)
+    c[1:, 1:] = a.cumsum(0).cumsum(1)
+    return c[k:, k:] - c[:-k, k:] - c[k:, :-k] + c[:-k, :-k]
+
+
+def main(h=272, w=480):
+    for seed in (0, 1):
+        seq = synth_sequence(3, h, w, seed=seed)
+        ref = O.intra_frame(seq[0], 16, 16, 4)["recon"].astype(np.int64)
+        cur = seq[1].astype(np.int64)
+        B8, B4 = boxsum(ref, 8), boxsum(ref, 4)
+        res = {k: [] for k in ("q4", "q8", "q8_top4", "q8_top16")}
+        for by in range(1, h // 16 - 1):
+            for bx in range(1, w // 16 - 1):
+                x, y = bx * 16, by * 16
+                blk = cur[y:y + 16, x:x + 16]
+                A8 = blk.reshape(2, 8, 2, 8).sum(axis=(1, 3))
+                A4 = blk.reshape(4, 4, 4, 4).sum(axis=(1, 3))
+                l8, l4, sads = [], [], []
+                for dx in range(-16, 17):
+                    for dy in range(-16, 17):
+                        if not (0 <= x + dx < w - 16 and 0 <= y + dy < h - 16):
+                            continue
+                        b8 = B8[y + dy:y + dy + 16:8, x + dx:x + dx + 16:8]
+                        b4 = B4[y + dy:y + dy + 16:4, x + dx:x + dx + 16:4]
+                        l8.append(64 * np.abs((A8 >> 6) - (b8 >> 6)).sum() - 252)
+                        l4.append(16 * np.abs((A4 >> 4) - (b4 >> 4)).sum() - 240)
+                        sads.append(np.abs(blk - ref[y + dy:y + dy + 16, x + dx:x + dx + 16]).sum())
+                sads, l8, l4 = np.array(sads), np.array(l8), np.array(l4)
+                res["q4"].append((l4 <= sads[np.argmin(l4)]).sum())
+                o8 = np.argsort(l8, kind="stable")
+                for k, top in (("q8", 1), ("q8_top4", 4), ("q8_top16", 16)):
+                    res[k].append((l8 <= sads[o8[:top]].min()).sum())
+        for k, a in res.items():
+            a = np.array(a)
+            print(f"seed {seed} {k}: survivors mean {a.mean():.1f} median {np.median(a):.0f} "
+                  f"p90 {np.percentile(a, 90):.0f} max {a.max()} frac>16 {(a > 16).mean():.3f}")
+
+
+if __name__ == "__main__":
+    main()
