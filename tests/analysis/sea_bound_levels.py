@@ -1,15 +1,16 @@
-"""Offline: how many candidates a successive-elimination lower bound leaves for a full SAD,
+"""Offline analysis (test infrastructure: it uses the C oracle as the checker's reference
+reconstruction, so it lives under tests/).  How many candidates a successive-elimination lower bound leaves for a full SAD,
 per cell size, on the bench content (synthetic frames, the C oracle's I-frame reconstruction
 as the reference).  For each block: U = the SAD of the candidate with the smallest bound (as
 sea2_tile does; for 8x8 also the best SAD of the k smallest bounds), survivors = candidates
 whose bound <= U.  4x4 uses the kernel's quantised bytes (16 * sum|q_c - q_r| - 240);
-8x8 bytes: 64 * sum|q_c - q_r| - 252.   python tools/sea_bound_levels.py"""
+8x8 bytes: 64 * sum|q_c - q_r| - 252.   python tests/analysis/sea_bound_levels.py"""
 import os
 import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from oracle import oracle as O  # noqa: E402
 from streamoptima_amd.synth import synth_sequence  # noqa: E402
 

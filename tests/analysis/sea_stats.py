@@ -1,4 +1,5 @@
-"""Offline survivor statistics of the exact SEA pruning in me_sea2_kernel (so_me.hip) on the
+"""Offline analysis (test infrastructure: uses the C oracle, so it lives under tests/).
+Offline survivor statistics of the exact SEA pruning in me_sea2_kernel (so_me.hip) on the
 bench content: per block, count the candidates whose 4x4-sum lower bound does not exceed the
 SAD of the smallest-bound candidate.  Uses the C oracle for the I-frame reconstruction."""
 import numpy as np, sys
