@@ -5,7 +5,7 @@ The reference reads frames from host memory and writes its bitstream text to fil
 (Encoder.py:1790-1898, transmit_bitstream :1544-1580).  Here the three engines of the card
 work at once:
 
-    copy stream A (H2D)   frame 0 | frames 1..C | frames C+1..2C | ...
+    copy stream A (H2D)   frame 0 | frames 1..C | frames C+1..2C | ... | next GOP's frames ...
     compute stream        I-frame | P-run 1..C (+ pack) | P-run C+1..2C (+ pack) | ...
     copy stream B (D2H)                  packed chunk 0 | packed chunk 1 | ...
 
@@ -15,78 +15,159 @@ QTC) is downloaded as soon as its byte counts are known, while the next chunk en
 The host waits for a chunk's byte counts only after it has enqueued the following chunk, so
 the compute stream never idles on the host.  Symbols are those of encode_device (the chunks
 are persistent P-runs with the previous chunk's reconstruction as their reference).
+
+encode_stream() runs several GOPs back to back with two sets of frame / packed buffers: the
+next GOP's upload is queued before the current GOP encodes, so the H2D engine never waits for
+the compute stream (a GOP then costs about its upload time).
 """
 from __future__ import annotations
+
+import time
 
 import torch
 
 from .engine import alloc_planes
 
 
+class _Buffers:
+    """One GOP in flight: device frames, packed streams and their pinned host copies."""
+
+    def __init__(self, eng, nframes: int, dev):
+        self.frames_dev = alloc_planes(nframes, eng.h, eng.w, dev)
+        self.offs = torch.empty((nframes, eng.nb + 1), dtype=torch.int32, device=dev)
+        self.packed = torch.empty((nframes, eng.pack_bound()), dtype=torch.uint8, device=dev)
+        self.tot_h = torch.empty(nframes, dtype=torch.int32).pin_memory()
+        self.packed_h = torch.empty(self.packed.shape, dtype=torch.uint8).pin_memory()
+        self.sse_h = torch.empty(nframes, dtype=torch.int64).pin_memory()
+        self.enc_done = None      # compute-stream event: this set's frames are no longer read
+        self.d2h_done = None      # D2H-stream event: this set's packed streams are downloaded
+        self.gop = None           # (index, frame types) of the GOP it holds
+
+
 class HostStreamEncoder:
-    def __init__(self, codec, nframes: int, chunk: int = 2):
+    def __init__(self, codec, nframes: int, chunk: int = 2, nbuf: int = 1):
         eng = codec.engine()
         self.codec, self.eng, self.nframes, self.chunk = codec, eng, int(nframes), int(chunk)
-        dev = codec.device
-        self.dev = dev
-        self.frames_dev = alloc_planes(self.nframes, eng.h, eng.w, dev)
-        self.h2d = torch.cuda.Stream(dev)
-        self.d2h = torch.cuda.Stream(dev)
+        self.dev = codec.device
+        self.h2d = torch.cuda.Stream(self.dev)
+        self.d2h = torch.cuda.Stream(self.dev)
         self.syms = None
-        self.offs = torch.empty((self.nframes, eng.nb + 1), dtype=torch.int32, device=dev)
-        self.packed = torch.empty((self.nframes, eng.pack_bound()), dtype=torch.uint8, device=dev)
-        self.tot_h = torch.empty(self.nframes, dtype=torch.int32).pin_memory()
-        self.packed_h = torch.empty(self.packed.shape, dtype=torch.uint8).pin_memory()
-        self.sse_h = torch.empty(self.nframes, dtype=torch.int64).pin_memory()
+        self.bufs = [_Buffers(eng, self.nframes, self.dev) for _ in range(max(1, int(nbuf)))]
+
+    @property
+    def frames_dev(self):
+        return self.bufs[0].frames_dev
+
+    def _check(self, frames_host):
+        if tuple(frames_host.shape) != tuple(self.bufs[0].frames_dev.shape) or not frames_host.is_pinned():
+            raise ValueError("frames_host must be pinned uint8 of the encoder's padded frame shape")
+
+    def _upload(self, b: _Buffers, frames_host) -> list:
+        up = []
+        with torch.cuda.stream(self.h2d):
+            if b.enc_done is not None:
+                self.h2d.wait_event(b.enc_done)      # the GOP that last used these frames is encoded
+            for i in range(self.nframes):
+                b.frames_dev[i].copy_(frames_host[i], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.h2d)
+                up.append(ev)
+        return up
+
+    def _result(self, b: _Buffers) -> dict:
+        nbytes = b.tot_h.tolist()
+        return {"packed": [b.packed_h[i, :n] for i, n in enumerate(nbytes)], "bytes": nbytes,
+                "sse": b.sse_h.clone(), "frame_type": b.gop[1]}
 
     def encode(self, frames_host: torch.Tensor, intra_dur: int) -> dict:
         """frames_host: pinned uint8 [F, Hp, Wp].  Returns {"packed": [host uint8 view per
         frame], "bytes": [...], "sse": host int64 [F], "frame_type": [...]} once everything
-        is in host memory."""
-        f = self.nframes
-        if tuple(frames_host.shape) != tuple(self.frames_dev.shape) or not frames_host.is_pinned():
-            raise ValueError("frames_host must be pinned uint8 of the encoder's padded frame shape")
-        eng, comp = self.eng, torch.cuda.current_stream(self.dev)
+        is in host memory (the views stay valid until the next call)."""
+        out = []
+        self.encode_stream([frames_host], intra_dur, lambda k, r: out.append(r))
+        return out[0]
+
+    def encode_stream(self, gops: list, intra_dur: int, consume, trace: list | None = None) -> None:
+        """Encode GOPs back to back; consume(k, result) is called for GOP k, in order, once its
+        symbols are in host memory and before its buffers are reused (the result's views are
+        valid only inside the call).  With two buffer sets (nbuf=2) GOP k+1's upload runs
+        during GOP k's encode."""
+        for g in gops:
+            self._check(g)
+        eng, comp, nb = self.eng, torch.cuda.current_stream(self.dev), len(self.bufs)
         if self.syms is None:
-            self.syms = [eng.new_symbols(0 if i % intra_dur == 0 else 1) for i in range(f)]
-        up = []
-        with torch.cuda.stream(self.h2d):
-            self.h2d.wait_stream(comp)        # the previous GOP's reads of frames_dev are done
-            for i in range(f):
-                self.frames_dev[i].copy_(frames_host[i], non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(self.h2d)
-                up.append(ev)
-        pending = []
+            self.syms = [eng.new_symbols(0 if i % intra_dur == 0 else 1) for i in range(self.nframes)]
+        pending, waiting = [], []      # chunks whose byte counts are on their way; finished GOPs
+
+        def mark(label, stream):       # tools/stream_probe.py: (label, event, host time)
+            if trace is not None:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(stream)
+                trace.append((label, ev, time.perf_counter()))
 
         def drain(upto_len):
             while len(pending) > upto_len:
-                k0, k1, ev = pending.pop(0)
+                b, k0, k1, ev = pending.pop(0)
                 ev.synchronize()                    # byte counts of frames [k0, k1) are in tot_h
                 self.d2h.wait_event(ev)
                 with torch.cuda.stream(self.d2h):
                     for i in range(k0, k1):
-                        n = int(self.tot_h[i])
-                        self.packed_h[i, :n].copy_(self.packed[i, :n], non_blocking=True)
+                        n = int(b.tot_h[i])
+                        b.packed_h[i, :n].copy_(b.packed[i, :n], non_blocking=True)
+                if k1 == self.nframes:              # the GOP's last chunk: its download is queued
+                    b.d2h_done = torch.cuda.Event()
+                    b.d2h_done.record(self.d2h)
+                    mark(f"d2h_end {b.gop[0] if b.gop else '?'}", self.d2h)
 
-        def wait_input(k0, k1):
-            comp.wait_event(up[k1 - 1])
+        def retire(b):
+            """Hand GOP b.gop to the caller (its chunks all drained) and free the set."""
+            if any(p[0] is b for p in pending):
+                drain(0)
+            while waiting and waiting[0] is b:
+                waiting.pop(0)
+                b.enc_done.synchronize()            # its SSE copy (compute stream)
+                b.d2h_done.synchronize()            # its packed streams (D2H stream)
+                consume(b.gop[0], self._result(b))
+                b.gop = None
 
-        def on_output(k0, k1, syms):
-            eng.pack_symbols(syms, self.offs[k0:k1], self.packed[k0:k1])
-            self.tot_h[k0:k1].copy_(self.offs[k0:k1, eng.nb], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(comp)
-            pending.append((k0, k1, ev))
-            drain(1)                                 # the chunk before this one
+        ups = {}
+        for k, g in enumerate(gops):
+            b = self.bufs[k % nb]
+            if b.gop is not None:
+                retire(b)                            # GOP k - nb: long finished when nb > 1
+            if k == 0 or nb == 1:
+                ups[k] = self._upload(b, g)
+                mark(f"up_end {k}", self.h2d)
+            if nb > 1 and k + 1 < len(gops):       # the next GOP's upload, queued before this encode
+                ups[k + 1] = self._upload(self.bufs[(k + 1) % nb], gops[k + 1])
+                mark(f"up_end {k + 1}", self.h2d)
+            up = ups.pop(k)
+            if b.d2h_done is not None:
+                comp.wait_event(b.d2h_done)         # this set's previous packed streams are down
+            b.gop = (k, None)
+            mark(f"enc_start {k}", comp)
 
-        res = self.codec.encode_device(self.frames_dev, intra_dur, symbols=self.syms, check=False, chunk=self.chunk,
-                                       wait_input=wait_input, on_output=on_output)
-        self.sse_h.copy_(res["sse"], non_blocking=True)
+            def wait_input(k0, k1, up=up):
+                comp.wait_event(up[k1 - 1])
+
+            def on_output(k0, k1, syms, b=b):
+                eng.pack_symbols(syms, b.offs[k0:k1], b.packed[k0:k1])
+                b.tot_h[k0:k1].copy_(b.offs[k0:k1, eng.nb], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(comp)
+                pending.append((b, k0, k1, ev))
+                drain(1)                             # the chunk before this one
+
+            res = self.codec.encode_device(b.frames_dev, intra_dur, symbols=self.syms, check=False,
+                                           chunk=self.chunk, wait_input=wait_input, on_output=on_output)
+            b.sse_h.copy_(res["sse"], non_blocking=True)
+            b.enc_done = torch.cuda.Event()
+            b.enc_done.record(comp)
+            mark(f"enc_end {k}", comp)
+            b.gop = (k, res["frame_type"])
+            waiting.append(b)
         drain(0)
+        for b in list(waiting):
+            retire(b)
         comp.synchronize()
-        self.d2h.synchronize()
         eng.check_run()
-        nbytes = self.tot_h.tolist()
-        return {"packed": [self.packed_h[i, :n] for i, n in enumerate(nbytes)], "bytes": nbytes,
-                "sse": self.sse_h.clone(), "frame_type": res["frame_type"]}

@@ -111,3 +111,32 @@ def test_host_stream_matches_resident_encode(gpu, h, w, frames, intra_dur, chunk
         assert torch.equal(got["sse"], sse)
         for i in range(frames):
             assert torch.equal(got["packed"][i], want[i]), i
+
+
+def test_host_stream_back_to_back_gops(gpu):
+    """encode_stream with two buffer sets: three GOPs (different content) back to back, each
+    GOP's packed streams equal to so_pack_frames of its resident encode."""
+    from streamoptima_amd.Encoder import Y_Video_codec
+    from streamoptima_amd.engine import alloc_planes
+    from streamoptima_amd.hoststream import HostStreamEncoder
+    from streamoptima_amd.synth import synth_sequence_torch
+    h, w, frames = 288, 384, 5
+    c = Y_Video_codec(h, w, frames, 16, 16, 4, frames, 0, 0.015, False, device=gpu)
+    hosts, wants = [], []
+    for seed in (1, 2, 3):
+        fr = alloc_planes(frames, h, w, gpu)
+        fr.copy_(synth_sequence_torch(frames, h, w, seed=seed, device=gpu))
+        res = c.encode_device(fr, frames)
+        offs, out = c.engine().pack_symbols(res["symbols"])
+        wants.append(([out[i, :int(offs[i, -1])].cpu() for i in range(frames)], res["sse"].cpu()))
+        hosts.append(fr.cpu().pin_memory())
+    hs = HostStreamEncoder(c, frames, chunk=2, nbuf=2)
+    seen = []
+
+    def consume(k, r):
+        pk, sse = wants[k]
+        assert torch.equal(r["sse"], sse), k
+        assert all(torch.equal(r["packed"][i], pk[i]) for i in range(frames)), k
+        seen.append(k)
+    hs.encode_stream(hosts, frames, consume)
+    assert seen == [0, 1, 2]
