@@ -1621,7 +1621,7 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
         if (pcu > per_cu) pcu = per_cu;
         if (const char* e = getenv("SO_RUN_PER_CU")) {   // A/B only: resident workgroups per CU
             const int v = atoi(e);
-            if (v > 0 && v < per_cu) pcu = v;
+            if (v > 0 && v <= per_cu) pcu = v;
         }
         long grid = (long)ncu * pcu;
         if (grid > ntiles * n) grid = ntiles * n;

@@ -1,5 +1,6 @@
-"""P-run per-frame time of the default library vs A/B builds (SO_LIB_PATH), each in a fresh
-process: python tools/ab_runs.py tools/_ab/a.so tools/_ab/b.so  (prints one JSON per lib)."""
+"""P-run per-frame time of the default library vs A/B builds (SO_LIB_PATH) or environment
+settings, each in a fresh process:
+    python tools/ab_runs.py tools/_ab/a.so SO_RUN_PER_CU=2 ...   (one JSON line per variant)"""
 import json
 import os
 import subprocess
@@ -34,7 +35,10 @@ print(json.dumps(out))
 def main():
     for lib in [""] + sys.argv[1:]:
         env = dict(os.environ)
-        if lib:
+        if "=" in lib:
+            k, v = lib.split("=", 1)
+            env[k] = v
+        elif lib:
             env["SO_LIB_PATH"] = lib
         r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
         line = [l for l in r.stdout.splitlines() if l.startswith("{")]
