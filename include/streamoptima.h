@@ -374,6 +374,13 @@ int so_sse_u8(const uint8_t* a, const uint8_t* b, int64_t n, uint64_t* out_sse,
               void* stream);
 
 /*
+ * out[i] = sum of rows[i][0..len) (int32 -> int64) for i < n: the per-frame SSE of a GOP from
+ * the encode kernels' per-block / per-row out_sse arrays (rows: a HOST array of device
+ * pointers), one launch.
+ */
+int so_sum_i32_rows(const int32_t* const* rows, int n, int len, int64_t* out, void* stream);
+
+/*
  * Packed symbol stream: the content of the reference's two text lines per frame
  * (differential_encoder_frame's MVs before differencing, Encoder.py:1419-1520, and
  * entropy_encoder_block's RLE token lists, :1086-1131 / :1522-1542) as zigzag LEB128

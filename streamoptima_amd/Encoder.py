@@ -358,7 +358,11 @@ class Y_Video_codec(BlockAPI):
         on_output = on_output or (lambda k0, k1, syms: None)
         eng = self.engine()
         nframes = frames_dev.shape[0]
-        ref_frames = [alloc_planes(1, eng.h, eng.w, self.device, fill=128)[0]]
+        # the reference's initial reference list: one all-128 frame (Encoder.py:1798), never
+        # written, so one plane per engine serves every GOP (no fill per call)
+        if getattr(eng, "_ref128", None) is None:
+            eng._ref128 = alloc_planes(1, eng.h, eng.w, self.device, fill=128)[0]
+        ref_frames = [eng._ref128]
         # the start frame is float64 in the reference (Encoder.py:1798): while it is in the
         # list the FME frac frame does not wrap its uint8 row sums (so_encode_p_rows_ex)
         ref_float = [True]
@@ -456,7 +460,7 @@ class Y_Video_codec(BlockAPI):
                 ref_float.append(False)
             i += 1
         # per-block / per-row SSE came out of the encode kernels; one reduction per GOP
-        sse = torch.stack([s.sse for s in out_syms]).sum(dim=1, dtype=torch.int64)
+        sse = eng.sum_rows([s.sse for s in out_syms])
         if check and pipelined:
             eng.check_run()
         return {"symbols": out_syms, "sse": sse, "frame_type": ftypes, "qp_rows": qp_rows}

@@ -191,6 +191,39 @@ static int make_refs(const char* fn, const uint8_t* const* refs, int nref, RefSe
         }                                               \
     } while (0)
 
+// ---- per-frame sums of the encode kernels' per-block / per-row SSE ---------------------------
+constexpr int kSumMax = 64;
+struct SumArgs {
+    const int32_t* p[kSumMax];
+};
+
+// one workgroup per array: int64 sum of len int32 values into out[blockIdx.x]; 16-byte loads,
+// eight in flight per thread (a dependent 4-byte load per step made this latency-bound)
+__global__ void __launch_bounds__(256) sum_rows_kernel(const SumArgs a, int len, long long* __restrict__ out) {
+    __shared__ long long part[4];
+    const int32_t* p = a.p[blockIdx.x];
+    long long acc = 0;
+    const int n4 = (reinterpret_cast<uintptr_t>(p) & 15) ? 0 : len / 4;
+    const int4* p4 = reinterpret_cast<const int4*>(p);
+    int i = threadIdx.x;
+    for (; i + 7 * 256 < n4; i += 8 * 256) {
+        int4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = p4[i + k * 256];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc += (long long)v[k].x + v[k].y + v[k].z + v[k].w;
+    }
+    for (; i < n4; i += 256) {
+        const int4 v = p4[i];
+        acc += (long long)v.x + v.y + v.z + v.w;
+    }
+    for (int j = 4 * n4 + threadIdx.x; j < len; j += 256) acc += p[j];
+    for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) out[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
 // ---- SSE (PSNR) -------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) sse_kernel(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b,
                                                   int64_t n, unsigned long long* __restrict__ out) {
@@ -828,6 +861,29 @@ int so_qp_map(const int32_t* tokens, int H, int W, int bs, int by0, int by1, int
     hipLaunchKernelGGL(qp_map_kernel, dim3(by1 - by0), dim3(256), 0, (hipStream_t)stream, tokens, W / bs, by0, qp_rd,
                        qp_row, roi, qp_lo, qp_hi, out_qp_map);
     return check_launch("qp_map_kernel");
+}
+
+int so_sum_i32_rows(const int32_t* const* rows, int n, int len, int64_t* out, void* stream) {
+    const char* fn = "so_sum_i32_rows";
+    if (n < 0 || len < 0) {
+        set_error("%s: n %d / len %d", fn, n, len);
+        return SO_E_INVALID;
+    }
+    if (n == 0) return SO_OK;
+    SO_NEED(rows, fn); SO_NEED(out, fn);
+    for (int i0 = 0; i0 < n; i0 += kSumMax) {
+        const int m = n - i0 < kSumMax ? n - i0 : kSumMax;
+        SumArgs a{};
+        for (int i = 0; i < m; ++i) {
+            SO_NEED(rows[i0 + i], fn);
+            a.p[i] = rows[i0 + i];
+        }
+        hipLaunchKernelGGL(sum_rows_kernel, dim3(m), dim3(256), 0, (hipStream_t)stream, a, len,
+                           reinterpret_cast<long long*>(out + i0));
+        const int rc = check_launch("sum_rows_kernel");
+        if (rc != SO_OK) return rc;
+    }
+    return SO_OK;
 }
 
 int so_sse_u8(const uint8_t* a, const uint8_t* b, int64_t n, uint64_t* out_sse, void* stream) {

@@ -28,7 +28,9 @@ SO_DEV int canvas_at(const uint8_t* left /* LDS row: cols x0-sr .. x0-1 */, int 
     return col < x0 ? (int)left[col - (x0 - sr)] : 128;
 }
 
-template <int BS, bool VBS>
+// SRM: the search range the left-pixel LDS rows are sized for (16 for the default sr 16:
+// 4 KB instead of 16 KB, three workgroups per CU instead of two)
+template <int BS, bool VBS, int SRM = kIntraMaxSr>
 __global__ void __launch_bounds__(256)
 intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int by0, int nrows, int sr, int qp_rd,
                 const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map, double lam,
@@ -40,19 +42,19 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int by0, int nrow
     constexpr int LDS_D = VBS ? 288 : BS * (BS + 1);
     __shared__ double ldsd[BPW * LDS_D];
     __shared__ uint8_t ldsf[BPW * BS * BS];
-    __shared__ uint8_t ldsl[BPW * BS * kIntraMaxSr];
+    __shared__ uint8_t ldsl[BPW * BS * SRM];
     const int tid = threadIdx.x, g = tid / G, l = tid % G;
     const int nbx = W / BS, nb = nbx * nrows;
     const int b = blockIdx.x * BPW + g;   // block index inside the stripe [by0, by0 + nrows)
     if (b >= nb) return;
     double* dl = ldsd + g * LDS_D;
     uint8_t* fl = ldsf + g * BS * BS;
-    uint8_t* left = ldsl + g * BS * kIntraMaxSr;
+    uint8_t* left = ldsl + g * BS * SRM;
     const int bx = b % nbx, by = by0 + b / nbx, x = bx * BS, y = by * BS;
     const int qpr = qp_map ? qp_map[(size_t)by * nbx + bx] : (qp_row ? qp_row[by] : qp_rd);
 
     // stage the original pixels left of the block (cols x-sr .. x-1, 0 where < 0)
-    uint8_t* lrow = left + l * kIntraMaxSr;
+    uint8_t* lrow = left + l * SRM;
     if (BS == 16 && sr == 16 && x != 0) {
         // x >= 16: one aligned 16-byte row load and one ds_write_b128
         *reinterpret_cast<uint4*>(lrow) = *reinterpret_cast<const uint4*>(cur + (size_t)(y + l) * W + x - 16);
@@ -180,7 +182,7 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int by0, int nrow
                     int s = 0;
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
-                        const uint8_t* lr = left + (oy + r0 + 4 * h) * kIntraMaxSr;
+                        const uint8_t* lr = left + (oy + r0 + 4 * h) * SRM;
 #pragma unroll
                         for (int c = 0; c < 8; ++c) s += abs(scur[h][c] - canvas_at(lr, sr, xs + dx + c, x));
                     }
@@ -195,7 +197,7 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int by0, int nrow
             int sres[2][8];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const uint8_t* lr = left + (oy + r0 + 4 * h) * kIntraMaxSr;
+                const uint8_t* lr = left + (oy + r0 + 4 * h) * SRM;
 #pragma unroll
                 for (int c = 0; c < 8; ++c) sres[h][c] = scur[h][c] - canvas_at(lr, sr, xs + smv + c, x);
             }
@@ -504,6 +506,9 @@ int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int by
         hipLaunchKernelGGL((intra_tq_kernel<16, true>), grid, blk, 0, st, cur, H, W, by0, nrows, sr, qp_rd, qp_row, qp_map,
                            lam,
                            out_split, out_mv, out_qtc, out_tokens, out_mae, idres);
+    else if (bs == 16 && sr <= 16)
+        hipLaunchKernelGGL((intra_tq_kernel<16, false, 16>), grid, blk, 0, st, cur, H, W, by0, nrows, sr, qp_rd, qp_row,
+                           qp_map, lam, out_split, out_mv, out_qtc, out_tokens, out_mae, idres);
     else if (bs == 16)
         hipLaunchKernelGGL((intra_tq_kernel<16, false>), grid, blk, 0, st, cur, H, W, by0, nrows, sr, qp_rd, qp_row, qp_map,
                            lam,

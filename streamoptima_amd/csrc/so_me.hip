@@ -1608,7 +1608,7 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
         // the task counter and the done flags; never the timeout count (the caller's)
         hipError_t e = hipMemsetAsync(ws, 0, kRunTimeoutWord * sizeof(uint32_t), st);
         if (e == hipSuccess)
-            e = hipMemsetAsync(ws + kRunDoneBase, 0, (p_run_workspace_words(H, W) - kRunDoneBase) * sizeof(uint32_t), st);
+            e = hipMemsetAsync(ws + kRunDoneBase, 0, (size_t)ntiles * n * sizeof(uint32_t), st);   // the flags it uses
         if (e != hipSuccess) {
             set_error("p_run_kernel: hipMemsetAsync: %s", hipGetErrorString(e));
             return (int)e;

@@ -310,6 +310,18 @@ class Engine:
         return offs, out
 
     # ---- metrics ---------------------------------------------------------------------------
+    def sum_rows(self, rows: list, out: torch.Tensor | None = None) -> torch.Tensor:
+        """int64 [n]: the sum of each int32 tensor in `rows` (equal lengths), one launch."""
+        n = len(rows)
+        length = rows[0].numel() if n else 0
+        if any(r.numel() != length or r.dtype != torch.int32 or not r.is_contiguous() for r in rows):
+            raise ValueError("sum_rows: contiguous int32 tensors of one length")
+        out = torch.empty(n, dtype=torch.int64, device=self.device) if out is None else out
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[r.data_ptr() for r in rows])
+        rc = self.lib.so_sum_i32_rows(ptrs, n, length, out.data_ptr(), _lib.stream_handle(self.device))
+        _lib.check(rc, "so_sum_i32_rows")
+        return out
+
     def sse_into(self, a: torch.Tensor, b: torch.Tensor, acc: torch.Tensor) -> None:
         """acc (uint64 view of an int64 device scalar) += sum((a-b)^2)."""
         rc = self.lib.so_sse_u8(a.data_ptr(), b.data_ptr(), a.numel(), acc.data_ptr(),
