@@ -391,7 +391,7 @@ intra_recon_kernel(int H, int W, int by0, const uint8_t* __restrict__ split, con
 // the values already produced (sr <= 64, so x - src <= 64 + BS - 1 < 128 never aliases the
 // block being written).  nbx dependent steps of one LDS round trip each, instead of the
 // pointer-jumping kernel's log2(nbx) passes over the whole row with a barrier each.
-template <int BS, bool NEAR>
+template <int BS, bool NEAR, bool UNSPLIT = false>
 __global__ void __launch_bounds__(256)
 intra_recon_seq_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict__ split, const int16_t* __restrict__ mv,
                        const int32_t* __restrict__ idres, const uint8_t* __restrict__ cur,
@@ -411,7 +411,10 @@ intra_recon_seq_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict__
     uint8_t* orow = out_recon + (size_t)yy * W;
     // the residuals and motion vectors of the next CH blocks are loaded while the current
     // CH blocks walk the chain (their loads do not depend on it)
-    constexpr int CH = 8;
+#ifndef SO_IRS_CH   // blocks whose inputs are loaded one group ahead: the load latency is
+#define SO_IRS_CH 32   // hidden behind 32 chain steps (4K I-frame 102 -> 95 us vs 8, tools/intra_ab.py)
+#endif
+    constexpr int CH = SO_IRS_CH;
     int resn[CH], dxn[CH], curn[CH];
     auto fetch = [&](int bx0, int (&rs)[CH], int (&dv)[CH], int (&cv)[CH]) {
 #pragma unroll
