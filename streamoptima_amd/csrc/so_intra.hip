@@ -391,7 +391,7 @@ intra_recon_kernel(int H, int W, int by0, const uint8_t* __restrict__ split, con
 // the values already produced (sr <= 64, so x - src <= 64 + BS - 1 < 128 never aliases the
 // block being written).  nbx dependent steps of one LDS round trip each, instead of the
 // pointer-jumping kernel's log2(nbx) passes over the whole row with a barrier each.
-template <int BS, bool NEAR, bool UNSPLIT = false>
+template <int BS, bool NEAR>
 __global__ void __launch_bounds__(256)
 intra_recon_seq_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict__ split, const int16_t* __restrict__ mv,
                        const int32_t* __restrict__ idres, const uint8_t* __restrict__ cur,
