@@ -126,10 +126,12 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
  * window reads are done (device-scope flags in `workspace`; reconstructions are
  * stored write-through), so consecutive frames overlap on the device with no host
  * round trip.  curs / out_* are host arrays of nframes device pointers; out_sse may be
- * NULL.  workspace: caller-owned uint32 [so_p_run_workspace_elems(H, W)]; the call zeroes
- * its task counter and done flags (hipMemsetAsync on `stream`) but NOT word 32
- * (SO_P_RUN_TIMEOUT_WORD), the timeout count: the caller zeroes it once and reads it after
- * the run (or after a whole GOP of runs).
+ * NULL.  workspace: caller-owned uint32 [so_p_run_workspace_elems(H, W)], ZEROED ONCE by the
+ * caller before its first use and then only passed back: each launch leaves its counters
+ * at 0 and its epoch in the workspace (done flags are compared with the launch's epoch, so
+ * nothing is reset between launches).  One workspace serves one stream at a time.  Word 32
+ * (SO_P_RUN_TIMEOUT_WORD) is the timeout count: the caller reads it after the run (or after a
+ * whole GOP of runs) and clears it.
  * Nonzero means a dependency wait passed 50 ms and the run's symbols may be wrong; the
  * facade raises (Engine.check_run).  Consumers poll the flags and then take an agent-scope
  * acquire before reading the reference rows.

@@ -1350,10 +1350,12 @@ struct PRunArgs {
     PFrameOut out[kRunMax];
 };
 
-// Workspace words: [0] task counter, [32] timeout count, [64 + f * ntiles + t] = 1 once tile t
-// of frame f is done.  The launcher zeroes [0, 32) and the done flags before every launch;
-// [32] is the CALLER's: it accumulates over launches and calls until the caller reads and
-// clears it (Engine.check_run), so a timeout in any launch of a GOP is seen.
+// Workspace words: [0] task counter, [1] exit counter, [2] epoch of the last finished launch,
+// [32] timeout count, [64 + f * ntiles + t] = the launch's epoch once tile t of frame f is
+// done.  The caller zeroes the workspace once; a launch runs with epoch [2] + 1 and its last
+// workgroup resets [0], [1] and stores the epoch in [2], so no launch needs a memset.  [32] is
+// the CALLER's: it accumulates over launches and calls until the caller reads and clears it
+// (Engine.check_run), so a timeout in any launch of a GOP is seen.
 #ifndef SO_RUN_ACQUIRE
 #define SO_RUN_ACQUIRE 1
 #endif
@@ -1369,6 +1371,7 @@ struct PRunArgs {
 // the task counter (hammered by every workgroup's dequeue), the timeout count and the done
 // flags live on separate 128-byte lines
 constexpr int kRunTimeoutWord = SO_RUN_TIMEOUT_WORD, kRunDoneBase = SO_RUN_DONE_BASE;
+constexpr int kRunExitWord = 1, kRunEpochWord = 2;   // on the task counter's line: touched once per workgroup
 // A rank's stripe of a frame shared across GPUs (so_encode_p_run_stripe): block rows [by0, by1)
 // of every frame, the reconstruction planes in uncached memory addressed by "virtual" full-frame
 // bases (row y at base + y * W; the allocation holds rows [16 * by0 - 16, 16 * by1 + 32)), and
@@ -1425,6 +1428,11 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lane = tid & 63;
     const uint32_t one = lane == 0 ? 1u : 0u;
+    // this launch's epoch: ws[2] + 1 (ws[2] = the last finished launch's; written by that
+    // launch's last workgroup, so every workgroup here reads it before it can change).  Done
+    // flags hold the epoch of the launch that set them: nothing is zeroed between launches.
+    const uint32_t ep = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(&ws[kRunEpochWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
     for (;;) {
         if (wave == 0) {
             const uint32_t v = __hip_atomic_fetch_add(&ws[0], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1487,7 +1495,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 if ((STRIPE || FPIPE) && rneed)
                     v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == sp.epoch ? 1u : 0u;
                 else
-                    v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ep ? 1u : 0u;
                 if (__builtin_amdgcn_ballot_w64((need || rneed) && v == 0u) == 0) break;
                 __builtin_amdgcn_s_sleep(1);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
@@ -1517,7 +1525,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                                                           nullptr, nullptr, a.out[f], wait_ref, hl);
             // ptile_body ended with every wave's stores (local and remote) retired and a barrier
             if (wave == 0) {
-                __hip_atomic_fetch_add(done + (size_t)f * ntiles + tile, one, __ATOMIC_RELAXED,
+                __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                 if (lane == 0)
                     __hip_atomic_store(sp.peer_dn_flags + (size_t)slot * ntiles + tile, sp.epoch, __ATOMIC_RELAXED,
@@ -1538,7 +1546,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                                                           nullptr, nullptr, a.out[f], wait_ref, hl);
             // ptile_body ended with every wave's stores (local and remote) retired and a barrier
             if (wave == 0) {
-                __hip_atomic_fetch_add(done + (size_t)f * ntiles + tile, one, __ATOMIC_RELAXED,
+                __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                 if (lane == 0 && hl.up)
                     __hip_atomic_store(sp.peer_up_flags + (size_t)gf * tiles_x + tx, sp.epoch, __ATOMIC_RELAXED,
@@ -1552,7 +1560,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                                 wait_ref);
             // ptile_body ended with every wave's write-through stores retired and a barrier
             if (wave == 0)
-                __hip_atomic_fetch_add(done + (size_t)f * ntiles + tile, one, __ATOMIC_RELAXED,
+                __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
         }
 #ifdef SO_STAMPS
@@ -1565,6 +1573,16 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             rec[13] = __builtin_amdgcn_s_memtime();
         }
 #endif
+    }
+    // the last workgroup out resets the task and exit counters and publishes the epoch
+    if (wave == 0) {
+        const uint32_t o = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_fetch_add(&ws[kRunExitWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (o == gridDim.x - 1) {
+            __hip_atomic_store(&ws[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ws[kRunExitWord], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ws[kRunEpochWord], ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -1605,14 +1623,8 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
             a.cur[i] = curs[f0 + i];
             a.out[i] = outs[f0 + i];
         }
-        // the task counter and the done flags; never the timeout count (the caller's)
-        hipError_t e = hipMemsetAsync(ws, 0, kRunTimeoutWord * sizeof(uint32_t), st);
-        if (e == hipSuccess)
-            e = hipMemsetAsync(ws + kRunDoneBase, 0, (size_t)ntiles * n * sizeof(uint32_t), st);   // the flags it uses
-        if (e != hipSuccess) {
-            set_error("p_run_kernel: hipMemsetAsync: %s", hipGetErrorString(e));
-            return (int)e;
-        }
+        // nothing to reset: the kernel leaves the task / exit counters at 0 and done flags are
+        // compared with the launch's epoch (the caller zeroes the workspace once)
         // A frame with fewer tiles than resident slots (1080p: 510 tiles, 768 slots) gets
         // ceil(ntiles / ncu) workgroups per CU: every CU then runs its share of a frame's tiles
         // side by side, instead of some CUs running three (slower) while the next frame's tiles
