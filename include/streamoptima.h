@@ -404,6 +404,16 @@ int so_pack_frames(int nframes, const int32_t* frame_types, const uint8_t* const
                    uint32_t* const* offs, uint8_t* const* out, unsigned long long cap,
                    void* stream);
 
+/*
+ * The inverse (the decoder side of the packed stream): frame i's bytes packed[i] with the
+ * block offsets offs[i][0..nb] so_pack_frames wrote, back to split / mv / qtc in the canonical
+ * layout (mv entries past an unsplit block's first are 0).  frame_types: HOST array.
+ * Malformed input sets the device int32 *err to 1 + a bad block's index (zero it first).
+ */
+int so_unpack_frames(int nframes, const int32_t* frame_types, const uint8_t* const* packed,
+                     const uint32_t* const* offs, int nb, int block_size, uint8_t* const* split,
+                     int16_t* const* mv, int16_t* const* qtc, int32_t* err, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

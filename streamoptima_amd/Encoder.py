@@ -481,6 +481,17 @@ class Y_Video_codec(BlockAPI):
     def get_encoded_package(self):
         return self.encoded_package
 
+    def transmit_packed(self, path: str) -> int:
+        """The encoded GOP as one binary file of packed symbols (packedfile.py: varint split /
+        MVs / RLE token lists packed on the GPU by so_pack_frames, ~2.4x smaller than the
+        int16 QTC and far smaller than the text lines).  decoder.decode_packed_file reads it.
+        Returns the file size in bytes."""
+        if not self.encoded_package_f or self._symbols is None:
+            print("[ERROR] No encoded package available, please run encode() first")
+            return 0
+        from . import packedfile
+        return packedfile.write(path, self.engine(), self._symbols, self.encoded_package["Qp_per_row_per_frame"])
+
     def transmit_bitstream(self, intra_dur=None, block_size=None, mv_file=None, residual_file=None,
                            qp_map_file=None):
         """Encoder.py:1544-1573, writing the differential MV/QP lines and the RLE residual

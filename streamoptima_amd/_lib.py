@@ -61,6 +61,7 @@ _SIGS = {
     "so_memset_d8": ([_vp, _i, _sz, _vp], _i),
     "so_pack_bound": ([_i, _i], _sz),
     "so_sum_i32_rows": ([_vp, _i, _i, _vp, _vp], _i),
+    "so_unpack_frames": ([_i, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp], _i),
     "so_encode_p_run_fpipe": ([_vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                _vp, _vp, _i, _vp, _vp, _i, ctypes.c_longlong, ctypes.c_uint32, _i, _vp], _i),
     "so_frame_push": ([_vp, _i, _i, _vp, _vp, ctypes.c_uint32, _vp], _i),

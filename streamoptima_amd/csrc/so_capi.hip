@@ -75,6 +75,15 @@ struct PackFrame {
     int frame_type;
 };
 size_t pack_block_bound(int bs);
+struct UnpackFrame {
+    const uint8_t* in;
+    const uint32_t* offs;
+    uint8_t* split;
+    int16_t* mv;
+    int16_t* qtc;
+    int frame_type;
+};
+int unpack_frames_launch(const UnpackFrame* frames, int nframes, int nb, int bs, int32_t* err, hipStream_t st);
 int pack_frames_launch(const PackFrame* frames, int nframes, int nb, int bs, unsigned long long cap, hipStream_t st);
 int stripe_halo_push_launch(const uint8_t* plane, int W, int by0, int by1, uint8_t* up, uint8_t* dn,
                             uint32_t* up_flags, uint32_t* dn_flags, int gf, uint32_t epoch, hipStream_t st);
@@ -935,6 +944,33 @@ int so_pack_frames(int nframes, const int32_t* frame_types, const uint8_t* const
         fr[i] = PackFrame{split[i], mv[i], qtc[i], offs[i], out[i], frame_types[i]};
     }
     return pack_frames_launch(fr.data(), nframes, nb, bs, cap, (hipStream_t)stream);
+}
+
+int so_unpack_frames(int nframes, const int32_t* frame_types, const uint8_t* const* packed, const uint32_t* const* offs,
+                     int nb, int bs, uint8_t* const* split, int16_t* const* mv, int16_t* const* qtc, int32_t* err,
+                     void* stream) {
+    const char* fn = "so_unpack_frames";
+    if (bs != 16 && bs != 8) {
+        set_error("%s: block_size %d not built", fn, bs);
+        return SO_E_UNSUPPORTED;
+    }
+    if (nb <= 0 || nframes < 0) {
+        set_error("%s: nb %d / nframes %d", fn, nb, nframes);
+        return SO_E_INVALID;
+    }
+    if (nframes == 0) return SO_OK;
+    SO_NEED(frame_types, fn); SO_NEED(packed, fn); SO_NEED(offs, fn); SO_NEED(split, fn); SO_NEED(mv, fn);
+    SO_NEED(qtc, fn); SO_NEED(err, fn);
+    std::vector<UnpackFrame> fr((size_t)nframes);
+    for (int i = 0; i < nframes; ++i) {
+        SO_NEED(packed[i], fn); SO_NEED(offs[i], fn); SO_NEED(split[i], fn); SO_NEED(mv[i], fn); SO_NEED(qtc[i], fn);
+        if (frame_types[i] != 0 && frame_types[i] != 1) {
+            set_error("%s: frame_types[%d] = %d", fn, i, frame_types[i]);
+            return SO_E_INVALID;
+        }
+        fr[i] = UnpackFrame{packed[i], offs[i], split[i], mv[i], qtc[i], frame_types[i]};
+    }
+    return unpack_frames_launch(fr.data(), nframes, nb, bs, err, (hipStream_t)stream);
 }
 
 }  // extern "C"

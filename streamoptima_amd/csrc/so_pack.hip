@@ -268,6 +268,96 @@ __global__ void __launch_bounds__(1024) pack_scan_kernel(const PackArgs a, int n
     if (t == 1023) offs[nb] = part[1023];
 }
 
+// ---- unpack (so_unpack_frames): the packed stream back to split / mv / qtc ----------------
+// One thread per block parses its bytes [offs[b], offs[b+1]) sequentially: the header, then
+// each (sub-)block's tokens -- "-L" and L values, "Z" zeros, "0" the trailing zeros -- into
+// the zeroed block in scan order.  Malformed input (a varint or token list running past the
+// block's bytes, bytes left over, a run past n*n) sets *err = 1 + that block's index.
+struct UnpackFrame {
+    const uint8_t* in;
+    const uint32_t* offs;
+    uint8_t* split;
+    int16_t* mv;
+    int16_t* qtc;
+    int frame_type;
+};
+struct UnpackArgs {
+    UnpackFrame f[kPackMax];
+};
+
+template <int BS>
+__global__ void __launch_bounds__(256) unpack_block_kernel(const UnpackArgs a, int nb, int32_t* __restrict__ err) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= nb) return;
+    const UnpackFrame& f = a.f[blockIdx.y];
+    const uint8_t* p = f.in + f.offs[b];
+    const uint8_t* const end = f.in + f.offs[b + 1];
+    bool bad = f.offs[b + 1] < f.offs[b];
+    auto next = [&]() -> int {
+        uint32_t z = 0;
+        for (int sh = 0; sh < 35; sh += 7) {
+            if (p >= end) break;
+            const uint32_t c = *p++;
+            z |= (c & 0x7Fu) << sh;
+            if (!(c & 0x80u)) return (int)(z >> 1) ^ -(int)(z & 1u);
+        }
+        bad = true;
+        return 0;
+    };
+    constexpr int NN = BS * BS;
+    int16_t* q = f.qtc + (size_t)b * NN;
+#pragma unroll
+    for (int i = 0; i < NN / 8; ++i) reinterpret_cast<uint4*>(q)[i] = make_uint4(0, 0, 0, 0);
+    const int sp = bad ? 0 : next();
+    if (sp != 0 && (sp != 1 || BS != 16)) bad = true;
+    f.split[b] = (uint8_t)(sp == 1 && !bad);
+    const int inter = f.frame_type == 1, nmv = (sp == 1) ? 4 : 1;
+    if (inter) {
+        int16_t* m = f.mv + (size_t)b * 12;
+        for (int j = 0; j < 12; ++j) m[j] = (int16_t)(j < 3 * nmv && !bad ? next() : 0);
+    } else {
+        int16_t* m = f.mv + (size_t)b * 4;
+        for (int j = 0; j < 4; ++j) m[j] = (int16_t)(j < nmv && !bad ? next() : 0);
+    }
+    const int nsub = sp == 1 ? 4 : 1, n = sp == 1 ? 8 : BS, nn = n * n;
+    const uint8_t* scan = n == 16 ? c_scan16 : c_scan8;
+    for (int j = 0; j < nsub && !bad; ++j) {
+        int16_t* qs = q + j * nn;
+        int k = 0;
+        while (k < nn && !bad) {
+            const int t = next();
+            if (t < 0) {
+                if (-t > nn - k) { bad = true; break; }
+                for (int i = 0; i < -t && !bad; ++i) qs[scan[k + i]] = (int16_t)next();
+                k -= t;
+            } else if (t == 0) {
+                break;
+            } else {
+                if (t > nn - k) { bad = true; break; }
+                k += t;
+            }
+        }
+    }
+    if (p != end) bad = true;
+    if (bad) __hip_atomic_store(err, b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+int unpack_frames_launch(const UnpackFrame* frames, int nframes, int nb, int bs, int32_t* err, hipStream_t st) {
+    const int trc = init_scan_tables();
+    if (trc != SO_OK) return trc;
+    for (int f0 = 0; f0 < nframes; f0 += kPackMax) {
+        const int n = nframes - f0 < kPackMax ? nframes - f0 : kPackMax;
+        UnpackArgs a{};
+        for (int i = 0; i < n; ++i) a.f[i] = frames[f0 + i];
+        const dim3 grid((nb + 255) / 256, n);
+        if (bs == 16) hipLaunchKernelGGL(unpack_block_kernel<16>, grid, dim3(256), 0, st, a, nb, err);
+        else hipLaunchKernelGGL(unpack_block_kernel<8>, grid, dim3(256), 0, st, a, nb, err);
+        const int rc = check_launch("unpack_block_kernel");
+        if (rc != SO_OK) return rc;
+    }
+    return SO_OK;
+}
+
 int pack_frames_launch(const PackFrame* frames, int nframes, int nb, int bs, unsigned long long cap, hipStream_t st) {
     const int trc = init_scan_tables();
     if (trc != SO_OK) return trc;

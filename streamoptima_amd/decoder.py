@@ -172,6 +172,25 @@ class decoder:
         return self.decode(ft, res, qps, mvs, intra_mode, intra_dur, bs, frames, width, height, save_decoded_frames,
                            qp_maps=maps)
 
+    def decode_packed_file(self, path: str, save_decoded_frames=True):
+        """Encoder.transmit_packed's file: the packed streams go to the GPU, so_unpack_frames
+        restores split / mv / qtc of every block in parallel, and the frames are rebuilt by the
+        same kernels as decode()."""
+        from . import packedfile
+        eng = self._eng()
+        meta = packedfile.read(path, eng.device)
+        if (meta["h"], meta["w"], meta["bs"], meta["nb"]) != (eng.h, eng.w, eng.bs, eng.nb):
+            raise ValueError(f"{path}: {meta['w']}x{meta['h']} bs {meta['bs']} does not match this decoder")
+        syms = eng.unpack_symbols(meta["frame_types"], meta["packed"], meta["offs"])
+        for s, q in zip(syms, meta["qp_rows"]):
+            s.qp_row = q or None
+        decoded = self.decode_symbols(syms, eng)
+        host = [d.cpu().numpy()[: self.h_pixels, : self.w_pixels] for d in decoded]
+        if save_decoded_frames:
+            self.decoded_vid_f = True
+            self.decoded_vid = host
+        return host
+
     def save_decoded_frames(self, filename="yuv/decoded_bitstream_frames.yuv"):
         if not self.decoded_vid_f:
             print("[ERROR] No decoded frames available.")

@@ -309,6 +309,26 @@ class Engine:
         _lib.check(rc, "so_pack_frames")
         return offs, out
 
+    def unpack_symbols(self, frame_types: list, packed: list, offs: list) -> list:
+        """so_unpack_frames: packed streams (device uint8) + their block offsets (device int32
+        [nb + 1], as pack_symbols wrote them) -> FrameSymbols with split / mv / qtc (no recon,
+        tokens or metrics).  Raises ValueError on a malformed stream (synchronises once)."""
+        n = len(packed)
+        syms = [self.new_symbols(int(t)) for t in frame_types]
+        err = torch.zeros(1, dtype=torch.int32, device=self.device)
+
+        def arr(ts):
+            return (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
+        types = (ctypes.c_int32 * n)(*[int(t) for t in frame_types])
+        rc = self.lib.so_unpack_frames(n, types, arr(packed), arr(offs), self.nb, self.bs, arr([s.split for s in syms]),
+                                       arr([s.mv for s in syms]), arr([s.qtc for s in syms]), err.data_ptr(),
+                                       _lib.stream_handle(self.device))
+        _lib.check(rc, "so_unpack_frames")
+        bad = int(err.item())
+        if bad:
+            raise ValueError(f"so_unpack_frames: malformed packed stream at block {bad - 1}")
+        return syms
+
     # ---- metrics ---------------------------------------------------------------------------
     def sum_rows(self, rows: list, out: torch.Tensor | None = None) -> torch.Tensor:
         """int64 [n]: the sum of each int32 tensor in `rows` (equal lengths), one launch."""

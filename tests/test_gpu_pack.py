@@ -140,3 +140,69 @@ def test_host_stream_back_to_back_gops(gpu):
         seen.append(k)
     hs.encode_stream(hosts, frames, consume)
     assert seen == [0, 1, 2]
+
+
+def test_unpack_round_trip_and_decode(gpu):
+    """so_unpack_frames inverts so_pack_frames (CIF with VBS splits, I and P frames), and the
+    decoder's GPU reconstruction from the unpacked symbols equals the encoder's."""
+    c, syms = _encode(gpu, 288, 352, 4, 2, True)
+    eng = c.engine()
+    offs, out = eng.pack_symbols(syms)
+    un = eng.unpack_symbols([s.frame_type for s in syms], list(out), list(offs))
+    for i, (s, u) in enumerate(zip(syms, un)):
+        h = _host(s)
+        assert torch.equal(u.split.cpu(), s.split.cpu()), i
+        assert torch.equal(u.qtc.cpu(), s.qtc.cpu()), i
+        mv_u, mv_s = u.mv.cpu().numpy(), h["mv"]
+        for b in range(eng.nb):
+            k = 4 if h["split"][b] else 1
+            assert (mv_u[b, :k] == mv_s[b, :k]).all(), (i, b)
+        if s.frame_type == 0:
+            rec = eng.recon_intra(u.split, u.mv, u.qtc, 4)
+        else:
+            rec = eng.recon_inter([syms[i - 1].recon], u.split, u.mv, u.qtc, 4)
+        torch.cuda.synchronize()
+        assert torch.equal(rec[:288, :352].cpu(), s.recon[:288, :352].cpu()), i
+
+
+def test_unpack_rejects_malformed(gpu):
+    c, syms = _encode(gpu, 288, 352, 2, 2, False)
+    eng = c.engine()
+    offs, out = eng.pack_symbols(syms[1:])
+    bad = offs.clone()
+    bad[0, 5] += 1                         # block 4 loses its last byte, block 5 gains one
+    with pytest.raises(ValueError):
+        eng.unpack_symbols([1], [out[0]], [bad[0]])
+    junk = out.clone()
+    junk[0, :16] = 0x80                    # varints that never end
+    with pytest.raises(ValueError):
+        eng.unpack_symbols([1], [junk[0]], [offs[0]])
+
+
+@pytest.mark.parametrize("rc", [None, 1])
+def test_transmit_packed_then_decode(gpu, tmp_path, monkeypatch, rc):
+    """encode() -> transmit_packed (packedfile.py) -> decode_packed_file reproduces the
+    encoder's reconstruction (VBS on, RC per-row QPs carried in the container), and the
+    file is smaller than the text bitstream."""
+    import json
+    import os
+    from conftest import GOLDEN
+    from streamoptima_amd.Encoder import Y_Video_codec
+    from streamoptima_amd.decoder import decoder
+    from streamoptima_amd.synth import synth_sequence
+    monkeypatch.chdir(tmp_path)
+    seq = synth_sequence(5, 96, 128, seed=23)
+    kw = {}
+    if rc:
+        tables = json.load(open(os.path.join(GOLDEN, "rc_schedule.json")))["tables"]
+        kw = dict(RCFlag=rc, targetBR="2 mbps", qp_rate_tables=tables)
+    enc = Y_Video_codec(96, 128, 5, 16, 16, 4, 3, 0, 0.015, True, y_only_frame_arr=seq, device=gpu, **kw)
+    enc.encode()
+    size = enc.transmit_packed(str(tmp_path / "gop.sopk"))
+    enc.transmit_bitstream(mv_file=str(tmp_path / "mv.txt"), residual_file=str(tmp_path / "res.txt"))
+    text = os.path.getsize(tmp_path / "mv.txt") + os.path.getsize(tmp_path / "res.txt")
+    assert 0 < size == os.path.getsize(tmp_path / "gop.sopk") < text
+    dec = decoder(0, 3, 16, 5, 96, 128, 4, 1, False, 0.015, True, device=gpu, **kw)
+    out = dec.decode_packed_file(str(tmp_path / "gop.sopk"))
+    for i in range(5):
+        assert (out[i] == enc._symbols[i].recon.cpu().numpy()).all(), i

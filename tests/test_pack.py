@@ -61,3 +61,45 @@ def test_pack_bound_covers_worst_case():
         worst = len(pack_frame(split, mv, dense[None], bs, 1))
         assert worst <= lib.so_pack_bound(1, bs)
     assert lib.so_pack_bound(0, 16) == 0 and lib.so_pack_bound(10, 12) == 0
+
+
+def test_packed_container_read(tmp_path):
+    """packedfile.read on a container written by hand from the plain-Python packer: block
+    offsets from the u16 lengths, per-row QPs, and the checks on malformed files."""
+    import struct
+
+    import torch
+    from streamoptima_amd import packedfile
+    rng = np.random.default_rng(9)
+    nb, bs = 12, 16
+    frames = []
+    for ft in (0, 1):
+        split, mv, qtc = random_symbols(rng, nb, bs, ft, vbs=True)
+        blocks = [pack_frame(split[b:b + 1], mv[b:b + 1], qtc[b:b + 1], bs, ft) for b in range(nb)]
+        frames.append((ft, blocks, split, qtc))
+    path = tmp_path / "x.sopk"
+
+    def write(extra=b"", fudge=0):
+        with open(path, "wb") as f:
+            f.write(b"SOPK" + struct.pack("<6I", 1, 64, 48, bs, len(frames), nb))
+            for ft, blocks, _, _ in frames:
+                q = [3, 4, 5, 6] if ft == 1 else []
+                body = b"".join(blocks)
+                lens = np.array([len(x) for x in blocks], np.uint16)
+                f.write(struct.pack("<BH", ft, len(q)) + np.array(q, np.int8).tobytes()
+                        + struct.pack("<I", len(body) + fudge) + lens.tobytes() + body)
+            f.write(extra)
+    write()
+    m = packedfile.read(str(path), torch.device("cpu"))
+    assert (m["h"], m["w"], m["bs"], m["nb"], m["frame_types"]) == (64, 48, bs, nb, [0, 1])
+    assert m["qp_rows"] == [[], [3, 4, 5, 6]]
+    for (ft, blocks, split, qtc), pk, off in zip(frames, m["packed"], m["offs"]):
+        assert off.tolist() == np.concatenate(([0], np.cumsum([len(x) for x in blocks]))).tolist()
+        got = bitstream.unpack_frame(pk.numpy(), nb, bs, ft)
+        assert np.array_equal(got["split"], split) and np.array_equal(got["qtc"], qtc)
+    write(extra=b"\x00")
+    with pytest.raises(ValueError):
+        packedfile.read(str(path), torch.device("cpu"))
+    write(fudge=1)
+    with pytest.raises(ValueError):
+        packedfile.read(str(path), torch.device("cpu"))
