@@ -268,7 +268,7 @@ def pmc_record(config: str):
     except (ValueError, OSError):
         return {}
     for k, v in ks.items():
-        if k.startswith("so::p_run_kernel<8"):      # p_run_kernel<8, 0> (one GPU, full frame)
+        if k.startswith("so::p_run_kernel<8"):      # p_run_kernel<8, 0, 128> (one GPU, full frame)
             return v
     return {}
 
@@ -294,7 +294,7 @@ def roofline_of(rl: dict, config: str) -> dict:
                 "kernel_cycles": round(cyc), "effective_clock_ghz": round(cyc / launch_s / 1e9, 3),
                 "source": "profiles/pmc_me_traffic.json (rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES "
                           "GRBM_GUI_ACTIVE ..., tools/gpu_traffic.sh)"}
-    return {"bound": "hbm", "kernel": "p_run_kernel<8, 0>", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
+    return {"bound": "hbm", "kernel": "p_run_kernel<8, 0, 128>", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
             "traffic_note": "HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE x 2, the "
                             "factor measured for 4-B and 16-B coalesced reads (tools/ubench_fetch.cpp)",
