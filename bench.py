@@ -559,12 +559,21 @@ def p2p_encoder(eng, frames, cfg, senc, world, max_wg=0):
     if int(flag.item()) == 0:
         return None, "all_gather (RCCL) per frame; p2p hand-off unavailable" + (f" ({why})" if why else "")
     k = min(4, cfg["frames"])
-    a = penc.encode(frames[:k], cfg["intra_dur"], cfg["qp"])
+    ok, why = 1, ""
+    try:                      # this rank's launches only (see fpipe_encoder)
+        a_syms = penc.r.encode(frames[:k], cfg["intra_dur"], cfg["qp"])
+        torch.cuda.synchronize()
+    except Exception as e:   # noqa: BLE001
+        ok, why = 0, f"self-check run: {e}"
+    flag = torch.tensor([ok], dtype=torch.int32, device=eng.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 0:
+        return None, "all_gather (RCCL) per frame; p2p self-check run failed" + (f" ({why})" if why else "")
     b = senc.encode(frames[:k], cfg["intra_dur"], cfg["qp"])
     torch.cuda.synchronize()
     good = not penc.r.timed_out()
     for i in range(k):
-        ga, gb = penc.gather_symbols(a["symbols"][i], i), senc.gather_symbols(b["symbols"][i])
+        ga, gb = penc.gather_symbols(a_syms[i], i), senc.gather_symbols(b["symbols"][i])
         da = frame_digest(ga["frame_type"], {n: (v.cpu().numpy() if torch.is_tensor(v) else v) for n, v in ga.items()})
         db = frame_digest(gb["frame_type"], {n: (v.cpu().numpy() if torch.is_tensor(v) else v) for n, v in gb.items()})
         good = good and da == db
@@ -596,10 +605,18 @@ def fpipe_encoder(codec, frames, cfg, world, max_wg=0):
     if int(flag.item()) == 0:
         return None, why or "unavailable on another rank"
     k = min(2 * world + 1, cfg["frames"])
-    a = penc.encode(frames[:k], k, cfg["qp"])
-    torch.cuda.synchronize()
-    got = penc.digests(a["symbols"], k)
-    ref = [symbols_digest(s) for s in codec.encode_device(frames[:k], k)["symbols"]]
+    ok, why = 1, ""
+    try:                      # this rank's launches only: a failure here must not strand the
+        a = penc.encode_local(frames[:k], k, cfg["qp"])     # other ranks in a collective
+        torch.cuda.synchronize()
+        ref = [symbols_digest(s) for s in codec.encode_device(frames[:k], k)["symbols"]]
+    except Exception as e:   # noqa: BLE001
+        ok, why = 0, f"self-check run: {e}"
+    flag = torch.tensor([ok], dtype=torch.int32, device=eng.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 0:
+        return None, why or "self-check run failed on another rank"
+    got = penc.digests(a, k)
     good = not penc.r.timed_out() and got == ref
     flag = torch.tensor([1 if good else 0], dtype=torch.int32, device=eng.device)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)

@@ -453,9 +453,14 @@ class FramePipelineGOPEncoder:
         self.r.connect(self.r.open(alls[(self.rank + 1) % self.world]))
         dist.barrier(group=group)
 
-    def encode(self, frames, intra_dur: int, qp: int) -> dict:
+    def encode_local(self, frames, intra_dur: int, qp: int) -> dict:
+        """This rank's launches only (no collective): {frame index: FrameSymbols}."""
+        return self.r.encode(frames, intra_dur, qp)
+
+    def encode(self, frames, intra_dur: int, qp: int, syms: dict | None = None) -> dict:
+        """encode_local (unless its result is passed in) + one all_reduce of the per-frame SSE."""
         import torch.distributed as dist
-        syms = self.r.encode(frames, intra_dur, qp)
+        syms = self.r.encode(frames, intra_dur, qp) if syms is None else syms
         nf = frames.shape[0]
         sse = torch.zeros(nf, dtype=torch.int64, device=self.eng.device)
         for k, s in syms.items():
