@@ -712,8 +712,8 @@ def main(argv=None):
             mode_note = f"frame pipeline x{world} (rank g encodes frames g, g+N, ...; {{}})"
             exchange_note = fpipe_note
 
-            def step():
-                return fenc.encode(frames, cfg["intra_dur"], cfg["qp"])
+            def step():      # the SSE all_reduce runs once, after timing (pipeline.py encode)
+                return fenc.encode(frames, cfg["intra_dur"], cfg["qp"], reduce=False)
         else:
             if args.exchange == "p2p" and plain:
                 penc, exchange_note = p2p_encoder(eng, frames, cfg, senc, world, max_wg=cap)
@@ -769,6 +769,7 @@ def main(argv=None):
     if parity_ok and not args.cpu_plumbing:
         if fenc is not None:
             fenc.check()
+            res["sse"] = fenc.sse(res["symbols"], f)
             got = fenc.digests(res["symbols"], f)
             if rank == 0:
                 fx = load_fixture(name)

@@ -457,16 +457,28 @@ class FramePipelineGOPEncoder:
         """This rank's launches only (no collective): {frame index: FrameSymbols}."""
         return self.r.encode(frames, intra_dur, qp)
 
-    def encode(self, frames, intra_dur: int, qp: int, syms: dict | None = None) -> dict:
-        """encode_local (unless its result is passed in) + one all_reduce of the per-frame SSE."""
-        import torch.distributed as dist
+    def encode(self, frames, intra_dur: int, qp: int, syms: dict | None = None, reduce: bool = True) -> dict:
+        """encode_local (unless its result is passed in) + one all_reduce of the per-frame SSE.
+
+        reduce=False leaves "sse" None (sse() computes it later): no collective then joins
+        the ranks between GOPs, so rank 0's next I-frame and the next GOP's first frames run
+        while the other ranks finish this GOP's last frames -- the pipeline fill is paid once
+        per stream, not once per GOP.  GOP k+1 may start on a rank as soon as its own GOP k
+        launch is done: every landing slot it overwrites was last read by a frame that its
+        own GOP k frames depend on."""
         syms = self.r.encode(frames, intra_dur, qp) if syms is None else syms
         nf = frames.shape[0]
-        sse = torch.zeros(nf, dtype=torch.int64, device=self.eng.device)
+        return {"symbols": syms, "sse": self.sse(syms, nf) if reduce else None,
+                "frame_type": [0 if k == 0 else 1 for k in range(nf)]}
+
+    def sse(self, syms: dict, nframes: int) -> torch.Tensor:
+        """The GOP's per-frame SSE on every rank (one all_reduce)."""
+        import torch.distributed as dist
+        sse = torch.zeros(nframes, dtype=torch.int64, device=self.eng.device)
         for k, s in syms.items():
             sse[k] = s.sse.sum(dtype=torch.int64)
         dist.all_reduce(sse, group=self.group)
-        return {"symbols": syms, "sse": sse, "frame_type": [0 if k == 0 else 1 for k in range(nf)]}
+        return sse
 
     def check(self) -> None:
         self.r.check()

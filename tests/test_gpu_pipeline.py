@@ -174,6 +174,56 @@ def test_frame_pipeline_in_process_matches_one_gpu(gpu, name, world, nframes):
         r.close()
 
 
+def test_frame_pipeline_back_to_back_gops(gpu):
+    """GOPs enqueued back to back with no synchronisation between them (bench.py's timed
+    loop, FramePipelineGOPEncoder.encode(reduce=False)): a rank starts GOP k+1 while the
+    other rank still encodes GOP k, overwriting landing slots under the next epoch.  Every
+    GOP must still match its one-GPU encode: A (the fixture), then B (A's frames in reverse,
+    against Y_Video_codec.encode_device), then A again."""
+    from streamoptima_amd.digest import symbols_digest
+    from streamoptima_amd.Encoder import Y_Video_codec
+    from streamoptima_amd.engine import Engine
+    from streamoptima_amd.pipeline import FramePipeRank
+    name, world, nframes = "1080p", 2, 10
+    cfg, fa = _frames(name, gpu, nframes)
+    fb = fa.flip(0).contiguous()
+    h, w = fa.shape[1:]
+    codec = Y_Video_codec(h, w, nframes, 16, 16, cfg["qp"], nframes, 0, 0.015, False, device=gpu)
+    exp_b = [symbols_digest(s) for s in codec.encode_device(fb, nframes)["symbols"]]
+    exp_a = FIX[name]["frame_sha256"][:nframes]
+    engines = [Engine(h, w, 16, 16, False, 0.015, gpu) for _ in range(world)]
+    streams = _streams(gpu)[:world]
+    ranks = [FramePipeRank(engines[r], world, r, nframes, stream=streams[r], max_wg=768 // (2 * world))
+             for r in range(world)]
+    torch.cuda.synchronize()
+    for r in range(world):
+        ranks[r].connect(ranks[(r + 1) % world].info())
+    saved = []
+    for fr in (fa, fb, fa):
+        syms = {}
+        for r in range(world):
+            with torch.cuda.stream(streams[r]):
+                syms.update(ranks[r].encode(fr, nframes, cfg["qp"]))
+                # keep this GOP's symbols: the next encode() reuses the rank's buffers
+                saved_r = {k: {f: getattr(s, f).clone() for f in ("split", "mv", "qtc", "tokens", "mae_num", "recon")}
+                           for k, s in syms.items() if k % world == r}
+                saved.append(saved_r)
+    torch.cuda.synchronize()
+    for r in ranks:
+        r.check()
+    import types
+    for g, exp in enumerate((exp_a, exp_b, exp_a)):
+        merged = {}
+        for d in saved[g * world:(g + 1) * world]:
+            merged.update(d)
+        got = [symbols_digest(types.SimpleNamespace(frame_type=0 if k == 0 else 1, extra=None, **merged[k]))
+               for k in range(nframes)]
+        bad = [i for i, (a, b) in enumerate(zip(got, exp)) if a != b]
+        assert not bad, f"GOP {g}: frames {bad[:10]} differ from the one-GPU encode"
+    for r in ranks:
+        r.close()
+
+
 def _fpipe_worker(rank, world, port, name, nframes, outdir):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
