@@ -79,6 +79,8 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-records", action="store_true", help="skip the 1080p record at N=1")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--gops-in-flight", type=lambda v: [int(x) for x in v.split(",") if x], default=[2],
+                    help="N=1 records of a GOP stream: k GOPs per step with interleaved P-runs (comma list; '' = none)")
     ap.add_argument("--no-pcie", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=20)
     ap.add_argument("--exchange", choices=("p2p", "allgather"), default="p2p",
@@ -540,6 +542,44 @@ def record_1080p(args, dev) -> dict:
     return rec
 
 
+def record_gops_in_flight(name: str, ngops: int, args, dev) -> dict:
+    """Throughput of a STREAM of GOPs: `ngops` independent GOPs of the workload per step
+    (copies of its frames in separate buffers), their P-runs interleaved in one persistent
+    launch (Y_Video_codec.encode_gops_device), so a frame of every GOP is in flight at once.
+    One GOP's frame-to-frame dependency leaves CUs idle where a frame has fewer tiles than
+    resident workgroups (1080p: 510 tiles, 768 slots); the other GOPs fill them.  Every GOP
+    of the timed output is checked against the oracle fixture."""
+    from streamoptima_amd.engine import alloc_planes
+    from streamoptima_amd.workloads import WORKLOADS
+    cfg = dict(WORKLOADS[name])
+    codec = build_codec(cfg, args, dev)
+    eng = codec.engine()
+    src = make_frames(cfg, dev, cfg["seed"])
+    gops = [src]
+    for _ in range(ngops - 1):
+        g = alloc_planes(*src.shape, dev)
+        g.copy_(src)
+        gops.append(g)
+    f = cfg["frames"]
+    pre = [[eng.new_symbols(0 if i % cfg["intra_dur"] == 0 else 1) for i in range(f)] for _ in gops]
+
+    def step():
+        return codec.encode_gops_device(gops, cfg["intra_dur"], symbols=pre, check=False)
+    elapsed, res = time_steps(step, 1, args.steps, args.warmup, dev)
+    eng.check_run()
+    mpx = args.steps * ngops * f * cfg["h"] * cfg["w"] / elapsed / 1e6
+    rec = {"workload": f"{ngops} independent copies of {cfg['workload']} per step, P-runs interleaved in one "
+                       "persistent launch (GOP-parallel stream encode)",
+           "value": round(mpx, 2), "unit": "Mpx/s", "gops_per_step": ngops,
+           "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+           "ms_per_gop": round(elapsed / args.steps / ngops * 1e3, 3)}
+    if not args.no_parity:
+        per = [parity_of(r["symbols"], name, cfg) for r in res]
+        rec["parity"] = {"bit_exact": all(p and p.get("bit_exact") for p in per),
+                         "gops_checked": len(per), "fixture": per[0].get("fixture") if per[0] else None}
+    return rec
+
+
 # ---- multi-GPU hand-off -------------------------------------------------------------------------
 def p2p_encoder(eng, frames, cfg, senc, world, max_wg=0):
     """The in-launch stripe hand-off (streamoptima_amd/pipeline.py), self-checked before
@@ -806,6 +846,9 @@ def main(argv=None):
     if rank == 0 and world == 1 and not args.cpu_plumbing and not args.no_records and name == "4k" \
             and args.me == "full" and not args.vbs:
         records = {"1080p": record_1080p(args, dev)}
+        for k in args.gops_in_flight:
+            for nm in ("1080p", "4k"):
+                records[f"{nm}_x{k}gop"] = record_gops_in_flight(nm, k, args, dev)
     pcie = None
     if rank == 0 and world == 1 and not args.cpu_plumbing and not args.no_pcie and args.me == "full":
         pcie = pcie_inclusive(codec, cfg, frames)

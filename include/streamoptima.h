@@ -145,6 +145,26 @@ int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0
                     uint32_t* workspace, void* stream);
 
 /*
+ * Several independent runs of P-frames in ONE persistent launch (the P-frames of several
+ * GOPs, or of the runs between a GOP's I-frames): frame i predicts from out_recon[j] when
+ * ref_frame[i] = j (j < i, a frame of this list: its tiles are waited for inside the launch
+ * as in so_encode_p_run) and from refs[i] when ref_frame[i] = -1 (a plane complete before
+ * the call, e.g. an I-frame's reconstruction).  Frames are taken in list order, so
+ * interleaving the runs (A1 B1 A2 B2 ...) keeps the tiles of one frame of every run in flight
+ * at once: where one frame has fewer tiles than the GPU's resident workgroups (1080p), the
+ * runs fill the GPU that one run's frame-to-frame dependency leaves idle.  Each run's
+ * output is identical to so_encode_p_run of that run alone (the reference's loop,
+ * Encoder.py:1839-1867, per GOP).  refs: host array of nframes device pointers (entries with
+ * ref_frame >= 0 are ignored); ref_frame: host int32[nframes]; the rest as so_encode_p_run.
+ */
+int so_encode_p_runs(const uint8_t* const* curs, int nframes, const uint8_t* const* refs,
+                     const int32_t* ref_frame, int H, int W, int bs, int sr, int qp_rd,
+                     const int32_t* qp_row, uint8_t* const* out_split, int16_t* const* out_mv,
+                     int16_t* const* out_qtc, int32_t* const* out_tokens, int32_t* const* out_mae_num,
+                     uint8_t* const* out_recon, int32_t* const* out_sse, uint32_t* workspace,
+                     void* stream);
+
+/*
  * ONE GOP across the GPUs of a node (BASELINE configs[3]): rank r encodes the block rows
  * [by0, by1) of every P-frame of a run with the persistent kernel of so_encode_p_run, and the
  * stripes hand their boundary rows to each other inside the launch -- the reference's frame

@@ -465,6 +465,52 @@ class Y_Video_codec(BlockAPI):
             eng.check_run()
         return {"symbols": out_syms, "sse": sse, "frame_type": ftypes, "qp_rows": qp_rows}
 
+    def encode_gops_device(self, gops: list, intra_dur: int, symbols=None, check: bool = True) -> list:
+        """Several GOPs (device-resident [F, Hp, Wp] each, e.g. consecutive GOPs of one stream
+        or GOPs of different streams) encoded together: every I-frame first (they depend on
+        nothing), then the P-frame runs of ALL the GOPs interleaved in one persistent launch
+        (Engine.encode_p_runs), so a frame of each run is in flight at once.  Where one frame
+        has fewer tiles than the GPU has resident workgroups (1080p) one GOP's frame-to-frame
+        dependency leaves CUs idle that the other GOPs fill.  Each GOP's symbols are identical
+        to encode_device of that GOP alone (the reference's encode() loop, Encoder.py:1839-1867,
+        once per GOP).  Covers the persistent-run configuration (no two-pass RC / ROI / RCFlag>1
+        P->I switch, nRefFrames 1); returns one encode_device-style dict per GOP.
+        symbols: optional per-GOP lists of preallocated FrameSymbols to reuse."""
+        eng = self.engine()
+        rc_switch = self.RCFlag is not None and self.RCFlag > 1 and (self.RCFlag == 2 or self.intra_thresh is not None)
+        if not (eng.pipelined_ok(1) and self.nRefFrames == 1 and not rc_switch and self.roi_block_offsets() is None
+                and not (self.RCFlag is not None and self.RCFlag >= 3)):
+            raise ValueError("encode_gops_device covers the persistent-run configuration only")
+        rc_on = self._rc_on()
+        qp_sched = self.row_qp_schedule(eng.nby) if rc_on else None
+        qp_sched_dev = eng.qp_row_tensor(qp_sched) if rc_on else None
+        self.set_Qp(self.const_init_Qp)
+        qp = self.Qp
+        outs, runs = [], []
+        for g, frames_dev in enumerate(gops):
+            n = frames_dev.shape[0]
+            pre = symbols[g] if symbols is not None else [None] * n
+            syms = [None] * n
+            for i in range(0, n, intra_dur):   # the I-frames
+                p = pre[i] if pre[i] is not None and pre[i].frame_type == 0 else None
+                syms[i] = eng.encode_i(frames_dev[i], qp, qp_sched, out=p, qp_row_dev=qp_sched_dev)
+            for i in range(0, n, intra_dur):   # the P-runs after each of them
+                ks = list(range(i + 1, min(i + intra_dur, n)))
+                for k in ks:
+                    syms[k] = pre[k] if pre[k] is not None and pre[k].frame_type == 1 else eng.new_symbols(1)
+                if ks:
+                    runs.append(([frames_dev[k] for k in ks], syms[i].recon, [syms[k] for k in ks]))
+            outs.append(syms)
+        eng.encode_p_runs(runs, qp, qp_row=qp_sched, qp_row_dev=qp_sched_dev)
+        res = []
+        for syms in outs:
+            res.append({"symbols": syms, "sse": eng.sum_rows([s.sse for s in syms]),
+                        "frame_type": [s.frame_type for s in syms],
+                        "qp_rows": [list(qp_sched) if rc_on else [] for _ in syms]})
+        if check:
+            eng.check_run()
+        return res
+
     def _save_recon(self, syms):
         d = os.path.dirname(self.recon_yuv_path)
         if d and not os.path.isdir(d):

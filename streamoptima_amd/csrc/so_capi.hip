@@ -49,6 +49,9 @@ struct PFrameOut {
 size_t p_run_workspace_words(int H, int W);
 int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                  const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, hipStream_t st);
+int p_runs_launch(const uint8_t* const* curs, int nframes, const uint8_t* const* refs, const int* deps, int conc,
+                  int H, int W, int qp_rd, const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws,
+                  hipStream_t st);
 struct PRunStripe {
     int by0, by1;
     uint8_t* peer_up0;
@@ -427,6 +430,51 @@ int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0
                             out_sse ? out_sse[i] : nullptr};
     }
     return p_run_launch(curs, nframes, ref0, H, W, qp_rd, qp_row, outs.data(), workspace, (hipStream_t)stream);
+}
+
+int so_encode_p_runs(const uint8_t* const* curs, int nframes, const uint8_t* const* refs, const int32_t* ref_frame,
+                     int H, int W, int bs, int sr, int qp_rd, const int32_t* qp_row, uint8_t* const* out_split,
+                     int16_t* const* out_mv, int16_t* const* out_qtc, int32_t* const* out_tokens,
+                     int32_t* const* out_mae_num, uint8_t* const* out_recon, int32_t* const* out_sse,
+                     uint32_t* workspace, void* stream) {
+    const char* fn = "so_encode_p_runs";
+    SO_TRY(check_geom(fn, H, W, bs, 0));
+    SO_TRY(check_sr(fn, sr));
+    SO_TRY(check_qp(fn, qp_rd));
+    if (bs != 16 || sr != 16 || W % 128 != 0) {
+        set_error("%s: covers bs 16 / sr 16 / W %% 128 == 0 (call so_encode_p_frame per frame)", fn);
+        return SO_E_UNSUPPORTED;
+    }
+    if (nframes <= 0) return SO_OK;
+    SO_NEED(curs, fn); SO_NEED(refs, fn); SO_NEED(ref_frame, fn); SO_NEED(out_split, fn); SO_NEED(out_mv, fn);
+    SO_NEED(out_qtc, fn); SO_NEED(out_tokens, fn); SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn);
+    SO_NEED(workspace, fn);
+    std::vector<PFrameOut> outs((size_t)nframes);
+    std::vector<int> deps((size_t)nframes);
+    int conc = 0;   // runs starting from a plane outside the list: interleaved chains
+    for (int i = 0; i < nframes; ++i) {
+        SO_NEED(curs[i], fn); SO_NEED(out_split[i], fn); SO_NEED(out_mv[i], fn); SO_NEED(out_qtc[i], fn);
+        SO_NEED(out_tokens[i], fn); SO_NEED(out_mae_num[i], fn); SO_NEED(out_recon[i], fn);
+        const int d = ref_frame[i];
+        if (d >= i || d < -1) {
+            set_error("%s: ref_frame[%d] = %d (must be -1 or an earlier frame of the list)", fn, i, d);
+            return SO_E_INVALID;
+        }
+        if (d < 0) {
+            SO_NEED(refs[i], fn);
+            ++conc;
+        }
+        deps[(size_t)i] = d;
+        for (int j = 0; j < nframes; ++j)
+            if ((j != i && out_recon[i] == out_recon[j]) || (ref_frame[j] < 0 && out_recon[i] == refs[j])) {
+                set_error("%s: out_recon[%d] aliases a reference plane or another frame's reconstruction", fn, i);
+                return SO_E_INVALID;
+            }
+        outs[(size_t)i] = PFrameOut{out_split[i], out_mv[i], out_qtc[i], out_tokens[i], out_mae_num[i], out_recon[i],
+                                    out_sse ? out_sse[i] : nullptr};
+    }
+    return p_runs_launch(curs, nframes, refs, deps.data(), conc, H, W, qp_rd, qp_row, outs.data(), workspace,
+                         (hipStream_t)stream);
 }
 
 // ---- one GOP across GPUs: a rank's stripe of every frame (so_me.hip PRunStripe) -------------

@@ -1345,8 +1345,15 @@ int p_tile_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int by0,
 
 // ---- persistent run of P-frames ------------------------------------------------------------
 constexpr int kRunMax = 32;   // frames per launch (kernel-argument table)
+// Frame i of a launch predicts from ref[i]; dep[i] = j >= 0 when that plane is frame j's
+// reconstruction in the same launch (its tiles are waited for), -1 when it is complete before
+// the launch (stream order).  One run: dep[i] = i - 1.  Several independent runs interleaved
+// (so_encode_p_runs: other GOPs' P-frames) keep more tiles in flight than one frame offers.
+// The stripe / frame-pipeline modes use i - 1 (and their own reference planes).
 struct PRunArgs {
     const uint8_t* cur[kRunMax];
+    const uint8_t* ref[kRunMax];
+    int dep[kRunMax];
     PFrameOut out[kRunMax];
 };
 
@@ -1448,6 +1455,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 #endif
         const int f = task / ntiles, tile = task - f * ntiles, ty = tile / tiles_x, tx = tile - ty * tiles_x;
         const bool first_row = ty == 0, last_row = ty == ntr - 1;
+        const int dep = MODE == kRunSingle ? a.dep[f] : f - 1;   // in-launch reference frame, or -1
         // the 3x3 tiles of frame f-1 around this one (the window's +-16 px), one flag per lane,
         // all polled in one round trip by wave 0 once the current tile is staged (ptile_body's
         // `pre`; the barrier after it releases the other waves).  Stripe: lanes 9-11 (12-14)
@@ -1460,12 +1468,12 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             const int gprev = (STRIPE ? sp.gbase : 0) + f - 1;   // global index of the reference frame
             const bool remote = STRIPE && (first_row ? sp.my_up_flags != nullptr : false);
             const bool remote_dn = STRIPE && (last_row ? sp.my_dn_flags != nullptr : false);
-            if (!FPIPE && f == 0 && !remote && !remote_dn) return;
+            if (!FPIPE && dep < 0 && !remote && !remote_dn) return;
 #ifdef SO_STAMPS
             if (lane == 0 && rec) rec[9] = __builtin_amdgcn_s_memrealtime();
 #endif
             const int nx = tx + lane % 3 - 1, ny = ty + lane / 3 - 1;
-            const bool need = (FPIPE || f > 0) && lane < 9 && nx >= 0 && nx < tiles_x && ny >= 0 && ny < ntr;
+            const bool need = (FPIPE || dep >= 0) && lane < 9 && nx >= 0 && nx < tiles_x && ny >= 0 && ny < ntr;
             // the timeout count, read once per tile: after one timeout the later tiles of the
             // run skip their waits (the run is already flagged wrong), so a lost flag cannot
             // stall the launch for 50 ms per remaining tile.  (Polling it in the loop put
@@ -1473,7 +1481,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 #if SO_RUN_ABORT_CHECK
             if (__hip_atomic_load(ws + kRunTimeoutWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
 #endif
-            const uint32_t* c = done + (size_t)(f > 0 ? f - 1 : 0) * ntiles + (need ? ny * tiles_x + nx : 0);
+            const uint32_t* c = done + (size_t)(dep > 0 ? dep : 0) * ntiles + (need ? ny * tiles_x + nx : 0);
             bool rneed = false;
             if constexpr (FPIPE) {   // the previous frame's tiles arrive from the previous rank
                 c = sp.my_dn_flags + (size_t)(sp.gbase + f) * ntiles + (need ? ny * tiles_x + nx : 0);
@@ -1515,7 +1523,8 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
         };
-        const uint8_t* ref = FPIPE ? sp.land0 + (long long)(sp.gbase + f) * sp.stride : (f ? a.out[f - 1].recon : ref0);
+        const uint8_t* ref = FPIPE ? sp.land0 + (long long)(sp.gbase + f) * sp.stride
+                                   : MODE == kRunSingle ? a.ref[f] : (f ? a.out[f - 1].recon : ref0);
         if constexpr (FPIPE) {
             const int slot = sp.gbase + f + sp.peer_slot_off;   // the next rank's slot of this frame
             PHalo hl{};
@@ -1601,10 +1610,14 @@ static void device_shape(int* ncu) {
         *ncu = 256;
 }
 
+// refs / deps (may be null: one run, frame g predicting from g - 1 and frame 0 from ref0): frame g
+// predicts from outs[deps[g]].recon when deps[g] >= 0 (0 <= deps[g] < g), else from refs[g].
+// conc: independent runs interleaved in the list (their tiles are in flight together).
 template <int MODE, int TPX>
 static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                           const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp0,
-                          int max_wg, hipStream_t st) {
+                          int max_wg, hipStream_t st, const uint8_t* const* refs = nullptr,
+                          const int* deps = nullptr, int conc = 1) {
     using G = Sea2GeoT<SO_PTILE_NW, TPX>;
     static int ncu = 0, per_cu = 0;
     if (ncu == 0) {
@@ -1620,8 +1633,12 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
         const int n = nframes - f0 < kRunMax ? nframes - f0 : kRunMax;
         PRunArgs a{};
         for (int i = 0; i < n; ++i) {
-            a.cur[i] = curs[f0 + i];
-            a.out[i] = outs[f0 + i];
+            const int g = f0 + i;
+            const int d = deps ? deps[g] : g - 1;
+            a.cur[i] = curs[g];
+            a.out[i] = outs[g];
+            a.ref[i] = d >= 0 ? outs[d].recon : (refs ? refs[g] : ref0);
+            a.dep[i] = d >= f0 ? d - f0 : -1;   // an earlier launch's frame is complete (stream order)
         }
         // nothing to reset: the kernel leaves the task / exit counters at 0 and done flags are
         // compared with the launch's epoch (the caller zeroes the workspace once)
@@ -1629,7 +1646,7 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
         // ceil(ntiles / ncu) workgroups per CU: every CU then runs its share of a frame's tiles
         // side by side, instead of some CUs running three (slower) while the next frame's tiles
         // wait on others -- a frame's time is its slowest tile's (1080p: 30 vs 33 us/frame).
-        int pcu = (int)((ntiles + ncu - 1) / ncu);
+        int pcu = (int)((ntiles * conc + ncu - 1) / ncu);
         if (pcu > per_cu) pcu = per_cu;
         if (const char* e = getenv("SO_RUN_PER_CU")) {   // A/B only: resident workgroups per CU
             const int v = atoi(e);
@@ -1661,6 +1678,18 @@ int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, i
     if (e && atoi(e) == 64)
         return p_run_launch_t<kRunSingle, 64>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, 0, st);
     return p_run_launch_t<kRunSingle, 128>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, 0, st);
+}
+
+// Several independent runs in one list (so_encode_p_runs): frame g predicts from
+// outs[deps[g]].recon (deps[g] < g) or, with deps[g] < 0, from refs[g].
+int p_runs_launch(const uint8_t* const* curs, int nframes, const uint8_t* const* refs, const int* deps, int conc,
+                  int H, int W, int qp_rd, const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws,
+                  hipStream_t st) {
+    PRunStripe sp{};
+    sp.by0 = 0;
+    sp.by1 = H / 16;
+    return p_run_launch_t<kRunSingle, 128>(curs, nframes, nullptr, H, W, qp_rd, qp_row, outs, ws, sp, 0, st, refs, deps,
+                                           conc);
 }
 
 int p_run_stripe_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,

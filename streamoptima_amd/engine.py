@@ -224,6 +224,49 @@ class Engine:
             o.qp_row = None if qp_row is None else list(qp_row)
         return outs
 
+    def encode_p_runs(self, runs: list, qp_rd: int, qp_row=None, qp_row_dev: torch.Tensor | None = None) -> list:
+        """so_encode_p_runs: several independent P-frame runs -- runs[r] = (curs, ref0, outs),
+        frame i of a run predicting from frame i-1's reconstruction and frame 0 from ref0 --
+        in ONE persistent launch, interleaved frame by frame (A1 B1 A2 B2 ...) so that a frame
+        of every run is in flight at once.  Each run's symbols are identical to encode_p_run
+        of that run alone; asynchronous."""
+        if not self.pipelined_ok():
+            raise ValueError("encode_p_runs covers bs 16 / sr 16 / full search / no VBS, FME / W % 128 == 0")
+        qrd = qp_row_dev if qp_row_dev is not None else self.qp_row_tensor(qp_row)
+        curs, refs, ref_frame, outs, last = [], [], [], [], {}
+        for k in range(max((len(r[0]) for r in runs), default=0)):
+            for r, (rc, r0, ro) in enumerate(runs):
+                if k >= len(rc):
+                    continue
+                if len(rc) != len(ro):
+                    raise ValueError("encode_p_runs: a run's curs and outs differ in length")
+                for t, name in ((rc[k], "cur"),) + (((r0, "ref0"),) if k == 0 else ()):
+                    self._check_plane(t, name)
+                curs.append(rc[k])
+                refs.append(r0 if k == 0 else None)
+                ref_frame.append(-1 if k == 0 else last[r])
+                last[r] = len(outs)
+                outs.append(ro[k])
+        n = len(curs)
+        if n == 0:
+            return []
+        if getattr(self, "_run_ws", None) is None:
+            self._run_ws = torch.zeros(self.lib.so_p_run_workspace_elems(self.h, self.w), dtype=torch.int32,
+                                       device=self.device)
+
+        def arr(ts):
+            return (ctypes.c_void_p * n)(*[0 if t is None else t.data_ptr() for t in ts])
+        rc = self.lib.so_encode_p_runs(
+            arr(curs), n, arr(refs), (ctypes.c_int32 * n)(*ref_frame), self.h, self.w, self.bs, self.sr, int(qp_rd),
+            _lib.ptr(qrd), arr([o.split for o in outs]), arr([o.mv for o in outs]), arr([o.qtc for o in outs]),
+            arr([o.tokens for o in outs]), arr([o.mae_num for o in outs]), arr([o.recon for o in outs]),
+            arr([o.sse for o in outs]), self._run_ws.data_ptr(), _lib.stream_handle(self.device))
+        _lib.check(rc, "so_encode_p_runs")
+        for o in outs:
+            o.frame_type, o.qp_rd = 1, int(qp_rd)
+            o.qp_row = None if qp_row is None else list(qp_row)
+        return [r[2] for r in runs]
+
     def run_timed_out(self) -> bool:
         """True if a dependency wait of any encode_p_run since the last check_run timed out
         (never expected: the run's symbols would then be unreliable).  Synchronises."""

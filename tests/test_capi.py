@@ -56,6 +56,36 @@ def test_host_side_validation_without_gpu():
         _lib.check(lib.so_me_full_search(None, None, 1, 64, 64, 16, 99, None, None, None), "me")
 
 
+def test_p_runs_validation_without_gpu():
+    """so_encode_p_runs refuses a frame whose in-list reference is not an earlier frame (the
+    persistent launch takes frames in list order: a later reference could deadlock it) and an
+    output plane that aliases a reference -- before anything touches the GPU."""
+    import ctypes
+    from streamoptima_amd import _lib
+    lib = _lib.load()
+    n = 2
+    fake = [ctypes.c_void_p(0x1000 * (i + 1)) for i in range(12)]
+
+    def arr(*ps):
+        return (ctypes.c_void_p * n)(*ps)
+    cur = arr(fake[0], fake[1])
+    outs = [arr(fake[2 + 2 * k], fake[3 + 2 * k]) for k in range(5)]
+
+    def call(refs, ref_frame, recon):
+        return lib.so_encode_p_runs(cur, n, refs, (ctypes.c_int32 * n)(*ref_frame), 64, 128, 16, 16, 4, None,
+                                    outs[0], outs[1], outs[2], outs[3], outs[4], recon, None,
+                                    ctypes.c_void_p(0x9000), None)
+    recon = arr(fake[10], fake[11])
+    assert call(arr(fake[8], fake[9]), [-1, 1], recon) == _lib.SO_E_INVALID
+    assert b"ref_frame[1]" in lib.so_last_error()
+    assert call(arr(fake[8], None), [-1, -1], recon) == _lib.SO_E_INVALID
+    assert call(arr(fake[10], None), [-1, 0], recon) == _lib.SO_E_INVALID
+    assert b"aliases" in lib.so_last_error()
+    assert lib.so_encode_p_runs(cur, n, arr(fake[8], None), (ctypes.c_int32 * n)(-1, 0), 64, 96, 16, 16, 4, None,
+                                outs[0], outs[1], outs[2], outs[3], outs[4], recon, None, ctypes.c_void_p(0x9000),
+                                None) == _lib.SO_E_UNSUPPORTED
+
+
 def test_product_never_imports_the_oracle():
     pkg = os.path.join(ROOT, "streamoptima_amd")
     for dirpath, _, files in os.walk(pkg):

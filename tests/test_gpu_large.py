@@ -60,6 +60,52 @@ def test_benchmarked_gop_bit_exact(gpu, name):
     _check(name, res["symbols"], psnr)
 
 
+def test_interleaved_gops_bit_exact(gpu):
+    """encode_gops_device: two copies of the 1080p GOP (configs[1]) and a third GOP of the
+    same frames reversed, their P-runs interleaved in ONE persistent launch: each copy equals
+    the oracle's digests frame by frame, the reversed GOP equals its own encode_device."""
+    from streamoptima_amd.digest import symbols_digest
+    cfg, codec = _codec("1080p", gpu)
+    from streamoptima_amd.engine import alloc_planes
+    a = _frames(cfg, gpu)
+    b = alloc_planes(*a.shape, gpu)
+    b.copy_(a)
+    c = alloc_planes(*a.shape, gpu)
+    c.copy_(a.flip(0))
+    ref_c = [symbols_digest(s) for s in codec.encode_device(c, cfg["intra_dur"])["symbols"]]
+    res = codec.encode_gops_device([a, c, b], cfg["intra_dur"])
+    torch.cuda.synchronize()
+    hp = a.shape[1]
+    for r in (res[0], res[2]):
+        sse = r["sse"].cpu().numpy()
+        _check("1080p", r["symbols"], [10 * np.log10(255 ** 2 / (float(s) / (hp * cfg["w"]))) for s in sse])
+    assert [symbols_digest(s) for s in res[1]["symbols"]] == ref_c
+
+
+def test_interleaved_gops_ragged_runs(gpu):
+    """Runs of different lengths and several I-frames per GOP (intra_dur 4 over 10 and 7
+    frames: runs of 3, 3, 1 and 3, 2), more frames than one launch holds in total (chunked
+    launches), on a frame with fewer tiles than the GPU's slots: equal to encode_device."""
+    from streamoptima_amd.Encoder import Y_Video_codec
+    from streamoptima_amd.digest import symbols_digest
+    from streamoptima_amd.engine import alloc_planes
+    from streamoptima_amd.synth import synth_sequence_torch
+    h, w = 96, 256
+    codec = Y_Video_codec(h, w, 10, 16, 16, 4, 4, 0, 0.015, False, device=gpu)
+
+    def gop(n, seed):
+        g = alloc_planes(n, h, w, gpu)
+        g.copy_(synth_sequence_torch(n, h, w, seed=seed, device=gpu))
+        return g
+    gops = [gop(10, 3), gop(7, 4)] + [gop(12, 5 + k) for k in range(3)]
+    exp = [[symbols_digest(s) for s in codec.encode_device(g, 4)["symbols"]] for g in gops]
+    res = codec.encode_gops_device(gops, 4)
+    torch.cuda.synchronize()
+    for g, r in enumerate(res):
+        assert [symbols_digest(s) for s in r["symbols"]] == exp[g], g
+        assert r["frame_type"] == [0 if i % 4 == 0 else 1 for i in range(gops[g].shape[0])]
+
+
 def test_1080p_drop_in_encode_pads_to_1088(gpu, tmp_path, monkeypatch):
     """The public encode() on 1920x1080 host frames: pad_hw's 128 rows (Encoder.py:140-155,
     :1833), the 1088-row encode, PSNR over the padded plane -- the bench's 1080p record."""
