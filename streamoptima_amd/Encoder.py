@@ -354,6 +354,7 @@ class Y_Video_codec(BlockAPI):
         `chunk` frames per launch; wait_input(k0, k1) is called before the work reading frames
         [k0, k1) is enqueued (to make the stream wait for their upload) and on_output(k0, k1,
         syms) after the work producing their symbols is enqueued.  Symbols are identical."""
+        wait_input_default, on_output_default = wait_input is None, on_output is None
         wait_input = wait_input or (lambda k0, k1: None)
         on_output = on_output or (lambda k0, k1, syms: None)
         eng = self.engine()
@@ -404,6 +405,10 @@ class Y_Video_codec(BlockAPI):
         # (engine.encode_p_run): same symbols, frames overlapped on the device
         pipelined = (not two_pass and roi_dev is None and not rc_switch and self.nRefFrames == 1
                      and eng.pipelined_ok(1) and os.environ.get("SO_PIPELINE", "1") != "0")
+        if pipelined and chunk is None and intra_dur < nframes - 1 and wait_input_default and on_output_default:
+            # several P-runs between I-frames: independent chains, interleaved in one launch
+            return self.encode_gops_device([frames_dev], intra_dur, symbols=[symbols] if symbols else None,
+                                           check=check)[0]
         i = 0
         while i < nframes:
             if pipelined and i % intra_dur != 0:
@@ -502,6 +507,8 @@ class Y_Video_codec(BlockAPI):
                     runs.append(([frames_dev[k] for k in ks], syms[i].recon, [syms[k] for k in ks]))
             outs.append(syms)
         eng.encode_p_runs(runs, qp, qp_row=qp_sched, qp_row_dev=qp_sched_dev)
+        if rc_on:   # the state encode_device leaves (each frame ends on its last row's QP)
+            self.set_Qp(qp_sched[-1])
         res = []
         for syms in outs:
             res.append({"symbols": syms, "sse": eng.sum_rows([s.sse for s in syms]),

@@ -82,10 +82,12 @@ def test_interleaved_gops_bit_exact(gpu):
     assert [symbols_digest(s) for s in res[1]["symbols"]] == ref_c
 
 
-def test_interleaved_gops_ragged_runs(gpu):
+def test_interleaved_gops_ragged_runs(gpu, monkeypatch):
     """Runs of different lengths and several I-frames per GOP (intra_dur 4 over 10 and 7
     frames: runs of 3, 3, 1 and 3, 2), more frames than one launch holds in total (chunked
-    launches), on a frame with fewer tiles than the GPU's slots: equal to encode_device."""
+    launches), on a frame with fewer tiles than the GPU's slots: equal to the per-frame
+    kernels (SO_PIPELINE=0), both through encode_gops_device and through encode_device
+    (which interleaves a GOP's own runs between I-frames)."""
     from streamoptima_amd.Encoder import Y_Video_codec
     from streamoptima_amd.digest import symbols_digest
     from streamoptima_amd.engine import alloc_planes
@@ -98,12 +100,15 @@ def test_interleaved_gops_ragged_runs(gpu):
         g.copy_(synth_sequence_torch(n, h, w, seed=seed, device=gpu))
         return g
     gops = [gop(10, 3), gop(7, 4)] + [gop(12, 5 + k) for k in range(3)]
+    monkeypatch.setenv("SO_PIPELINE", "0")
     exp = [[symbols_digest(s) for s in codec.encode_device(g, 4)["symbols"]] for g in gops]
+    monkeypatch.delenv("SO_PIPELINE")
     res = codec.encode_gops_device(gops, 4)
     torch.cuda.synchronize()
     for g, r in enumerate(res):
         assert [symbols_digest(s) for s in r["symbols"]] == exp[g], g
         assert r["frame_type"] == [0 if i % 4 == 0 else 1 for i in range(gops[g].shape[0])]
+    assert [symbols_digest(s) for s in codec.encode_device(gops[0], 4)["symbols"]] == exp[0]
 
 
 def test_1080p_drop_in_encode_pads_to_1088(gpu, tmp_path, monkeypatch):
