@@ -185,6 +185,41 @@ SO_DEV void xform2d_rows(double* lds, int l, const T* in_row, double* out_row) {
     wave_sync();   // lds free for reuse
 }
 
+// xform2d_rows<16> with half the LDS (16 x 9 doubles): each transpose goes through the buffer in
+// two halves -- rows' columns 0-7 then 8-15 (lanes l < 8 take their column from the first, the
+// others from the second), and back.  The same arithmetic bit for bit; 50 % more LDS
+// instructions for half the scratch (the persistent kernel's LDS per workgroup, SO_TQ_HALF).
+template <bool INVERSE, class T>
+SO_DEV void xform2d_rows_half(double* lds, int l, const T* in_row, double* out_row) {
+    constexpr int N = 16, P = 9;
+    const int hl = l >> 3, cl = l & 7;
+    double v[N];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {   // rows -> columns
+#pragma unroll
+        for (int c = 0; c < 8; ++c) lds[l * P + c] = (double)in_row[8 * h + c];
+        wave_sync();
+        if (hl == h) {
+#pragma unroll
+            for (int r = 0; r < N; ++r) v[r] = lds[r * P + cl];
+        }
+        wave_sync();
+    }
+    if constexpr (INVERSE) dct::dct3<N>(v); else dct::dct2<N>(v);   // axis 0 (columns)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {   // columns -> rows
+        if (hl == h) {
+#pragma unroll
+            for (int r = 0; r < N; ++r) lds[r * P + cl] = v[r];
+        }
+        wave_sync();
+#pragma unroll
+        for (int c = 0; c < 8; ++c) out_row[8 * h + c] = lds[l * P + c];
+        wave_sync();
+    }
+    if constexpr (INVERSE) dct::dct3<N>(out_row); else dct::dct2<N>(out_row);   // axis 1 (rows)
+}
+
 // Four 8x8 sub-blocks by 16 lanes: lane l owns sub-block j = l >> 2 and rows
 // (l & 3), (l & 3) + 4 on input and output.  lds: 4 x 8 x 9 doubles.
 template <bool INVERSE, class T>

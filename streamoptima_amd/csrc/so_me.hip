@@ -1092,11 +1092,17 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
 // tools/sea_stamps.py).  Per-tile flags (not per-row counters) matter at 1080p, where
 // fewer tiles than resident workgroups make the frame-to-frame latency the limit.
 // ---------------------------------------------------------------------------------------
+// FP64 transpose scratch per block of the fused tile: 16 x 17 doubles, or 16 x 9 with the
+// two-half transposes (SO_TQ_HALF: 18 KB instead of 35 KB of LDS per workgroup)
+#ifndef SO_TQ_HALF
+#define SO_TQ_HALF 0
+#endif
+constexpr int kTqScratch = SO_TQ_HALF ? 16 * 9 : 16 * 17;
 template <class G>
 struct PTileGeo {
     static constexpr int B4 = (G::B4RS * G::B4P + 4) / 4;             // dwords
     static constexpr int LIST = G::NW * G::CAP / 2;                   // dwords
-    static constexpr int TQD = G::NBLK * 16 * 17;                     // doubles
+    static constexpr int TQD = G::NBLK * kTqScratch;                  // doubles
     static constexpr int U64 = ((B4 + LIST + 1) / 2 > TQD) ? (B4 + LIST + 1) / 2 : TQD;
 };
 
@@ -1181,7 +1187,8 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
             }
         }
         double tcr[16];
-        xform2d_rows<16, false>(dl, l, res, tcr);
+        if constexpr (SO_TQ_HALF) xform2d_rows_half<false>(dl, l, res, tcr);
+        else xform2d_rows<16, false>(dl, l, res, tcr);
         // np.round to int by the 1.5 * 2^52 shift (|values| < 2^51): x + kRne rounds x to an
         // integer half-to-even, held in the low mantissa dword as two's complement -- one
         // v_add_f64 instead of v_rndne + v_cvt_i32
@@ -1195,7 +1202,8 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
         store_row_i16<16>(o.qtc + b * 256 + l * 16, q);
         double dq[16], rd[16];
         dequant_row_i<16>(q, l, qpr, dq);
-        xform2d_rows<16, true>(dl, l, dq, rd);
+        if constexpr (SO_TQ_HALF) xform2d_rows_half<true>(dl, l, dq, rd);
+        else xform2d_rows<16, true>(dl, l, dq, rd);
         int rec[16];
         {
             uint32_t pw[4];
@@ -1295,7 +1303,7 @@ SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur
         const int wq = SO_TQ_MAP == 1 ? ((w & 1) ? 1 << 20 : w >> 1) : w;
         const int gq = wq * BPW + (ln >> 4);
         if (ln < 16 * BPW && gq < G::NBLK)
-            tq16_exact<G, SC1, HALO>(S, gq, ln & 15, S.un + gq * (16 * 17), bx0, byt0, nbx, by0, by1, W, qp_rd, qp_row,
+            tq16_exact<G, SC1, HALO>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by0, by1, W, qp_rd, qp_row,
                                      qp_map, o, hl);
     }
     SO_SEA_STAMP(7, __builtin_amdgcn_s_memtime());
