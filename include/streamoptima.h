@@ -145,6 +145,27 @@ int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0
                     uint32_t* workspace, void* stream);
 
 /*
+ * A run of P-frames with two-pass rate control (build extension, RCFlag 3)
+ * as ONE persistent launch: per frame, pass 1 at the rate-control row QP (qp_row, or qp_rd)
+ * gives each block's token count t, the per-block QP is clamp(row QP + delta + roi, qp_lo,
+ * qp_hi) with delta = [t n >= 2m] + [t n >= 4m] - [2 t n < m] - [4 t n < m] (m = the block
+ * row's pass-1 token sum over its n blocks; so_qp_map's rule), and pass 2 re-runs the
+ * transforms at those QPs on pass 1's motion vectors.  Identical to the per-frame sequence
+ * so_encode_p_rows_ex (pass 1) + so_qp_map + so_encode_p_rows_ex(SO_REUSE_ME) (pass 2);
+ * out_qp_map[i] (int32 [nb]) receives frame i's QPs.  roi: int32 [nb] offsets or NULL.  Each
+ * tile is two tasks of the launch; a pass-2 task waits for its tile row's pass 1.  Frame i
+ * predicts from frame i-1's pass-2 reconstruction, frame 0 from ref0.  Same coverage and
+ * workspace as so_encode_p_run (W <= 8192).
+ */
+int so_encode_p_run_2pass(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W,
+                          int bs, int sr, int qp_rd, const int32_t* qp_row, const int32_t* roi,
+                          int qp_lo, int qp_hi, uint8_t* const* out_split, int16_t* const* out_mv,
+                          int16_t* const* out_qtc, int32_t* const* out_tokens,
+                          int32_t* const* out_mae_num, uint8_t* const* out_recon,
+                          int32_t* const* out_sse, int32_t* const* out_qp_map, uint32_t* workspace,
+                          void* stream);
+
+/*
  * Several independent runs of P-frames in ONE persistent launch (the P-frames of several
  * GOPs, or of the runs between a GOP's I-frames): frame i predicts from out_recon[j] when
  * ref_frame[i] = j (j < i, a frame of this list: its tiles are waited for inside the launch

@@ -403,15 +403,17 @@ class Y_Video_codec(BlockAPI):
         rc_switch = self.RCFlag is not None and self.RCFlag > 1 and (self.RCFlag == 2 or self.intra_thresh is not None)
         # runs of P-frames with nothing per frame on the host go through one persistent launch
         # (engine.encode_p_run): same symbols, frames overlapped on the device
-        pipelined = (not two_pass and roi_dev is None and not rc_switch and self.nRefFrames == 1
-                     and eng.pipelined_ok(1) and os.environ.get("SO_PIPELINE", "1") != "0")
+        run_ok = not rc_switch and self.nRefFrames == 1 and eng.pipelined_ok(1) and os.environ.get("SO_PIPELINE", "1") != "0"
+        pipelined = run_ok and not two_pass and roi_dev is None
+        # two-pass RC (with or without ROI): both passes of a P-run in one persistent launch
+        pipelined2 = run_ok and two_pass
         if pipelined and chunk is None and intra_dur < nframes - 1 and wait_input_default and on_output_default:
             # several P-runs between I-frames: independent chains, interleaved in one launch
             return self.encode_gops_device([frames_dev], intra_dur, symbols=[symbols] if symbols else None,
                                            check=check)[0]
         i = 0
         while i < nframes:
-            if pipelined and i % intra_dur != 0:
+            if (pipelined or pipelined2) and i % intra_dur != 0:
                 j = i
                 while j < nframes and j % intra_dur != 0 and (chunk is None or j - i < chunk):
                     j += 1
@@ -421,8 +423,15 @@ class Y_Video_codec(BlockAPI):
                 for k in range(i, j):
                     pre = symbols[k] if symbols is not None else None
                     outs.append(pre if pre is not None and pre.frame_type == 1 else eng.new_symbols(1))
-                eng.encode_p_run([frames_dev[k] for k in range(i, j)], ref_frames[-1], self.Qp, outs,
-                                 qp_row=qp_sched, qp_row_dev=qp_sched_dev)
+                if pipelined2:
+                    maps = [o.extra["qp_map"] if "qp_map" in o.extra else
+                            torch.empty(eng.nb, dtype=torch.int32, device=self.device) for o in outs]
+                    eng.encode_p_run_2pass([frames_dev[k] for k in range(i, j)], ref_frames[-1], self.Qp, outs, maps,
+                                           qp_row=qp_sched, qp_row_dev=qp_sched_dev, roi_dev=roi_dev, qp_lo=lo,
+                                           qp_hi=hi)
+                else:
+                    eng.encode_p_run([frames_dev[k] for k in range(i, j)], ref_frames[-1], self.Qp, outs,
+                                     qp_row=qp_sched, qp_row_dev=qp_sched_dev)
                 for sym in outs:
                     out_syms.append(sym)
                     ftypes.append(1)
@@ -466,7 +475,7 @@ class Y_Video_codec(BlockAPI):
             i += 1
         # per-block / per-row SSE came out of the encode kernels; one reduction per GOP
         sse = eng.sum_rows([s.sse for s in out_syms])
-        if check and pipelined:
+        if check and (pipelined or pipelined2):
             eng.check_run()
         return {"symbols": out_syms, "sse": sse, "frame_type": ftypes, "qp_rows": qp_rows}
 

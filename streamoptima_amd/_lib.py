@@ -40,6 +40,8 @@ _SIGS = {
                           _vp, _vp, _vp, _vp, _vp], _i),
     "so_p_run_workspace_elems": ([_i, _i], _sz),
     "so_encode_p_run": ([_vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
+    "so_encode_p_run_2pass": ([_vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                               _vp, _vp, _vp], _i),
     "so_encode_p_runs": ([_vp, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
                          _i),
     "so_i_frame_scratch_elems": ([_i, _i, _i], _sz),

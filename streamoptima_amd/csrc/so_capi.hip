@@ -45,8 +45,12 @@ struct PFrameOut {
     int32_t* mae;
     uint8_t* recon;
     int32_t* sse;
+    int32_t* qpmap;
 };
 size_t p_run_workspace_words(int H, int W);
+int p_run_2pass_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
+                       const int32_t* qp_row, const int32_t* roi, int qp_lo, int qp_hi, const PFrameOut* outs,
+                       uint32_t* ws, hipStream_t st);
 int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                  const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, hipStream_t st);
 int p_runs_launch(const uint8_t* const* curs, int nframes, const uint8_t* const* refs, const int* deps, int conc,
@@ -65,6 +69,11 @@ struct PRunStripe {
     int gbase;
     const uint8_t* land0;
     int peer_slot_off;
+    uint32_t* p1done;   // two-pass runs only (layout shared with so_me.hip)
+    int32_t* t1;
+    const int32_t* roi;
+    int qp_lo, qp_hi;
+    int p2lag;
 };
 int p_run_stripe_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                         const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg,
@@ -475,6 +484,43 @@ int so_encode_p_runs(const uint8_t* const* curs, int nframes, const uint8_t* con
     }
     return p_runs_launch(curs, nframes, refs, deps.data(), conc, H, W, qp_rd, qp_row, outs.data(), workspace,
                          (hipStream_t)stream);
+}
+
+int so_encode_p_run_2pass(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int bs, int sr,
+                          int qp_rd, const int32_t* qp_row, const int32_t* roi, int qp_lo, int qp_hi,
+                          uint8_t* const* out_split, int16_t* const* out_mv, int16_t* const* out_qtc,
+                          int32_t* const* out_tokens, int32_t* const* out_mae_num, uint8_t* const* out_recon,
+                          int32_t* const* out_sse, int32_t* const* out_qp_map, uint32_t* workspace, void* stream) {
+    const char* fn = "so_encode_p_run_2pass";
+    SO_TRY(check_geom(fn, H, W, bs, 0));
+    SO_TRY(check_sr(fn, sr));
+    SO_TRY(check_qp(fn, qp_rd));
+    if (bs != 16 || sr != 16 || W % 128 != 0 || W > 8192) {
+        set_error("%s: covers bs 16 / sr 16 / W %% 128 == 0, W <= 8192 (encode per frame otherwise)", fn);
+        return SO_E_UNSUPPORTED;
+    }
+    if (qp_lo < 0 || qp_hi > 20 || qp_lo > qp_hi) {
+        set_error("%s: QP clamp [%d, %d] outside [0, 20]", fn, qp_lo, qp_hi);
+        return SO_E_INVALID;
+    }
+    if (nframes <= 0) return SO_OK;
+    SO_NEED(curs, fn); SO_NEED(ref0, fn); SO_NEED(out_split, fn); SO_NEED(out_mv, fn); SO_NEED(out_qtc, fn);
+    SO_NEED(out_tokens, fn); SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn); SO_NEED(out_qp_map, fn);
+    SO_NEED(workspace, fn);
+    std::vector<PFrameOut> outs((size_t)nframes);
+    for (int i = 0; i < nframes; ++i) {
+        SO_NEED(curs[i], fn); SO_NEED(out_split[i], fn); SO_NEED(out_mv[i], fn); SO_NEED(out_qtc[i], fn);
+        SO_NEED(out_tokens[i], fn); SO_NEED(out_mae_num[i], fn); SO_NEED(out_recon[i], fn); SO_NEED(out_qp_map[i], fn);
+        for (int j = -1; j < i; ++j)
+            if (out_recon[i] == (j < 0 ? ref0 : out_recon[j])) {
+                set_error("%s: out_recon[%d] aliases ref0 or another frame's reconstruction", fn, i);
+                return SO_E_INVALID;
+            }
+        outs[(size_t)i] = PFrameOut{out_split[i], out_mv[i], out_qtc[i], out_tokens[i], out_mae_num[i], out_recon[i],
+                                    out_sse ? out_sse[i] : nullptr, out_qp_map[i]};
+    }
+    return p_run_2pass_launch(curs, nframes, ref0, H, W, qp_rd, qp_row, roi, qp_lo, qp_hi, outs.data(), workspace,
+                              (hipStream_t)stream);
 }
 
 // ---- one GOP across GPUs: a rank's stripe of every frame (so_me.hip PRunStripe) -------------

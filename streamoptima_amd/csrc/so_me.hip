@@ -1131,6 +1131,7 @@ struct PTileLds {
     unsigned long long keys[G::NBLK];
     uint32_t st[2];
     int32_t mer[G::NBLK][4];               // decoded ME records (dx, dy, ref, sad)
+    int32_t msum[G::TBY];                  // two-pass runs: pass-1 token sum of each block row
     double un[PTileGeo<G>::U64];           // byte sums + survivor lists | FP64 transposes
 };
 
@@ -1143,6 +1144,7 @@ struct PFrameOut {
     int32_t* mae;
     uint8_t* recon;
     int32_t* sse;
+    int32_t* qpmap;   // two-pass runs: the per-block QP used (so_encode_p_run_2pass); else null
 };
 
 
@@ -1312,6 +1314,175 @@ SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur
     __syncthreads();
 }
 
+// ---- two-pass rate control inside the persistent run (so_encode_p_run_2pass) ---------------
+// The per-frame flow of encode() with RCFlag 3: pass 1 encodes the frame
+// at the rate-control row QP, so_qp_map turns each block's pass-1 token count t against its
+// block row's sum m (n blocks) into delta = [t n >= 2m] + [t n >= 4m] - [2 t n < m] -
+// [4 t n < m], qp = clamp(row QP + delta + roi, lo, hi), and pass 2 re-runs the transforms
+// with those QPs on pass 1's motion vectors.  In the run a tile is two tasks: pass 1 (search +
+// forward transform + token count: the pass-1 QTC and reconstruction are never used) and
+// pass 2 (the transforms at the block QPs, from the ME records pass 1 stored); a pass-2 task
+// starts once every tile of its tile row finished pass 1 (the row sums).
+
+SO_DEV void store_sc1_i16(int16_t* p, int v) {
+    asm volatile("global_store_short %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+SO_DEV void store_sc1_i32(int32_t* p, int v) {
+    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+// pass 1 of one block (16 lanes, l = row): residual from the LDS window / tile as tq16_exact,
+// the forward transform, quantisation at the row QP and the token count.  Stores the ME
+// record (mv / mae / split: final, pass 2 keeps them) and the pass-1 tokens to t1, write-
+// through (pass-2 tasks on other CUs read them).
+template <class G>
+SO_DEV void tq16_pass1(PTileLds<G>& S, int g, int l, double* scratch, int bx0, int byt0, int nbx, int by1, int qp_rd,
+                       const int32_t* __restrict__ qp_row, const PFrameOut& o, int32_t* __restrict__ t1) {
+    constexpr int SR = G::SR, TBX = G::TBX;
+    const int bxl = g % TBX, byl = g / TBX;
+    const int gbx = bx0 + bxl, gby = byt0 + byl;
+    if (gbx < nbx && gby < by1) {   // uniform over the block's 16 lanes
+        const size_t b = (size_t)gby * nbx + gbx;
+        const int qpr = qp_row ? qp_row[gby] : qp_rd;
+        const int dx = S.mer[g][0], dy = S.mer[g][1], rf = S.mer[g][2], sad = S.mer[g][3];
+        const int prow = byl * 16 + SR + dy + l, pcol = bxl * 16 + SR + dx;
+        const uint32_t* crow = S.curt + (byl * 16 + l) * G::CPD + bxl * 4;
+        int res[16];
+        {
+            uint32_t pw[4];
+            win_row16<G::RP>(S.win, prow, pcol, pw);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t cw = crow[k];
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    res[4 * k + e] = (int)((cw >> (8 * e)) & 255) - (int)((pw[k] >> (8 * e)) & 255);
+            }
+        }
+        double tcr[16];
+        xform2d_rows<16, false>(scratch, l, res, tcr);
+        constexpr double kRne = 0x1.8p52;
+        int q[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c)
+            q[c] = (int)(uint32_t)__builtin_bit_cast(
+                uint64_t, __builtin_amdgcn_ldexp(__builtin_rint(tcr[c]), -q_exp_fast<16>(l, c, qpr)) + kRne);
+        const int tok = block_tokens<16>(nullptr, l, q);
+        if (l < 12) store_sc1_i16(o.mv + b * 12 + l, l == 0 ? dx : l == 1 ? dy : l == 2 ? rf : 0);
+        if (l == 0) {
+            o.split[b] = 0;
+            o.mae[b] = sad;
+            store_sc1_i32(t1 + b, tok);
+        }
+    }
+}
+
+// pass 2 of one block: the QP from the row's pass-1 statistics, then tq16_exact's transform
+// path with the prediction / current rows read from the planes (this task staged no window)
+// at pass 1's motion vector.  Stores QTC, tokens, reconstruction (write-through), SSE, QP.
+// 16 bytes of a plane row from byte `p` (any alignment): five aligned dwords + v_alignbyte (at a
+// valid candidate, x + dx + 16 < W, the last dword ends at most 3 bytes past the row)
+SO_DEV void row16_any(const uint8_t* p, uint32_t (&w)[4]) {
+    const uint32_t* pa = reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+    uint32_t q5[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) q5[k] = pa[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = __builtin_amdgcn_alignbyte(q5[k + 1], q5[k], sh);
+}
+SO_DEV void row16_aligned(const uint8_t* p, uint32_t (&w)[4]) {
+    const so_v4u c4 = *reinterpret_cast<const so_v4u*>(p);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = c4[k];
+}
+
+// pass 2 of one block: the QP from the row's pass-1 statistics, then tq16_exact's transform
+// path with the prediction / current rows read from the planes (this task staged no window)
+// at pass 1's motion vector -- read again (L1 / L2) after the transforms instead of being
+// held across them.  Stores QTC, tokens, reconstruction (write-through), SSE, QP.
+template <class G>
+SO_DEV void tq16_pass2(PTileLds<G>& S, int g, int l, double* scratch, int bx0, int byt0, int nbx, int by1, int W,
+                       int qp_rd, const int32_t* __restrict__ qp_row, const int32_t* __restrict__ roi, int qp_lo,
+                       int qp_hi, const uint8_t* __restrict__ cur, const uint8_t* ref, const PFrameOut& o,
+                       const int32_t* __restrict__ t1) {
+    constexpr int TBX = G::TBX;
+    const int bxl = g % TBX, byl = g / TBX;
+    const int gbx = bx0 + bxl, gby = byt0 + byl;
+    if (gbx < nbx && gby < by1) {
+        const size_t b = (size_t)gby * nbx + gbx;
+        const int x = gbx * 16, y = gby * 16;
+        const int dx = o.mv[b * 12], dy = o.mv[b * 12 + 1];
+        int qpr;
+        {   // qp_map_kernel (so_capi.hip), per block
+            const long long tn = (long long)t1[b] * nbx, m = S.msum[byl];
+            const int d = (tn >= 2 * m) + (tn >= 4 * m) - (2 * tn < m) - (4 * tn < m);
+            qpr = (qp_row ? qp_row[gby] : qp_rd) + d + (roi ? roi[b] : 0);
+            qpr = qpr < qp_lo ? qp_lo : (qpr > qp_hi ? qp_hi : qpr);
+        }
+        const uint8_t* crow = cur + (size_t)(y + l) * W + x;
+        const uint8_t* prow = ref + (size_t)(y + dy + l) * W + (x + dx);
+        int res[16];
+        {
+            uint32_t cw[4], pw[4];
+            row16_aligned(crow, cw);
+            row16_any(prow, pw);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    res[4 * k + e] = (int)((cw[k] >> (8 * e)) & 255) - (int)((pw[k] >> (8 * e)) & 255);
+        }
+        double tcr[16];
+        xform2d_rows<16, false>(scratch, l, res, tcr);
+        constexpr double kRne = 0x1.8p52;
+        int q[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c)
+            q[c] = (int)(uint32_t)__builtin_bit_cast(
+                uint64_t, __builtin_amdgcn_ldexp(__builtin_rint(tcr[c]), -q_exp_fast<16>(l, c, qpr)) + kRne);
+        const int tok = block_tokens<16>(nullptr, l, q);
+        store_row_i16<16>(o.qtc + b * 256 + l * 16, q);
+        double dq[16], rd[16];
+        dequant_row_i<16>(q, l, qpr, dq);
+        xform2d_rows<16, true>(scratch, l, dq, rd);
+        int rec[16];
+        {
+            uint32_t pw[4];
+            row16_any(prow, pw);
+#pragma unroll
+            for (int c = 0; c < 16; ++c)
+                rec[c] = (int)((pw[c >> 2] >> (8 * (c & 3))) & 255) +
+                         (int)(uint32_t)__builtin_bit_cast(uint64_t, rd[c] + kRne);
+        }
+        so_v4u v;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            v[k] = (uint32_t)(rec[4 * k] & 255) | ((uint32_t)(rec[4 * k + 1] & 255) << 8) |
+                   ((uint32_t)(rec[4 * k + 2] & 255) << 16) | ((uint32_t)(rec[4 * k + 3] & 255) << 24);
+        uint8_t* rp = o.recon + (size_t)(y + l) * W + x;
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(rp), "v"(v) : "memory");
+        int sse = 0;
+        if (o.sse) {
+            uint32_t cw[4];
+            row16_aligned(crow, cw);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int dd = (int)((cw[k] >> (8 * e)) & 255) - (rec[4 * k + e] & 255);
+                    sse += dd * dd;
+                }
+            sse = group_sum<16>(sse);
+        }
+        if (l == 0) {
+            o.tokens[b] = tok;
+            if (o.sse) o.sse[b] = sse;
+            if (o.qpmap) o.qpmap[b] = qpr;
+        }
+    }
+}
+
 #ifndef SO_PTILE_NW
 #define SO_PTILE_NW 8
 #endif
@@ -1418,8 +1589,16 @@ struct PRunStripe {
     // peer_dn_flags[(j + peer_slot_off) * ntiles + tile].  gbase = slot of the launch's first frame.
     const uint8_t* land0;
     int peer_slot_off;
+    // two-pass runs (kRunTwoPass): pass-1 done flags [f * ntiles + tile] = epoch, pass-1 token
+    // counts [f * nb + b] (both in the workspace), the ROI offsets (int32 [nb] or null) and the
+    // QP clamp
+    uint32_t* p1done;
+    int32_t* t1;
+    const int32_t* roi;
+    int qp_lo, qp_hi;
+    int p2lag;   // tile rows between a row's pass-1 and pass-2 tasks in the queue (1..ntr)
 };
-constexpr int kRunSingle = 0, kRunStripe = 1, kRunFPipe = 2;
+constexpr int kRunSingle = 0, kRunStripe = 1, kRunFPipe = 2, kRunTwoPass = 3;
 
 template <int NW, int MODE, int TPX = 128>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE)))
@@ -1431,10 +1610,14 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     __shared__ int s_task;
     const int tid = threadIdx.x;
     const int nbx = W / 16;
-    constexpr bool STRIPE = MODE == kRunStripe, FPIPE = MODE == kRunFPipe;
+    constexpr bool STRIPE = MODE == kRunStripe, FPIPE = MODE == kRunFPipe, TWOP = MODE == kRunTwoPass;
     const int by0 = STRIPE ? sp.by0 : 0, by1 = STRIPE ? sp.by1 : H / 16;
     const int tiles_x = (nbx + G::TBX - 1) / G::TBX, ntr = (by1 - by0 + G::TBY - 1) / G::TBY;
-    const int ntiles = tiles_x * ntr, ntasks = ntiles * nframes;
+    const int ntiles = tiles_x * ntr;
+    // two-pass: 2 tasks per tile; per frame the pass-1 tasks of tile row r + 1 are queued ahead
+    // of the pass-2 tasks of row r (which wait for all of row r's pass 1), so every wait is
+    // on tasks earlier in the queue
+    const int per_frame = TWOP ? 2 * ntiles : ntiles, ntasks = per_frame * nframes;
     uint32_t* const done = ws + kRunDoneBase;
     // Every queue / flag access is made by ALL lanes of wave 0 under a wave-uniform branch
     // (lane 0 adds 1, the others 0): a `tid == 0` branch ahead of a barrier inside this loop
@@ -1461,9 +1644,32 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
         SO_STAMP_REC_SET(rec);
         if (tid == 0 && rec) rec[8] = __builtin_amdgcn_s_memrealtime();
 #endif
-        const int f = task / ntiles, tile = task - f * ntiles, ty = tile / tiles_x, tx = tile - ty * tiles_x;
+        const int f = task / per_frame;
+        int tile = task - f * per_frame, pass = 1;
+        if constexpr (TWOP) {
+            // [P1 rows 0..L-1] [P1 row L][P2 row 0] [P1 row L+1][P2 row 1] ... [P2 rows ntr-L..]:
+            // a pass-2 task is queued L tile rows after its row's pass 1 (L = sp.p2lag, about
+            // one grid's worth of tasks), so it rarely waits holding its slot
+            const int L = sp.p2lag, k = tile, k1 = k - L * tiles_x, nb2 = (ntr - L) * 2 * tiles_x;
+            if (k1 < 0) {
+                tile = k;
+            } else if (k1 < nb2) {
+                const int j = k1 / (2 * tiles_x), rem = k1 - j * 2 * tiles_x;
+                if (rem < tiles_x) {
+                    tile = (j + L) * tiles_x + rem;
+                } else {
+                    pass = 2;
+                    tile = j * tiles_x + rem - tiles_x;
+                }
+            } else {
+                pass = 2;
+                tile = (ntr - L) * tiles_x + (k1 - nb2);
+            }
+        }
+        const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
         const bool first_row = ty == 0, last_row = ty == ntr - 1;
-        const int dep = MODE == kRunSingle ? a.dep[f] : f - 1;   // in-launch reference frame, or -1
+        // in-launch reference frame, or -1
+        const int dep = (MODE == kRunSingle || TWOP) ? a.dep[f] : f - 1;
         // the 3x3 tiles of frame f-1 around this one (the window's +-16 px), one flag per lane,
         // all polled in one round trip by wave 0 once the current tile is staged (ptile_body's
         // `pre`; the barrier after it releases the other waves).  Stripe: lanes 9-11 (12-14)
@@ -1532,8 +1738,71 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 #endif
         };
         const uint8_t* ref = FPIPE ? sp.land0 + (long long)(sp.gbase + f) * sp.stride
-                                   : MODE == kRunSingle ? a.ref[f] : (f ? a.out[f - 1].recon : ref0);
-        if constexpr (FPIPE) {
+                                   : (MODE == kRunSingle || TWOP) ? a.ref[f] : (f ? a.out[f - 1].recon : ref0);
+        if constexpr (TWOP) {
+            const int nb = nbx * (H / 16);
+            int32_t* const t1 = sp.t1 + (size_t)f * nb;
+            const int bx0 = tx * G::TBX, byt0 = ty * G::TBY;
+            const int ln = tid & 63, w = tid >> 6, gq = w * G::TQ_BPW + (ln >> 4);
+            if (pass == 1) {
+                using P = PTileGeo<G>;
+                uint32_t* const b4w = reinterpret_cast<uint32_t*>(S.un);
+                const Sea2Lds L{S.win, b4w, S.curt, S.a4, reinterpret_cast<uint16_t*>(b4w + P::B4), S.lcount, S.keys,
+                                S.st};
+                RefSet refs{};
+                refs.p[0] = ref;
+                sea2_tile<G>(L, tile, a.cur[f], refs, 1, H, W, 0, by1, 0, wait_ref);   // ends with a barrier
+                for (int i = tid; i < G::NBLK; i += G::NTHREADS) decode_key(S.keys[i], G::SR, S.mer[i]);
+                __syncthreads();
+                if (ln < 16 * G::TQ_BPW && gq < G::NBLK)
+                    tq16_pass1<G>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by1, qp_rd, qp_row, a.out[f],
+                                  t1);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (wave == 0)
+                    __hip_atomic_store(sp.p1done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                if (wave == 0) {   // every tile of this tile row finished pass 1 (tiles_x <= 64)
+                    const uint32_t* c = sp.p1done + (size_t)f * ntiles + ty * tiles_x + (lane < tiles_x ? lane : 0);
+                    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#if SO_RUN_ABORT_CHECK
+                    const bool skip =
+                        __hip_atomic_load(ws + kRunTimeoutWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+#else
+                    const bool skip = false;
+#endif
+                    while (!skip) {
+                        const bool v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ep;
+                        if (__builtin_amdgcn_ballot_w64(lane < tiles_x && !v) == 0) break;
+                        __builtin_amdgcn_s_sleep(1);
+                        if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
+                            __hip_atomic_fetch_add(&ws[kRunTimeoutWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            break;
+                        }
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __syncthreads();
+                if (wave < G::TBY) {   // pass-1 token sum of block row byt0 + wave
+                    const int row = byt0 + wave;
+                    uint32_t sum = 0;
+                    if (row < by1)
+                        for (int bx = lane; bx < nbx; bx += 64) sum += (uint32_t)t1[(size_t)row * nbx + bx];
+                    sum = wave_sum_u32(sum);
+                    if (lane == 0) S.msum[wave] = (int32_t)sum;
+                }
+                __syncthreads();
+                if (ln < 16 * G::TQ_BPW && gq < G::NBLK)
+                    tq16_pass2<G>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by1, W, qp_rd, qp_row, sp.roi,
+                                  sp.qp_lo, sp.qp_hi, a.cur[f], ref, a.out[f], t1);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (wave == 0)
+                    __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else if constexpr (FPIPE) {
             const int slot = sp.gbase + f + sp.peer_slot_off;   // the next rank's slot of this frame
             PHalo hl{};
             hl.dn = sp.peer_dn0 + (long long)slot * sp.stride;   // every row of the tile
@@ -1603,10 +1872,16 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     }
 }
 
+// [kRunDoneBase, +kRunMax * ntiles64) done flags, then (two-pass runs) kRunMax * ntiles128
+// pass-1 done flags and kRunMax * nb pass-1 token counts
+static size_t run_tiles(int H, int W, int tbx, int tby) {
+    return (size_t)((W / 16 + tbx - 1) / tbx) * ((H / 16 + tby - 1) / tby);
+}
 size_t p_run_workspace_words(int H, int W) {
     using G64 = Sea2GeoT<8, 64>;   // the narrower tiles: the larger tile count
-    const size_t ntiles = (size_t)((W / 16 + G64::TBX - 1) / G64::TBX) * ((H / 16 + G64::TBY - 1) / G64::TBY);
-    return (size_t)kRunDoneBase + (size_t)kRunMax * ntiles;
+    using G128 = Sea2GeoT<8, 128>;
+    return (size_t)kRunDoneBase + (size_t)kRunMax * run_tiles(H, W, G64::TBX, G64::TBY) +
+           (size_t)kRunMax * run_tiles(H, W, G128::TBX, G128::TBY) + (size_t)kRunMax * (W / 16) * (H / 16);
 }
 
 // Launch the run in <= kRunMax-frame launches.  max_wg > 0 caps the resident grid (several
@@ -1665,6 +1940,12 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
         if (max_wg > 0 && grid > max_wg) grid = max_wg;
         PRunStripe sp = sp0;
         sp.gbase = sp0.gbase + f0;
+        if (MODE == kRunTwoPass) {   // pass 2 of a row about one grid's worth of tasks after its pass 1
+            const int tiles_x = (nbx + G::TBX - 1) / G::TBX, ntr = (rows + G::TBY - 1) / G::TBY;
+            int lag = (int)((grid + tiles_x - 1) / tiles_x);
+            if (const char* e = getenv("SO_P2LAG")) lag = atoi(e);   // A/B only
+            sp.p2lag = lag < 1 ? 1 : (lag > ntr ? ntr : lag);
+        }
         hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, MODE, TPX>), dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), 0, st, a, n,
                            f0 ? outs[f0 - 1].recon : ref0, H, W, qp_rd, qp_row, ws, (int)(f0 * ntiles), sp);
         const int rc = check_launch("p_run_kernel");
@@ -1698,6 +1979,25 @@ int p_runs_launch(const uint8_t* const* curs, int nframes, const uint8_t* const*
     sp.by1 = H / 16;
     return p_run_launch_t<kRunSingle, 128>(curs, nframes, nullptr, H, W, qp_rd, qp_row, outs, ws, sp, 0, st, refs, deps,
                                            conc);
+}
+
+// Two-pass rate control over a run (so_encode_p_run_2pass): one run as p_run_launch, each tile
+// as a pass-1 and a pass-2 task (kRunTwoPass).
+int p_run_2pass_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
+                       const int32_t* qp_row, const int32_t* roi, int qp_lo, int qp_hi, const PFrameOut* outs,
+                       uint32_t* ws, hipStream_t st) {
+    using G64 = Sea2GeoT<8, 64>;
+    using G128 = Sea2GeoT<8, 128>;
+    PRunStripe sp{};
+    sp.by0 = 0;
+    sp.by1 = H / 16;
+    sp.p1done = ws + kRunDoneBase + (size_t)kRunMax * run_tiles(H, W, G64::TBX, G64::TBY);
+    sp.t1 = reinterpret_cast<int32_t*>(sp.p1done + (size_t)kRunMax * run_tiles(H, W, G128::TBX, G128::TBY));
+    sp.roi = roi;
+    sp.qp_lo = qp_lo;
+    sp.qp_hi = qp_hi;
+    return p_run_launch_t<kRunTwoPass, 128>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, 0, st, nullptr,
+                                            nullptr, 2);
 }
 
 int p_run_stripe_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,

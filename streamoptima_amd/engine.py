@@ -224,6 +224,44 @@ class Engine:
             o.qp_row = None if qp_row is None else list(qp_row)
         return outs
 
+    def encode_p_run_2pass(self, curs: list, ref0: torch.Tensor, qp_rd: int, outs: list, qp_maps: list,
+                           qp_row=None, qp_row_dev: torch.Tensor | None = None, roi_dev: torch.Tensor | None = None,
+                           qp_lo: int = 0, qp_hi: int = 12) -> list:
+        """so_encode_p_run_2pass: a run of P-frames with two-pass rate control (pass 1 at the
+        row QP, per-block QPs from the row's pass-1 token statistics and the ROI, pass 2 at
+        those QPs on pass 1's motion vectors) as ONE persistent launch.  qp_maps[i] (int32
+        [nb]) receives frame i's QPs.  Symbols identical to encode_p + qp_map + encode_p
+        (reuse_me) per frame; asynchronous."""
+        if not self.pipelined_ok():
+            raise ValueError("encode_p_run_2pass covers bs 16 / sr 16 / full search / no VBS, FME / W % 128 == 0")
+        n = len(curs)
+        if n == 0:
+            return []
+        qrd = qp_row_dev if qp_row_dev is not None else self.qp_row_tensor(qp_row)
+        for t, name in [(ref0, "ref0")] + [(c, "cur") for c in curs]:
+            self._check_plane(t, name)
+        for m in qp_maps:
+            if m.dtype != torch.int32 or m.numel() != self.nb or m.device != self.device or not m.is_contiguous():
+                raise ValueError(f"qp_maps entries must be contiguous int32 [{self.nb}] on {self.device}")
+        if getattr(self, "_run_ws", None) is None:
+            self._run_ws = torch.zeros(self.lib.so_p_run_workspace_elems(self.h, self.w), dtype=torch.int32,
+                                       device=self.device)
+
+        def arr(ts):
+            return (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
+        rc = self.lib.so_encode_p_run_2pass(
+            arr(curs), n, ref0.data_ptr(), self.h, self.w, self.bs, self.sr, int(qp_rd), _lib.ptr(qrd),
+            _lib.ptr(roi_dev), int(qp_lo), int(qp_hi),
+            arr([o.split for o in outs]), arr([o.mv for o in outs]), arr([o.qtc for o in outs]),
+            arr([o.tokens for o in outs]), arr([o.mae_num for o in outs]), arr([o.recon for o in outs]),
+            arr([o.sse for o in outs]), arr(qp_maps), self._run_ws.data_ptr(), _lib.stream_handle(self.device))
+        _lib.check(rc, "so_encode_p_run_2pass")
+        for o, m in zip(outs, qp_maps):
+            o.frame_type, o.qp_rd = 1, int(qp_rd)
+            o.qp_row = None if qp_row is None else list(qp_row)
+            o.extra["qp_map"] = m
+        return outs
+
     def encode_p_runs(self, runs: list, qp_rd: int, qp_row=None, qp_row_dev: torch.Tensor | None = None) -> list:
         """so_encode_p_runs: several independent P-frame runs -- runs[r] = (curs, ref0, outs),
         frame i of a run predicting from frame i-1's reconstruction and frame 0 from ref0 --

@@ -111,6 +111,33 @@ def test_interleaved_gops_ragged_runs(gpu, monkeypatch):
     assert [symbols_digest(s) for s in codec.encode_device(gops[0], 4)["symbols"]] == exp[0]
 
 
+@pytest.mark.parametrize("roi", [None, [(100, 40, 400, 200, -2), (0, 150, 260, 272, 3)]])
+def test_two_pass_run_matches_per_frame(gpu, monkeypatch, roi):
+    """so_encode_p_run_2pass (both passes of every P-frame in one persistent launch) against
+    the per-frame sequence pass 1 -> so_qp_map -> pass 2 (SO_PIPELINE=0), frame by frame
+    including the QP maps, on a 640x272 GOP (5 x 9 tiles: pass-2 tasks of the 5-tile rows
+    waiting on their row's pass 1), with and without ROI, two runs (intra_dur 5 of 11)."""
+    from streamoptima_amd.Encoder import Y_Video_codec
+    from streamoptima_amd.digest import symbols_digest
+    from streamoptima_amd.engine import alloc_planes
+    from streamoptima_amd.synth import synth_sequence_torch
+    from streamoptima_amd.workloads import RC_TABLES
+    h, w, f = 272, 640, 11
+    codec = Y_Video_codec(h, w, f, 16, 16, 4, 5, 0, 0.015, False, RCFlag=3, targetBR="2 mbps",
+                          qp_rate_tables=RC_TABLES, roi=roi, device=gpu)
+    fr = alloc_planes(f, h, w, gpu)
+    fr.copy_(synth_sequence_torch(f, h, w, seed=7, device=gpu))
+    monkeypatch.setenv("SO_PIPELINE", "0")
+    exp = codec.encode_device(fr, 5)
+    exp_d = [symbols_digest(s) for s in exp["symbols"]]
+    monkeypatch.delenv("SO_PIPELINE")
+    got = codec.encode_device(fr, 5)
+    torch.cuda.synchronize()
+    assert all("qp_map" in s.extra for s in got["symbols"])
+    assert [symbols_digest(s) for s in got["symbols"]] == exp_d
+    assert torch.equal(got["sse"], exp["sse"])
+
+
 def test_1080p_drop_in_encode_pads_to_1088(gpu, tmp_path, monkeypatch):
     """The public encode() on 1920x1080 host frames: pad_hw's 128 rows (Encoder.py:140-155,
     :1833), the 1088-row encode, PSNR over the padded plane -- the bench's 1080p record."""
