@@ -1743,7 +1743,6 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             const int nb = nbx * (H / 16);
             int32_t* const t1 = sp.t1 + (size_t)f * nb;
             const int bx0 = tx * G::TBX, byt0 = ty * G::TBY;
-            const int ln = tid & 63, w = tid >> 6, gq = w * G::TQ_BPW + (ln >> 4);
             if (pass == 1) {
                 using P = PTileGeo<G>;
                 uint32_t* const b4w = reinterpret_cast<uint32_t*>(S.un);
@@ -1754,6 +1753,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 sea2_tile<G>(L, tile, a.cur[f], refs, 1, H, W, 0, by1, 0, wait_ref);   // ends with a barrier
                 for (int i = tid; i < G::NBLK; i += G::NTHREADS) decode_key(S.keys[i], G::SR, S.mer[i]);
                 __syncthreads();
+                const int t2 = opaque_tid(), ln = t2 & 63, gq = (t2 >> 6) * G::TQ_BPW + (ln >> 4);
                 if (ln < 16 * G::TQ_BPW && gq < G::NBLK)
                     tq16_pass1<G>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by1, qp_rd, qp_row, a.out[f],
                                   t1);
@@ -1794,6 +1794,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                     if (lane == 0) S.msum[wave] = (int32_t)sum;
                 }
                 __syncthreads();
+                const int t2 = opaque_tid(), ln = t2 & 63, gq = (t2 >> 6) * G::TQ_BPW + (ln >> 4);
                 if (ln < 16 * G::TQ_BPW && gq < G::NBLK)
                     tq16_pass2<G>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by1, W, qp_rd, qp_row, sp.roi,
                                   sp.qp_lo, sp.qp_hi, a.cur[f], ref, a.out[f], t1);
