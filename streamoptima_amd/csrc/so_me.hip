@@ -1599,6 +1599,15 @@ struct PRunStripe {
     int p2lag;   // tile rows between a row's pass-1 and pass-2 tasks in the queue (1..ntr)
 };
 constexpr int kRunSingle = 0, kRunStripe = 1, kRunFPipe = 2, kRunTwoPass = 3;
+// SO_RUN_PROFILE builds (tools/rc2p_ab.py): per-phase shader cycles >> 10 accumulated by wave 0
+// into workspace words 48.. (48 pass-1 task, 49 pass-2 task, 50 pass-2 row wait, 51 reference
+// wait); A/B diagnostics only
+#ifdef SO_RUN_PROFILE
+#define SO_RUN_PROF(word, cyc) \
+    do { if (wave == 0) __hip_atomic_fetch_add(&ws[(word)], lane == 0 ? (uint32_t)((cyc) >> 10) : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); } while (0)
+#else
+#define SO_RUN_PROF(word, cyc) do { } while (0)
+#endif
 
 template <int NW, int MODE, int TPX = 128>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE)))
@@ -1725,6 +1734,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                     break;
                 }
             }
+            SO_RUN_PROF(51, (__builtin_amdgcn_s_memrealtime() - t0) * 25);   // 100 MHz ticks -> ~2.5 GHz cycles
 #ifdef SO_STAMPS
             if (lane == 0 && rec) rec[10] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1743,6 +1753,9 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             const int nb = nbx * (H / 16);
             int32_t* const t1 = sp.t1 + (size_t)f * nb;
             const int bx0 = tx * G::TBX, byt0 = ty * G::TBY;
+#ifdef SO_RUN_PROFILE
+            const unsigned long long pt0 = __builtin_amdgcn_s_memtime();
+#endif
             if (pass == 1) {
                 using P = PTileGeo<G>;
                 uint32_t* const b4w = reinterpret_cast<uint32_t*>(S.un);
@@ -1762,6 +1775,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 if (wave == 0)
                     __hip_atomic_store(sp.p1done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
+                SO_RUN_PROF(48, __builtin_amdgcn_s_memtime() - pt0);
             } else {
                 if (wave == 0) {   // every tile of this tile row finished pass 1 (tiles_x <= 64)
                     const uint32_t* c = sp.p1done + (size_t)f * ntiles + ty * tiles_x + (lane < tiles_x ? lane : 0);
@@ -1783,6 +1797,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                     }
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    SO_RUN_PROF(50, __builtin_amdgcn_s_memtime() - pt0);
                 }
                 __syncthreads();
                 if (wave < G::TBY) {   // pass-1 token sum of block row byt0 + wave
@@ -1802,6 +1817,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 __syncthreads();
                 if (wave == 0)
                     __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                SO_RUN_PROF(49, __builtin_amdgcn_s_memtime() - pt0);
             }
         } else if constexpr (FPIPE) {
             const int slot = sp.gbase + f + sp.peer_slot_off;   // the next rank's slot of this frame
@@ -1843,8 +1859,12 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                                        __HIP_MEMORY_SCOPE_SYSTEM);
             }
         } else {
+#ifdef SO_RUN_PROFILE
+            const unsigned long long pt0 = __builtin_amdgcn_s_memtime();
+#endif
             ptile_body<G, true>(S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd, qp_row, nullptr, nullptr, a.out[f],
                                 wait_ref);
+            SO_RUN_PROF(52, __builtin_amdgcn_s_memtime() - pt0);
             // ptile_body ended with every wave's write-through stores retired and a barrier
             if (wave == 0)
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,

@@ -131,6 +131,7 @@ def test_two_pass_run_matches_per_frame(gpu, monkeypatch, roi):
     exp = codec.encode_device(fr, 5)
     exp_d = [symbols_digest(s) for s in exp["symbols"]]
     monkeypatch.delenv("SO_PIPELINE")
+    monkeypatch.setenv("SO_RUN_2PASS", "1")
     got = codec.encode_device(fr, 5)
     torch.cuda.synchronize()
     assert all("qp_map" in s.extra for s in got["symbols"])
