@@ -132,7 +132,8 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
  * nothing is reset between launches).  One workspace serves one stream at a time.  Word 32
  * (SO_P_RUN_TIMEOUT_WORD) is the timeout count: the caller reads it after the run (or after a
  * whole GOP of runs) and clears it.
- * Nonzero means a dependency wait passed 50 ms and the run's symbols may be wrong; the
+ * Nonzero means a dependency wait passed 50 ms (2 s for another rank's flags) and the run's
+ * symbols may be wrong; the
  * facade raises (Engine.check_run).  Consumers poll the flags and then take an agent-scope
  * acquire before reading the reference rows.
  */

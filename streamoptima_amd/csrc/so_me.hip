@@ -1720,6 +1720,10 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                     rneed = true;
                 }
             }
+            // 50 ms within one GPU; 2 s where the flags come from another rank, whose host may
+            // enqueue its launch late (a rank's kernel can start waiting on a neighbour whose
+            // process is descheduled, e.g. several ranks time-sharing one GPU)
+            constexpr unsigned long long kWaitLimit = (STRIPE || FPIPE) ? 200000000ull : 5000000ull;
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
             for (;;) {
                 uint32_t v;
@@ -1729,7 +1733,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                     v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ep ? 1u : 0u;
                 if (__builtin_amdgcn_ballot_w64((need || rneed) && v == 0u) == 0) break;
                 __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitLimit) {
                     __hip_atomic_fetch_add(&ws[kRunTimeoutWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
