@@ -341,8 +341,12 @@ int so_me_search_ex(const uint8_t* cur, const uint8_t* const* refs, int nref, in
  *           (the VBS RD decision keeps qp_rd, like the reference's); see so_qp_map
  *   flags   SO_REUSE_ME: skip the ME; `scratch` (and fme_planes) still hold the ME records
  *           of a previous call on the same cur / refs / rows (pass 2 of two-pass RC)
+ *           SO_TOKENS_ONLY: pass 1 of two-pass RC -- only out_tokens and the ME records in
+ *           `scratch` are guaranteed (the fused full-search path skips the rest of the
+ *           transform); the other outputs are left for the SO_REUSE_ME pass to write
  */
 #define SO_REUSE_ME 1
+#define SO_TOKENS_ONLY 2
 int so_encode_p_rows_ex(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W,
                         int bs, int sr, int by0, int by1, int qp_rd, const int32_t* qp_row,
                         const int32_t* qp_map, int vbs, double lam, int me_mode, int fme,

@@ -384,11 +384,12 @@ class Y_Video_codec(BlockAPI):
                 enc = lambda o, qm: eng.encode_i(cur, qp_rd, qp_sched, out=o, qp_row_dev=qp_sched_dev,  # noqa: E731
                                                  qp_map_dev=qm)
             else:
-                enc = lambda o, qm, reuse=False: eng.encode_p(  # noqa: E731
+                enc = lambda o, qm, reuse=False, tok=False: eng.encode_p(  # noqa: E731
                     cur, ref_frames, qp_rd, qp_sched, out=o, qp_row_dev=qp_sched_dev, fme_wrap=wrap, qp_map_dev=qm,
-                    **({"reuse_me": reuse} if reuse else {}))
+                    **({"reuse_me": reuse} if reuse else {}), **({"tokens_only": tok} if tok else {}))
             if two_pass:
-                sym = enc(out, None)
+                # pass 1 needs only the token counts (and the ME records pass 2 reuses)
+                sym = enc(out, None) if intra else enc(out, None, tok=True)
                 eng.qp_map(sym.tokens, qp_rd, qp_sched_dev, roi_dev, qmap, qp_lo=lo, qp_hi=hi)
                 sym = enc(sym, qmap) if intra else enc(sym, qmap, True)
             elif roi_dev is not None:

@@ -86,6 +86,7 @@ _SIGS = {
 # ME modes (include/streamoptima.h)
 ME_FULL, ME_FAST, ME_FAST_PAR = 0, 1, 2
 REUSE_ME = 1   # so_encode_p_rows_ex flags
+TOKENS_ONLY = 2
 
 EXPORTED = tuple(_SIGS)
 

@@ -35,7 +35,7 @@ int me_fastpred_launch(const uint8_t* cur, const uint8_t* const* ptrs, int nptr,
 int p_tile_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int by0, int by1, int qp_rd,
                   const int32_t* qp_row, const int32_t* qp_map, int32_t* out_best, uint8_t* out_split,
                   int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon,
-                  int32_t* out_sse, hipStream_t st);
+                  int32_t* out_sse, hipStream_t st, bool tokens_only = false);
 
 struct PFrameOut {
     uint8_t* split;
@@ -865,7 +865,7 @@ int so_encode_p_rows_ex(const uint8_t* cur, const uint8_t* const* refs, int nref
                         int32_t* out_tokens, int32_t* out_mae_num, uint8_t* out_recon, int32_t* out_sse,
                         int32_t* scratch, void* stream) {
     const char* fn = "so_encode_p_rows_ex";
-    if (me_mode == SO_ME_FULL && !fme && !qp_map && !(flags & SO_REUSE_ME))
+    if (me_mode == SO_ME_FULL && !fme && !qp_map && !(flags & (SO_REUSE_ME | SO_TOKENS_ONLY)))
         return so_encode_p_rows(cur, refs, nref, H, W, bs, sr, by0, by1, qp_rd, qp_row, vbs, lam, out_split, out_mv,
                                 out_qtc, out_tokens, out_mae_num, out_recon, out_sse, scratch, stream);
     SO_TRY(check_geom(fn, H, W, bs, vbs));
@@ -890,7 +890,7 @@ int so_encode_p_rows_ex(const uint8_t* cur, const uint8_t* const* refs, int nref
         if (fme) SO_NEED(fme_planes, fn);
     } else if (me_mode == SO_ME_FULL && !fme && use_fused(bs, sr, vbs, nref)) {
         return p_tile_launch(cur, rs, H, W, by0, by1, qp_rd, qp_row, qp_map, best, out_split, out_mv, out_qtc,
-                             out_tokens, out_mae_num, out_recon, out_sse, st);
+                             out_tokens, out_mae_num, out_recon, out_sse, st, (flags & SO_TOKENS_ONLY) != 0);
     } else {
         SO_TRY(me_ex(fn, cur, refs, nref, rs, H, W, bs, sr, by0, by1, me_mode, fme, fme_wrap, fme_planes, best, sub,
                      st));

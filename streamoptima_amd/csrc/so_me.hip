@@ -1161,7 +1161,7 @@ struct PHalo {
 // The exact transform path of one block: 16 lanes (l = row) run scipy.fftpack's pocketfft
 // DCT-II / DCT-III sequence in FP64 (so_dct.h) -- the arithmetic of inter_tq_kernel<16,
 // false, false>.  `scratch` = 16 x 17 doubles of LDS owned by the calling lanes.
-template <class G, bool SC1, bool HALO = false>
+template <class G, bool SC1, bool HALO = false, bool TOK = false>
 SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, int byt0, int nbx, int by0, int by1,
                        int W, int qp_rd, const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map,
                        const PFrameOut& o, const PHalo& hl = PHalo{}) {
@@ -1201,6 +1201,10 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
             q[c] = (int)(uint32_t)__builtin_bit_cast(
                 uint64_t, __builtin_amdgcn_ldexp(__builtin_rint(tcr[c]), -q_exp_fast<16>(l, c, qpr)) + kRne);
         const int tok = block_tokens<16>(nullptr, l, q);
+        if constexpr (TOK) {   // pass 1 of two-pass RC: the token count is all that is used
+            if (l == 0) o.tokens[b] = tok;
+            return;
+        }
         store_row_i16<16>(o.qtc + b * 256 + l * 16, q);
         double dq[16], rd[16];
         dequant_row_i<16>(q, l, qpr, dq);
@@ -1265,7 +1269,7 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
 // write-through (global_store sc1), so another XCD that later reads them (p_run_kernel's
 // next frame) gets them from memory without a release fence.  Ends with every wave's
 // stores retired (s_waitcnt vmcnt(0)) and a workgroup barrier.  `pre`: as sea2_tile's.
-template <class G, bool SC1, class Pre = NoPre, bool HALO = false>
+template <class G, bool SC1, class Pre = NoPre, bool HALO = false, bool TOK = false>
 SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur, const uint8_t* ref, int H, int W,
                        int by0, int by1, int qp_rd, const int32_t* __restrict__ qp_row,
                        const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best, const PFrameOut& o,
@@ -1305,7 +1309,7 @@ SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur
         const int wq = SO_TQ_MAP == 1 ? ((w & 1) ? 1 << 20 : w >> 1) : w;
         const int gq = wq * BPW + (ln >> 4);
         if (ln < 16 * BPW && gq < G::NBLK)
-            tq16_exact<G, SC1, HALO>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by0, by1, W, qp_rd, qp_row,
+            tq16_exact<G, SC1, HALO, TOK>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by0, by1, W, qp_rd, qp_row,
                                      qp_map, o, hl);
     }
     SO_SEA_STAMP(7, __builtin_amdgcn_s_memtime());
@@ -1486,7 +1490,7 @@ SO_DEV void tq16_pass2(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
 #ifndef SO_PTILE_NW
 #define SO_PTILE_NW 8
 #endif
-template <int NW>
+template <int NW, bool TOK = false>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE)))
 p_tile_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W, int by0, int by1, int qp_rd,
               const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best,
@@ -1494,7 +1498,8 @@ p_tile_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W, int by
     using G = Sea2GeoT<NW>;
     __shared__ PTileLds<G> S;
     SO_STAMP_REC_SET(g_sea_stamps ? g_sea_stamps + (size_t)blockIdx.x * 12 : nullptr);
-    ptile_body<G, false>(S, blockIdx.x, cur, refs.p[0], H, W, by0, by1, qp_rd, qp_row, qp_map, out_best, o);
+    ptile_body<G, false, NoPre, false, TOK>(S, blockIdx.x, cur, refs.p[0], H, W, by0, by1, qp_rd, qp_row, qp_map,
+                                            out_best, o);
 #ifdef SO_STAMPS
     const int tid = threadIdx.x;
     if (tid == 0) {   // tools/sea_stamps.py (STAMP_FUSED=1): epilogue = records + transforms
@@ -1512,13 +1517,17 @@ p_tile_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W, int by
 int p_tile_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int by0, int by1, int qp_rd,
                   const int32_t* qp_row, const int32_t* qp_map, int32_t* out_best, uint8_t* out_split,
                   int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon,
-                  int32_t* out_sse, hipStream_t st) {
+                  int32_t* out_sse, hipStream_t st, bool tokens_only) {
     const int nbx = W / 16, nrows = by1 - by0;
     if (nrows <= 0) return SO_OK;
     const dim3 grid(((nbx + Sea2Geo::TBX - 1) / Sea2Geo::TBX) * ((nrows + Sea2Geo::TBY - 1) / Sea2Geo::TBY));
-    const PFrameOut o{out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon, out_sse};
-    hipLaunchKernelGGL(p_tile_kernel<SO_PTILE_NW>, grid, dim3(SO_PTILE_NW * 64), 0, st, cur, refs, H, W, by0, by1,
-                       qp_rd, qp_row, qp_map, out_best, o);
+    const PFrameOut o{out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon, out_sse, nullptr};
+    if (tokens_only)
+        hipLaunchKernelGGL((p_tile_kernel<SO_PTILE_NW, true>), grid, dim3(SO_PTILE_NW * 64), 0, st, cur, refs, H, W,
+                           by0, by1, qp_rd, qp_row, qp_map, out_best, o);
+    else
+        hipLaunchKernelGGL((p_tile_kernel<SO_PTILE_NW, false>), grid, dim3(SO_PTILE_NW * 64), 0, st, cur, refs, H, W,
+                           by0, by1, qp_rd, qp_row, qp_map, out_best, o);
     return check_launch("p_tile_kernel");
 }
 

@@ -110,14 +110,16 @@ class Engine:
     def encode_p(self, cur: torch.Tensor, refs: list, qp_rd: int, qp_row=None,
                  out: FrameSymbols | None = None, qp_row_dev: torch.Tensor | None = None,
                  fme_wrap: bool = True, qp_map_dev: torch.Tensor | None = None,
-                 reuse_me: bool = False) -> FrameSymbols:
+                 reuse_me: bool = False, tokens_only: bool = False) -> FrameSymbols:
         """complete_inter_flow (Encoder.py:1644) for one frame; asynchronous.
         fme_wrap: see so_encode_p_rows_ex (False while refs hold the float64 start frame);
         qp_map_dev: per-block QP (ROI / two-pass RC); reuse_me: keep the ME records of the
-        previous encode_p of the same frame (pass 2)."""
+        previous encode_p of the same frame (pass 2); tokens_only: pass 1 of two-pass RC (only
+        the tokens and the ME records are guaranteed, SO_TOKENS_ONLY)."""
         return self.encode_p_rows(cur, refs, 0, self.nby, qp_rd, out or self.new_symbols(1),
                                   qp_row_dev if qp_row_dev is not None else self.qp_row_tensor(qp_row),
-                                  fme_wrap=fme_wrap, qp_map_dev=qp_map_dev, reuse_me=reuse_me, qp_row=qp_row)
+                                  fme_wrap=fme_wrap, qp_map_dev=qp_map_dev, reuse_me=reuse_me, qp_row=qp_row,
+                                  tokens_only=tokens_only)
 
     def encode_i(self, cur: torch.Tensor, qp_rd: int, qp_row=None, out: FrameSymbols | None = None,
                  qp_row_dev: torch.Tensor | None = None, qp_map_dev: torch.Tensor | None = None) -> FrameSymbols:
@@ -156,7 +158,8 @@ class Engine:
 
     def encode_p_rows(self, cur, refs, by0: int, by1: int, qp_rd: int, out: FrameSymbols,
                       qp_row_dev: torch.Tensor | None = None, fme_wrap: bool = True,
-                      qp_map_dev: torch.Tensor | None = None, reuse_me: bool = False, qp_row=None) -> FrameSymbols:
+                      qp_map_dev: torch.Tensor | None = None, reuse_me: bool = False, qp_row=None,
+                      tokens_only: bool = False) -> FrameSymbols:
         """so_encode_p_rows(_ex): block rows [by0, by1) of a P-frame; asynchronous."""
         self._check_plane(cur, "cur")
         for k, r in enumerate(refs):
@@ -164,7 +167,7 @@ class Engine:
         if not 1 <= len(refs) <= _lib.MAX_REF:
             raise ValueError(f"nRefFrames must be in [1, {_lib.MAX_REF}]")
         st = _lib.stream_handle(self.device)
-        if self.me_mode == _lib.ME_FULL and not self.fme and qp_map_dev is None and not reuse_me:
+        if self.me_mode == _lib.ME_FULL and not self.fme and qp_map_dev is None and not reuse_me and not tokens_only:
             rc = self.lib.so_encode_p_rows(
                 cur.data_ptr(), _lib.ref_array(refs), len(refs), self.h, self.w, self.bs, self.sr, int(by0), int(by1),
                 int(qp_rd), _lib.ptr(qp_row_dev), int(self.vbs), self.lam, out.split.data_ptr(), out.mv.data_ptr(),
@@ -176,7 +179,7 @@ class Engine:
             rc = self.lib.so_encode_p_rows_ex(
                 cur.data_ptr(), _lib.ref_array(refs), len(refs), self.h, self.w, self.bs, self.sr, int(by0), int(by1),
                 int(qp_rd), _lib.ptr(qp_row_dev), _lib.ptr(qp_map_dev), int(self.vbs), self.lam, self.me_mode,
-                int(self.fme), int(bool(fme_wrap)), _lib.ptr(ws), _lib.REUSE_ME if reuse_me else 0,
+                int(self.fme), int(bool(fme_wrap)), _lib.ptr(ws), (_lib.REUSE_ME if reuse_me else 0) | (_lib.TOKENS_ONLY if tokens_only else 0),
                 out.split.data_ptr(), out.mv.data_ptr(), out.qtc.data_ptr(), out.tokens.data_ptr(),
                 out.mae_num.data_ptr(), out.recon.data_ptr(), _lib.ptr(out.sse), self.scratch.data_ptr(), st)
             _lib.check(rc, "so_encode_p_rows_ex")
