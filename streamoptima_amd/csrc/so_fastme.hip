@@ -159,12 +159,116 @@ me_fastpred_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, int H,
                              out_sub ? out_sub + (size_t)b * 16 : nullptr);
 }
 
+// ---- the serial chain, speculated by segments ----------------------------------------------
+// The chain mv(b) = F_b(mv(b - 1)) is a local descent: from different predictors it falls into
+// the same minimum within a few blocks.  So (1) one wavefront per segment of K blocks first
+// runs the chain over the WARM blocks before its segment from (0, 0, 0) -- its guess of the
+// segment's true predictor -- then the segment itself, storing every record; (2) one wavefront
+// walks the segments in order: segment s is exact iff its guessed predictor equals the last mv
+// of segment s - 1 (F is deterministic, so equal inputs give equal records), else it re-runs
+// the segment from the true predictor.  Bit-identical to the serial walk by construction; the
+// chain of 32,400 dependent steps (a 4K frame) becomes K + WARM steps per wavefront plus one
+// compare per segment and a K-step redo per wrong guess.
+constexpr int kFastSegMax = 4096;                 // segments per launch (the fix kernel's LDS)
+__device__ int32_t g_fast_seg[kFastSegMax * 6];   // per segment: guessed predictor, last mv
+// (a library-level buffer: serial fast-ME searches must not run concurrently on two streams)
+
+template <bool FME, int BS>
+SO_DEV Mvp fast_chain_mv(const uint8_t* __restrict__ cur, const FastRefs& R, int nref, int H, int W, int x, int y,
+                         Mvp mvp, int lane) {
+    int32_t rec[4];
+    const int i = BS == 16 ? lane >> 2 : lane >> 1, c = BS == 16 ? lane & 3 : lane & 1;
+    const bool act = BS == 16 || lane < 16;
+    fast_search<FME, BS == 16 ? 64 : 16>(cur, R, nref, H, W, x, y, BS, mvp, i, c, act, rec);
+    return Mvp{__shfl(rec[0], 0, 64), __shfl(rec[1], 0, 64), __shfl(rec[2], 0, 64)};
+}
+
+template <bool FME, bool SUB, int BS>
+__global__ void __launch_bounds__(64)
+me_fastchain_spec_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, int H, int W, int by0, int by1, int K,
+                         int warm, int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub) {
+    const int nbx = W / BS, nb = nbx * (by1 - by0);
+    const int lane = threadIdx.x;
+    const int s = blockIdx.x, b0 = s * K, b1 = b0 + K < nb ? b0 + K : nb;
+    Mvp mvp{0, 0, 0};
+    for (int b = (b0 - warm > 0 ? b0 - warm : 0); b < b0; ++b)
+        mvp = fast_chain_mv<FME, BS>(cur, R, nref, H, W, (b % nbx) * BS, (by0 + b / nbx) * BS, mvp, lane);
+    if (lane == 0) {
+        g_fast_seg[s * 6 + 0] = mvp.dx; g_fast_seg[s * 6 + 1] = mvp.dy; g_fast_seg[s * 6 + 2] = mvp.ref;
+    }
+    for (int b = b0; b < b1; ++b)
+        mvp = fast_block<FME, SUB, BS>(cur, R, nref, H, W, (b % nbx) * BS, (by0 + b / nbx) * BS, mvp, lane,
+                                       out_best + (size_t)b * 4, out_sub ? out_sub + (size_t)b * 16 : nullptr);
+    if (lane == 0) {
+        g_fast_seg[s * 6 + 3] = mvp.dx; g_fast_seg[s * 6 + 4] = mvp.dy; g_fast_seg[s * 6 + 5] = mvp.ref;
+    }
+}
+
+template <bool FME, bool SUB, int BS>
+__global__ void __launch_bounds__(64)
+me_fastchain_fix_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, int H, int W, int by0, int by1, int K,
+                        int nseg, int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub,
+                        int32_t* __restrict__ nfixed) {
+    __shared__ int32_t seg[kFastSegMax * 6];
+    const int nbx = W / BS, nb = nbx * (by1 - by0);
+    const int lane = threadIdx.x;
+    for (int i = lane; i < nseg * 6; i += 64) seg[i] = g_fast_seg[i];
+    __syncthreads();
+    Mvp truth{seg[3], seg[4], seg[5]};   // segment 0 started from the true (0, 0, 0)
+    int fixed = 0;
+    for (int s = 1; s < nseg; ++s) {
+        if (seg[s * 6] == truth.dx && seg[s * 6 + 1] == truth.dy && seg[s * 6 + 2] == truth.ref) {
+            truth = Mvp{seg[s * 6 + 3], seg[s * 6 + 4], seg[s * 6 + 5]};
+            continue;
+        }
+        ++fixed;   // wrong guess: the segment again from the true predictor
+        const int b0 = s * K, b1 = b0 + K < nb ? b0 + K : nb;
+        for (int b = b0; b < b1; ++b)
+            truth = fast_block<FME, SUB, BS>(cur, R, nref, H, W, (b % nbx) * BS, (by0 + b / nbx) * BS, truth, lane,
+                                             out_best + (size_t)b * 4, out_sub ? out_sub + (size_t)b * 16 : nullptr);
+    }
+    if (lane == 0 && nfixed) *nfixed = fixed;
+}
+
+__device__ int32_t g_fast_fixed;   // segments redone by the last chain (tools / tests)
+extern "C" int so_debug_fast_chain_fixed(int* out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fast_fixed), sizeof(int));
+}
+
 int me_fastpred_launch(const uint8_t* cur, const uint8_t* const* ptrs, int nptr, int nref, int H, int W, int bs,
                        int fme, int by0, int by1, int serial, int32_t* out_best, int32_t* out_sub, hipStream_t st) {
     FastRefs R{};
     for (int i = 0; i < nptr && i < 4 * kMaxRef; ++i) R.p[i] = ptrs[i];
     const int nb = (W / bs) * (by1 - by0);
     if (nb <= 0) return SO_OK;
+    const char* ser = getenv("SO_FASTME_SERIAL");   // A/B: the one-wavefront walk
+    if (serial && !(ser && atoi(ser) == 1)) {
+        int K = 32, warm = 32;
+        if (const char* e = getenv("SO_FASTME_K")) K = atoi(e) > 0 ? atoi(e) : K;
+        if (const char* e = getenv("SO_FASTME_WARM")) warm = atoi(e) >= 0 ? atoi(e) : warm;
+        if ((nb + K - 1) / K > kFastSegMax) K = (nb + kFastSegMax - 1) / kFastSegMax;
+        const int nseg = (nb + K - 1) / K;
+        int32_t* nfixed = nullptr;
+        if (hipGetSymbolAddress(reinterpret_cast<void**>(&nfixed), HIP_SYMBOL(g_fast_fixed)) != hipSuccess)
+            nfixed = nullptr;
+        const bool sub = out_sub != nullptr;
+#define SO_FASTCHAIN(F, S, B)                                                                                       \
+        do {                                                                                                        \
+            hipLaunchKernelGGL((me_fastchain_spec_kernel<F, S, B>), dim3(nseg), dim3(64), 0, st, cur, R, nref, H,   \
+                               W, by0, by1, K, warm, out_best, out_sub);                                            \
+            hipLaunchKernelGGL((me_fastchain_fix_kernel<F, S, B>), dim3(1), dim3(64), 0, st, cur, R, nref, H, W,    \
+                               by0, by1, K, nseg, out_best, out_sub, nfixed);                                       \
+        } while (0)
+        if (bs == 16) {
+            if (fme) { if (sub) SO_FASTCHAIN(true, true, 16); else SO_FASTCHAIN(true, false, 16); }
+            else { if (sub) SO_FASTCHAIN(false, true, 16); else SO_FASTCHAIN(false, false, 16); }
+        } else {
+            if (fme) { if (sub) SO_FASTCHAIN(true, true, 8); else SO_FASTCHAIN(true, false, 8); }
+            else { if (sub) SO_FASTCHAIN(false, true, 8); else SO_FASTCHAIN(false, false, 8); }
+        }
+#undef SO_FASTCHAIN
+        return check_launch("me_fastchain_kernel");
+    }
     const dim3 grid(serial ? 1 : (nb + 3) / 4), blk(serial ? 64 : 256);
     const bool sub = out_sub != nullptr;
 #define SO_FASTPRED(F, S, B)                                                                                 \

@@ -171,3 +171,30 @@ def test_4k120_poisoned_outputs(gpu):
     fx = FIX["4k120"]
     bad = [i for i, s in enumerate(res["symbols"]) if symbols_digest(s) != fx["frame_sha256"][i]]
     assert not bad, bad
+
+
+@pytest.mark.parametrize("vbs,fme", [(False, False), (True, False), (False, True), (True, True)])
+def test_fast_me_chain_speculation_matches_serial_walk(gpu, monkeypatch, vbs, fme):
+    """fast_me mode 0 (Encoder.py:719-742, the predictor chain of :462-585): the segmented
+    speculative chain (one wavefront per 32-block segment, warm-up guess, in-order check and
+    redo) against the one-wavefront serial walk (SO_FASTME_SERIAL=1), frame by frame, on
+    1920x1088 with and without VBS / FME -- and with no warm-up and 8-block segments, where
+    nearly every guess is wrong and the redo path carries the result."""
+    from streamoptima_amd.Encoder import Y_Video_codec
+    from streamoptima_amd.digest import symbols_digest
+    from streamoptima_amd.engine import alloc_planes
+    from streamoptima_amd.synth import synth_sequence_torch
+    h, w, f = 1088, 1920, 3
+    codec = Y_Video_codec(h, w, f, 16, 16, 4, f, 0, 0.015, vbs, fast_me=True, FMEEnable=fme, device=gpu)
+    fr = alloc_planes(f, h, w, gpu)
+    fr.copy_(synth_sequence_torch(f, h, w, seed=11, device=gpu))
+
+    def run():
+        return [symbols_digest(s) for s in codec.encode_device(fr, f)["symbols"]]
+    monkeypatch.setenv("SO_FASTME_SERIAL", "1")
+    exp = run()
+    monkeypatch.delenv("SO_FASTME_SERIAL")
+    assert run() == exp
+    monkeypatch.setenv("SO_FASTME_WARM", "0")
+    monkeypatch.setenv("SO_FASTME_K", "8")
+    assert run() == exp
