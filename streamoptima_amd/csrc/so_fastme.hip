@@ -221,11 +221,20 @@ me_fastchain_fix_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, i
             truth = Mvp{seg[s * 6 + 3], seg[s * 6 + 4], seg[s * 6 + 5]};
             continue;
         }
-        ++fixed;   // wrong guess: the segment again from the true predictor
+        // wrong guess: the segment again from the true predictor, until the true chain meets
+        // the speculated one -- from a block whose true mv equals the stored (speculated) mv,
+        // every later block of the segment already had the true predictor
+        ++fixed;
         const int b0 = s * K, b1 = b0 + K < nb ? b0 + K : nb;
-        for (int b = b0; b < b1; ++b)
+        bool joined = false;
+        for (int b = b0; b < b1 && !joined; ++b) {
+            const int32_t* ob = out_best + (size_t)b * 4;
+            const int odx = ob[0], ody = ob[1], oref = ob[2];   // the speculated record (before the store)
             truth = fast_block<FME, SUB, BS>(cur, R, nref, H, W, (b % nbx) * BS, (by0 + b / nbx) * BS, truth, lane,
                                              out_best + (size_t)b * 4, out_sub ? out_sub + (size_t)b * 16 : nullptr);
+            joined = truth.dx == odx && truth.dy == ody && truth.ref == oref;
+        }
+        if (joined) truth = Mvp{seg[s * 6 + 3], seg[s * 6 + 4], seg[s * 6 + 5]};
     }
     if (lane == 0 && nfixed) *nfixed = fixed;
 }
