@@ -681,7 +681,10 @@ struct NoPre {
 // `pre` runs (on every wave) after the current tile is staged and before the first
 // reference's window is read: p_run_kernel waits there for the reference's tiles, so the
 // current-tile staging overlaps that wait.
-template <class G, class Pre = NoPre>
+template <class G>
+SO_DEV void sea2_subblocks(const Sea2Lds& L, int u, int bxl, int byl, int x, int y, int W, int H, int r, int tid);
+
+template <class G, class Pre = NoPre, bool VBS = false>
 SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cur, const RefSet& refs, int nref,
                       int H, int W, int by0, int by1, int probe, const Pre& pre = Pre()) {
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RP = G::RP, NT = G::NT;
@@ -709,7 +712,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
     SO_SEA_STAMP(1, __builtin_amdgcn_s_memtime());
 #endif
 
-    for (int i = tid; i < G::NBLK; i += G::NTHREADS) keys[i] = kNoKey;
+    for (int i = tid; i < G::NBLK * (VBS ? 5 : 1); i += G::NTHREADS) keys[i] = kNoKey;
     // interior window (uniform): thread = (row, column phase) with immediate per-dword offsets
     constexpr int WTPR = G::NTHREADS / G::WR, WNPT = (RP + WTPR - 1) / WTPR;
     static_assert(G::NTHREADS % G::WR == 0, "window staging");
@@ -1023,6 +1026,14 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             best = wave_min_u64_dpp(best);
             if (lane == 0 && best < keys[u]) keys[u] = best;
         }
+        if constexpr (VBS) {   // the sub-blocks, after their block (its best mv bounds them too)
+#pragma unroll 1
+            for (int u = wave; u < G::NBLK; u += G::NW) {
+                const int bxl = u % TBX, byl = u / TBX;
+                if (bx0 + bxl >= nbx || byt0 + byl >= by1) continue;   // wave-uniform
+                sea2_subblocks<G>(L, u, bxl, byl, x0 + bxl * 16, y0 + byl * 16, W, H, r, tid);
+            }
+        }
     }
     __syncthreads();
 }
@@ -1065,6 +1076,204 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
         SO_SEA_STAMP(9, ((unsigned long long)st[0] << 32) | st[1]);
     }
 #endif
+}
+
+// ---- VBS: exact SEA for the four 8x8 sub-blocks (me_sea2_vbs_kernel) -------------------------
+// The sub-block searches of inter_prediction (Encoder.py:512-544: find_best_match(sub, bs/2)
+// for blocks with x != 0 and y != 0) on the same LDS window and 4x4 byte sums as the block's
+// own SEA.  A sub-block covers 2 x 2 of the block's 4x4 cells: its bound is the block bound's
+// v_sad over the two cells of each of its two cell rows (the cell-sum dwords masked to bytes
+// 2a, 2a+1), SAD >= 16 sum|dq| - 4 * 15; U = the exact SAD of the smallest-bound candidate;
+// every valid candidate with bound <= U is evaluated exactly (four lanes per candidate), more
+// than CAP survivors take every valid candidate.  Candidate validity and the key are the
+// sub-block's own: 0 <= xs + dx < W - 8, 0 <= ys + dy < H - 8; (SAD, |dx|+|dy|, ref, scan).
+template <class G>
+SO_DEV void sea2_subblocks(const Sea2Lds& L, int u, int bxl, int byl, int x, int y, int W, int H, int r, int tid) {
+    constexpr int SR = G::SR, NT = G::NT, RP = G::RP, B4P = G::B4P, CAP = G::CAP, CPD = G::CPD;
+    if (x == 0 || y == 0) return;   // no sub-block search there (Encoder.py:512); uniform
+    int lane = tid & 63;
+    asm volatile("" : "+v"(lane));
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int xi = lane & 31, hh = lane >> 5;
+    const int d2 = lane < 33 ? lane : 32;
+    uint32_t A[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) A[j] = L.a4[u * 4 + j];
+    const int cB = bxl * 16 + xi;
+    const int lb0 = (byl * 16 + 16 * hh) * B4P + (cB & 3) * G::WD + (cB >> 2);
+    const uint32_t bsh = (uint32_t)lb0 & 3;
+    int lo1 = lb0 >> 2;
+    asm volatile("" : "+v"(lo1));
+    lds_vu32p p1 = (lds_vu32p)(L.b4w + lo1);
+    int lo2 = ((byl * 16 + d2) * B4P + ((bxl * 16 + 32) >> 2)) >> 2;
+    asm volatile("" : "+v"(lo2));
+    lds_vu32p p2 = (lds_vu32p)(L.b4w + lo2);
+    uint16_t* const mylist = L.list + wave * CAP;
+    constexpr uint32_t kBig = 0x7FFFFFFFu;
+#pragma unroll 1
+    for (int bq = 0; bq < 2; ++bq) {
+        const int ys = y + 8 * bq;
+        // bounds of the two sub-blocks of this half: (LBq << 16) | t, left (a = 0) and right
+        uint32_t lbL[NT], lbR[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) { lbL[t] = (uint32_t)t; lbR[t] = (uint32_t)t; }
+        const uint32_t AL0 = A[2 * bq] & 0xFFFFu, AR0 = A[2 * bq] & 0xFFFF0000u;
+        const uint32_t AL1 = A[2 * bq + 1] & 0xFFFFu, AR1 = A[2 * bq + 1] & 0xFFFF0000u;
+#pragma unroll
+        for (int k = 0; k < NT + 4; ++k) {   // byte-sum row 8 bq + k: cell row 0 of t = k, row 1 of t = k - 4
+            const int row = 8 * bq + k;
+            const uint32_t w0 = p1[row * (B4P / 4)], w1 = p1[row * (B4P / 4) + 1];
+            const uint32_t P = __builtin_amdgcn_alignbyte(w1, w0, bsh);
+            const uint32_t PL = P & 0xFFFFu, PR = P & 0xFFFF0000u;
+            if (k < NT) {
+                lbL[k] = __builtin_amdgcn_sad_hi_u8(AL0, PL, lbL[k]);
+                lbR[k] = __builtin_amdgcn_sad_hi_u8(AR0, PR, lbR[k]);
+            }
+            if (k >= 4) {
+                lbL[k - 4] = __builtin_amdgcn_sad_hi_u8(AL1, PL, lbL[k - 4]);
+                lbR[k - 4] = __builtin_amdgcn_sad_hi_u8(AR1, PR, lbR[k - 4]);
+            }
+        }
+        uint32_t l2L = 0, l2R = 0;
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+            const uint32_t q = p2[(8 * bq + 4 * rr) * (B4P / 4)];
+            l2L = __builtin_amdgcn_sad_u8(A[2 * bq + rr] & 0xFFFFu, q & 0xFFFFu, l2L);
+            l2R = __builtin_amdgcn_sad_u8(A[2 * bq + rr] & 0xFFFF0000u, q & 0xFFFF0000u, l2R);
+        }
+        int dlo = SR - ys;              dlo = dlo < 0 ? 0 : dlo;
+        int dhi = H - 8 - ys + SR - 1;  dhi = dhi > 32 ? 32 : dhi;
+#pragma unroll 1
+        for (int a = 0; a < 2; ++a) {
+            const int xs = x + 8 * a, j = 2 * bq + a;
+            uint32_t lb[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) lb[t] = a ? lbR[t] : lbL[t];
+            const uint32_t lb2 = a ? l2R : l2L;
+            const bool xok = (xs + xi - 16 >= 0) && (xs + xi - 16 < W - 8);
+            const bool ok2 = lane < 33 && (xs + 16 < W - 8) && d2 >= dlo && d2 <= dhi;
+            {
+                const int tlo = dlo - 16 * hh, thi = dhi - 16 * hh;
+#pragma unroll
+                for (int t = 0; t < NT; ++t) lb[t] = (t < tlo || t > thi) ? kBig : lb[t];
+            }
+            uint32_t kt = lb[0];
+#pragma unroll
+            for (int t = 1; t < NT; ++t) kt = lb[t] < kt ? lb[t] : kt;
+            uint32_t kl = (xok && kt != kBig) ? ((kt >> 16) << 11) | (uint32_t)(xi * 33 + 16 * hh + (kt & 31))
+                                              : 0xFFFFFFFFu;
+            {
+                const uint32_t k2 = (lb2 << 11) | (uint32_t)(32 * 33 + d2);
+                kl = (ok2 && k2 < kl) ? k2 : kl;
+            }
+            const uint32_t kmin = wave_min_u32(kl);
+            if (kmin == 0xFFFFFFFFu) continue;   // no valid candidate: the sub key stays none
+            const int cs = (int)(kmin & 2047), cdx = cs / 33, cdi = cs - cdx * 33;
+            const int crow0 = (byl * 16 + 8 * bq) * CPD + bxl * 4 + 2 * a;   // sub-block in curt (dwords)
+            uint32_t U;
+            {
+                const int row = (lane >> 1) & 7, kk = lane & 1;
+                const uint32_t w = win_u32<RP>(L.win, byl * 16 + 8 * bq + cdi + row, bxl * 16 + 8 * a + cdx + 4 * kk);
+                const uint32_t sd = __builtin_amdgcn_sad_u8(L.curt[crow0 + row * CPD + kk], w, 0u);
+                U = wave_sum_u32(lane < 16 ? sd : 0u);
+            }
+            {   // the block's best mv so far (this reference): valid for its sub-blocks too
+                const unsigned long long kb = L.keys[u];
+                if (kb != kNoKey && (int)((kb >> 16) & 0xFF) == r) {
+                    const int bs_ = (int)(kb & 0xFFFF), bdx = bs_ / 33, bdi = bs_ - bdx * 33;
+                    const int row = (lane >> 1) & 7, kk = lane & 1;
+                    const uint32_t w = win_u32<RP>(L.win, byl * 16 + 8 * bq + bdi + row, bxl * 16 + 8 * a + bdx + 4 * kk);
+                    const uint32_t sd = __builtin_amdgcn_sad_u8(L.curt[crow0 + row * CPD + kk], w, 0u);
+                    const uint32_t Ub = wave_sum_u32(lane < 16 ? sd : 0u);
+                    U = Ub < U ? Ub : U;
+                }
+            }
+            const uint32_t qU = (U + 60) >> 4;
+            int thr = xok ? (int)((qU << 16) | 0xFFFFu) : -1;
+            asm volatile("" : "+v"(thr));
+            const int cbase = xi * 33 + 16 * hh;
+            uint32_t nsur = 0;
+#pragma unroll
+            for (int t = 0; t <= NT; ++t) {
+                const bool pass = t < NT ? (int)lb[t] <= thr : (ok2 && lb2 <= qU);
+                const uint64_t bal = __builtin_amdgcn_ballot_w64(pass);
+                if (bal) {
+                    const uint32_t pos = nsur + lane_prefix(bal);
+                    if (pass && pos < (uint32_t)CAP) mylist[pos] = (uint16_t)(t < NT ? cbase + t : 32 * 33 + d2);
+                    nsur += (uint32_t)__builtin_popcountll(bal);
+                }
+            }
+            const bool dense = nsur > (uint32_t)CAP;   // every candidate instead of the list
+            const uint32_t ncand = dense ? 33u * 33u : nsur;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // four lanes (a quad) per candidate, rows 2q, 2q + 1 of the sub-block per lane
+            const int sidx = lane >> 2, q = lane & 3;
+            uint32_t cr[2][2];
+#pragma unroll
+            for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+                for (int k = 0; k < 2; ++k) cr[rr][k] = L.curt[crow0 + (2 * q + rr) * CPD + k];
+            uint64_t best = kNoKey;
+#pragma unroll 1
+            for (uint32_t s0 = 0; s0 < ncand; s0 += 16) {
+                const uint32_t ci = s0 + (uint32_t)sidx;
+                bool act = ci < ncand;
+                int cand = act ? (dense ? (int)ci : (int)mylist[ci]) : cs;
+                const int dxi = cand / 33, di = cand - dxi * 33;
+                if (dense)
+                    act = act && xs + dxi - 16 >= 0 && xs + dxi - 16 < W - 8 && ys + di - 16 >= 0 && ys + di - 16 < H - 8;
+                const int col = bxl * 16 + 8 * a + dxi;
+                const int row0 = byl * 16 + 8 * bq + di + 2 * q;
+                uint32_t sad = 0;
+#pragma unroll
+                for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+                    for (int k = 0; k < 2; ++k)
+                        sad = __builtin_amdgcn_sad_u8(cr[rr][k], win_u32<RP>(L.win, row0 + rr, col + 4 * k), sad);
+                sad = quad_sum_u32(sad);
+                const int dx = dxi - 16, dy = di - 16;
+                const uint64_t key = me_key(sad, (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)), (uint32_t)r,
+                                            (uint32_t)cand);
+                best = (act && key < best) ? key : best;
+            }
+            best = wave_min_u64_dpp(best);
+            if (lane == 0 && best < L.keys[G::NBLK + 4 * u + j]) L.keys[G::NBLK + 4 * u + j] = best;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // mylist reused by the next sub-block
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+}
+
+__global__ void __launch_bounds__(Sea2Geo::NTHREADS) __attribute__((amdgpu_waves_per_eu(SO_SEA2_WPE)))
+me_sea2_vbs_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
+                   int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub) {
+    using G = Sea2Geo;
+    constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RP = G::RP, B4P = G::B4P;
+    __shared__ uint32_t win[G::WR * RP + 4];
+    __shared__ uint32_t b4w[(G::B4RS * B4P + 4) / 4];
+    __shared__ uint32_t curt[G::TPY * G::CPD];
+    __shared__ uint32_t a4[G::NBLK * 4];
+    __shared__ uint16_t list[G::NW * G::CAP];
+    __shared__ uint32_t lcount[G::NW];
+    __shared__ unsigned long long keys[G::NBLK * 5];
+    __shared__ uint32_t st[2];
+    const Sea2Lds L{win, b4w, curt, a4, list, lcount, keys, st};
+    sea2_tile<Sea2Geo, NoPre, true>(L, blockIdx.x, cur, refs, nref, H, W, by0, by1, 0);
+    const int tid = threadIdx.x;
+    const int nbx = W / 16;
+    const int tiles_x = (nbx + TBX - 1) / TBX;
+    const int bx0 = (blockIdx.x % tiles_x) * TBX, byt0 = by0 + (blockIdx.x / tiles_x) * TBY;
+    for (int i = tid; i < G::NBLK * 5; i += G::NTHREADS) {
+        const int blk = i < G::NBLK ? i : (i - G::NBLK) >> 2;
+        const int gbx = bx0 + blk % TBX, gby = byt0 + blk / TBX;
+        if (gbx >= nbx || gby >= by1) continue;
+        const size_t b = (size_t)(gby - by0) * nbx + gbx;
+        if (i < G::NBLK) decode_key(keys[i], SR, out_best + b * 4);
+        else decode_key(keys[i], SR, out_sub + (b * 4 + ((i - G::NBLK) & 3)) * 4);
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2189,6 +2398,16 @@ int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, in
             hipLaunchKernelGGL(me_sea2_kernel, sgrid, dim3(Sea2Geo::NTHREADS), 0, st, cur, refs, nref, H, W, by0, by1,
                                out_best, pr ? atoi(pr) : 0);
             return check_launch("me_sea2_kernel");
+        }
+        // VBS: the block + sub-block SEA is opt-in (SO_ME_IMPL=sea_vbs): measured slower than the
+        // dense wave search, whose v_sad_u8 work yields the four sub-block SADs for free
+        // (4K VBS GOP 8.36 vs 5.94 ms)
+        const bool sea_vbs = impl && strcmp(impl, "sea_vbs") == 0;
+        if (sea_vbs && bs == 16 && out_sub != nullptr) {
+            const dim3 sgrid(((nbx + Sea2Geo::TBX - 1) / Sea2Geo::TBX) * ((nrows + Sea2Geo::TBY - 1) / Sea2Geo::TBY));
+            hipLaunchKernelGGL(me_sea2_vbs_kernel, sgrid, dim3(Sea2Geo::NTHREADS), 0, st, cur, refs, nref, H, W, by0,
+                               by1, out_best, out_sub);
+            return check_launch("me_sea2_vbs_kernel");
         }
         const bool sub = out_sub != nullptr;
         const int tbx = 128 / bs;

@@ -198,3 +198,23 @@ def test_fast_me_chain_speculation_matches_serial_walk(gpu, monkeypatch, vbs, fm
     monkeypatch.setenv("SO_FASTME_WARM", "0")
     monkeypatch.setenv("SO_FASTME_K", "8")
     assert run() == exp
+
+
+def test_vbs_sea_matches_dense_search(gpu, monkeypatch):
+    """VBSEnable: the block + sub-block SEA (me_sea2_vbs_kernel, SO_ME_IMPL=sea_vbs) against the dense wave search
+    (SO_ME_IMPL=dense, me_wave_kernel<16, true>) frame by frame on a 1920x1088 GOP -- block
+    and sub-block MVs, split decisions, QTC, reconstruction (Encoder.py:512-578)."""
+    from streamoptima_amd.Encoder import Y_Video_codec
+    from streamoptima_amd.digest import symbols_digest
+    from streamoptima_amd.engine import alloc_planes
+    from streamoptima_amd.synth import synth_sequence_torch
+    h, w, f = 1088, 1920, 4
+    codec = Y_Video_codec(h, w, f, 16, 16, 4, f, 0, 0.015, True, device=gpu)
+    fr = alloc_planes(f, h, w, gpu)
+    fr.copy_(synth_sequence_torch(f, h, w, seed=13, device=gpu))
+    monkeypatch.setenv("SO_ME_IMPL", "dense")
+    exp = [symbols_digest(s) for s in codec.encode_device(fr, f)["symbols"]]
+    monkeypatch.setenv("SO_ME_IMPL", "sea_vbs")   # opt-in: slower than the dense search
+    got = codec.encode_device(fr, f)
+    assert [symbols_digest(s) for s in got["symbols"]] == exp
+    assert int(sum(int(s.split.sum()) for s in got["symbols"][1:])) > 0   # some blocks split
