@@ -8,7 +8,9 @@ already resident in HBM; bs 16, full-search ME +-16, QP 4, intra_mode 0, nRefFra
 VBS off):
   N = 1 (default --config 4k): configs[2], one 4K 30-frame I+P GOP per step; the line also
         carries a `records.1080p` entry for configs[1] (1920x1080 padded to 1088 rows),
-        measured the same way in the same run.
+        measured the same way in the same run, and `records.<cfg>_x<k>gop` entries: k
+        independent GOPs per step with their P-runs interleaved in one persistent launch
+        (--gops-in-flight, default 2; a GOP stream's throughput, every GOP parity-checked).
   N > 1 (default --config 4k120): configs[3], ONE 4K 120-frame GOP per step, sharded over
         the N ranks (strong scaling): by default the frame pipeline (rank g encodes frames
         g, g+N, ..., each reference arriving tile by tile from the previous rank over xGMI;
