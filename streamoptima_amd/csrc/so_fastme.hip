@@ -102,6 +102,89 @@ SO_DEV void fast_search(const uint8_t* __restrict__ cur, const FastRefs& R, int 
     }
 }
 
+// The nine candidates' bytes of one lane for the search of fast_search (clamped addresses).
+template <bool FME>
+SO_DEV void fast_loads(const FastRefs& R, int r, int H, int W, int X, int Y, Mvp mvp, int lane_i, int lane_c,
+                       uint32_t (&wv)[9]) {
+#pragma unroll
+    for (int ci = 0; ci < 9; ++ci) {
+        const int px = X + mvp.dx - 1 + ci / 3, py = Y + mvp.dy - 1 + ci % 3;
+        const uint8_t* p;
+        if constexpr (FME) {
+            int row = (py >> 1) + lane_i, col = (px >> 1) + 4 * lane_c;
+            row = row < 0 ? 0 : (row > H - 1 ? H - 1 : row);
+            col = col < 0 ? 0 : (col > W - 4 ? W - 4 : col);
+            p = R.p[4 * r + 2 * (py & 1) + (px & 1)] + (size_t)row * W + col;
+        } else {
+            int row = py + lane_i, col = px + 4 * lane_c;
+            row = row < 0 ? 0 : (row > H - 1 ? H - 1 : row);
+            col = col < 0 ? 0 : (col > W - 4 ? W - 4 : col);
+            p = R.p[r] + (size_t)row * W + col;
+        }
+        wv[ci] = unaligned_u32(p);
+    }
+}
+
+// fast_search's key update for one reference from the loaded bytes
+template <bool FME, int G>
+SO_DEV uint32_t fast_keys(uint32_t best, uint32_t cw, const uint32_t (&wv)[9], int r, int H, int W, int X, int Y, int n,
+                          Mvp mvp, bool act) {
+    const int PW = FME ? 2 * W - 1 : W, PH = FME ? 2 * H - 1 : H;
+#pragma unroll
+    for (int ci = 0; ci < 9; ++ci) {
+        const int px = X + mvp.dx - 1 + ci / 3, py = Y + mvp.dy - 1 + ci % 3;
+        const bool ok = 0 <= px && px < PW - n && 0 <= py && py < PH - n && px + 2 * n < PW - n && py + 2 * n < PH - n;
+        const uint32_t sv = group_sum_u32<G>(act ? __builtin_amdgcn_sad_u8(cw, wv[ci], 0u) : 0u);
+        const uint32_t key = (sv << 8) | (uint32_t)(r * 9 + ci);
+        best = (ok && key < best) ? key : best;
+    }
+    return best;
+}
+
+SO_DEV void fast_record(uint32_t best, Mvp mvp, int n, int32_t out[4]) {
+    if (best == 0xFFFFFFFFu) {
+        out[0] = mvp.dx; out[1] = mvp.dy; out[2] = mvp.ref; out[3] = 0;
+    } else {
+        const int c = (int)(best & 255), r = c / 9, ci = c % 9;
+        out[0] = mvp.dx - 1 + ci / 3; out[1] = mvp.dy - 1 + ci % 3; out[2] = r; out[3] = r * n * n;
+    }
+}
+
+// fast_block with the sub-block and block searches' loads issued together (one memory latency
+// per reference and chain step instead of two); same records.  bs 16 only.
+template <bool FME>
+SO_DEV Mvp fast_block_vbs16(const uint8_t* __restrict__ cur, const FastRefs& R, int nref, int H, int W, int x, int y,
+                            Mvp mvp, int lane, int32_t* __restrict__ ob, int32_t* __restrict__ os) {
+    const int k = FME ? 2 : 1;
+    const bool sub = x != 0 && y != 0;
+    const int j = lane >> 4, si = (lane >> 1) & 7, sc = lane & 1;   // sub-block j, its row / dword
+    const int xs = x + (j & 1) * 8, ys = y + (j >> 1) * 8;
+    const int fi = lane >> 2, fc = lane & 3;                        // block row / dword
+    const uint32_t cws = *reinterpret_cast<const uint32_t*>(cur + (size_t)(ys + si) * W + xs + 4 * sc);
+    const uint32_t cwf = *reinterpret_cast<const uint32_t*>(cur + (size_t)(y + fi) * W + x + 4 * fc);
+    uint32_t bs_ = 0xFFFFFFFFu, bf = 0xFFFFFFFFu;
+#pragma unroll 1
+    for (int r = 0; r < nref; ++r) {
+        uint32_t ws[9], wf[9];
+        if (sub) fast_loads<FME>(R, r, H, W, k * xs, k * ys, mvp, si, sc, ws);
+        fast_loads<FME>(R, r, H, W, k * x, k * y, mvp, fi, fc, wf);
+        if (sub) bs_ = fast_keys<FME, 16>(bs_, cws, ws, r, H, W, k * xs, k * ys, 8, mvp, true);
+        bf = fast_keys<FME, 64>(bf, cwf, wf, r, H, W, k * x, k * y, 16, mvp, true);
+    }
+    if (sub) {
+        int32_t rec[4];
+        fast_record(bs_, mvp, 8, rec);
+        const int e = lane - 16 * j;   // lanes 16j .. 16j+3 store the sub-block's record
+        const int32_t v = e == 0 ? rec[0] : e == 1 ? rec[1] : e == 2 ? rec[2] : rec[3];
+        if (e >= 0 && e < 4) os[j * 4 + e] = v;
+    }
+    int32_t rec[4];
+    fast_record(bf, mvp, 16, rec);
+    const int32_t v = lane == 0 ? rec[0] : lane == 1 ? rec[1] : lane == 2 ? rec[2] : rec[3];
+    if (lane < 4) ob[lane] = v;
+    return Mvp{__shfl(rec[0], 0, 64), __shfl(rec[1], 0, 64), __shfl(rec[2], 0, 64)};
+}
+
 // bs 16: full block on 64 lanes (row l >> 2, dword l & 3); sub-blocks on the four 16-lane
 // rows (sub j = l >> 4, row (l >> 1) & 7, dword l & 1).  bs 8: full block on lanes 0..15
 // (row l >> 1, dword l & 1); 4x4 sub-blocks on 4 lanes each (sub l >> 2, row l & 3).
@@ -109,6 +192,7 @@ SO_DEV void fast_search(const uint8_t* __restrict__ cur, const FastRefs& R, int 
 template <bool FME, bool SUB, int BS>
 SO_DEV Mvp fast_block(const uint8_t* __restrict__ cur, const FastRefs& R, int nref, int H, int W, int x, int y,
                       Mvp mvp, int lane, int32_t* __restrict__ ob, int32_t* __restrict__ os) {
+    if constexpr (SUB && BS == 16) return fast_block_vbs16<FME>(cur, R, nref, H, W, x, y, mvp, lane, ob, os);
     constexpr int SBS = BS / 2;
     if constexpr (SUB) {
         if (x != 0 && y != 0) {
@@ -170,7 +254,7 @@ me_fastpred_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, int H,
 // chain of 32,400 dependent steps (a 4K frame) becomes K + WARM steps per wavefront plus one
 // compare per segment and a K-step redo per wrong guess.
 constexpr int kFastSegMax = 4096;                 // segments per launch (the fix kernel's LDS)
-__device__ int32_t g_fast_seg[kFastSegMax * 6];   // per segment: guessed predictor, last mv
+__device__ int32_t g_fast_seg[2][kFastSegMax * 6];   // per segment: guessed predictor, last mv (ping-pong)
 // (a library-level buffer: serial fast-ME searches must not run concurrently on two streams)
 
 template <bool FME, int BS>
@@ -194,25 +278,57 @@ me_fastchain_spec_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, 
     for (int b = (b0 - warm > 0 ? b0 - warm : 0); b < b0; ++b)
         mvp = fast_chain_mv<FME, BS>(cur, R, nref, H, W, (b % nbx) * BS, (by0 + b / nbx) * BS, mvp, lane);
     if (lane == 0) {
-        g_fast_seg[s * 6 + 0] = mvp.dx; g_fast_seg[s * 6 + 1] = mvp.dy; g_fast_seg[s * 6 + 2] = mvp.ref;
+        g_fast_seg[0][s * 6 + 0] = mvp.dx; g_fast_seg[0][s * 6 + 1] = mvp.dy; g_fast_seg[0][s * 6 + 2] = mvp.ref;
     }
     for (int b = b0; b < b1; ++b)
         mvp = fast_block<FME, SUB, BS>(cur, R, nref, H, W, (b % nbx) * BS, (by0 + b / nbx) * BS, mvp, lane,
                                        out_best + (size_t)b * 4, out_sub ? out_sub + (size_t)b * 16 : nullptr);
     if (lane == 0) {
-        g_fast_seg[s * 6 + 3] = mvp.dx; g_fast_seg[s * 6 + 4] = mvp.dy; g_fast_seg[s * 6 + 5] = mvp.ref;
+        g_fast_seg[0][s * 6 + 3] = mvp.dx; g_fast_seg[0][s * 6 + 4] = mvp.dy; g_fast_seg[0][s * 6 + 5] = mvp.ref;
+    }
+}
+
+// A correction round, every segment in parallel: a segment whose guess differs from the
+// previous segment's last mv of the round before runs again from that mv (right whenever
+// the previous segment was right), so each round fixes the first wrong segment of every run
+// of wrong ones.  Reads buffer `src`, writes buffer 1 - src.
+template <bool FME, bool SUB, int BS>
+__global__ void __launch_bounds__(64)
+me_fastchain_round_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, int H, int W, int by0, int by1, int K,
+                          int src, int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub) {
+    const int nbx = W / BS, nb = nbx * (by1 - by0);
+    const int lane = threadIdx.x;
+    const int s = blockIdx.x, b0 = s * K, b1 = b0 + K < nb ? b0 + K : nb;
+    const int32_t* in = g_fast_seg[src];
+    int32_t* out = g_fast_seg[1 - src];
+    const int32_t* me = in + s * 6;
+    Mvp g{me[0], me[1], me[2]}, last{me[3], me[4], me[5]};
+    if (s > 0) {
+        const Mvp t{in[s * 6 - 3], in[s * 6 - 2], in[s * 6 - 1]};
+        if (t.dx != g.dx || t.dy != g.dy || t.ref != g.ref) {
+            g = t;
+            Mvp mvp = t;
+            for (int b = b0; b < b1; ++b)
+                mvp = fast_block<FME, SUB, BS>(cur, R, nref, H, W, (b % nbx) * BS, (by0 + b / nbx) * BS, mvp, lane,
+                                               out_best + (size_t)b * 4, out_sub ? out_sub + (size_t)b * 16 : nullptr);
+            last = mvp;
+        }
+    }
+    if (lane == 0) {
+        out[s * 6 + 0] = g.dx; out[s * 6 + 1] = g.dy; out[s * 6 + 2] = g.ref;
+        out[s * 6 + 3] = last.dx; out[s * 6 + 4] = last.dy; out[s * 6 + 5] = last.ref;
     }
 }
 
 template <bool FME, bool SUB, int BS>
 __global__ void __launch_bounds__(64)
 me_fastchain_fix_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, int H, int W, int by0, int by1, int K,
-                        int nseg, int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub,
+                        int nseg, int src, int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub,
                         int32_t* __restrict__ nfixed) {
     __shared__ int32_t seg[kFastSegMax * 6];
     const int nbx = W / BS, nb = nbx * (by1 - by0);
     const int lane = threadIdx.x;
-    for (int i = lane; i < nseg * 6; i += 64) seg[i] = g_fast_seg[i];
+    for (int i = lane; i < nseg * 6; i += 64) seg[i] = g_fast_seg[src][i];
     __syncthreads();
     Mvp truth{seg[3], seg[4], seg[5]};   // segment 0 started from the true (0, 0, 0)
     int fixed = 0;
@@ -252,9 +368,10 @@ int me_fastpred_launch(const uint8_t* cur, const uint8_t* const* ptrs, int nptr,
     if (nb <= 0) return SO_OK;
     const char* ser = getenv("SO_FASTME_SERIAL");   // A/B: the one-wavefront walk
     if (serial && !(ser && atoi(ser) == 1)) {
-        int K = 32, warm = 32;
+        int K = 32, warm = 32, rounds = 0;   // correction rounds: measured no gain
         if (const char* e = getenv("SO_FASTME_K")) K = atoi(e) > 0 ? atoi(e) : K;
         if (const char* e = getenv("SO_FASTME_WARM")) warm = atoi(e) >= 0 ? atoi(e) : warm;
+        if (const char* e = getenv("SO_FASTME_ROUNDS")) rounds = atoi(e) >= 0 ? atoi(e) : rounds;
         if ((nb + K - 1) / K > kFastSegMax) K = (nb + kFastSegMax - 1) / kFastSegMax;
         const int nseg = (nb + K - 1) / K;
         int32_t* nfixed = nullptr;
@@ -265,8 +382,11 @@ int me_fastpred_launch(const uint8_t* cur, const uint8_t* const* ptrs, int nptr,
         do {                                                                                                        \
             hipLaunchKernelGGL((me_fastchain_spec_kernel<F, S, B>), dim3(nseg), dim3(64), 0, st, cur, R, nref, H,   \
                                W, by0, by1, K, warm, out_best, out_sub);                                            \
+            for (int k = 0; k < rounds; ++k)                                                                        \
+                hipLaunchKernelGGL((me_fastchain_round_kernel<F, S, B>), dim3(nseg), dim3(64), 0, st, cur, R, nref, \
+                                   H, W, by0, by1, K, k & 1, out_best, out_sub);                                    \
             hipLaunchKernelGGL((me_fastchain_fix_kernel<F, S, B>), dim3(1), dim3(64), 0, st, cur, R, nref, H, W,    \
-                               by0, by1, K, nseg, out_best, out_sub, nfixed);                                       \
+                               by0, by1, K, nseg, rounds & 1, out_best, out_sub, nfixed);                           \
         } while (0)
         if (bs == 16) {
             if (fme) { if (sub) SO_FASTCHAIN(true, true, 16); else SO_FASTCHAIN(true, false, 16); }

@@ -17,7 +17,8 @@ dev = torch.device("cuda:0")
 h, w = 2160, 3840
 fr = alloc_planes(3, h, w, dev)
 fr.copy_(synth_sequence_torch(3, h, w, seed=0, device=dev))
-eng = Engine(h, w, 16, 16, False, 0.015, dev, me_mode=_lib.ME_FAST)
+import os
+eng = Engine(h, w, 16, 16, os.environ.get("PROBE_VBS") == "1", 0.015, dev, me_mode=_lib.ME_FAST)
 i0 = eng.encode_i(fr[0], 4)
 p1 = eng.encode_p(fr[1], [i0.recon], 4)
 out = eng.new_symbols(1)
@@ -36,7 +37,7 @@ print(json.dumps({"ms_per_p_frame_min_median": [round(ts[0] * 1e3, 3), round(ts[
 
 
 def main():
-    for v in ["SO_FASTME_SERIAL=1", ""] + sys.argv[1:]:
+    for v in ["SO_FASTME_SERIAL=1", ""] + sys.argv[1:]:   # PROBE_VBS=1 in a variant: VBSEnable
         env = dict(os.environ)
         for kv in v.split(","):
             if kv:
