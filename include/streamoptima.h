@@ -85,7 +85,8 @@ int so_inter_tq_recon(const uint8_t* cur, const uint8_t* const* refs, int nref, 
                       int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
                       int32_t* out_mae_num, uint8_t* out_recon, int32_t* out_sse, void* stream);
 
-/* int32 elements of scratch so_encode_p_frame needs: nb*4 (+ nb*16 with vbs) */
+/* int32 elements of scratch so_encode_p_frame needs: nb*4 (+ nb*16 with vbs), + 49,152 for the
+ * segment records of the speculated fast-ME predictor chain (so_encode_p_rows_ex) */
 size_t so_p_frame_scratch_elems(int H, int W, int bs, int vbs);
 
 /*

@@ -31,7 +31,9 @@ int me_fme_launch(const uint8_t* cur, const uint8_t* planes, size_t pstride, int
                   int32_t* out_best, int32_t* out_sub, hipStream_t st);
 int fme_planes_launch(const uint8_t* ref, int H, int W, int wrap, uint8_t* out, size_t pstride, hipStream_t st);
 int me_fastpred_launch(const uint8_t* cur, const uint8_t* const* ptrs, int nptr, int nref, int H, int W, int bs,
-                       int fme, int by0, int by1, int serial, int32_t* out_best, int32_t* out_sub, hipStream_t st);
+                       int fme, int by0, int by1, int serial, int32_t* out_best, int32_t* out_sub, int32_t* seg_ws,
+                       hipStream_t st);
+constexpr size_t kFastSegWords = 2 * 4096 * 6;   // so_fastme.hip: the speculated chain's segment records
 int p_tile_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int by0, int by1, int qp_rd,
                   const int32_t* qp_row, const int32_t* qp_map, int32_t* out_best, uint8_t* out_split,
                   int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon,
@@ -360,7 +362,7 @@ int so_inter_tq_recon(const uint8_t* cur, const uint8_t* const* refs, int nref, 
 size_t so_p_frame_scratch_elems(int H, int W, int bs, int vbs) {
     if (bs <= 0) return 0;
     const size_t nb = (size_t)(W / bs) * (size_t)(H / bs);
-    return nb * 4 + (vbs ? nb * 16 : 0);
+    return nb * 4 + (vbs ? nb * 16 : 0) + kFastSegWords;
 }
 
 int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W, int bs, int sr,
@@ -804,7 +806,7 @@ int so_fme_planes(const uint8_t* ref, int H, int W, int wrap, uint8_t* out_plane
 // shared validation + dispatch of the ME variants into best / sub
 static int me_ex(const char* fn, const uint8_t* cur, const uint8_t* const* refs, int nref, const RefSet& rs, int H,
                  int W, int bs, int sr, int by0, int by1, int me_mode, int fme, int fme_wrap, uint8_t* planes,
-                 int32_t* best, int32_t* sub, hipStream_t st) {
+                 int32_t* best, int32_t* sub, hipStream_t st, int32_t* seg_ws = nullptr) {
     if (me_mode < SO_ME_FULL || me_mode > SO_ME_FAST_PAR) {
         set_error("%s: me_mode %d", fn, me_mode);
         return SO_E_INVALID;
@@ -842,7 +844,8 @@ static int me_ex(const char* fn, const uint8_t* cur, const uint8_t* const* refs,
         else
             ptrs[nptr++] = refs[r];
     }
-    return me_fastpred_launch(cur, ptrs, nptr, nfast, H, W, bs, fme, by0, by1, me_mode == SO_ME_FAST, best, sub, st);
+    return me_fastpred_launch(cur, ptrs, nptr, nfast, H, W, bs, fme, by0, by1, me_mode == SO_ME_FAST, best, sub, seg_ws,
+                              st);
 }
 
 int so_me_search_ex(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W, int bs, int sr,
@@ -893,7 +896,7 @@ int so_encode_p_rows_ex(const uint8_t* cur, const uint8_t* const* refs, int nref
                              out_tokens, out_mae_num, out_recon, out_sse, st, (flags & SO_TOKENS_ONLY) != 0);
     } else {
         SO_TRY(me_ex(fn, cur, refs, nref, rs, H, W, bs, sr, by0, by1, me_mode, fme, fme_wrap, fme_planes, best, sub,
-                     st));
+                     st, scratch + nbs * 4 + (vbs ? nbs * 16 : 0)));
     }
     return inter_tq_launch(cur, rs, fme ? fme_planes : nullptr, so_fme_plane_stride(H, W), H, W, bs, by0, by1, best,
                            sub, qp_rd, qp_row, qp_map, vbs, lam, out_split, out_mv, out_qtc, out_tokens, out_mae_num, out_recon,

@@ -254,8 +254,9 @@ me_fastpred_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, int H,
 // chain of 32,400 dependent steps (a 4K frame) becomes K + WARM steps per wavefront plus one
 // compare per segment and a K-step redo per wrong guess.
 constexpr int kFastSegMax = 4096;                 // segments per launch (the fix kernel's LDS)
-__device__ int32_t g_fast_seg[2][kFastSegMax * 6];   // per segment: guessed predictor, last mv (ping-pong)
-// (a library-level buffer: serial fast-ME searches must not run concurrently on two streams)
+// per segment: guessed predictor, last mv; two buffers (correction rounds ping-pong) in the
+// caller's scratch (kFastSegWords int32 after the ME records, so_p_frame_scratch_elems)
+constexpr int kFastSegBuf = kFastSegMax * 6;
 
 template <bool FME, int BS>
 SO_DEV Mvp fast_chain_mv(const uint8_t* __restrict__ cur, const FastRefs& R, int nref, int H, int W, int x, int y,
@@ -270,7 +271,8 @@ SO_DEV Mvp fast_chain_mv(const uint8_t* __restrict__ cur, const FastRefs& R, int
 template <bool FME, bool SUB, int BS>
 __global__ void __launch_bounds__(64)
 me_fastchain_spec_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, int H, int W, int by0, int by1, int K,
-                         int warm, int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub) {
+                         int warm, int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub,
+                         int32_t* __restrict__ seg) {
     const int nbx = W / BS, nb = nbx * (by1 - by0);
     const int lane = threadIdx.x;
     const int s = blockIdx.x, b0 = s * K, b1 = b0 + K < nb ? b0 + K : nb;
@@ -278,13 +280,13 @@ me_fastchain_spec_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, 
     for (int b = (b0 - warm > 0 ? b0 - warm : 0); b < b0; ++b)
         mvp = fast_chain_mv<FME, BS>(cur, R, nref, H, W, (b % nbx) * BS, (by0 + b / nbx) * BS, mvp, lane);
     if (lane == 0) {
-        g_fast_seg[0][s * 6 + 0] = mvp.dx; g_fast_seg[0][s * 6 + 1] = mvp.dy; g_fast_seg[0][s * 6 + 2] = mvp.ref;
+        seg[s * 6 + 0] = mvp.dx; seg[s * 6 + 1] = mvp.dy; seg[s * 6 + 2] = mvp.ref;
     }
     for (int b = b0; b < b1; ++b)
         mvp = fast_block<FME, SUB, BS>(cur, R, nref, H, W, (b % nbx) * BS, (by0 + b / nbx) * BS, mvp, lane,
                                        out_best + (size_t)b * 4, out_sub ? out_sub + (size_t)b * 16 : nullptr);
     if (lane == 0) {
-        g_fast_seg[0][s * 6 + 3] = mvp.dx; g_fast_seg[0][s * 6 + 4] = mvp.dy; g_fast_seg[0][s * 6 + 5] = mvp.ref;
+        seg[s * 6 + 3] = mvp.dx; seg[s * 6 + 4] = mvp.dy; seg[s * 6 + 5] = mvp.ref;
     }
 }
 
@@ -295,12 +297,12 @@ me_fastchain_spec_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, 
 template <bool FME, bool SUB, int BS>
 __global__ void __launch_bounds__(64)
 me_fastchain_round_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, int H, int W, int by0, int by1, int K,
-                          int src, int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub) {
+                          int src, int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub, int32_t* seg) {
     const int nbx = W / BS, nb = nbx * (by1 - by0);
     const int lane = threadIdx.x;
     const int s = blockIdx.x, b0 = s * K, b1 = b0 + K < nb ? b0 + K : nb;
-    const int32_t* in = g_fast_seg[src];
-    int32_t* out = g_fast_seg[1 - src];
+    const int32_t* in = seg + src * kFastSegBuf;
+    int32_t* out = seg + (1 - src) * kFastSegBuf;
     const int32_t* me = in + s * 6;
     Mvp g{me[0], me[1], me[2]}, last{me[3], me[4], me[5]};
     if (s > 0) {
@@ -324,11 +326,11 @@ template <bool FME, bool SUB, int BS>
 __global__ void __launch_bounds__(64)
 me_fastchain_fix_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, int H, int W, int by0, int by1, int K,
                         int nseg, int src, int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub,
-                        int32_t* __restrict__ nfixed) {
+                        const int32_t* __restrict__ segws, int32_t* __restrict__ nfixed) {
     __shared__ int32_t seg[kFastSegMax * 6];
     const int nbx = W / BS, nb = nbx * (by1 - by0);
     const int lane = threadIdx.x;
-    for (int i = lane; i < nseg * 6; i += 64) seg[i] = g_fast_seg[src][i];
+    for (int i = lane; i < nseg * 6; i += 64) seg[i] = segws[src * kFastSegBuf + i];
     __syncthreads();
     Mvp truth{seg[3], seg[4], seg[5]};   // segment 0 started from the true (0, 0, 0)
     int fixed = 0;
@@ -361,13 +363,14 @@ extern "C" int so_debug_fast_chain_fixed(int* out) {
 }
 
 int me_fastpred_launch(const uint8_t* cur, const uint8_t* const* ptrs, int nptr, int nref, int H, int W, int bs,
-                       int fme, int by0, int by1, int serial, int32_t* out_best, int32_t* out_sub, hipStream_t st) {
+                       int fme, int by0, int by1, int serial, int32_t* out_best, int32_t* out_sub, int32_t* seg_ws,
+                       hipStream_t st) {
     FastRefs R{};
     for (int i = 0; i < nptr && i < 4 * kMaxRef; ++i) R.p[i] = ptrs[i];
     const int nb = (W / bs) * (by1 - by0);
     if (nb <= 0) return SO_OK;
     const char* ser = getenv("SO_FASTME_SERIAL");   // A/B: the one-wavefront walk
-    if (serial && !(ser && atoi(ser) == 1)) {
+    if (serial && seg_ws && !(ser && atoi(ser) == 1)) {   // no workspace (so_me_search_ex): the walk
         int K = 32, warm = 32, rounds = 0;   // correction rounds: measured no gain
         if (const char* e = getenv("SO_FASTME_K")) K = atoi(e) > 0 ? atoi(e) : K;
         if (const char* e = getenv("SO_FASTME_WARM")) warm = atoi(e) >= 0 ? atoi(e) : warm;
@@ -381,12 +384,12 @@ int me_fastpred_launch(const uint8_t* cur, const uint8_t* const* ptrs, int nptr,
 #define SO_FASTCHAIN(F, S, B)                                                                                       \
         do {                                                                                                        \
             hipLaunchKernelGGL((me_fastchain_spec_kernel<F, S, B>), dim3(nseg), dim3(64), 0, st, cur, R, nref, H,   \
-                               W, by0, by1, K, warm, out_best, out_sub);                                            \
+                               W, by0, by1, K, warm, out_best, out_sub, seg_ws);                                    \
             for (int k = 0; k < rounds; ++k)                                                                        \
                 hipLaunchKernelGGL((me_fastchain_round_kernel<F, S, B>), dim3(nseg), dim3(64), 0, st, cur, R, nref, \
-                                   H, W, by0, by1, K, k & 1, out_best, out_sub);                                    \
+                                   H, W, by0, by1, K, k & 1, out_best, out_sub, seg_ws);                            \
             hipLaunchKernelGGL((me_fastchain_fix_kernel<F, S, B>), dim3(1), dim3(64), 0, st, cur, R, nref, H, W,    \
-                               by0, by1, K, nseg, rounds & 1, out_best, out_sub, nfixed);                           \
+                               by0, by1, K, nseg, rounds & 1, out_best, out_sub, seg_ws, nfixed);                   \
         } while (0)
         if (bs == 16) {
             if (fme) { if (sub) SO_FASTCHAIN(true, true, 16); else SO_FASTCHAIN(true, false, 16); }

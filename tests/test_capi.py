@@ -50,7 +50,7 @@ def test_host_side_validation_without_gpu():
     bad = lib.so_encode_i_frame(None, 60, 64, 16, 16, 4, None, 0, 0.0, None, None, None, None, None, None, None,
                                 None, None)
     assert bad == _lib.SO_E_INVALID
-    assert lib.so_p_frame_scratch_elems(2160, 3840, 16, 1) == 32400 * 20
+    assert lib.so_p_frame_scratch_elems(2160, 3840, 16, 1) == 32400 * 20 + 2 * 4096 * 6   # + fast-ME segments
     assert lib.so_i_frame_scratch_elems(64, 64, 16) == 16 * 256 + 16 * 8
     with pytest.raises(NotImplementedError):
         _lib.check(lib.so_me_full_search(None, None, 1, 64, 64, 16, 99, None, None, None), "me")
