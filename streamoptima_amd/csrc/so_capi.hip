@@ -53,6 +53,7 @@ size_t p_run_workspace_words(int H, int W);
 int p_run_2pass_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                        const int32_t* qp_row, const int32_t* roi, int qp_lo, int qp_hi, const PFrameOut* outs,
                        uint32_t* ws, hipStream_t st);
+int32_t* p_run_t1_region(uint32_t* ws, int H, int W);
 int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                  const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, hipStream_t st);
 int p_runs_launch(const uint8_t* const* curs, int nframes, const uint8_t* const* refs, const int* deps, int conc,
@@ -521,8 +522,29 @@ int so_encode_p_run_2pass(const uint8_t* const* curs, int nframes, const uint8_t
         outs[(size_t)i] = PFrameOut{out_split[i], out_mv[i], out_qtc[i], out_tokens[i], out_mae_num[i], out_recon[i],
                                     out_sse ? out_sse[i] : nullptr, out_qp_map[i]};
     }
-    return p_run_2pass_launch(curs, nframes, ref0, H, W, qp_rd, qp_row, roi, qp_lo, qp_hi, outs.data(), workspace,
-                              (hipStream_t)stream);
+    hipStream_t st = (hipStream_t)stream;
+    const char* fused = getenv("SO_RUN_2PASS_FUSED");   // opt-in: both passes in one persistent launch
+    if (fused && atoi(fused) == 1)
+        return p_run_2pass_launch(curs, nframes, ref0, H, W, qp_rd, qp_row, roi, qp_lo, qp_hi, outs.data(), workspace,
+                                  st);
+    // default (faster): per frame, pass 1 (fused search + tokens only),
+    // the QP map, pass 2 (transforms on pass 1's ME records, kept in the workspace), enqueued
+    // from here with no host round trip per frame
+    int32_t* best = p_run_t1_region(workspace, H, W);
+    const int nbx = W / 16, nby = H / 16;
+    for (int i = 0; i < nframes; ++i) {
+        RefSet rs{};
+        rs.p[0] = i ? out_recon[i - 1] : ref0;
+        const PFrameOut& o = outs[(size_t)i];
+        SO_TRY(p_tile_launch(curs[i], rs, H, W, 0, nby, qp_rd, qp_row, nullptr, best, o.split, o.mv, o.qtc, o.tokens,
+                             o.mae, o.recon, o.sse, st, true));
+        hipLaunchKernelGGL(qp_map_kernel, dim3(nby), dim3(256), 0, st, o.tokens, nbx, 0, qp_rd, qp_row, roi, qp_lo,
+                           qp_hi, o.qpmap);
+        SO_TRY(check_launch("qp_map_kernel"));
+        SO_TRY(inter_tq_launch(curs[i], rs, nullptr, so_fme_plane_stride(H, W), H, W, 16, 0, nby, best, nullptr, qp_rd,
+                               qp_row, o.qpmap, 0, 0.0, o.split, o.mv, o.qtc, o.tokens, o.mae, o.recon, o.sse, st));
+    }
+    return SO_OK;
 }
 
 // ---- one GOP across GPUs: a rank's stripe of every frame (so_me.hip PRunStripe) -------------

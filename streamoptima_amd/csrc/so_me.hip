@@ -2224,6 +2224,15 @@ int p_runs_launch(const uint8_t* const* curs, int nframes, const uint8_t* const*
                                            conc);
 }
 
+// The workspace's pass-1 token region (kRunMax * nb words; the per-frame two-pass sequence of
+// so_encode_p_run_2pass keeps its ME records there)
+int32_t* p_run_t1_region(uint32_t* ws, int H, int W) {
+    using G64 = Sea2GeoT<8, 64>;
+    using G128 = Sea2GeoT<8, 128>;
+    return reinterpret_cast<int32_t*>(ws + kRunDoneBase + (size_t)kRunMax * run_tiles(H, W, G64::TBX, G64::TBY) +
+                                      (size_t)kRunMax * run_tiles(H, W, G128::TBX, G128::TBY));
+}
+
 // Two-pass rate control over a run (so_encode_p_run_2pass): one run as p_run_launch, each tile
 // as a pass-1 and a pass-2 task (kRunTwoPass).
 int p_run_2pass_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,

@@ -111,11 +111,13 @@ def test_interleaved_gops_ragged_runs(gpu, monkeypatch):
     assert [symbols_digest(s) for s in codec.encode_device(gops[0], 4)["symbols"]] == exp[0]
 
 
+@pytest.mark.parametrize("fused", ["0", "1"])
 @pytest.mark.parametrize("roi", [None, [(100, 40, 400, 200, -2), (0, 150, 260, 272, 3)]])
-def test_two_pass_run_matches_per_frame(gpu, monkeypatch, roi):
-    """so_encode_p_run_2pass (both passes of every P-frame in one persistent launch) against
-    the per-frame sequence pass 1 -> so_qp_map -> pass 2 (SO_PIPELINE=0), frame by frame
-    including the QP maps, on a 640x272 GOP (5 x 9 tiles: pass-2 tasks of the 5-tile rows
+def test_two_pass_run_matches_per_frame(gpu, monkeypatch, roi, fused):
+    """so_encode_p_run_2pass -- the library-enqueued per-frame sequence (default) and both
+    passes of every P-frame in one persistent launch (SO_RUN_2PASS_FUSED=1) -- against the
+    Python-driven per-frame sequence pass 1 -> so_qp_map -> pass 2 (SO_PIPELINE=0), frame by
+    frame including the QP maps, on a 640x272 GOP (5 x 9 tiles: pass-2 tasks of the 5-tile rows
     waiting on their row's pass 1), with and without ROI, two runs (intra_dur 5 of 11)."""
     from streamoptima_amd.Encoder import Y_Video_codec
     from streamoptima_amd.digest import symbols_digest
@@ -132,6 +134,7 @@ def test_two_pass_run_matches_per_frame(gpu, monkeypatch, roi):
     exp_d = [symbols_digest(s) for s in exp["symbols"]]
     monkeypatch.delenv("SO_PIPELINE")
     monkeypatch.setenv("SO_RUN_2PASS", "1")
+    monkeypatch.setenv("SO_RUN_2PASS_FUSED", fused)
     got = codec.encode_device(fr, 5)
     torch.cuda.synchronize()
     assert all("qp_map" in s.extra for s in got["symbols"])
