@@ -148,16 +148,19 @@ int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0
 
 /*
  * A run of P-frames with two-pass rate control (build extension, RCFlag 3)
- * as ONE persistent launch: per frame, pass 1 at the rate-control row QP (qp_row, or qp_rd)
+ * in one call: per frame, pass 1 at the rate-control row QP (qp_row, or qp_rd)
  * gives each block's token count t, the per-block QP is clamp(row QP + delta + roi, qp_lo,
  * qp_hi) with delta = [t n >= 2m] + [t n >= 4m] - [2 t n < m] - [4 t n < m] (m = the block
  * row's pass-1 token sum over its n blocks; so_qp_map's rule), and pass 2 re-runs the
  * transforms at those QPs on pass 1's motion vectors.  Identical to the per-frame sequence
  * so_encode_p_rows_ex (pass 1) + so_qp_map + so_encode_p_rows_ex(SO_REUSE_ME) (pass 2);
- * out_qp_map[i] (int32 [nb]) receives frame i's QPs.  roi: int32 [nb] offsets or NULL.  Each
- * tile is two tasks of the launch; a pass-2 task waits for its tile row's pass 1.  Frame i
- * predicts from frame i-1's pass-2 reconstruction, frame 0 from ref0.  Same coverage and
- * workspace as so_encode_p_run (W <= 8192).
+ * out_qp_map[i] (int32 [nb]) receives frame i's QPs.  roi: int32 [nb] offsets or NULL.  By
+ * default the library enqueues that per-frame kernel sequence itself (pass 1 tokens-only, the
+ * QP map, pass 2; the ME records kept in the workspace); with SO_RUN_2PASS_FUSED=1 in the
+ * environment both passes run in ONE persistent launch instead (each tile two tasks, a pass-2
+ * task waiting for its tile row's pass 1; measured slower).  Frame i predicts from frame i-1's
+ * pass-2 reconstruction, frame 0 from ref0.  Same coverage and workspace as so_encode_p_run
+ * (W <= 8192).
  */
 int so_encode_p_run_2pass(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W,
                           int bs, int sr, int qp_rd, const int32_t* qp_row, const int32_t* roi,
