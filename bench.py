@@ -12,8 +12,9 @@ VBS off):
         independent GOPs per step with their P-runs interleaved in one persistent launch
         (--gops-in-flight, default 2; a GOP stream's throughput, every GOP parity-checked).
   N > 1 (default --config 4k120): configs[3], ONE 4K 120-frame GOP per step, sharded over
-        the N ranks (strong scaling): by default the frame pipeline (rank g encodes frames
-        g, g+N, ..., each reference arriving tile by tile from the previous rank over xGMI;
+        the N ranks (strong scaling): by default the frame pipeline (each rank encodes one
+        frame of every block of N, each reference arriving tile by tile from a ring
+        neighbour over xGMI, the ring direction alternating per block;
         streamoptima_amd/pipeline.py FramePipelineGOPEncoder), self-checked before timing,
         else block-row stripes (--shard stripe; dist.py / pipeline.py).  --shard gop is the
         opt-in weak-scaling mode (an independent GOP per rank).
@@ -751,7 +752,8 @@ def main(argv=None):
         if args.shard == "fpipe" and plain:
             fenc, fpipe_note = fpipe_encoder(codec, frames, cfg, world, max_wg=cap)
         if fenc is not None:
-            mode_note = f"frame pipeline x{world} (rank g encodes frames g, g+N, ...; {{}})"
+            mode_note = (f"frame pipeline x{world} (one frame per rank per block of N frames, ring direction "
+                         f"alternating per block; {{}})")
             exchange_note = fpipe_note
 
             def step():      # the SSE all_reduce runs once, after timing (pipeline.py encode)

@@ -103,7 +103,7 @@ int pack_frames_launch(const PackFrame* frames, int nframes, int nb, int bs, uns
 int stripe_halo_push_launch(const uint8_t* plane, int W, int by0, int by1, uint8_t* up, uint8_t* dn,
                             uint32_t* up_flags, uint32_t* dn_flags, int gf, uint32_t epoch, hipStream_t st);
 int p_run_fpipe_launch(const uint8_t* const* curs, int nframes, int H, int W, int qp_rd, const int32_t* qp_row,
-                       const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg, hipStream_t st);
+                       const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg, hipStream_t st, const int* push = nullptr);
 int frame_push_launch(const uint8_t* plane, int H, int W, uint8_t* dst, uint32_t* flags, uint32_t epoch,
                       hipStream_t st);
 
@@ -648,6 +648,54 @@ int so_encode_p_run_fpipe(const uint8_t* const* curs, int nframes, int H, int W,
                   epoch, slot0, land0, peer_slot_off};
     return p_run_fpipe_launch(curs, nframes, H, W, qp_rd, qp_row, outs.data(), workspace, sp, max_wg,
                               (hipStream_t)stream);
+}
+
+int so_encode_p_run_fpipe2(const uint8_t* const* curs, int nframes, int H, int W, int bs, int sr, int qp_rd,
+                           const int32_t* qp_row, uint8_t* const* out_split, int16_t* const* out_mv,
+                           int16_t* const* out_qtc, int32_t* const* out_tokens, int32_t* const* out_mae_num,
+                           uint8_t* const* out_recon, int32_t* const* out_sse, uint32_t* workspace,
+                           const uint8_t* land0, const uint32_t* land_flags, int slot0, uint8_t* peer_land0,
+                           uint32_t* peer_flags, uint8_t* peer2_land0, uint32_t* peer2_flags, const int32_t* push_to,
+                           long long stride, uint32_t epoch, int max_wg, void* stream) {
+    const char* fn = "so_encode_p_run_fpipe2";
+    SO_TRY(check_geom(fn, H, W, bs, 0));
+    SO_TRY(check_sr(fn, sr));
+    SO_TRY(check_qp(fn, qp_rd));
+    if (bs != 16 || sr != 16 || W % 128 != 0) {
+        set_error("%s: covers bs 16 / sr 16 / W %% 128 == 0", fn);
+        return SO_E_UNSUPPORTED;
+    }
+    if (slot0 < 0 || stride < (long long)H * W) {
+        set_error("%s: slot0 %d / stride %lld", fn, slot0, stride);
+        return SO_E_INVALID;
+    }
+    if (nframes <= 0) return SO_OK;
+    SO_NEED(curs, fn); SO_NEED(out_split, fn); SO_NEED(out_mv, fn); SO_NEED(out_qtc, fn); SO_NEED(out_tokens, fn);
+    SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn); SO_NEED(workspace, fn); SO_NEED(land0, fn);
+    SO_NEED(land_flags, fn); SO_NEED(peer_land0, fn); SO_NEED(peer_flags, fn); SO_NEED(peer2_land0, fn);
+    SO_NEED(peer2_flags, fn); SO_NEED(push_to, fn);
+    std::vector<PFrameOut> outs((size_t)nframes);
+    std::vector<int> push((size_t)nframes);
+    const uint8_t* land_end = land0 + (long long)(slot0 + nframes) * stride;
+    for (int i = 0; i < nframes; ++i) {
+        SO_NEED(curs[i], fn); SO_NEED(out_split[i], fn); SO_NEED(out_mv[i], fn); SO_NEED(out_qtc[i], fn);
+        SO_NEED(out_tokens[i], fn); SO_NEED(out_mae_num[i], fn); SO_NEED(out_recon[i], fn);
+        if (out_recon[i] >= land0 && out_recon[i] < land_end) {
+            set_error("%s: out_recon[%d] lies in the landing planes", fn, i);
+            return SO_E_INVALID;
+        }
+        if (push_to[i] < 0) {
+            set_error("%s: push_to[%d] = %d", fn, i, push_to[i]);
+            return SO_E_INVALID;
+        }
+        push[(size_t)i] = push_to[i];
+        outs[i] = PFrameOut{out_split[i], out_mv[i], out_qtc[i], out_tokens[i], out_mae_num[i], out_recon[i],
+                            out_sse ? out_sse[i] : nullptr};
+    }
+    PRunStripe sp{0, H / 16, peer2_land0, peer_land0, stride, nullptr, land_flags, peer2_flags, peer_flags,
+                  epoch, slot0, land0, 0};
+    return p_run_fpipe_launch(curs, nframes, H, W, qp_rd, qp_row, outs.data(), workspace, sp, max_wg,
+                              (hipStream_t)stream, push.data());
 }
 
 int so_frame_push(const uint8_t* plane, int H, int W, uint8_t* peer_plane, uint32_t* peer_flags, uint32_t epoch,

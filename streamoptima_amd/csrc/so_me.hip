@@ -2042,9 +2042,22 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 SO_RUN_PROF(49, __builtin_amdgcn_s_memtime() - pt0);
             }
         } else if constexpr (FPIPE) {
-            const int slot = sp.gbase + f + sp.peer_slot_off;   // the next rank's slot of this frame
+            // the rank encoding frame + 1 and its slot: the next rank, this rank's slot +
+            // peer_slot_off; or, with a second peer (the ring direction alternating per block of N
+            // frames), a.dep[f] = slot * 2 + (0: peer_dn, 1: peer_up)
+            int slot = sp.gbase + f + sp.peer_slot_off;
+            uint8_t* pbase = sp.peer_dn0;
+            uint32_t* pflags = sp.peer_dn_flags;
+            if (sp.peer_up0 != nullptr) {
+                const int code = a.dep[f];
+                slot = code >> 1;
+                if (code & 1) {
+                    pbase = sp.peer_up0;
+                    pflags = sp.peer_up_flags;
+                }
+            }
             PHalo hl{};
-            hl.dn = sp.peer_dn0 + (long long)slot * sp.stride;   // every row of the tile
+            hl.dn = pbase + (long long)slot * sp.stride;   // every row of the tile
             hl.dn_begin = 0;
             ptile_body<G, true, decltype(wait_ref), true>(S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd, qp_row,
                                                           nullptr, nullptr, a.out[f], wait_ref, hl);
@@ -2053,7 +2066,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                 if (lane == 0)
-                    __hip_atomic_store(sp.peer_dn_flags + (size_t)slot * ntiles + tile, sp.epoch, __ATOMIC_RELAXED,
+                    __hip_atomic_store(pflags + (size_t)slot * ntiles + tile, sp.epoch, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_SYSTEM);
             }
         } else if constexpr (STRIPE) {
@@ -2163,6 +2176,11 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
             const int d = deps ? deps[g] : g - 1;
             a.cur[i] = curs[g];
             a.out[i] = outs[g];
+            if (MODE == kRunFPipe) {   // deps = the per-frame push codes (slot * 2 + peer)
+                a.ref[i] = nullptr;
+                a.dep[i] = deps ? deps[g] : -1;
+                continue;
+            }
             a.ref[i] = d >= 0 ? outs[d].recon : (refs ? refs[g] : ref0);
             a.dep[i] = d >= f0 ? d - f0 : -1;   // an earlier launch's frame is complete (stream order)
         }
@@ -2259,8 +2277,10 @@ int p_run_stripe_launch(const uint8_t* const* curs, int nframes, const uint8_t* 
 }
 
 int p_run_fpipe_launch(const uint8_t* const* curs, int nframes, int H, int W, int qp_rd, const int32_t* qp_row,
-                       const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg, hipStream_t st) {
-    return p_run_launch_t<kRunFPipe, 128>(curs, nframes, nullptr, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st);
+                       const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg, hipStream_t st,
+                       const int* push) {
+    return p_run_launch_t<kRunFPipe, 128>(curs, nframes, nullptr, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st,
+                                          nullptr, push);
 }
 
 // The I-frame's hand-off (the P-frame run's frame 0 reads its boundary rows): copy the

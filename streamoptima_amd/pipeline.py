@@ -293,25 +293,48 @@ class PipelinedStripeGOPEncoder:
 
 
 # ---- frame pipeline: consecutive frames on consecutive ranks -----------------------------------
+def fpipe_rank_of(world: int, f: int) -> int:
+    """The rank encoding frame f: blocks of `world` consecutive frames are dealt to the ranks in
+    alternating ring directions -- block k even: position i -> rank i; odd: rank (-i) mod N --
+    so frame f + 1 is on rank(f) + 1 in even blocks and rank(f) - 1 in odd ones (across a
+    block boundary too): every rank hands its reconstructions alternately to its two ring
+    neighbours, and both directions of every xGMI link carry half the frames."""
+    k, i = divmod(f, world)
+    return i if k % 2 == 0 else (world - i) % world
+
+
 def fpipe_plan(world: int, rank: int, nframes: int) -> dict:
     """Which frames rank `rank` of `world` encodes and where its references land.
-    frames: its global frame indices (k = rank + world * slot); run: the P-frames of its
-    persistent launch (rank 0's frame 0 is the I-frame); slot0: the slot of run[0] (its
-    reference, frame run[0] - 1, arrives in that landing slot); peer_slot_off: frame k of this
-    rank is the reference of frame k + 1, slot (k + 1 - next) / world on the next rank, i.e.
-    this rank's slot + peer_slot_off (1 on the last rank, whose next is rank 0)."""
-    frames = list(range(rank, nframes, world))
+    frames: its global frame indices, one per block of `world` frames (slot j <-> block j);
+    run: the P-frames of its persistent launch (rank 0's frame 0 is the I-frame); slot0: the
+    slot of run[0] (its reference, frame run[0] - 1, arrives in that landing slot); push: per
+    run frame f, where frame f's reconstruction goes -- slot (f + 1) // world of rank
+    fpipe_rank_of(f + 1), coded slot * 2 + (0: the next rank, 1: the previous rank)."""
+    nblocks = -(-nframes // world)
+    frames = []
+    for k in range(nblocks):
+        f = k * world + (rank if k % 2 == 0 else (world - rank) % world)
+        if f < nframes:
+            frames.append(f)
     run = [k for k in frames if k > 0]
-    return {"frames": frames, "run": run, "slot0": (run[0] - rank) // world if run else 0,
-            "peer_slot_off": 1 if rank == world - 1 else 0, "nslots": -(-nframes // world) + 1}
+    push = []
+    for f in run:
+        r = fpipe_rank_of(world, f + 1)
+        if r not in ((rank + 1) % world, (rank - 1) % world):
+            raise AssertionError("fpipe_plan: frame f + 1 is not on a ring neighbour")
+        push.append(((f + 1) // world) * 2 + (0 if r == (rank + 1) % world else 1))
+    return {"frames": frames, "run": run, "slot0": run[0] // world if run else 0, "push": push,
+            "nslots": nblocks + 1}
 
 
 class FramePipeRank:
     """One rank of a GOP whose frames are dealt round-robin over the ranks:
-    rank g encodes frames k = g + N*j (rank 0's frame 0 is the I-frame) with ONE persistent
-    launch (so_encode_p_run_fpipe); frame k's reference, frame k-1, arrives tile by tile from
-    rank g-1 into this rank's uncached landing plane of slot j, and every tile of frame k is
-    pushed on into rank g+1's plane as it completes.  Each rank encodes whole frames at full
+    rank g encodes one frame of every block of N consecutive frames (fpipe_plan: ranks 0..N-1
+    in even blocks, 0, N-1, ..., 1 in odd ones; rank 0's frame 0 is the I-frame) with ONE
+    persistent launch (so_encode_p_run_fpipe2); frame k's reference, frame k-1, arrives tile
+    by tile from a ring neighbour into this rank's uncached landing plane of slot j (block j),
+    and every tile of frame k is pushed on into the plane of the rank encoding frame k+1 (the
+    next rank in even blocks, the previous one in odd blocks) as it completes.  Each rank encodes whole frames at full
     chip throughput while the frames of the other ranks run a couple of tile rows behind or
     ahead, so N ranks encode N frames at once; the only traffic is each reconstruction,
     once, over the xGMI link to the next rank."""
@@ -335,7 +358,7 @@ class FramePipeRank:
         _lib.check(lib.so_memset_d8(self._planes, 0, self.nslots * self.stride, self._st()), "so_memset_d8")
         _lib.check(lib.so_memset_d8(self._flags, 0, self.nslots * self.ntiles * 4, self._st()), "so_memset_d8")
         self.epoch = 0
-        self.peer = None
+        self.peer = self.peer2 = None
         self._opened = []
         self._ws = torch.zeros(lib.so_p_run_workspace_elems(e.h, e.w), dtype=torch.int32, device=e.device)
         self._syms = None
@@ -344,7 +367,7 @@ class FramePipeRank:
         return self.stream.cuda_stream if self.stream is not None else _lib.stream_handle(self.eng.device)
 
     def frames_of(self, nframes: int) -> list:
-        """Global indices of this rank's frames, in order (slot j <-> frame rank + N*j)."""
+        """Global indices of this rank's frames, in order (slot j <-> block j)."""
         return fpipe_plan(self.world, self.rank, nframes)["frames"]
 
     def info(self) -> dict:
@@ -366,11 +389,16 @@ class FramePipeRank:
             out[k] = p.value
         return out
 
-    def connect(self, nxt: dict) -> None:
-        """nxt: the next rank's info() as mapped in this process."""
+    def connect(self, nxt: dict, prv: dict | None = None) -> None:
+        """nxt / prv: the next / previous rank's info() as mapped in this process (with two
+        ranks they are the same rank; prv defaults to nxt then)."""
         if nxt["rank"] != (self.rank + 1) % self.world:
             raise ValueError("connect() takes the next rank")
+        prv = nxt if prv is None and self.world == 2 else prv
+        if prv is None or prv["rank"] != (self.rank - 1) % self.world:
+            raise ValueError("connect() takes the previous rank too")
         self.peer = (nxt["planes"], nxt["flags"])
+        self.peer2 = (prv["planes"], prv["flags"])
 
     def close(self) -> None:
         for p in self._opened:
@@ -414,14 +442,15 @@ class FramePipeRank:
             slot0 = plan["slot0"]
             arr = lambda xs: (ctypes.c_void_p * n)(*xs)  # noqa: E731
             ss = [syms[k] for k in ks]
-            _lib.check(lib.so_encode_p_run_fpipe(
+            p2planes, p2flags = self.peer2
+            _lib.check(lib.so_encode_p_run_fpipe2(
                 arr([frames[k].data_ptr() for k in ks]), n, e.h, e.w, e.bs, e.sr, int(qp), None,
                 arr([s.split.data_ptr() for s in ss]), arr([s.mv.data_ptr() for s in ss]),
                 arr([s.qtc.data_ptr() for s in ss]), arr([s.tokens.data_ptr() for s in ss]),
                 arr([s.mae_num.data_ptr() for s in ss]), arr([s.recon.data_ptr() for s in ss]),
                 arr([s.sse.data_ptr() for s in ss]), self._ws.data_ptr(), self._planes.value, self._flags.value,
-                slot0, pplanes, pflags, plan["peer_slot_off"], self.stride, ep,
-                int(self.max_wg), st), "so_encode_p_run_fpipe")
+                slot0, pplanes, pflags, p2planes, p2flags, (ctypes.c_int32 * n)(*plan["push"]), self.stride, ep,
+                int(self.max_wg), st), "so_encode_p_run_fpipe2")
             for s in ss:
                 s.frame_type, s.qp_rd = 1, int(qp)
         return syms
@@ -450,7 +479,9 @@ class FramePipelineGOPEncoder:
         torch.cuda.synchronize(engine.device)
         alls = [None] * self.world
         dist.all_gather_object(alls, self.r.export(), group=group)
-        self.r.connect(self.r.open(alls[(self.rank + 1) % self.world]))
+        nxt = self.r.open(alls[(self.rank + 1) % self.world])
+        prv = nxt if self.world == 2 else self.r.open(alls[(self.rank - 1) % self.world])
+        self.r.connect(nxt, prv)
         dist.barrier(group=group)
 
     def encode_local(self, frames, intra_dur: int, qp: int) -> dict:

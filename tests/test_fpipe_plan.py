@@ -6,7 +6,7 @@ import itertools
 
 import pytest
 
-from streamoptima_amd.pipeline import fpipe_plan
+from streamoptima_amd.pipeline import fpipe_plan, fpipe_rank_of
 
 
 @pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
@@ -14,16 +14,21 @@ from streamoptima_amd.pipeline import fpipe_plan
 def test_reference_slots_match(world, nframes):
     plans = [fpipe_plan(world, g, nframes) for g in range(world)]
     assert sorted(itertools.chain.from_iterable(p["frames"] for p in plans)) == list(range(nframes))
+    owner = {k: g for g, p in enumerate(plans) for k in p["frames"]}
+    assert all(owner[k] == fpipe_rank_of(world, k) for k in range(nframes))
     for g, p in enumerate(plans):
+        assert p["frames"] == sorted(p["frames"])
         for i, k in enumerate(p["run"]):
             slot = p["slot0"] + i                      # the slot this frame's launch reads
-            assert slot == (k - g) // world and slot < p["nslots"]
-            prod = (k - 1) % world                     # who encodes frame k-1 ...
-            pp = plans[prod]
-            pslot = ((k - 1) - prod) // world          # ... in its slot ...
-            push = 0 if k - 1 == 0 else pslot + pp["peer_slot_off"]   # ... and where it pushes it
-            assert (prod + 1) % world == g and push == slot
-            assert push < plans[(prod + 1) % world]["nslots"]
+            assert slot == k // world and slot < p["nslots"]
+            # where this frame's reconstruction goes: the rank of frame k + 1, its slot
+            code = p["push"][i]
+            dst = (g + 1) % world if code % 2 == 0 else (g - 1) % world
+            assert dst == fpipe_rank_of(world, k + 1) and code // 2 == (k + 1) // world
+            assert code // 2 < plans[dst]["nslots"]
+    if world > 2 and nframes >= 2 * world:   # both ring directions carry frames
+        codes = [c % 2 for p in plans for c in p["push"]]
+        assert 0 < sum(codes) < len(codes)
 
 
 def _simulate(world, nframes, tiles_x, tiles_y, wgs):

@@ -157,7 +157,7 @@ def test_frame_pipeline_in_process_matches_one_gpu(gpu, name, world, nframes):
     ranks = [FramePipeRank(engines[r], world, r, nframes, stream=streams[r], max_wg=cap) for r in range(world)]
     torch.cuda.synchronize()
     for r in range(world):
-        ranks[r].connect(ranks[(r + 1) % world].info())
+        ranks[r].connect(ranks[(r + 1) % world].info(), ranks[(r - 1) % world].info())
     for rep in range(2):
         syms = {}
         for r in range(world):
@@ -197,7 +197,7 @@ def test_frame_pipeline_back_to_back_gops(gpu):
              for r in range(world)]
     torch.cuda.synchronize()
     for r in range(world):
-        ranks[r].connect(ranks[(r + 1) % world].info())
+        ranks[r].connect(ranks[(r + 1) % world].info(), ranks[(r - 1) % world].info())
     saved = []
     for fr in (fa, fb, fa):
         syms = {}

@@ -54,7 +54,7 @@ def main():
         ranks = [FramePipeRank(engines[r], world, r, f, stream=streams[r], max_wg=cap) for r in range(world)]
         torch.cuda.synchronize()
         for r in range(world):
-            ranks[r].connect(ranks[(r + 1) % world].info())
+            ranks[r].connect(ranks[(r + 1) % world].info(), ranks[(r - 1) % world].info())
         best = None
         for _ in range(a.reps + 1):
             torch.cuda.synchronize()
