@@ -89,9 +89,10 @@ def parse(argv=None):
     ap.add_argument("--exchange", choices=("p2p", "allgather"), default="p2p",
                     help="stripe hand-off: inside the persistent launch over xGMI (p2p, self-checked against "
                          "allgather before timing) or an RCCL all_gather of every reconstruction (allgather)")
-    ap.add_argument("--shard", choices=("fpipe", "stripe", "gop"), default="fpipe",
+    ap.add_argument("--shard", choices=("fpipe", "stripe", "gop"), default=None,
                     help="N>1: ONE GOP (strong, configs[3]) as a frame pipeline over the ranks (fpipe; falls back to "
-                         "stripes if its self-check fails) or as block-row stripes, or a GOP per rank (weak)")
+                         "stripes if its self-check fails) or as block-row stripes, or a GOP per rank (weak); "
+                         "default: stripes at N=2, fpipe from N=3")
     ap.add_argument("--me", choices=("full", "fme", "fast", "fastpar", "fast_fme"), default="full",
                     help="ME variant: full search (headline), FMEEnable, fast_me (serial chain), fast_me under "
                          "ParallelMode 2, fast_me + FMEEnable")
@@ -720,6 +721,13 @@ def main(argv=None):
         cfg["frames"] = args.frames
         cfg["intra_dur"] = min(cfg["intra_dur"], args.frames)
     parity_ok = not (args.no_parity or args.frames or args.vbs or args.me != "full")
+    if args.shard is None:
+        # two GPUs share ONE xGMI link: the frame pipeline would push every reconstruction
+        # (8.3 MB per ~71 us frame, ~117 GB/s) over it one way, more than a link direction
+        # carries, while two block-row stripes exchange 16-row halos and run 1,020 tiles each
+        # at full throughput; from three ranks on the pipeline spreads over two links per
+        # rank (alternating ring) and the stripes turn latency-bound
+        args.shard = "stripe" if world == 2 else "fpipe"
     stripe = world > 1 and args.shard in ("stripe", "fpipe")    # one GOP over the ranks
     dev = torch.device("cpu") if args.cpu_plumbing else torch.device("cuda", local)
     h, w, f = cfg["h"], cfg["w"], cfg["frames"]
