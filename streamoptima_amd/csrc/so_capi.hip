@@ -221,31 +221,38 @@ struct SumArgs {
     const int32_t* p[kSumMax];
 };
 
-// one workgroup per array: int64 sum of len int32 values into out[blockIdx.x]; 16-byte loads,
-// eight in flight per thread (a dependent 4-byte load per step made this latency-bound)
-__global__ void __launch_bounds__(256) sum_rows_kernel(const SumArgs a, int len, long long* __restrict__ out) {
-    __shared__ long long part[4];
+// one workgroup of 1024 threads per array: int64 sum of len int32 values into out[blockIdx.x];
+// 16-byte loads, eight in flight per thread (a 4K frame's 32,400 per-block values are ~130 KB:
+// 256 threads left it latency-bound at 10 us for 30 frames)
+constexpr int kSumThreads = 1024;
+__global__ void __launch_bounds__(kSumThreads) sum_rows_kernel(const SumArgs a, int len, long long* __restrict__ out) {
+    __shared__ long long part[kSumThreads / 64];
     const int32_t* p = a.p[blockIdx.x];
     long long acc = 0;
     const int n4 = (reinterpret_cast<uintptr_t>(p) & 15) ? 0 : len / 4;
     const int4* p4 = reinterpret_cast<const int4*>(p);
     int i = threadIdx.x;
-    for (; i + 7 * 256 < n4; i += 8 * 256) {
+    for (; i + 7 * kSumThreads < n4; i += 8 * kSumThreads) {
         int4 v[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = p4[i + k * 256];
+        for (int k = 0; k < 8; ++k) v[k] = p4[i + k * kSumThreads];
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc += (long long)v[k].x + v[k].y + v[k].z + v[k].w;
     }
-    for (; i < n4; i += 256) {
+    for (; i < n4; i += kSumThreads) {
         const int4 v = p4[i];
         acc += (long long)v.x + v.y + v.z + v.w;
     }
-    for (int j = 4 * n4 + threadIdx.x; j < len; j += 256) acc += p[j];
+    for (int j = 4 * n4 + threadIdx.x; j < len; j += kSumThreads) acc += p[j];
     for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
     __syncthreads();
-    if (threadIdx.x == 0) out[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+    if (threadIdx.x == 0) {
+        long long t = 0;
+#pragma unroll
+        for (int w = 0; w < kSumThreads / 64; ++w) t += part[w];
+        out[blockIdx.x] = t;
+    }
 }
 
 // ---- SSE (PSNR) -------------------------------------------------------------------------------
@@ -1054,7 +1061,7 @@ int so_sum_i32_rows(const int32_t* const* rows, int n, int len, int64_t* out, vo
             SO_NEED(rows[i0 + i], fn);
             a.p[i] = rows[i0 + i];
         }
-        hipLaunchKernelGGL(sum_rows_kernel, dim3(m), dim3(256), 0, (hipStream_t)stream, a, len,
+        hipLaunchKernelGGL(sum_rows_kernel, dim3(m), dim3(kSumThreads), 0, (hipStream_t)stream, a, len,
                            reinterpret_cast<long long*>(out + i0));
         const int rc = check_launch("sum_rows_kernel");
         if (rc != SO_OK) return rc;
