@@ -182,7 +182,8 @@ SO_DEV Mvp fast_block_vbs16(const uint8_t* __restrict__ cur, const FastRefs& R, 
     fast_record(bf, mvp, 16, rec);
     const int32_t v = lane == 0 ? rec[0] : lane == 1 ? rec[1] : lane == 2 ? rec[2] : rec[3];
     if (lane < 4) ob[lane] = v;
-    return Mvp{__shfl(rec[0], 0, 64), __shfl(rec[1], 0, 64), __shfl(rec[2], 0, 64)};
+    return Mvp{__builtin_amdgcn_readfirstlane(rec[0]), __builtin_amdgcn_readfirstlane(rec[1]),
+               __builtin_amdgcn_readfirstlane(rec[2])};   // lane 0 holds the record (all lanes active)
 }
 
 // bs 16: full block on 64 lanes (row l >> 2, dword l & 3); sub-blocks on the four 16-lane
@@ -216,7 +217,8 @@ SO_DEV Mvp fast_block(const uint8_t* __restrict__ cur, const FastRefs& R, int nr
     const int32_t v = lane == 0 ? rec[0] : lane == 1 ? rec[1] : lane == 2 ? rec[2] : rec[3];
     if (lane < 4) ob[lane] = v;
     // the record is identical in the lanes of the block's group; lane 0 is in it
-    return Mvp{__shfl(rec[0], 0, 64), __shfl(rec[1], 0, 64), __shfl(rec[2], 0, 64)};
+    return Mvp{__builtin_amdgcn_readfirstlane(rec[0]), __builtin_amdgcn_readfirstlane(rec[1]),
+               __builtin_amdgcn_readfirstlane(rec[2])};   // lane 0 holds the record (all lanes active)
 }
 
 template <bool FME, bool SUB, int BS>
@@ -265,7 +267,8 @@ SO_DEV Mvp fast_chain_mv(const uint8_t* __restrict__ cur, const FastRefs& R, int
     const int i = BS == 16 ? lane >> 2 : lane >> 1, c = BS == 16 ? lane & 3 : lane & 1;
     const bool act = BS == 16 || lane < 16;
     fast_search<FME, BS == 16 ? 64 : 16>(cur, R, nref, H, W, x, y, BS, mvp, i, c, act, rec);
-    return Mvp{__shfl(rec[0], 0, 64), __shfl(rec[1], 0, 64), __shfl(rec[2], 0, 64)};
+    return Mvp{__builtin_amdgcn_readfirstlane(rec[0]), __builtin_amdgcn_readfirstlane(rec[1]),
+               __builtin_amdgcn_readfirstlane(rec[2])};   // lane 0 holds the record (all lanes active)
 }
 
 template <bool FME, bool SUB, int BS>
