@@ -373,7 +373,7 @@ class Y_Video_codec(BlockAPI):
         qp_sched_dev = eng.qp_row_tensor(qp_sched) if rc_on else None
         two_pass = self.RCFlag is not None and self.RCFlag >= 3
         roi = self.roi_block_offsets()
-        roi_dev = torch.from_numpy(roi).to(self.device) if roi is not None else None
+        roi_dev = eng.device_const_i32(roi) if roi is not None else None
         use_map = two_pass or roi_dev is not None
         lo, hi = self.qp_clamp
 

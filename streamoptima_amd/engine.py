@@ -71,6 +71,19 @@ class Engine:
         self.me_mode = int(me_mode)
         self.fme = bool(fme)
         self._fme_ws = None
+        self._consts: dict = {}
+
+    def device_const_i32(self, values) -> torch.Tensor:
+        """A read-only int32 device copy of `values`, uploaded once per distinct content, so
+        a GOP replayed from a captured HIP graph issues no host->device copy."""
+        host = torch.as_tensor(values, dtype=torch.int32).contiguous()
+        key = (tuple(host.shape), host.numpy().tobytes())
+        t = self._consts.get(key)
+        if t is None:
+            if len(self._consts) >= 64:
+                self._consts.clear()
+            t = self._consts[key] = host.to(self.device)
+        return t
 
     def fme_workspace(self, nref: int) -> torch.Tensor:
         """Phase planes of the references' frac frames (rebuilt by every FME call)."""
@@ -98,7 +111,7 @@ class Engine:
         t = torch.as_tensor(list(qp_row), dtype=torch.int32)
         if t.numel() != self.nby:
             raise ValueError(f"qp_row needs {self.nby} entries, got {t.numel()}")
-        return t.to(self.device, non_blocking=True)
+        return self.device_const_i32(t)
 
     def _check_plane(self, t: torch.Tensor, name: str):
         if t.dtype != torch.uint8 or t.device != self.device or tuple(t.shape) != (self.h, self.w):
