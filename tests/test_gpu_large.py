@@ -142,6 +142,46 @@ def test_two_pass_run_matches_per_frame(gpu, monkeypatch, roi, fused):
     assert torch.equal(got["sse"], exp["sse"])
 
 
+@pytest.mark.parametrize("roi", [None, [(100, 40, 400, 200, -2)]])
+def test_two_pass_gop_replayed_as_hip_graph(gpu, roi):
+    """bench.py --graph: a ROI / two-pass GOP captured once as a HIP graph (no host->device
+    copy inside the capture: ROI offsets and row-QP schedules are uploaded once per content,
+    Engine.device_const_i32) and replayed into poisoned outputs equals the eager encode."""
+    from streamoptima_amd.Encoder import Y_Video_codec
+    from streamoptima_amd.digest import symbols_digest
+    from streamoptima_amd.engine import alloc_planes
+    from streamoptima_amd.synth import synth_sequence_torch
+    from streamoptima_amd.workloads import RC_TABLES
+    h, w, f = 272, 640, 6
+    codec = Y_Video_codec(h, w, f, 16, 16, 4, f, 0, 0.015, False, RCFlag=3, targetBR="2 mbps",
+                          qp_rate_tables=RC_TABLES, roi=roi, device=gpu)
+    fr = alloc_planes(f, h, w, gpu)
+    fr.copy_(synth_sequence_torch(f, h, w, seed=11, device=gpu))
+    exp = codec.encode_device(fr, f)
+    exp_d = [symbols_digest(s) for s in exp["symbols"]]
+    exp_sse = exp["sse"].clone()
+    eng = codec.engine()
+    pre = [eng.new_symbols(0 if i == 0 else 1) for i in range(f)]
+    codec.encode_device(fr, f, symbols=pre, check=False)     # warm-up: workspaces, constants
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    cap = torch.cuda.Stream(gpu)
+    cap.wait_stream(torch.cuda.current_stream(gpu))
+    with torch.cuda.stream(cap):
+        with torch.cuda.graph(g, stream=cap):
+            got = codec.encode_device(fr, f, symbols=pre, check=False)
+    torch.cuda.current_stream(gpu).wait_stream(cap)
+    for s in pre:
+        s.qtc.fill_(0x5A5A)
+        s.recon.fill_(3)
+        s.tokens.fill_(-1)
+    g.replay()
+    torch.cuda.synchronize()
+    eng.check_run()
+    assert [symbols_digest(s) for s in got["symbols"]] == exp_d
+    assert torch.equal(got["sse"], exp_sse)
+
+
 def test_1080p_drop_in_encode_pads_to_1088(gpu, tmp_path, monkeypatch):
     """The public encode() on 1920x1080 host frames: pad_hw's 128 rows (Encoder.py:140-155,
     :1833), the 1088-row encode, PSNR over the padded plane -- the bench's 1080p record."""
