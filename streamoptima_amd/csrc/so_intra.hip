@@ -432,11 +432,42 @@ intra_recon_seq_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict__
     fetch(0, resn, dxn, curn);
     volatile int* vr = rg;   // one wave: LDS ops retire in order; volatile keeps their order
     int pv = 0;              // NEAR: this lane's value in the previous block
+    (void)vr;
     for (int bx0 = 0; bx0 < nbx; bx0 += CH) {
         int resc[CH], dxc[CH], curc[CH];
 #pragma unroll
         for (int s = 0; s < CH; ++s) { resc[s] = resn[s]; dxc[s] = dxn[s]; curc[s] = curn[s]; }
         if (bx0 + CH < nbx) fetch(bx0 + CH, resn, dxn, curn);
+        if constexpr (NEAR) {
+            // sr <= BS: every source is in the previous block, whose values the group's lanes
+            // still hold.  Only the ds_bpermute and two adds stay on the serial chain: the
+            // permute address (bit 0 = "no left source": 128 instead) and res + 128 are set up
+            // for the whole group first, the stores and the SSE come after it.
+#pragma unroll
+            for (int s = 0; s < CH; ++s) {
+                const int x = (bx0 + s) * BS, rel = c + dxc[s];
+                const bool use = x != 0 && rel < 0;
+                dxc[s] = (((lane & ~(BS - 1)) + ((rel + BS) & (BS - 1))) << 2) | (use ? 0 : 1);
+                resc[s] += use ? 0 : 128;
+            }
+#pragma unroll
+            for (int s = 0; s < CH; ++s) {   // past nbx: clamped inputs, values never stored
+                const int pvv = __builtin_amdgcn_ds_bpermute(dxc[s], pv);
+                pv = (pvv & ((dxc[s] & 1) - 1)) + resc[s];
+                resc[s] = pv;
+            }
+#pragma unroll
+            for (int s = 0; s < CH; ++s) {
+                const int x = (bx0 + s) * BS;
+                if (bx0 + s < nbx && act) {
+                    const int o = resc[s] & 255;
+                    orow[x + c] = (uint8_t)o;
+                    const int d = curc[s] - o;
+                    sse += d * d;
+                }
+            }
+            continue;
+        }
 #pragma unroll
         for (int s = 0; s < CH; ++s) {
             const int bx = bx0 + s;
@@ -444,17 +475,8 @@ intra_recon_seq_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict__
                 const int x = bx * BS;
                 int v = resc[s] + 128;
                 const int src = x + c + dxc[s];
-                if constexpr (NEAR) {
-                    // sr <= BS: every source is in the previous block, whose values the
-                    // group's lanes still hold -- one ds_bpermute, no LDS round trip
-                    const int idx = src - x + BS;        // in [0, BS) when src < x
-                    const int pvv = __shfl(pv, (lane & ~(BS - 1)) + (idx & (BS - 1)), 64);
-                    if (x != 0 && src < x) v = resc[s] + pvv;
-                    pv = v;
-                } else {
-                    if (x != 0 && src < x) v = resc[s] + vr[src & (RING - 1)];
-                    vr[(x + c) & (RING - 1)] = v;
-                }
+                if (x != 0 && src < x) v = resc[s] + vr[src & (RING - 1)];
+                vr[(x + c) & (RING - 1)] = v;
                 const int o = v & 255;
                 if (act) {
                     orow[x + c] = (uint8_t)o;
