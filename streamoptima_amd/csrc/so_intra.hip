@@ -400,7 +400,7 @@ intra_recon_seq_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict__
     __shared__ int ring[4 * RPW][RING];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int g = lane / BS, c = lane - g * BS;            // row group, column within the block
-    const int yl = (blockIdx.x * 4 + wv) * RPW + g;        // stripe-local pixel row
+    const int yl = (blockIdx.x * (blockDim.x >> 6) + wv) * RPW + g;   // stripe-local pixel row
     const bool act = yl < nrows_px;
     const int ylc = act ? yl : nrows_px - 1;
     const int yy = by0 * BS + ylc, byl = ylc / BS, i = ylc - byl * BS, nbx = W / BS;
@@ -499,11 +499,16 @@ static int intra_recon_rows(int W, int bs, int sr, int by0, int nrows_px, const 
                             hipStream_t st) {
     if (nrows_px <= 0) return SO_OK;
     if (sr <= 64) {
-        const int rows_per_blk = 4 * (64 / bs);
+        // SO_IRS_WPB waves per workgroup (the kernel is a latency chain per wave; 1 spreads
+        // the 4K I-frame's 540 waves over all 256 CUs instead of 135)
+#ifndef SO_IRS_WPB
+#define SO_IRS_WPB 1
+#endif
+        const int rows_per_blk = SO_IRS_WPB * (64 / bs);
         const dim3 grid((nrows_px + rows_per_blk - 1) / rows_per_blk);
 #define SO_IRS(B, N)                                                                                              \
-    hipLaunchKernelGGL((intra_recon_seq_kernel<B, N>), grid, dim3(256), 0, st, W, nrows_px, by0, split, mv, idres, \
-                       cur, out_recon, out_sse)
+    hipLaunchKernelGGL((intra_recon_seq_kernel<B, N>), grid, dim3(64 * SO_IRS_WPB), 0, st, W, nrows_px, by0, split, \
+                       mv, idres, cur, out_recon, out_sse)
         if (bs == 16) { if (sr <= 16) SO_IRS(16, true); else SO_IRS(16, false); }
         else { if (sr <= 8) SO_IRS(8, true); else SO_IRS(8, false); }
 #undef SO_IRS
