@@ -86,6 +86,49 @@ def test_p_runs_validation_without_gpu():
                                 None) == _lib.SO_E_UNSUPPORTED
 
 
+def test_two_pass_run_and_frame_pipe_validation_without_gpu():
+    """so_encode_p_run_2pass and so_encode_p_run_fpipe2 reject unsupported geometry, a bad QP
+    clamp, a reconstruction aliasing the reference or lying in the landing planes, a short
+    landing stride and a negative push code -- on the host, before any launch."""
+    from streamoptima_amd import _lib
+    lib = _lib.load()
+    n, H, W = 2, 64, 128
+    fake = [ctypes.c_void_p(0x100000 * (i + 1)) for i in range(16)]
+
+    def arr(*ps):
+        return (ctypes.c_void_p * n)(*ps)
+    cur = arr(fake[0], fake[1])
+    outs = [arr(fake[2 + 2 * k], fake[3 + 2 * k]) for k in range(5)]
+    qmap = arr(fake[12], fake[13])
+    ws = ctypes.c_void_p(0x9000)
+
+    def two_pass(ref0, recon, bs=16, w=W, lo=0, hi=20):
+        return lib.so_encode_p_run_2pass(cur, n, ref0, H, w, bs, 16, 4, None, None, lo, hi, outs[0], outs[1], outs[2],
+                                         outs[3], outs[4], recon, None, qmap, ws, None)
+    recon = arr(fake[10], fake[11])
+    assert two_pass(fake[14], recon, bs=8) == _lib.SO_E_UNSUPPORTED
+    assert two_pass(fake[14], recon, w=96) == _lib.SO_E_UNSUPPORTED
+    assert two_pass(fake[14], recon, lo=5, hi=3) == _lib.SO_E_INVALID
+    assert b"QP clamp" in lib.so_last_error()
+    assert two_pass(fake[10], recon) == _lib.SO_E_INVALID
+    assert b"aliases" in lib.so_last_error()
+
+    stride = H * W
+    land0, land_flags = 0x4000000, ctypes.c_void_p(0x5000000)
+
+    def fpipe(recon, push, stride=stride, slot0=0):
+        return lib.so_encode_p_run_fpipe2(cur, n, H, W, 16, 16, 4, None, outs[0], outs[1], outs[2], outs[3], outs[4],
+                                          recon, None, ws, ctypes.c_void_p(land0), land_flags, slot0, fake[14],
+                                          fake[15], fake[14], fake[15], (ctypes.c_int32 * n)(*push), stride, 1, 0,
+                                          None)
+    assert fpipe(recon, [0, 2], stride=stride - 1) == _lib.SO_E_INVALID
+    assert fpipe(recon, [0, 2], slot0=-1) == _lib.SO_E_INVALID
+    assert fpipe(recon, [0, -1]) == _lib.SO_E_INVALID
+    assert b"push_to[1]" in lib.so_last_error()
+    assert fpipe(arr(fake[10], ctypes.c_void_p(land0 + stride)), [0, 2]) == _lib.SO_E_INVALID
+    assert b"landing planes" in lib.so_last_error()
+
+
 def test_product_never_imports_the_oracle():
     pkg = os.path.join(ROOT, "streamoptima_amd")
     for dirpath, _, files in os.walk(pkg):
