@@ -77,6 +77,7 @@ struct PRunStripe {
     const int32_t* roi;
     int qp_lo, qp_hi;
     int p2lag;
+    int xq;
 };
 int p_run_stripe_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                         const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg,

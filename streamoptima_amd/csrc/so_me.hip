@@ -1775,7 +1775,9 @@ struct PRunArgs {
 // the task counter (hammered by every workgroup's dequeue), the timeout count and the done
 // flags live on separate 128-byte lines
 constexpr int kRunTimeoutWord = SO_RUN_TIMEOUT_WORD, kRunDoneBase = SO_RUN_DONE_BASE;
-constexpr int kRunExitWord = 1, kRunEpochWord = 2;   // on the task counter's line: touched once per workgroup
+// [1], [2] on the task counter's line: touched once per workgroup; [16, 24) the XCD-banded
+// queue heads (SO_RUN_XCDQ=1)
+constexpr int kRunExitWord = 1, kRunEpochWord = 2, kRunXqWord = 16;
 // A rank's stripe of a frame shared across GPUs (so_encode_p_run_stripe): block rows [by0, by1)
 // of every frame, the reconstruction planes in uncached memory addressed by "virtual" full-frame
 // bases (row y at base + y * W; the allocation holds rows [16 * by0 - 16, 16 * by1 + 32)), and
@@ -1815,6 +1817,7 @@ struct PRunStripe {
     const int32_t* roi;
     int qp_lo, qp_hi;
     int p2lag;   // tile rows between a row's pass-1 and pass-2 tasks in the queue (1..ntr)
+    int xq;      // one GPU (kRunSingle): 8 = one queue per XCD (a band of tile rows each), 0 = one queue
 };
 constexpr int kRunSingle = 0, kRunStripe = 1, kRunFPipe = 2, kRunTwoPass = 3;
 // SO_RUN_PROFILE builds (tools/rc2p_ab.py): per-phase shader cycles >> 10 accumulated by wave 0
@@ -1858,10 +1861,36 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     // flags hold the epoch of the launch that set them: nothing is zeroed between launches.
     const uint32_t ep = __builtin_amdgcn_readfirstlane(
         __hip_atomic_load(&ws[kRunEpochWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+    // XCD-banded queues (sp.xq == 8, kRunSingle, grid >= 8): queue k = the tasks of tile rows
+    // [k * ntr / 8, (k + 1) * ntr / 8), frame-major, at ws[kRunXqWord + k]; a workgroup takes
+    // from queue blockIdx mod 8 (its XCD under round-robin dispatch, so the 3x3 neighbours
+    // sharing its window's rows run under the same L2) and steals from the others once that
+    // is empty.  Every queue has a home workgroup and is frame-major, so the oldest
+    // unfinished frame's tiles are always held by running workgroups: deadlock-free as the
+    // single queue.
+    const bool xq = MODE == kRunSingle && sp.xq == 8;
     for (;;) {
         if (wave == 0) {
-            const uint32_t v = __hip_atomic_fetch_add(&ws[0], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_task = (int)__builtin_amdgcn_readfirstlane(v);
+            int t = ntasks;
+            if (xq) {
+                const int home = (int)(blockIdx.x & 7u);
+                for (int qi = 0; qi < 8; ++qi) {
+                    const int k = (home + qi) & 7;
+                    const int r0 = k * ntr / 8, r1 = (k + 1) * ntr / 8, bt = (r1 - r0) * tiles_x;
+                    if (bt == 0) continue;
+                    const uint32_t v = __builtin_amdgcn_readfirstlane(__hip_atomic_fetch_add(
+                        &ws[kRunXqWord + k], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    if ((int)v < bt * nframes) {
+                        const int fq = (int)v / bt;
+                        t = fq * per_frame + r0 * tiles_x + ((int)v - fq * bt);
+                        break;
+                    }
+                }
+            } else {
+                t = (int)__builtin_amdgcn_readfirstlane(
+                    __hip_atomic_fetch_add(&ws[0], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            }
+            s_task = t;
         }
         __syncthreads();
         const int task = __builtin_amdgcn_readfirstlane(s_task);
@@ -2122,6 +2151,9 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             __hip_atomic_fetch_add(&ws[kRunExitWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (o == gridDim.x - 1) {
             __hip_atomic_store(&ws[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (xq)
+                for (int k = 0; k < 8; ++k)
+                    __hip_atomic_store(&ws[kRunXqWord + k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&ws[kRunExitWord], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&ws[kRunEpochWord], ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -2201,6 +2233,9 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
         if (max_wg > 0 && grid > max_wg) grid = max_wg;
         PRunStripe sp = sp0;
         sp.gbase = sp0.gbase + f0;
+        sp.xq = 0;
+        if (MODE == kRunSingle && grid >= 8)
+            if (const char* e = getenv("SO_RUN_XCDQ")) sp.xq = atoi(e) == 1 ? 8 : 0;
         if (MODE == kRunTwoPass) {   // pass 2 of a row about one grid's worth of tasks after its pass 1
             const int tiles_x = (nbx + G::TBX - 1) / G::TBX, ntr = (rows + G::TBY - 1) / G::TBY;
             int lag = (int)((grid + tiles_x - 1) / tiles_x);
