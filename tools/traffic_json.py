@@ -60,6 +60,10 @@ for k, v in sorted(vals.items()):
                   "dispatches": v["FETCH_SIZE_dispatches"]}
         if k in insts:
             per[k].update({c.lower(): sum(x) / len(x) for c, x in insts[k].items()})
+if not per:   # no counter CSVs for this tag (e.g. the GPU call never ran): keep the committed file
+    sys.exit(f"no FETCH_SIZE / WRITE_SIZE rows under {base}/{tag}_{cfg}_*: nothing written")
+if not calib:
+    sys.exit(f"no calibration rows under {base}/{tag}_calib: nothing written")
 out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_me_traffic.json")
 doc = json.load(open(out)) if os.path.exists(out) else {}
 doc["_note"] = ("per launch: hbm_bytes = calib_b32 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 from separate rocprofv3 "
