@@ -78,8 +78,11 @@ def parse(argv=None):
     ap.add_argument("--config", default=None,
                     help="workload (streamoptima_amd/workloads.py); default 4k at N=1, 4k120 at N>1")
     ap.add_argument("--frames", type=int, default=None, help="override the workload's frame count (no parity)")
-    ap.add_argument("--vbs", action="store_true", help="VBSEnable=True (lambda 0.015); no parity fixture")
-    ap.add_argument("--cpu-rows", type=int, default=4, help="block rows per frame type for the serial CPU sample")
+    ap.add_argument("--vbs", action="store_true",
+                    help="VBSEnable=True (lambda 0.015): the workload's VBS-on variant (workloads.py, own fixture)")
+    ap.add_argument("--cpu-rows", type=int, default=8,
+                    help="block rows per frame type for the serial CPU sample (BASELINE.md §3: 8), spread over the "
+                         "frame's height, edges included")
     ap.add_argument("--cpu-pool-rows", type=int, default=16, help="block rows for the Pool CPU sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-records", action="store_true", help="skip the 1080p record at N=1")
@@ -97,7 +100,10 @@ def parse(argv=None):
                          "default: stripes at N=2, fpipe from N=3")
     ap.add_argument("--me", choices=("full", "fme", "fast", "fastpar", "fast_fme"), default="full",
                     help="ME variant: full search (headline), FMEEnable, fast_me (serial chain), fast_me under "
-                         "ParallelMode 2, fast_me + FMEEnable")
+                         "ParallelMode 2, fast_me + FMEEnable; selects the workload's variant where workloads.py "
+                         "has one (1080p: 10-frame GOPs with oracle fixtures)")
+    ap.add_argument("--no-content-records", action="store_true",
+                    help="skip the N=1 records on low-texture / noise-only content")
     ap.add_argument("--graph", action="store_true",
                     help="replay the GOP as one captured HIP graph (measured slower than host launches here)")
     ap.add_argument("--share-gpu", action="store_true",
@@ -336,33 +342,37 @@ def cpu_model() -> str:
 
 
 def cpu_baseline(cfg, rows: int, pool_rows: int) -> dict:
-    """The numpy port of the reference loops (oracle/ref_numpy.py) on `rows` interior block
-    rows of one P-frame and one I-frame, serially (the reference's ParallelMode 0), and on
-    `pool_rows` P-frame rows over a process Pool (the ParallelMode-2 analogue), each
-    extrapolated to the whole GOP (1 I + frames-1 P)."""
+    """The numpy port of the reference loops (oracle/ref_numpy.py) on `rows` block rows of one
+    P-frame and one I-frame, spread evenly over the frame's height with the first and last
+    rows included (8 rows per frame type; edge rows have fewer valid
+    candidates), serially (the reference's ParallelMode 0), and on `pool_rows` P-frame rows
+    over a process Pool (the ParallelMode-2 analogue), each extrapolated to the whole GOP
+    (1 I + frames-1 P).  The frames are the workload's own (synth.py, padded to 16 rows)."""
     from oracle.ref_numpy import inter_rows, inter_rows_pool, intra_rows
     from streamoptima_amd.synth import synth_sequence
     h, w = cfg["h"], cfg["w"]
     hp = -(-h // 16) * 16
-    band = max(rows, pool_rows) * 16 + 48
-    seq = synth_sequence(2, band, w, seed=cfg["seed"])
+    nrows, f = hp // 16, cfg["frames"]
+    seq = np.full((2, hp, w), 128, np.uint8)
+    seq[:, :h] = synth_sequence(2, h, w, seed=cfg["seed"], content=cfg.get("content", "bench"))
     cur = seq[1].astype(np.float64)
     ref = seq[0]
+    sample = sorted({int(round(r)) for r in np.linspace(0, nrows - 1, rows)})
+    psample = sorted({int(round(r)) for r in np.linspace(0, nrows - 1, pool_rows)})
     t0 = time.perf_counter()
-    inter_rows(cur, ref, range(1, 1 + rows), qp=cfg["qp"])
-    tp = (time.perf_counter() - t0) / rows
+    inter_rows(cur, ref, sample, qp=cfg["qp"])
+    tp = (time.perf_counter() - t0) / len(sample)
     t0 = time.perf_counter()
-    intra_rows(cur, range(1, 1 + rows), qp=cfg["qp"])
-    ti = (time.perf_counter() - t0) / rows
-    nrows, f = hp // 16, cfg["frames"]
+    intra_rows(cur, sample, qp=cfg["qp"])
+    ti = (time.perf_counter() - t0) / len(sample)
     t_gop = nrows * (ti + (f - 1) * tp)
     try:
         procs = min(len(os.sched_getaffinity(0)), 16)   # the box's CPU share is 16
     except AttributeError:
         procs = min(os.cpu_count() or 1, 16)
     t0 = time.perf_counter()
-    inter_rows_pool(cur, ref, range(1, 1 + pool_rows), procs, qp=cfg["qp"])
-    tpp = (time.perf_counter() - t0) / pool_rows
+    inter_rows_pool(cur, ref, psample, procs, qp=cfg["qp"])
+    tpp = (time.perf_counter() - t0) / len(psample)
     t_gop_pool = nrows * (ti / procs + (f - 1) * tpp)   # intra rows are as parallel (row-level, mode 2)
     calib = None
     cp = os.path.join(ROOT, "profiles", "cpu_port_calibration.json")
@@ -371,12 +381,12 @@ def cpu_baseline(cfg, rows: int, pool_rows: int) -> dict:
         calib = {"port_over_reference_time": c["p_frame"]["port_over_reference_time"],
                  "tokens_equal": c["tokens_equal"], "host": c["host"], "source": "profiles/cpu_port_calibration.json"}
     return {"value": round(f * h * w / t_gop / 1e6, 6), "unit": "Mpx/s", "cores": 1, "kind": "port",
-            "sample": f"{rows} interior block rows of a P-frame and of an I-frame at {w}x{h} "
-                      f"({rows * w // 16} blocks each), numpy port of Encoder.py loops (oracle/ref_numpy.py), "
+            "sample": f"{len(sample)} block rows {sample} of a P-frame and of an I-frame at {w}x{hp} "
+                      f"({len(sample) * w // 16} blocks each), numpy port of Encoder.py loops (oracle/ref_numpy.py), "
                       f"extrapolated to {nrows} rows x (1 I + {f - 1} P); "
                       f"P {tp * nrows:.1f} s/frame, I {ti * nrows:.2f} s/frame",
             "pool": {"value": round(f * h * w / t_gop_pool / 1e6, 6), "unit": "Mpx/s", "cores": procs,
-                     "sample": f"{pool_rows} P-frame block rows over Pool({procs}), one row per task "
+                     "sample": f"{len(psample)} P-frame block rows (spread over the frame) over Pool({procs}), one row per task "
                                f"(ParallelMode-2 analogue); P {tpp * nrows:.2f} s/frame"},
             "host": cpu_model(), "os_cpu_count": os.cpu_count(), "calibration": calib}
 
@@ -433,7 +443,8 @@ def pcie_inclusive(codec, cfg, frames_dev, reps: int = 6) -> dict:
     best_p, d2h_p = timed(packed_run)
     same = all(torch.equal(got["packed"][i], packed[i, :int(offs[i, -1])].cpu()) for i in range(f))
     px = f * cfg["h"] * cfg["w"]
-    return {"mpx_s": round(px / best_p / 1e6, 2), "ms_per_gop": round(best_p * 1e3, 3),
+    return {"region": "BASELINE.md §4 (pinned host Y planes in, symbols back in pinned host memory)",
+            "mpx_s": round(px / best_p / 1e6, 2), "ms_per_gop": round(best_p * 1e3, 3),
             "ms_per_gop_median": round(med["packed_run"] * 1e3, 3), "reps": reps,
             "h2d_bytes": int(host.numel()), "d2h_bytes": int(d2h_p), "packed_equals_resident_symbols": bool(same),
             "note": "streamoptima_amd/hoststream.py: per-frame H2D on one copy stream, P-runs of 2 frames + "
@@ -446,14 +457,13 @@ def pcie_inclusive(codec, cfg, frames_dev, reps: int = 6) -> dict:
 # ---- one workload ---------------------------------------------------------------------------------
 def build_codec(cfg, args, dev):
     from streamoptima_amd.Encoder import Y_Video_codec
-    from streamoptima_amd.workloads import RC_TABLES
-    me_kw = {"full": {}, "fme": dict(FMEEnable=True), "fast": dict(fast_me=True),
-             "fastpar": dict(fast_me=True, ParallelMode=2), "fast_fme": dict(fast_me=True, FMEEnable=True)}[args.me]
+    from streamoptima_amd.workloads import ME_KW, RC_TABLES
+    me_kw = dict(ME_KW[cfg.get("me", "full")])
     if cfg.get("rc"):
         # RCFlag 3 without intra_thresh: no P->I switch, so no host read per frame
         me_kw.update(RCFlag=cfg["rc"], targetBR=cfg["target"], qp_rate_tables=RC_TABLES, roi=cfg.get("roi"))
-    return Y_Video_codec(cfg["h"], cfg["w"], cfg["frames"], 16, 16, cfg["qp"], cfg["intra_dur"], 0, 0.015, args.vbs,
-                         y_only_frame_arr=None, device=dev, **me_kw)
+    return Y_Video_codec(cfg["h"], cfg["w"], cfg["frames"], 16, 16, cfg["qp"], cfg["intra_dur"], 0, 0.015,
+                         bool(cfg.get("vbs")), y_only_frame_arr=None, device=dev, **me_kw)
 
 
 def make_frames(cfg, dev, seed):
@@ -462,7 +472,7 @@ def make_frames(cfg, dev, seed):
     from streamoptima_amd.workloads import padded
     h, w, f = cfg["h"], cfg["w"], cfg["frames"]
     frames = alloc_planes(f, padded(h), padded(w), dev, fill=128)     # pad_hw: 128 below row h
-    frames[:, :h, :w].copy_(synth_sequence_torch(f, h, w, seed=seed, device=dev))
+    frames[:, :h, :w].copy_(synth_sequence_torch(f, h, w, seed=seed, device=dev, content=cfg.get("content", "bench")))
     return frames
 
 
@@ -512,14 +522,33 @@ def run_single(cfg, args, dev, parity: bool):
     return codec, frames, pre, step
 
 
-def parity_of(res, name, cfg, redo=None) -> dict | None:
+def psnr_delta(sse, fx, hp: int, w: int) -> dict | None:
+    """PSNR per frame from the timed output's SSE (calculate_metrics, Encoder.py:934-935, over
+    the padded plane as encode() computes it, :1869) against the oracle fixture's PSNR list:
+    the metric's "PSNR delta vs reference"."""
+    if sse is None or fx is None or "psnr" not in fx:
+        return None
+    vals = sse.cpu().numpy() if torch.is_tensor(sse) else np.asarray(sse)
+    got = [float("inf") if s == 0 else 10 * np.log10(255 ** 2 / (float(s) / (hp * w))) for s in vals]
+    d = [abs(a - b) for a, b in zip(got, fx["psnr"]) if np.isfinite(a) and np.isfinite(b)]
+    return {"psnr_delta_db_max": float(max(d)) if d else None, "frames": len(got),
+            "psnr_mean_db": round(float(np.mean([g for g in got if np.isfinite(g)])), 4),
+            "tolerance_db": 1e-4}
+
+
+def parity_of(res, name, cfg, redo=None, sse=None) -> dict | None:
     """Digests of the timed output vs the oracle fixture; `redo()` re-runs one step into
-    poisoned buffers and returns its symbols."""
+    poisoned buffers and returns its symbols; `sse` (per-frame, device or host) adds the PSNR
+    delta against the fixture's PSNR list."""
+    from streamoptima_amd.workloads import padded
     fx = load_fixture(name)
     if fx is None:
         return {"bit_exact": None, "note": f"no oracle fixture for workload {name!r}"}
     got = frame_digests(res)
     out = compare_digests(got, fx)
+    pd = psnr_delta(sse, fx, padded(cfg["h"]), cfg["w"])
+    if pd is not None:
+        out["psnr_delta_db"] = pd["psnr_delta_db_max"]
     if redo is not None:
         again = compare_digests(frame_digests(redo()), fx)
         out["poisoned_rerun_bit_exact"] = again["bit_exact"]
@@ -540,24 +569,37 @@ def time_steps_median(step, args, dev):
     return elapsed, res, [round(e / args.steps * 1e3, 3) for e, _ in runs]
 
 
-def record_1080p(args, dev) -> dict:
-    """configs[1] measured like the headline: a 1080p GOP per step, parity-checked."""
-    from streamoptima_amd.workloads import WORKLOADS
-    cfg = dict(WORKLOADS["1080p"])
+def record_single(name: str, args, dev) -> dict:
+    """Another workload measured like the headline (one GOP per step, median of
+    --record-repeats timed runs, parity-checked): configs[1] (1080p) and the content-dependence
+    records (4k_lowtex, 4k_noise), which also report the fraction of P-frame blocks whose exact
+    SEA search took the dense fallback."""
+    from streamoptima_amd.workloads import WORKLOADS, padded
+    cfg = dict(WORKLOADS[name])
     codec, frames, pre, step = run_single(cfg, args, dev, True)
+    eng = codec.engine()
     elapsed, res, runs = time_steps_median(step, args, dev)
-    codec.engine().check_run()
+    eng.check_run()
     mpx = args.steps * cfg["frames"] * cfg["h"] * cfg["w"] / elapsed / 1e6
     rec = {"workload": cfg["workload"], "value": round(mpx, 2), "unit": "Mpx/s",
            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "ms_per_step_runs": runs, "width": cfg["w"],
-           "height": cfg["h"], "encoded_height": 1088, "frames": cfg["frames"]}
+           "height": cfg["h"], "encoded_height": padded(cfg["h"]), "frames": cfg["frames"],
+           "content": cfg.get("content", "bench")}
+    eng.take_fallback_count()
+    step()
+    eng.check_run()
+    p_blocks = (cfg["frames"] - -(-cfg["frames"] // cfg["intra_dur"])) * eng.nb
+    fb = eng.take_fallback_count()
+    rec["sea_dense_fallback"] = {"blocks": fb, "p_blocks": p_blocks, "frac": round(fb / p_blocks, 5),
+                                 "note": "P-frame blocks whose 4x4-cell bound left more than 192 survivors "
+                                         "(SO_P_RUN_FALLBACK_WORD, one GOP)"}
     if not args.no_parity:
         def redo():
             poison(pre)
             r = step()
-            codec.engine().check_run()
+            eng.check_run()
             return r["symbols"]
-        rec["parity"] = parity_of(res["symbols"], "1080p", cfg, redo)
+        rec["parity"] = parity_of(res["symbols"], name, cfg, redo, sse=res["sse"])
     return rec
 
 
@@ -593,7 +635,7 @@ def record_gops_in_flight(name: str, ngops: int, args, dev) -> dict:
            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
            "ms_per_gop": round(elapsed / args.steps / ngops * 1e3, 3), "ms_per_step_runs": runs}
     if not args.no_parity:
-        per = [parity_of(r["symbols"], name, cfg) for r in res]
+        per = [parity_of(r["symbols"], name, cfg, sse=r["sse"]) for r in res]
         rec["parity"] = {"bit_exact": all(p and p.get("bit_exact") for p in per),
                          "gops_checked": len(per), "fixture": per[0].get("fixture") if per[0] else None}
     return rec
@@ -729,13 +771,18 @@ def main(argv=None):
         torch.cuda.set_device(0)
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}")
-    from streamoptima_amd.workloads import WORKLOADS
-    name = args.config or ("4k" if world == 1 else "4k120")
+    from streamoptima_amd.workloads import WORKLOADS, variant_name
+    name = variant_name(args.config or ("4k" if world == 1 else "4k120"), args.vbs, args.me)
     cfg = dict(WORKLOADS[name])
+    if args.vbs:
+        cfg["vbs"] = True
+    if args.me != "full":
+        cfg["me"] = args.me          # a mode without a fixture variant runs unchecked (parity None)
     if args.frames:
         cfg["frames"] = args.frames
         cfg["intra_dur"] = min(cfg["intra_dur"], args.frames)
-    parity_ok = not (args.no_parity or args.frames or args.vbs or args.me != "full")
+    plain_cfg = cfg.get("me", "full") == "full" and not cfg.get("vbs")
+    parity_ok = not (args.no_parity or args.frames)
     if args.shard is None:
         # two GPUs share ONE xGMI link: the frame pipeline would push every reconstruction
         # (8.3 MB per ~71 us frame, ~117 GB/s) over it one way, more than a link direction
@@ -770,7 +817,7 @@ def main(argv=None):
         senc = StripeGOPEncoder(eng)
         rc = cfg.get("rc")
         cap = 768 // (2 * world) if args.share_gpu else 0
-        plain = not rc and args.me == "full" and not args.vbs and eng.pipelined_ok(1)
+        plain = not rc and plain_cfg and eng.pipelined_ok(1)
         fpipe_note = ""
         if args.shard == "fpipe" and plain:
             fenc, fpipe_note = fpipe_encoder(codec, frames, cfg, world, max_wg=cap)
@@ -779,8 +826,12 @@ def main(argv=None):
                          f"alternating per block; {{}})")
             exchange_note = fpipe_note
 
-            def step():      # the SSE all_reduce runs once, after timing (pipeline.py encode)
-                return fenc.encode(frames, cfg["intra_dur"], cfg["qp"], reduce=False)
+            # the SSE all_reduce runs once, after timing (pipeline.py encode), unless every rank
+            # does not hold a P-frame (frames <= ranks): then it orders back-to-back GOPs
+            b2b = f > world
+
+            def step():
+                return fenc.encode(frames, cfg["intra_dur"], cfg["qp"], reduce=not b2b)
         else:
             if args.exchange == "p2p" and plain:
                 penc, exchange_note = p2p_encoder(eng, frames, cfg, senc, world, max_wg=cap)
@@ -806,13 +857,15 @@ def main(argv=None):
     elapsed, res = time_steps(step, world, args.steps, args.warmup, dev)
     if codec is not None and not stripe:
         codec.engine().check_run()
+    timeouts = None
     if penc is not None or fenc is not None:
         # a lost hand-off anywhere voids the timed run: time the all_gather path instead
         import torch.distributed as dist
         r_ = (penc or fenc).r
-        lost = torch.tensor([1 if r_.timed_out() else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(lost, op=dist.ReduceOp.MAX)
-        if int(lost.item()):
+        lost = torch.tensor([int(r_._ws[32].item())], dtype=torch.int32, device=dev)
+        dist.all_reduce(lost, op=dist.ReduceOp.SUM)
+        timeouts = int(lost.item())
+        if timeouts:
             r_._ws[32].zero_()
             penc = fenc = None
             mode_note = f"stripe x{world} (block rows of one GOP; hand-off: {{}})"
@@ -824,8 +877,7 @@ def main(argv=None):
 
     # ---- right after timing (GPU still at its working clock): the dominant kernel's roofline ----
     rl = None
-    if rank == 0 and not args.cpu_plumbing and args.me == "full" and codec.engine().pipelined_ok(1) \
-            and not cfg.get("rc") and not args.vbs:
+    if rank == 0 and not args.cpu_plumbing and plain_cfg and codec.engine().pipelined_ok(1) and not cfg.get("rc"):
         # stripe mode: the kernel is timed on rank 0's GPU alone over the full frame (a
         # one-GPU GOP supplies the reference reconstructions it replays)
         syms = res["symbols"] if not stripe else codec.encode_device(frames, cfg["intra_dur"])["symbols"]
@@ -843,6 +895,7 @@ def main(argv=None):
                 parity = compare_digests(got, fx) if fx else {"bit_exact": None, "note": "no fixture"}
                 if fx:
                     parity["fixture"] = "tests/golden/large_gops.json (C oracle, tests/golden/make_large_fixtures.py)"
+                    parity["psnr_delta_db"] = psnr_delta(res["sse"], fx, -(-h // 16) * 16, w)["psnr_delta_db_max"]
         elif stripe:
             if penc is not None:
                 penc.check()
@@ -851,7 +904,7 @@ def main(argv=None):
                 full = [senc.gather_symbols(s) for s in res["symbols"]]
             if rank == 0:
                 hosts = [{k: (v.cpu().numpy() if torch.is_tensor(v) else v) for k, v in g.items()} for g in full]
-                parity = parity_of(hosts, name, cfg) if not cfg.get("rc") else {
+                parity = parity_of(hosts, name, cfg, sse=res["sse"]) if not cfg.get("rc") else {
                     "bit_exact": None, "note": "per-block QP maps are stripe-local; checked by tests/test_gpu_large.py"}
         elif rank == 0 or world == 1:
             def redo():
@@ -859,7 +912,7 @@ def main(argv=None):
                 r = step()
                 codec.engine().check_run()
                 return r["symbols"]
-            parity = parity_of(res["symbols"], name, cfg, redo)
+            parity = parity_of(res["symbols"], name, cfg, redo, sse=res["sse"])
     barrier(world)
 
     psnr_mean = None
@@ -870,14 +923,16 @@ def main(argv=None):
         psnr_mean = float(np.mean(vals)) if vals else None
 
     records = None
-    if rank == 0 and world == 1 and not args.cpu_plumbing and not args.no_records and name == "4k" \
-            and args.me == "full" and not args.vbs:
-        records = {"1080p": record_1080p(args, dev)}
+    if rank == 0 and world == 1 and not args.cpu_plumbing and not args.no_records and name == "4k":
+        records = {"1080p": record_single("1080p", args, dev)}
         for k in args.gops_in_flight:
             for nm in ("1080p", "4k"):
                 records[f"{nm}_x{k}gop"] = record_gops_in_flight(nm, k, args, dev)
+        if not args.no_content_records:
+            for nm in ("4k_lowtex", "4k_noise"):
+                records[nm] = record_single(nm, args, dev)
     pcie = None
-    if rank == 0 and world == 1 and not args.cpu_plumbing and not args.no_pcie and args.me == "full":
+    if rank == 0 and world == 1 and not args.cpu_plumbing and not args.no_pcie and plain_cfg:
         pcie = pcie_inclusive(codec, cfg, frames)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.cpu_plumbing:
@@ -894,11 +949,13 @@ def main(argv=None):
         "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
         "scaling": "strong" if (stripe or args.cpu_plumbing) else "weak",
         "vs_baseline": None, "dtype": "u8",
+        "value_region": "hbm_resident",
         "data": ("plumbing self-test: trivial CPU stand-in engine, nothing encoded" if args.cpu_plumbing else
                  "synthetic (splitmix64 texture, +2/+1 px/frame motion, streamoptima_amd/synth.py)"),
         "config": {"workload": cfg["workload"], "name": name, "width": w, "height": h, "frames": f,
                    "intra_dur": cfg["intra_dur"], "block_size": 16, "search_range": 16, "qp": cfg["qp"],
-                   "seed": cfg["seed"], "vbs": bool(args.vbs), "nRefFrames": 1, "me": args.me,
+                   "seed": cfg["seed"], "vbs": bool(cfg.get("vbs")), "nRefFrames": 1, "me": cfg.get("me", "full"),
+                   "content": cfg.get("content", "bench"),
                    "transform": "fp64 pocketfft-exact DCT",
                    "parallelism": (mode_note.format(exchange_note) if stripe else f"gop-per-rank x{world}"),
                    "launch": "hip-graph (one GOP per replay)" if args.graph else "host launches"},
@@ -906,7 +963,12 @@ def main(argv=None):
         "roofline": roofline_of(rl, name) if rl else None,
         "cpu_baseline": cpu,
         "psnr_mean_db": round(psnr_mean, 4) if psnr_mean is not None else None,
+        "psnr_delta_db": parity.get("psnr_delta_db") if parity else None,
     }
+    if world > 1:
+        # dependency waits of the in-launch hand-off that passed their bound during the timed
+        # run, summed over ranks (nonzero: that run was discarded and the stripes timed instead)
+        line["timeouts"] = timeouts
     if records:
         line["records"] = records
     if pcie:

@@ -139,6 +139,10 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
  * acquire before reading the reference rows.
  */
 #define SO_P_RUN_TIMEOUT_WORD 32
+/* Word 40: the number of blocks whose exact SEA search took the dense fallback (more than 192
+ * candidates survived the 4x4-cell bound: flat or noise-like content), summed over launches
+ * like the timeout count until the caller clears it (a content statistic, not an error). */
+#define SO_P_RUN_FALLBACK_WORD 40
 size_t so_p_run_workspace_elems(int H, int W);
 int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W,
                     int bs, int sr, int qp_rd, const int32_t* qp_row, uint8_t* const* out_split,
@@ -245,22 +249,6 @@ int so_stripe_halo_push(const uint8_t* plane, int H, int W, int by0, int by1, in
  * are those of so_encode_p_run over the same frames.  so_frame_push sends a finished frame
  * (the I-frame) the same way.  workspace: so_p_run_workspace_elems(H, W), as so_encode_p_run.
  */
-int so_encode_p_run_fpipe(const uint8_t* const* curs, int nframes, int H, int W, int bs, int sr,
-                          int qp_rd, const int32_t* qp_row, uint8_t* const* out_split,
-                          int16_t* const* out_mv, int16_t* const* out_qtc, int32_t* const* out_tokens,
-                          int32_t* const* out_mae_num, uint8_t* const* out_recon,
-                          int32_t* const* out_sse, uint32_t* workspace, const uint8_t* land0,
-                          const uint32_t* land_flags, int slot0, uint8_t* peer_land0,
-                          uint32_t* peer_flags, int peer_slot_off, long long stride, uint32_t epoch,
-                          int max_wg, void* stream);
-/*
- * so_encode_p_run_fpipe with the frames of each block of N consecutive frames dealt to the
- * ranks in alternating ring directions (ranks 0, 1, ..., N-1, then 0, N-1, ..., 1, ...), so a
- * rank hands its reconstructions alternately to the next and to the previous rank -- both
- * directions of every xGMI link carry half the frames instead of one direction all of them.
- * Frame i of the run is pushed into slot push_to[i] >> 1 of peer (push_to[i] & 1 ? peer2 :
- * peer); host int32 [nframes].  Everything else as so_encode_p_run_fpipe.
- */
 int so_encode_p_run_fpipe2(const uint8_t* const* curs, int nframes, int H, int W, int bs, int sr,
                            int qp_rd, const int32_t* qp_row, uint8_t* const* out_split,
                            int16_t* const* out_mv, int16_t* const* out_qtc, int32_t* const* out_tokens,
@@ -268,8 +256,8 @@ int so_encode_p_run_fpipe2(const uint8_t* const* curs, int nframes, int H, int W
                            int32_t* const* out_sse, uint32_t* workspace, const uint8_t* land0,
                            const uint32_t* land_flags, int slot0, uint8_t* peer_land0,
                            uint32_t* peer_flags, uint8_t* peer2_land0, uint32_t* peer2_flags,
-                           const int32_t* push_to, long long stride, uint32_t epoch, int max_wg,
-                           void* stream);
+                           const int32_t* push_to, int nslots, long long stride, uint32_t epoch,
+                           int max_wg, void* stream);
 int so_frame_push(const uint8_t* plane, int H, int W, uint8_t* peer_plane, uint32_t* peer_flags,
                   uint32_t epoch, void* stream);
 

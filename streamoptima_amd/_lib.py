@@ -66,10 +66,9 @@ _SIGS = {
     "so_pack_bound": ([_i, _i], _sz),
     "so_sum_i32_rows": ([_vp, _i, _i, _vp, _vp], _i),
     "so_unpack_frames": ([_i, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp], _i),
-    "so_encode_p_run_fpipe": ([_vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                               _vp, _vp, _i, _vp, _vp, _i, ctypes.c_longlong, ctypes.c_uint32, _i, _vp], _i),
     "so_encode_p_run_fpipe2": ([_vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, ctypes.c_longlong, ctypes.c_uint32, _i, _vp],
+                                _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _i, ctypes.c_longlong, ctypes.c_uint32, _i,
+                                _vp],
                                _i),
     "so_frame_push": ([_vp, _i, _i, _vp, _vp, ctypes.c_uint32, _vp], _i),
     "so_pack_frames": ([_i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, ctypes.c_ulonglong, _vp], _i),

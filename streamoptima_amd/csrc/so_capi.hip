@@ -11,6 +11,7 @@
 #include <hip/hip_ext.h>
 
 #include "so_common.h"
+#include "so_run.h"
 
 namespace so {
 
@@ -39,49 +40,6 @@ int p_tile_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int by0,
                   int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon,
                   int32_t* out_sse, hipStream_t st, bool tokens_only = false);
 
-struct PFrameOut {
-    uint8_t* split;
-    int16_t* mv;
-    int16_t* qtc;
-    int32_t* tokens;
-    int32_t* mae;
-    uint8_t* recon;
-    int32_t* sse;
-    int32_t* qpmap;
-};
-size_t p_run_workspace_words(int H, int W);
-int p_run_2pass_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
-                       const int32_t* qp_row, const int32_t* roi, int qp_lo, int qp_hi, const PFrameOut* outs,
-                       uint32_t* ws, hipStream_t st);
-int32_t* p_run_t1_region(uint32_t* ws, int H, int W);
-int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
-                 const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, hipStream_t st);
-int p_runs_launch(const uint8_t* const* curs, int nframes, const uint8_t* const* refs, const int* deps, int conc,
-                  int H, int W, int qp_rd, const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws,
-                  hipStream_t st);
-struct PRunStripe {
-    int by0, by1;
-    uint8_t* peer_up0;
-    uint8_t* peer_dn0;
-    long long stride;
-    const uint32_t* my_up_flags;
-    const uint32_t* my_dn_flags;
-    uint32_t* peer_up_flags;
-    uint32_t* peer_dn_flags;
-    uint32_t epoch;
-    int gbase;
-    const uint8_t* land0;
-    int peer_slot_off;
-    uint32_t* p1done;   // two-pass runs only (layout shared with so_me.hip)
-    int32_t* t1;
-    const int32_t* roi;
-    int qp_lo, qp_hi;
-    int p2lag;
-    int xq;
-};
-int p_run_stripe_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
-                        const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg,
-                        hipStream_t st);
 struct PackFrame {
     const uint8_t* split;
     const int16_t* mv;
@@ -103,8 +61,6 @@ int unpack_frames_launch(const UnpackFrame* frames, int nframes, int nb, int bs,
 int pack_frames_launch(const PackFrame* frames, int nframes, int nb, int bs, unsigned long long cap, hipStream_t st);
 int stripe_halo_push_launch(const uint8_t* plane, int W, int by0, int by1, uint8_t* up, uint8_t* dn,
                             uint32_t* up_flags, uint32_t* dn_flags, int gf, uint32_t epoch, hipStream_t st);
-int p_run_fpipe_launch(const uint8_t* const* curs, int nframes, int H, int W, int qp_rd, const int32_t* qp_row,
-                       const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg, hipStream_t st, const int* push = nullptr);
 int frame_push_launch(const uint8_t* plane, int H, int W, uint8_t* dst, uint32_t* flags, uint32_t epoch,
                       hipStream_t st);
 
@@ -592,7 +548,7 @@ int so_encode_p_run_stripe(const uint8_t* const* curs, int nframes, const uint8_
                             out_sse ? out_sse[i] : nullptr};
     }
     PRunStripe sp{by0, by1, peer_up0, peer_dn0, stride, my_up_flags, my_dn_flags, peer_up_flags, peer_dn_flags,
-                  epoch, gbase, nullptr, 0};
+                  epoch, gbase, nullptr};
     return p_run_stripe_launch(curs, nframes, ref0, H, W, qp_rd, qp_row, outs.data(), workspace, sp, max_wg,
                                (hipStream_t)stream);
 }
@@ -617,54 +573,13 @@ int so_stripe_halo_push(const uint8_t* plane, int H, int W, int by0, int by1, in
 }
 
 // ---- one GOP across GPUs: consecutive frames on consecutive ranks (so_me.hip kRunFPipe) -----
-int so_encode_p_run_fpipe(const uint8_t* const* curs, int nframes, int H, int W, int bs, int sr, int qp_rd,
-                          const int32_t* qp_row, uint8_t* const* out_split, int16_t* const* out_mv,
-                          int16_t* const* out_qtc, int32_t* const* out_tokens, int32_t* const* out_mae_num,
-                          uint8_t* const* out_recon, int32_t* const* out_sse, uint32_t* workspace,
-                          const uint8_t* land0, const uint32_t* land_flags, int slot0, uint8_t* peer_land0,
-                          uint32_t* peer_flags, int peer_slot_off, long long stride, uint32_t epoch, int max_wg,
-                          void* stream) {
-    const char* fn = "so_encode_p_run_fpipe";
-    SO_TRY(check_geom(fn, H, W, bs, 0));
-    SO_TRY(check_sr(fn, sr));
-    SO_TRY(check_qp(fn, qp_rd));
-    if (bs != 16 || sr != 16 || W % 128 != 0) {
-        set_error("%s: covers bs 16 / sr 16 / W %% 128 == 0", fn);
-        return SO_E_UNSUPPORTED;
-    }
-    if (slot0 < 0 || peer_slot_off < 0 || peer_slot_off > 1 || stride < (long long)H * W) {
-        set_error("%s: slot0 %d / peer_slot_off %d / stride %lld", fn, slot0, peer_slot_off, stride);
-        return SO_E_INVALID;
-    }
-    if (nframes <= 0) return SO_OK;
-    SO_NEED(curs, fn); SO_NEED(out_split, fn); SO_NEED(out_mv, fn); SO_NEED(out_qtc, fn); SO_NEED(out_tokens, fn);
-    SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn); SO_NEED(workspace, fn); SO_NEED(land0, fn);
-    SO_NEED(land_flags, fn); SO_NEED(peer_land0, fn); SO_NEED(peer_flags, fn);
-    std::vector<PFrameOut> outs((size_t)nframes);
-    const uint8_t* land_end = land0 + (long long)(slot0 + nframes) * stride;
-    for (int i = 0; i < nframes; ++i) {
-        SO_NEED(curs[i], fn); SO_NEED(out_split[i], fn); SO_NEED(out_mv[i], fn); SO_NEED(out_qtc[i], fn);
-        SO_NEED(out_tokens[i], fn); SO_NEED(out_mae_num[i], fn); SO_NEED(out_recon[i], fn);
-        if (out_recon[i] >= land0 && out_recon[i] < land_end) {
-            set_error("%s: out_recon[%d] lies in the landing planes", fn, i);
-            return SO_E_INVALID;
-        }
-        outs[i] = PFrameOut{out_split[i], out_mv[i], out_qtc[i], out_tokens[i], out_mae_num[i], out_recon[i],
-                            out_sse ? out_sse[i] : nullptr};
-    }
-    PRunStripe sp{0, H / 16, nullptr, peer_land0, stride, nullptr, land_flags, nullptr, peer_flags,
-                  epoch, slot0, land0, peer_slot_off};
-    return p_run_fpipe_launch(curs, nframes, H, W, qp_rd, qp_row, outs.data(), workspace, sp, max_wg,
-                              (hipStream_t)stream);
-}
-
 int so_encode_p_run_fpipe2(const uint8_t* const* curs, int nframes, int H, int W, int bs, int sr, int qp_rd,
                            const int32_t* qp_row, uint8_t* const* out_split, int16_t* const* out_mv,
                            int16_t* const* out_qtc, int32_t* const* out_tokens, int32_t* const* out_mae_num,
                            uint8_t* const* out_recon, int32_t* const* out_sse, uint32_t* workspace,
                            const uint8_t* land0, const uint32_t* land_flags, int slot0, uint8_t* peer_land0,
                            uint32_t* peer_flags, uint8_t* peer2_land0, uint32_t* peer2_flags, const int32_t* push_to,
-                           long long stride, uint32_t epoch, int max_wg, void* stream) {
+                           int nslots, long long stride, uint32_t epoch, int max_wg, void* stream) {
     const char* fn = "so_encode_p_run_fpipe2";
     SO_TRY(check_geom(fn, H, W, bs, 0));
     SO_TRY(check_sr(fn, sr));
@@ -673,8 +588,10 @@ int so_encode_p_run_fpipe2(const uint8_t* const* curs, int nframes, int H, int W
         set_error("%s: covers bs 16 / sr 16 / W %% 128 == 0", fn);
         return SO_E_UNSUPPORTED;
     }
-    if (slot0 < 0 || stride < (long long)H * W) {
-        set_error("%s: slot0 %d / stride %lld", fn, slot0, stride);
+    // every rank owns `nslots` landing slots: this run reads slots [slot0, slot0 + nframes) and
+    // writes (system scope, over xGMI) only slots below nslots of its peers
+    if (slot0 < 0 || nslots < 1 || slot0 + nframes > nslots || stride < (long long)H * W) {
+        set_error("%s: slot0 %d + %d frames / nslots %d / stride %lld", fn, slot0, nframes, nslots, stride);
         return SO_E_INVALID;
     }
     if (nframes <= 0) return SO_OK;
@@ -692,8 +609,8 @@ int so_encode_p_run_fpipe2(const uint8_t* const* curs, int nframes, int H, int W
             set_error("%s: out_recon[%d] lies in the landing planes", fn, i);
             return SO_E_INVALID;
         }
-        if (push_to[i] < 0) {
-            set_error("%s: push_to[%d] = %d", fn, i, push_to[i]);
+        if (push_to[i] < -1 || (push_to[i] >> 1) >= nslots) {   // -1: nothing follows, no push
+            set_error("%s: push_to[%d] = %d (nslots %d)", fn, i, push_to[i], nslots);
             return SO_E_INVALID;
         }
         push[(size_t)i] = push_to[i];
@@ -701,7 +618,7 @@ int so_encode_p_run_fpipe2(const uint8_t* const* curs, int nframes, int H, int W
                             out_sse ? out_sse[i] : nullptr};
     }
     PRunStripe sp{0, H / 16, peer2_land0, peer_land0, stride, nullptr, land_flags, peer2_flags, peer_flags,
-                  epoch, slot0, land0, 0};
+                  epoch, slot0, land0};
     return p_run_fpipe_launch(curs, nframes, H, W, qp_rd, qp_row, outs.data(), workspace, sp, max_wg,
                               (hipStream_t)stream, push.data());
 }

@@ -256,9 +256,8 @@ me_fastpred_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, int H,
 // chain of 32,400 dependent steps (a 4K frame) becomes K + WARM steps per wavefront plus one
 // compare per segment and a K-step redo per wrong guess.
 constexpr int kFastSegMax = 4096;                 // segments per launch (the fix kernel's LDS)
-// per segment: guessed predictor, last mv; two buffers (correction rounds ping-pong) in the
-// caller's scratch (kFastSegWords int32 after the ME records, so_p_frame_scratch_elems)
-constexpr int kFastSegBuf = kFastSegMax * 6;
+// per segment: guessed predictor, last mv, in the caller's scratch (kFastSegWords int32 after
+// the ME records, so_p_frame_scratch_elems; the second half of that region is unused)
 
 template <bool FME, int BS>
 SO_DEV Mvp fast_chain_mv(const uint8_t* __restrict__ cur, const FastRefs& R, int nref, int H, int W, int x, int y,
@@ -293,47 +292,15 @@ me_fastchain_spec_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, 
     }
 }
 
-// A correction round, every segment in parallel: a segment whose guess differs from the
-// previous segment's last mv of the round before runs again from that mv (right whenever
-// the previous segment was right), so each round fixes the first wrong segment of every run
-// of wrong ones.  Reads buffer `src`, writes buffer 1 - src.
-template <bool FME, bool SUB, int BS>
-__global__ void __launch_bounds__(64)
-me_fastchain_round_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, int H, int W, int by0, int by1, int K,
-                          int src, int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub, int32_t* seg) {
-    const int nbx = W / BS, nb = nbx * (by1 - by0);
-    const int lane = threadIdx.x;
-    const int s = blockIdx.x, b0 = s * K, b1 = b0 + K < nb ? b0 + K : nb;
-    const int32_t* in = seg + src * kFastSegBuf;
-    int32_t* out = seg + (1 - src) * kFastSegBuf;
-    const int32_t* me = in + s * 6;
-    Mvp g{me[0], me[1], me[2]}, last{me[3], me[4], me[5]};
-    if (s > 0) {
-        const Mvp t{in[s * 6 - 3], in[s * 6 - 2], in[s * 6 - 1]};
-        if (t.dx != g.dx || t.dy != g.dy || t.ref != g.ref) {
-            g = t;
-            Mvp mvp = t;
-            for (int b = b0; b < b1; ++b)
-                mvp = fast_block<FME, SUB, BS>(cur, R, nref, H, W, (b % nbx) * BS, (by0 + b / nbx) * BS, mvp, lane,
-                                               out_best + (size_t)b * 4, out_sub ? out_sub + (size_t)b * 16 : nullptr);
-            last = mvp;
-        }
-    }
-    if (lane == 0) {
-        out[s * 6 + 0] = g.dx; out[s * 6 + 1] = g.dy; out[s * 6 + 2] = g.ref;
-        out[s * 6 + 3] = last.dx; out[s * 6 + 4] = last.dy; out[s * 6 + 5] = last.ref;
-    }
-}
-
 template <bool FME, bool SUB, int BS>
 __global__ void __launch_bounds__(64)
 me_fastchain_fix_kernel(const uint8_t* __restrict__ cur, FastRefs R, int nref, int H, int W, int by0, int by1, int K,
-                        int nseg, int src, int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub,
+                        int nseg, int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub,
                         const int32_t* __restrict__ segws, int32_t* __restrict__ nfixed) {
     __shared__ int32_t seg[kFastSegMax * 6];
     const int nbx = W / BS, nb = nbx * (by1 - by0);
     const int lane = threadIdx.x;
-    for (int i = lane; i < nseg * 6; i += 64) seg[i] = segws[src * kFastSegBuf + i];
+    for (int i = lane; i < nseg * 6; i += 64) seg[i] = segws[i];
     __syncthreads();
     Mvp truth{seg[3], seg[4], seg[5]};   // segment 0 started from the true (0, 0, 0)
     int fixed = 0;
@@ -374,10 +341,9 @@ int me_fastpred_launch(const uint8_t* cur, const uint8_t* const* ptrs, int nptr,
     if (nb <= 0) return SO_OK;
     const char* ser = getenv("SO_FASTME_SERIAL");   // A/B: the one-wavefront walk
     if (serial && seg_ws && !(ser && atoi(ser) == 1)) {   // no workspace (so_me_search_ex): the walk
-        int K = 32, warm = 32, rounds = 0;   // correction rounds: measured no gain
+        int K = 32, warm = 32;
         if (const char* e = getenv("SO_FASTME_K")) K = atoi(e) > 0 ? atoi(e) : K;
         if (const char* e = getenv("SO_FASTME_WARM")) warm = atoi(e) >= 0 ? atoi(e) : warm;
-        if (const char* e = getenv("SO_FASTME_ROUNDS")) rounds = atoi(e) >= 0 ? atoi(e) : rounds;
         if ((nb + K - 1) / K > kFastSegMax) K = (nb + kFastSegMax - 1) / kFastSegMax;
         const int nseg = (nb + K - 1) / K;
         int32_t* nfixed = nullptr;
@@ -388,11 +354,8 @@ int me_fastpred_launch(const uint8_t* cur, const uint8_t* const* ptrs, int nptr,
         do {                                                                                                        \
             hipLaunchKernelGGL((me_fastchain_spec_kernel<F, S, B>), dim3(nseg), dim3(64), 0, st, cur, R, nref, H,   \
                                W, by0, by1, K, warm, out_best, out_sub, seg_ws);                                    \
-            for (int k = 0; k < rounds; ++k)                                                                        \
-                hipLaunchKernelGGL((me_fastchain_round_kernel<F, S, B>), dim3(nseg), dim3(64), 0, st, cur, R, nref, \
-                                   H, W, by0, by1, K, k & 1, out_best, out_sub, seg_ws);                            \
             hipLaunchKernelGGL((me_fastchain_fix_kernel<F, S, B>), dim3(1), dim3(64), 0, st, cur, R, nref, H, W,    \
-                               by0, by1, K, nseg, rounds & 1, out_best, out_sub, seg_ws, nfixed);                   \
+                               by0, by1, K, nseg, out_best, out_sub, seg_ws, nfixed);                               \
         } while (0)
         if (bs == 16) {
             if (fme) { if (sub) SO_FASTCHAIN(true, true, 16); else SO_FASTCHAIN(true, false, 16); }

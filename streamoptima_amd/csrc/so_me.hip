@@ -22,6 +22,7 @@
 #include "so_block.h"
 #include "so_common.h"
 #include "so_dpp.h"
+#include "so_run.h"
 
 namespace so {
 
@@ -600,8 +601,7 @@ int me_fme_launch(const uint8_t* cur, const uint8_t* planes, size_t pstride, int
 #endif
 // NW_ waves per workgroup: 8 (two blocks per wave; me_sea2_kernel) or 16 (one block per
 // wave; p_tile_kernel at 8 waves/SIMD)
-// TPX_: tile width, 128 (16 blocks; the default) or 64 (8 blocks: p_run_kernel when a frame
-// has fewer 128-wide tiles than resident workgroups, where a tile's latency sets the frame time)
+// TPX_: tile width, 128 (16 blocks)
 template <int NW_, int TPX_ = 128>
 struct Sea2GeoT {
     static constexpr int SR = 16, NT = 17;
@@ -681,10 +681,7 @@ struct NoPre {
 // `pre` runs (on every wave) after the current tile is staged and before the first
 // reference's window is read: p_run_kernel waits there for the reference's tiles, so the
 // current-tile staging overlaps that wait.
-template <class G>
-SO_DEV void sea2_subblocks(const Sea2Lds& L, int u, int bxl, int byl, int x, int y, int W, int H, int r, int tid);
-
-template <class G, class Pre = NoPre, bool VBS = false>
+template <class G, class Pre = NoPre>
 SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cur, const RefSet& refs, int nref,
                       int H, int W, int by0, int by1, int probe, const Pre& pre = Pre()) {
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RP = G::RP, NT = G::NT;
@@ -704,15 +701,18 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
     const int x0 = bx0 * 16, y0 = byt0 * 16;
     const int tid = opaque_tid();
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-#ifdef SO_STAMPS
+    // st[0]: blocks of this tile that took the dense fallback (the run adds it to its workspace
+    // fallback count: the content-dependence records of bench.py)
     uint32_t& st_fb = L.st[0];
+    if (tid == 0) st_fb = 0;
+#ifdef SO_STAMPS
     uint32_t& st_sur = L.st[1];
-    if (tid == 0) { st_fb = 0; st_sur = 0; }
+    if (tid == 0) st_sur = 0;
     SO_SEA_STAMP(0, __builtin_amdgcn_s_memrealtime());
     SO_SEA_STAMP(1, __builtin_amdgcn_s_memtime());
 #endif
 
-    for (int i = tid; i < G::NBLK * (VBS ? 5 : 1); i += G::NTHREADS) keys[i] = kNoKey;
+    for (int i = tid; i < G::NBLK; i += G::NTHREADS) keys[i] = kNoKey;
     // interior window (uniform): thread = (row, column phase) with immediate per-dword offsets
     constexpr int WTPR = G::NTHREADS / G::WR, WNPT = (RP + WTPR - 1) / WTPR;
     static_assert(G::NTHREADS % G::WR == 0, "window staging");
@@ -950,9 +950,10 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
                 }
             }
 #ifdef SO_STAMPS
-            if (lane == 0) { atomicAdd(&st_sur, nsur); if (nsur > (uint32_t)CAP) atomicAdd(&st_fb, 1u); }
+            if (lane == 0) atomicAdd(&st_sur, nsur);
 #endif
             if (nsur > (uint32_t)CAP) {
+                if (lane == 0) atomicAdd(&st_fb, 1u);
                 if (probe == 3) continue;
                 // fallback: the dense wave search on the single-copy window
                 wave_dense_block<16, false, RP, 0, false, true>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u, tid,
@@ -1026,14 +1027,6 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             best = wave_min_u64_dpp(best);
             if (lane == 0 && best < keys[u]) keys[u] = best;
         }
-        if constexpr (VBS) {   // the sub-blocks, after their block (its best mv bounds them too)
-#pragma unroll 1
-            for (int u = wave; u < G::NBLK; u += G::NW) {
-                const int bxl = u % TBX, byl = u / TBX;
-                if (bx0 + bxl >= nbx || byt0 + byl >= by1) continue;   // wave-uniform
-                sea2_subblocks<G>(L, u, bxl, byl, x0 + bxl * 16, y0 + byl * 16, W, H, r, tid);
-            }
-        }
     }
     __syncthreads();
 }
@@ -1078,204 +1071,6 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
 #endif
 }
 
-// ---- VBS: exact SEA for the four 8x8 sub-blocks (me_sea2_vbs_kernel) -------------------------
-// The sub-block searches of inter_prediction (Encoder.py:512-544: find_best_match(sub, bs/2)
-// for blocks with x != 0 and y != 0) on the same LDS window and 4x4 byte sums as the block's
-// own SEA.  A sub-block covers 2 x 2 of the block's 4x4 cells: its bound is the block bound's
-// v_sad over the two cells of each of its two cell rows (the cell-sum dwords masked to bytes
-// 2a, 2a+1), SAD >= 16 sum|dq| - 4 * 15; U = the exact SAD of the smallest-bound candidate;
-// every valid candidate with bound <= U is evaluated exactly (four lanes per candidate), more
-// than CAP survivors take every valid candidate.  Candidate validity and the key are the
-// sub-block's own: 0 <= xs + dx < W - 8, 0 <= ys + dy < H - 8; (SAD, |dx|+|dy|, ref, scan).
-template <class G>
-SO_DEV void sea2_subblocks(const Sea2Lds& L, int u, int bxl, int byl, int x, int y, int W, int H, int r, int tid) {
-    constexpr int SR = G::SR, NT = G::NT, RP = G::RP, B4P = G::B4P, CAP = G::CAP, CPD = G::CPD;
-    if (x == 0 || y == 0) return;   // no sub-block search there (Encoder.py:512); uniform
-    int lane = tid & 63;
-    asm volatile("" : "+v"(lane));
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int xi = lane & 31, hh = lane >> 5;
-    const int d2 = lane < 33 ? lane : 32;
-    uint32_t A[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) A[j] = L.a4[u * 4 + j];
-    const int cB = bxl * 16 + xi;
-    const int lb0 = (byl * 16 + 16 * hh) * B4P + (cB & 3) * G::WD + (cB >> 2);
-    const uint32_t bsh = (uint32_t)lb0 & 3;
-    int lo1 = lb0 >> 2;
-    asm volatile("" : "+v"(lo1));
-    lds_vu32p p1 = (lds_vu32p)(L.b4w + lo1);
-    int lo2 = ((byl * 16 + d2) * B4P + ((bxl * 16 + 32) >> 2)) >> 2;
-    asm volatile("" : "+v"(lo2));
-    lds_vu32p p2 = (lds_vu32p)(L.b4w + lo2);
-    uint16_t* const mylist = L.list + wave * CAP;
-    constexpr uint32_t kBig = 0x7FFFFFFFu;
-#pragma unroll 1
-    for (int bq = 0; bq < 2; ++bq) {
-        const int ys = y + 8 * bq;
-        // bounds of the two sub-blocks of this half: (LBq << 16) | t, left (a = 0) and right
-        uint32_t lbL[NT], lbR[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) { lbL[t] = (uint32_t)t; lbR[t] = (uint32_t)t; }
-        const uint32_t AL0 = A[2 * bq] & 0xFFFFu, AR0 = A[2 * bq] & 0xFFFF0000u;
-        const uint32_t AL1 = A[2 * bq + 1] & 0xFFFFu, AR1 = A[2 * bq + 1] & 0xFFFF0000u;
-#pragma unroll
-        for (int k = 0; k < NT + 4; ++k) {   // byte-sum row 8 bq + k: cell row 0 of t = k, row 1 of t = k - 4
-            const int row = 8 * bq + k;
-            const uint32_t w0 = p1[row * (B4P / 4)], w1 = p1[row * (B4P / 4) + 1];
-            const uint32_t P = __builtin_amdgcn_alignbyte(w1, w0, bsh);
-            const uint32_t PL = P & 0xFFFFu, PR = P & 0xFFFF0000u;
-            if (k < NT) {
-                lbL[k] = __builtin_amdgcn_sad_hi_u8(AL0, PL, lbL[k]);
-                lbR[k] = __builtin_amdgcn_sad_hi_u8(AR0, PR, lbR[k]);
-            }
-            if (k >= 4) {
-                lbL[k - 4] = __builtin_amdgcn_sad_hi_u8(AL1, PL, lbL[k - 4]);
-                lbR[k - 4] = __builtin_amdgcn_sad_hi_u8(AR1, PR, lbR[k - 4]);
-            }
-        }
-        uint32_t l2L = 0, l2R = 0;
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr) {
-            const uint32_t q = p2[(8 * bq + 4 * rr) * (B4P / 4)];
-            l2L = __builtin_amdgcn_sad_u8(A[2 * bq + rr] & 0xFFFFu, q & 0xFFFFu, l2L);
-            l2R = __builtin_amdgcn_sad_u8(A[2 * bq + rr] & 0xFFFF0000u, q & 0xFFFF0000u, l2R);
-        }
-        int dlo = SR - ys;              dlo = dlo < 0 ? 0 : dlo;
-        int dhi = H - 8 - ys + SR - 1;  dhi = dhi > 32 ? 32 : dhi;
-#pragma unroll 1
-        for (int a = 0; a < 2; ++a) {
-            const int xs = x + 8 * a, j = 2 * bq + a;
-            uint32_t lb[NT];
-#pragma unroll
-            for (int t = 0; t < NT; ++t) lb[t] = a ? lbR[t] : lbL[t];
-            const uint32_t lb2 = a ? l2R : l2L;
-            const bool xok = (xs + xi - 16 >= 0) && (xs + xi - 16 < W - 8);
-            const bool ok2 = lane < 33 && (xs + 16 < W - 8) && d2 >= dlo && d2 <= dhi;
-            {
-                const int tlo = dlo - 16 * hh, thi = dhi - 16 * hh;
-#pragma unroll
-                for (int t = 0; t < NT; ++t) lb[t] = (t < tlo || t > thi) ? kBig : lb[t];
-            }
-            uint32_t kt = lb[0];
-#pragma unroll
-            for (int t = 1; t < NT; ++t) kt = lb[t] < kt ? lb[t] : kt;
-            uint32_t kl = (xok && kt != kBig) ? ((kt >> 16) << 11) | (uint32_t)(xi * 33 + 16 * hh + (kt & 31))
-                                              : 0xFFFFFFFFu;
-            {
-                const uint32_t k2 = (lb2 << 11) | (uint32_t)(32 * 33 + d2);
-                kl = (ok2 && k2 < kl) ? k2 : kl;
-            }
-            const uint32_t kmin = wave_min_u32(kl);
-            if (kmin == 0xFFFFFFFFu) continue;   // no valid candidate: the sub key stays none
-            const int cs = (int)(kmin & 2047), cdx = cs / 33, cdi = cs - cdx * 33;
-            const int crow0 = (byl * 16 + 8 * bq) * CPD + bxl * 4 + 2 * a;   // sub-block in curt (dwords)
-            uint32_t U;
-            {
-                const int row = (lane >> 1) & 7, kk = lane & 1;
-                const uint32_t w = win_u32<RP>(L.win, byl * 16 + 8 * bq + cdi + row, bxl * 16 + 8 * a + cdx + 4 * kk);
-                const uint32_t sd = __builtin_amdgcn_sad_u8(L.curt[crow0 + row * CPD + kk], w, 0u);
-                U = wave_sum_u32(lane < 16 ? sd : 0u);
-            }
-            {   // the block's best mv so far (this reference): valid for its sub-blocks too
-                const unsigned long long kb = L.keys[u];
-                if (kb != kNoKey && (int)((kb >> 16) & 0xFF) == r) {
-                    const int bs_ = (int)(kb & 0xFFFF), bdx = bs_ / 33, bdi = bs_ - bdx * 33;
-                    const int row = (lane >> 1) & 7, kk = lane & 1;
-                    const uint32_t w = win_u32<RP>(L.win, byl * 16 + 8 * bq + bdi + row, bxl * 16 + 8 * a + bdx + 4 * kk);
-                    const uint32_t sd = __builtin_amdgcn_sad_u8(L.curt[crow0 + row * CPD + kk], w, 0u);
-                    const uint32_t Ub = wave_sum_u32(lane < 16 ? sd : 0u);
-                    U = Ub < U ? Ub : U;
-                }
-            }
-            const uint32_t qU = (U + 60) >> 4;
-            int thr = xok ? (int)((qU << 16) | 0xFFFFu) : -1;
-            asm volatile("" : "+v"(thr));
-            const int cbase = xi * 33 + 16 * hh;
-            uint32_t nsur = 0;
-#pragma unroll
-            for (int t = 0; t <= NT; ++t) {
-                const bool pass = t < NT ? (int)lb[t] <= thr : (ok2 && lb2 <= qU);
-                const uint64_t bal = __builtin_amdgcn_ballot_w64(pass);
-                if (bal) {
-                    const uint32_t pos = nsur + lane_prefix(bal);
-                    if (pass && pos < (uint32_t)CAP) mylist[pos] = (uint16_t)(t < NT ? cbase + t : 32 * 33 + d2);
-                    nsur += (uint32_t)__builtin_popcountll(bal);
-                }
-            }
-            const bool dense = nsur > (uint32_t)CAP;   // every candidate instead of the list
-            const uint32_t ncand = dense ? 33u * 33u : nsur;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // four lanes (a quad) per candidate, rows 2q, 2q + 1 of the sub-block per lane
-            const int sidx = lane >> 2, q = lane & 3;
-            uint32_t cr[2][2];
-#pragma unroll
-            for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-                for (int k = 0; k < 2; ++k) cr[rr][k] = L.curt[crow0 + (2 * q + rr) * CPD + k];
-            uint64_t best = kNoKey;
-#pragma unroll 1
-            for (uint32_t s0 = 0; s0 < ncand; s0 += 16) {
-                const uint32_t ci = s0 + (uint32_t)sidx;
-                bool act = ci < ncand;
-                int cand = act ? (dense ? (int)ci : (int)mylist[ci]) : cs;
-                const int dxi = cand / 33, di = cand - dxi * 33;
-                if (dense)
-                    act = act && xs + dxi - 16 >= 0 && xs + dxi - 16 < W - 8 && ys + di - 16 >= 0 && ys + di - 16 < H - 8;
-                const int col = bxl * 16 + 8 * a + dxi;
-                const int row0 = byl * 16 + 8 * bq + di + 2 * q;
-                uint32_t sad = 0;
-#pragma unroll
-                for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-                    for (int k = 0; k < 2; ++k)
-                        sad = __builtin_amdgcn_sad_u8(cr[rr][k], win_u32<RP>(L.win, row0 + rr, col + 4 * k), sad);
-                sad = quad_sum_u32(sad);
-                const int dx = dxi - 16, dy = di - 16;
-                const uint64_t key = me_key(sad, (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)), (uint32_t)r,
-                                            (uint32_t)cand);
-                best = (act && key < best) ? key : best;
-            }
-            best = wave_min_u64_dpp(best);
-            if (lane == 0 && best < L.keys[G::NBLK + 4 * u + j]) L.keys[G::NBLK + 4 * u + j] = best;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // mylist reused by the next sub-block
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-    }
-}
-
-__global__ void __launch_bounds__(Sea2Geo::NTHREADS) __attribute__((amdgpu_waves_per_eu(SO_SEA2_WPE)))
-me_sea2_vbs_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, int W, int by0, int by1,
-                   int32_t* __restrict__ out_best, int32_t* __restrict__ out_sub) {
-    using G = Sea2Geo;
-    constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RP = G::RP, B4P = G::B4P;
-    __shared__ uint32_t win[G::WR * RP + 4];
-    __shared__ uint32_t b4w[(G::B4RS * B4P + 4) / 4];
-    __shared__ uint32_t curt[G::TPY * G::CPD];
-    __shared__ uint32_t a4[G::NBLK * 4];
-    __shared__ uint16_t list[G::NW * G::CAP];
-    __shared__ uint32_t lcount[G::NW];
-    __shared__ unsigned long long keys[G::NBLK * 5];
-    __shared__ uint32_t st[2];
-    const Sea2Lds L{win, b4w, curt, a4, list, lcount, keys, st};
-    sea2_tile<Sea2Geo, NoPre, true>(L, blockIdx.x, cur, refs, nref, H, W, by0, by1, 0);
-    const int tid = threadIdx.x;
-    const int nbx = W / 16;
-    const int tiles_x = (nbx + TBX - 1) / TBX;
-    const int bx0 = (blockIdx.x % tiles_x) * TBX, byt0 = by0 + (blockIdx.x / tiles_x) * TBY;
-    for (int i = tid; i < G::NBLK * 5; i += G::NTHREADS) {
-        const int blk = i < G::NBLK ? i : (i - G::NBLK) >> 2;
-        const int gbx = bx0 + blk % TBX, gby = byt0 + blk / TBX;
-        if (gbx >= nbx || gby >= by1) continue;
-        const size_t b = (size_t)(gby - by0) * nbx + gbx;
-        if (i < G::NBLK) decode_key(keys[i], SR, out_best + b * 4);
-        else decode_key(keys[i], SR, out_sub + (b * 4 + ((i - G::NBLK) & 3)) * 4);
-    }
-}
-
 // ---------------------------------------------------------------------------------------
 // Fused P-frame tile (p_tile_kernel, the default for bs 16 / sr 16 / no VBS / one reference):
 // the SEA search of a 128x32 tile (sea2_tile) followed, in the same workgroup, by the
@@ -1301,12 +1096,9 @@ me_sea2_vbs_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H
 // tools/sea_stamps.py).  Per-tile flags (not per-row counters) matter at 1080p, where
 // fewer tiles than resident workgroups make the frame-to-frame latency the limit.
 // ---------------------------------------------------------------------------------------
-// FP64 transpose scratch per block of the fused tile: 16 x 17 doubles, or 16 x 9 with the
-// two-half transposes (SO_TQ_HALF: 18 KB instead of 35 KB of LDS per workgroup)
-#ifndef SO_TQ_HALF
-#define SO_TQ_HALF 0
-#endif
-constexpr int kTqScratch = SO_TQ_HALF ? 16 * 9 : 16 * 17;
+// FP64 transpose scratch per block of the fused tile: 16 x 17 doubles.  (Two-half transposes,
+// 16 x 9, would let 4 workgroups fit per CU but spill at 64-80 VGPRs: measured slower, DESIGN.md.)
+constexpr int kTqScratch = 16 * 17;
 template <class G>
 struct PTileGeo {
     static constexpr int B4 = (G::B4RS * G::B4P + 4) / 4;             // dwords
@@ -1343,19 +1135,6 @@ struct PTileLds {
     int32_t msum[G::TBY];                  // two-pass runs: pass-1 token sum of each block row
     double un[PTileGeo<G>::U64];           // byte sums + survivor lists | FP64 transposes
 };
-
-// Outputs of one frame (pointers relative to block row by0 of the launch).
-struct PFrameOut {
-    uint8_t* split;
-    int16_t* mv;
-    int16_t* qtc;
-    int32_t* tokens;
-    int32_t* mae;
-    uint8_t* recon;
-    int32_t* sse;
-    int32_t* qpmap;   // two-pass runs: the per-block QP used (so_encode_p_run_2pass); else null
-};
-
 
 // Boundary rows of a rank's stripe that the neighbouring ranks read (so_encode_p_run_stripe):
 // rows [y0s, up_end) are also stored into the up neighbour's landing plane of the frame, rows
@@ -1398,8 +1177,7 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
             }
         }
         double tcr[16];
-        if constexpr (SO_TQ_HALF) xform2d_rows_half<false>(dl, l, res, tcr);
-        else xform2d_rows<16, false>(dl, l, res, tcr);
+        xform2d_rows<16, false>(dl, l, res, tcr);
         // np.round to int by the 1.5 * 2^52 shift (|values| < 2^51): x + kRne rounds x to an
         // integer half-to-even, held in the low mantissa dword as two's complement -- one
         // v_add_f64 instead of v_rndne + v_cvt_i32
@@ -1417,8 +1195,7 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
         store_row_i16<16>(o.qtc + b * 256 + l * 16, q);
         double dq[16], rd[16];
         dequant_row_i<16>(q, l, qpr, dq);
-        if constexpr (SO_TQ_HALF) xform2d_rows_half<true>(dl, l, dq, rd);
-        else xform2d_rows<16, true>(dl, l, dq, rd);
+        xform2d_rows<16, true>(dl, l, dq, rd);
         int rec[16];
         {
             uint32_t pw[4];
@@ -1508,16 +1285,11 @@ SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur
     __syncthreads();
     SO_SEA_STAMP(6, __builtin_amdgcn_s_memtime());
     {   // block g = wave * TQ_BPW + (lane >> 4) on lanes [0, 16 * TQ_BPW) of waves 0..NBLK/TQ_BPW-1
-        // (SO_TQ_MAP A/B builds: 1 = the even waves, 2 = every wave with 2 blocks -- measured
-        // 4K 71.8 / 79.8 vs 67.2 us per frame, 1088p 30.7 / 31.7 vs 28.7: waves 0-3 it is)
-#ifndef SO_TQ_MAP
-#define SO_TQ_MAP 0
-#endif
+        // (the even waves, or every wave with 2 blocks, measured slower: 4K 71.8 / 79.8 vs
+        // 67.2 us per frame, 1088p 30.7 / 31.7 vs 28.7)
         const int ln = tid & 63, w = tid >> 6;
-        constexpr int BPW = SO_TQ_MAP == 2 ? 2 : G::TQ_BPW;
-        const int wq = SO_TQ_MAP == 1 ? ((w & 1) ? 1 << 20 : w >> 1) : w;
-        const int gq = wq * BPW + (ln >> 4);
-        if (ln < 16 * BPW && gq < G::NBLK)
+        const int gq = w * G::TQ_BPW + (ln >> 4);
+        if (ln < 16 * G::TQ_BPW && gq < G::NBLK)
             tq16_exact<G, SC1, HALO, TOK>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by0, by1, W, qp_rd, qp_row,
                                      qp_map, o, hl);
     }
@@ -1741,7 +1513,6 @@ int p_tile_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int by0,
 }
 
 // ---- persistent run of P-frames ------------------------------------------------------------
-constexpr int kRunMax = 32;   // frames per launch (kernel-argument table)
 // Frame i of a launch predicts from ref[i]; dep[i] = j >= 0 when that plane is frame j's
 // reconstruction in the same launch (its tiles are waited for), -1 when it is complete before
 // the launch (stream order).  One run: dep[i] = i - 1.  Several independent runs interleaved
@@ -1775,50 +1546,10 @@ struct PRunArgs {
 // the task counter (hammered by every workgroup's dequeue), the timeout count and the done
 // flags live on separate 128-byte lines
 constexpr int kRunTimeoutWord = SO_RUN_TIMEOUT_WORD, kRunDoneBase = SO_RUN_DONE_BASE;
-// [1], [2] on the task counter's line: touched once per workgroup; [16, 24) the XCD-banded
-// queue heads (SO_RUN_XCDQ=1)
-constexpr int kRunExitWord = 1, kRunEpochWord = 2, kRunXqWord = 16;
-// A rank's stripe of a frame shared across GPUs (so_encode_p_run_stripe): block rows [by0, by1)
-// of every frame, the reconstruction planes in uncached memory addressed by "virtual" full-frame
-// bases (row y at base + y * W; the allocation holds rows [16 * by0 - 16, 16 * by1 + 32)), and
-// the hand-off with the neighbouring ranks:
-//   * a tile in the stripe's first (last) tile row also stores its top (bottom) 16 recon rows
-//     into the up (down) neighbour's plane of the frame (PHalo: system-scope write-through
-//     stores over xGMI) and, once every storing wave has drained, sets that neighbour's flag
-//     dn_flags[gf * tiles_x + tx] (up_flags[...]) to `epoch` (system scope);
-//   * a tile in the first (last) tile row additionally waits for my_up (my_dn) flags
-//     [(gf - 1) * tiles_x + tx - 1 .. tx + 1] == epoch: the rows its window reads from the
-//     neighbour's stripe.  Epochs (one per GOP) mean the flag arrays are never reset, so a fast
-//     neighbour can never have its flag erased by a slow rank's reset.
-// peer planes of global frame gf: peer_*0 + gf * stride.  All-null peers / flags: one GPU.
-struct PRunStripe {
-    int by0, by1;
-    uint8_t* peer_up0;
-    uint8_t* peer_dn0;
-    long long stride;
-    const uint32_t* my_up_flags;
-    const uint32_t* my_dn_flags;
-    uint32_t* peer_up_flags;   // the up neighbour's my_dn_flags, mapped here
-    uint32_t* peer_dn_flags;   // the down neighbour's my_up_flags
-    uint32_t epoch;
-    int gbase;                 // global frame index of the launch's first frame
-    // frame pipeline (kRunFPipe): frame j of this rank's run (its slot) predicts from the
-    // reconstruction the previous rank pushed into land0 + j * stride, with my_dn_flags
-    // [j * ntiles + tile] == epoch once that tile arrived; every tile of frame j is pushed
-    // into the next rank's plane peer_dn0 + (j + peer_slot_off) * stride and flagged in
-    // peer_dn_flags[(j + peer_slot_off) * ntiles + tile].  gbase = slot of the launch's first frame.
-    const uint8_t* land0;
-    int peer_slot_off;
-    // two-pass runs (kRunTwoPass): pass-1 done flags [f * ntiles + tile] = epoch, pass-1 token
-    // counts [f * nb + b] (both in the workspace), the ROI offsets (int32 [nb] or null) and the
-    // QP clamp
-    uint32_t* p1done;
-    int32_t* t1;
-    const int32_t* roi;
-    int qp_lo, qp_hi;
-    int p2lag;   // tile rows between a row's pass-1 and pass-2 tasks in the queue (1..ntr)
-    int xq;      // one GPU (kRunSingle): 8 = one queue per XCD (a band of tile rows each), 0 = one queue
-};
+// [1], [2] on the task counter's line: touched once per workgroup.  [40] (the timeout word's
+// line, written rarely): blocks whose SEA search took the dense fallback, summed over launches
+// until the caller clears it (SO_P_RUN_FALLBACK_WORD)
+constexpr int kRunExitWord = 1, kRunEpochWord = 2, kRunFallbackWord = 40;
 constexpr int kRunSingle = 0, kRunStripe = 1, kRunFPipe = 2, kRunTwoPass = 3;
 // SO_RUN_PROFILE builds (tools/rc2p_ab.py): per-phase shader cycles >> 10 accumulated by wave 0
 // into workspace words 48.. (48 pass-1 task, 49 pass-2 task, 50 pass-2 row wait, 51 reference
@@ -1830,12 +1561,12 @@ constexpr int kRunSingle = 0, kRunStripe = 1, kRunFPipe = 2, kRunTwoPass = 3;
 #define SO_RUN_PROF(word, cyc) do { } while (0)
 #endif
 
-template <int NW, int MODE, int TPX = 128>
+template <int NW, int MODE>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE)))
 p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, int H, int W,
              int qp_rd, const int32_t* __restrict__ qp_row, uint32_t* __restrict__ ws, int ws_stamp_base,
              const PRunStripe sp) {
-    using G = Sea2GeoT<NW, TPX>;
+    using G = Sea2GeoT<NW>;
     __shared__ PTileLds<G> S;
     __shared__ int s_task;
     const int tid = threadIdx.x;
@@ -1861,35 +1592,10 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     // flags hold the epoch of the launch that set them: nothing is zeroed between launches.
     const uint32_t ep = __builtin_amdgcn_readfirstlane(
         __hip_atomic_load(&ws[kRunEpochWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
-    // XCD-banded queues (sp.xq == 8, kRunSingle, grid >= 8): queue k = the tasks of tile rows
-    // [k * ntr / 8, (k + 1) * ntr / 8), frame-major, at ws[kRunXqWord + k]; a workgroup takes
-    // from queue blockIdx mod 8 (its XCD under round-robin dispatch, so the 3x3 neighbours
-    // sharing its window's rows run under the same L2) and steals from the others once that
-    // is empty.  Every queue has a home workgroup and is frame-major, so the oldest
-    // unfinished frame's tiles are always held by running workgroups: deadlock-free as the
-    // single queue.
-    const bool xq = MODE == kRunSingle && sp.xq == 8;
     for (;;) {
         if (wave == 0) {
-            int t = ntasks;
-            if (xq) {
-                const int home = (int)(blockIdx.x & 7u);
-                for (int qi = 0; qi < 8; ++qi) {
-                    const int k = (home + qi) & 7;
-                    const int r0 = k * ntr / 8, r1 = (k + 1) * ntr / 8, bt = (r1 - r0) * tiles_x;
-                    if (bt == 0) continue;
-                    const uint32_t v = __builtin_amdgcn_readfirstlane(__hip_atomic_fetch_add(
-                        &ws[kRunXqWord + k], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                    if ((int)v < bt * nframes) {
-                        const int fq = (int)v / bt;
-                        t = fq * per_frame + r0 * tiles_x + ((int)v - fq * bt);
-                        break;
-                    }
-                }
-            } else {
-                t = (int)__builtin_amdgcn_readfirstlane(
-                    __hip_atomic_fetch_add(&ws[0], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            }
+            const int t = (int)__builtin_amdgcn_readfirstlane(
+                __hip_atomic_fetch_add(&ws[0], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             s_task = t;
         }
         __syncthreads();
@@ -2071,22 +1777,15 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 SO_RUN_PROF(49, __builtin_amdgcn_s_memtime() - pt0);
             }
         } else if constexpr (FPIPE) {
-            // the rank encoding frame + 1 and its slot: the next rank, this rank's slot +
-            // peer_slot_off; or, with a second peer (the ring direction alternating per block of N
-            // frames), a.dep[f] = slot * 2 + (0: peer_dn, 1: peer_up)
-            int slot = sp.gbase + f + sp.peer_slot_off;
-            uint8_t* pbase = sp.peer_dn0;
-            uint32_t* pflags = sp.peer_dn_flags;
-            if (sp.peer_up0 != nullptr) {
-                const int code = a.dep[f];
-                slot = code >> 1;
-                if (code & 1) {
-                    pbase = sp.peer_up0;
-                    pflags = sp.peer_up_flags;
-                }
-            }
+            // where frame f's reconstruction goes (the ring direction alternates per block of N
+            // frames): a.dep[f] = slot * 2 + (0: peer_dn, 1: peer_up) of the rank encoding frame
+            // f + 1, or -1 when no frame follows (the GOP's last frame: nothing is pushed)
+            const int code = a.dep[f];
+            const int slot = code >> 1;
+            uint8_t* const pbase = (code & 1) ? sp.peer_up0 : sp.peer_dn0;
+            uint32_t* const pflags = (code & 1) ? sp.peer_up_flags : sp.peer_dn_flags;
             PHalo hl{};
-            hl.dn = pbase + (long long)slot * sp.stride;   // every row of the tile
+            hl.dn = code >= 0 ? pbase + (long long)slot * sp.stride : nullptr;   // every row of the tile
             hl.dn_begin = 0;
             ptile_body<G, true, decltype(wait_ref), true>(S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd, qp_row,
                                                           nullptr, nullptr, a.out[f], wait_ref, hl);
@@ -2094,7 +1793,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             if (wave == 0) {
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-                if (lane == 0)
+                if (lane == 0 && code >= 0)
                     __hip_atomic_store(pflags + (size_t)slot * ntiles + tile, sp.epoch, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_SYSTEM);
             }
@@ -2134,6 +1833,12 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
         }
+#ifndef SO_RUN_FALLBACK_COUNT
+#define SO_RUN_FALLBACK_COUNT 1
+#endif
+        if (SO_RUN_FALLBACK_COUNT && pass == 1 && wave == 0 && S.st[0] != 0u)   // this tile's dense-fallback blocks
+            __hip_atomic_fetch_add(&ws[kRunFallbackWord], lane == 0 ? S.st[0] : 0u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
 #ifdef SO_STAMPS
         if (tid == 0 && rec) {
             uint32_t hw, xcc;
@@ -2151,9 +1856,6 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             __hip_atomic_fetch_add(&ws[kRunExitWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (o == gridDim.x - 1) {
             __hip_atomic_store(&ws[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (xq)
-                for (int k = 0; k < 8; ++k)
-                    __hip_atomic_store(&ws[kRunXqWord + k], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&ws[kRunExitWord], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&ws[kRunEpochWord], ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -2166,10 +1868,9 @@ static size_t run_tiles(int H, int W, int tbx, int tby) {
     return (size_t)((W / 16 + tbx - 1) / tbx) * ((H / 16 + tby - 1) / tby);
 }
 size_t p_run_workspace_words(int H, int W) {
-    using G64 = Sea2GeoT<8, 64>;   // the narrower tiles: the larger tile count
-    using G128 = Sea2GeoT<8, 128>;
-    return (size_t)kRunDoneBase + (size_t)kRunMax * run_tiles(H, W, G64::TBX, G64::TBY) +
-           (size_t)kRunMax * run_tiles(H, W, G128::TBX, G128::TBY) + (size_t)kRunMax * (W / 16) * (H / 16);
+    using G = Sea2Geo;
+    return (size_t)kRunDoneBase + 2 * (size_t)kRunMax * run_tiles(H, W, G::TBX, G::TBY) +
+           (size_t)kRunMax * (W / 16) * (H / 16);
 }
 
 // Launch the run in <= kRunMax-frame launches.  max_wg > 0 caps the resident grid (several
@@ -2184,16 +1885,16 @@ static void device_shape(int* ncu) {
 // refs / deps (may be null: one run, frame g predicting from g - 1 and frame 0 from ref0): frame g
 // predicts from outs[deps[g]].recon when deps[g] >= 0 (0 <= deps[g] < g), else from refs[g].
 // conc: independent runs interleaved in the list (their tiles are in flight together).
-template <int MODE, int TPX>
+template <int MODE>
 static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                           const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp0,
                           int max_wg, hipStream_t st, const uint8_t* const* refs = nullptr,
                           const int* deps = nullptr, int conc = 1) {
-    using G = Sea2GeoT<SO_PTILE_NW, TPX>;
+    using G = Sea2GeoT<SO_PTILE_NW>;
     static int ncu = 0, per_cu = 0;
     if (ncu == 0) {
         device_shape(&ncu);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p_run_kernel<SO_PTILE_NW, MODE, TPX>,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p_run_kernel<SO_PTILE_NW, MODE>,
                                                          SO_PTILE_NW * 64, 0) != hipSuccess || per_cu <= 0)
             per_cu = 1;
     }
@@ -2233,16 +1934,13 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
         if (max_wg > 0 && grid > max_wg) grid = max_wg;
         PRunStripe sp = sp0;
         sp.gbase = sp0.gbase + f0;
-        sp.xq = 0;
-        if (MODE == kRunSingle && grid >= 8)
-            if (const char* e = getenv("SO_RUN_XCDQ")) sp.xq = atoi(e) == 1 ? 8 : 0;
         if (MODE == kRunTwoPass) {   // pass 2 of a row about one grid's worth of tasks after its pass 1
             const int tiles_x = (nbx + G::TBX - 1) / G::TBX, ntr = (rows + G::TBY - 1) / G::TBY;
             int lag = (int)((grid + tiles_x - 1) / tiles_x);
             if (const char* e = getenv("SO_P2LAG")) lag = atoi(e);   // A/B only
             sp.p2lag = lag < 1 ? 1 : (lag > ntr ? ntr : lag);
         }
-        hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, MODE, TPX>), dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), 0, st, a, n,
+        hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, MODE>), dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), 0, st, a, n,
                            f0 ? outs[f0 - 1].recon : ref0, H, W, qp_rd, qp_row, ws, (int)(f0 * ntiles), sp);
         const int rc = check_launch("p_run_kernel");
         if (rc != SO_OK) return rc;
@@ -2250,19 +1948,15 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
     return SO_OK;
 }
 
-// One GPU: 128-px tiles.  SO_RUN_TPX=64 runs the 64-px variant (8 blocks per tile: one per
-// wave in the search, two per wave in the transforms) -- measured no faster where a frame has
-// fewer tiles than resident workgroups (1088p 29.5 vs 28.3 us per frame, 3840x272 24.2 vs
-// 25.3) and 1.56x slower at 4K (tools/tpx_ab.py), so it is an A/B option only.
+// One GPU: 128-px tiles (64-px tiles -- 8 blocks, one per wave in the search -- measured no
+// faster where a frame has fewer tiles than resident workgroups, 1088p 29.5 vs 28.3 us per
+// frame, and 1.56x slower at 4K: removed).
 int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                  const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, hipStream_t st) {
     PRunStripe sp{};
     sp.by0 = 0;
     sp.by1 = H / 16;
-    const char* e = getenv("SO_RUN_TPX");
-    if (e && atoi(e) == 64)
-        return p_run_launch_t<kRunSingle, 64>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, 0, st);
-    return p_run_launch_t<kRunSingle, 128>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, 0, st);
+    return p_run_launch_t<kRunSingle>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, 0, st);
 }
 
 // Several independent runs in one list (so_encode_p_runs): frame g predicts from
@@ -2273,17 +1967,14 @@ int p_runs_launch(const uint8_t* const* curs, int nframes, const uint8_t* const*
     PRunStripe sp{};
     sp.by0 = 0;
     sp.by1 = H / 16;
-    return p_run_launch_t<kRunSingle, 128>(curs, nframes, nullptr, H, W, qp_rd, qp_row, outs, ws, sp, 0, st, refs, deps,
+    return p_run_launch_t<kRunSingle>(curs, nframes, nullptr, H, W, qp_rd, qp_row, outs, ws, sp, 0, st, refs, deps,
                                            conc);
 }
 
 // The workspace's pass-1 token region (kRunMax * nb words; the per-frame two-pass sequence of
 // so_encode_p_run_2pass keeps its ME records there)
 int32_t* p_run_t1_region(uint32_t* ws, int H, int W) {
-    using G64 = Sea2GeoT<8, 64>;
-    using G128 = Sea2GeoT<8, 128>;
-    return reinterpret_cast<int32_t*>(ws + kRunDoneBase + (size_t)kRunMax * run_tiles(H, W, G64::TBX, G64::TBY) +
-                                      (size_t)kRunMax * run_tiles(H, W, G128::TBX, G128::TBY));
+    return reinterpret_cast<int32_t*>(ws + kRunDoneBase + 2 * (size_t)kRunMax * run_tiles(H, W, Sea2Geo::TBX, Sea2Geo::TBY));
 }
 
 // Two-pass rate control over a run (so_encode_p_run_2pass): one run as p_run_launch, each tile
@@ -2291,30 +1982,28 @@ int32_t* p_run_t1_region(uint32_t* ws, int H, int W) {
 int p_run_2pass_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                        const int32_t* qp_row, const int32_t* roi, int qp_lo, int qp_hi, const PFrameOut* outs,
                        uint32_t* ws, hipStream_t st) {
-    using G64 = Sea2GeoT<8, 64>;
-    using G128 = Sea2GeoT<8, 128>;
     PRunStripe sp{};
     sp.by0 = 0;
     sp.by1 = H / 16;
-    sp.p1done = ws + kRunDoneBase + (size_t)kRunMax * run_tiles(H, W, G64::TBX, G64::TBY);
-    sp.t1 = reinterpret_cast<int32_t*>(sp.p1done + (size_t)kRunMax * run_tiles(H, W, G128::TBX, G128::TBY));
+    sp.p1done = ws + kRunDoneBase + (size_t)kRunMax * run_tiles(H, W, Sea2Geo::TBX, Sea2Geo::TBY);
+    sp.t1 = reinterpret_cast<int32_t*>(sp.p1done + (size_t)kRunMax * run_tiles(H, W, Sea2Geo::TBX, Sea2Geo::TBY));
     sp.roi = roi;
     sp.qp_lo = qp_lo;
     sp.qp_hi = qp_hi;
-    return p_run_launch_t<kRunTwoPass, 128>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, 0, st, nullptr,
+    return p_run_launch_t<kRunTwoPass>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, 0, st, nullptr,
                                             nullptr, 2);
 }
 
 int p_run_stripe_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                         const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg,
                         hipStream_t st) {
-    return p_run_launch_t<kRunStripe, 128>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st);
+    return p_run_launch_t<kRunStripe>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st);
 }
 
 int p_run_fpipe_launch(const uint8_t* const* curs, int nframes, int H, int W, int qp_rd, const int32_t* qp_row,
                        const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg, hipStream_t st,
                        const int* push) {
-    return p_run_launch_t<kRunFPipe, 128>(curs, nframes, nullptr, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st,
+    return p_run_launch_t<kRunFPipe>(curs, nframes, nullptr, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st,
                                           nullptr, push);
 }
 
@@ -2462,16 +2151,6 @@ int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, in
             hipLaunchKernelGGL(me_sea2_kernel, sgrid, dim3(Sea2Geo::NTHREADS), 0, st, cur, refs, nref, H, W, by0, by1,
                                out_best, pr ? atoi(pr) : 0);
             return check_launch("me_sea2_kernel");
-        }
-        // VBS: the block + sub-block SEA is opt-in (SO_ME_IMPL=sea_vbs): measured slower than the
-        // dense wave search, whose v_sad_u8 work yields the four sub-block SADs for free
-        // (4K VBS GOP 8.36 vs 5.94 ms)
-        const bool sea_vbs = impl && strcmp(impl, "sea_vbs") == 0;
-        if (sea_vbs && bs == 16 && out_sub != nullptr) {
-            const dim3 sgrid(((nbx + Sea2Geo::TBX - 1) / Sea2Geo::TBX) * ((nrows + Sea2Geo::TBY - 1) / Sea2Geo::TBY));
-            hipLaunchKernelGGL(me_sea2_vbs_kernel, sgrid, dim3(Sea2Geo::NTHREADS), 0, st, cur, refs, nref, H, W, by0,
-                               by1, out_best, out_sub);
-            return check_launch("me_sea2_vbs_kernel");
         }
         const bool sub = out_sub != nullptr;
         const int tbx = 128 / bs;

@@ -18,6 +18,7 @@ from . import _lib
 
 SLACK = 64  # bytes readable past every plane (kernels read aligned words at row ends)
 RUN_TIMEOUT_WORD = 32   # so_encode_p_run workspace: the timeout count (include/streamoptima.h)
+RUN_FALLBACK_WORD = 40  # ... and the count of blocks whose SEA search took the dense fallback
 
 
 def alloc_planes(n: int, h: int, w: int, device, fill: int | None = None) -> torch.Tensor:
@@ -73,17 +74,30 @@ class Engine:
         self._fme_ws = None
         self._consts: dict = {}
 
+    MAX_CONSTS = 4096
+
     def device_const_i32(self, values) -> torch.Tensor:
         """A read-only int32 device copy of `values`, uploaded once per distinct content, so
-        a GOP replayed from a captured HIP graph issues no host->device copy."""
+        a GOP replayed from a captured HIP graph issues no host->device copy.
+
+        Entries are never evicted behind the caller's back: a captured graph holds their raw
+        device pointers, so freeing one would make a later replay read freed memory.  Past
+        MAX_CONSTS distinct contents this raises; a caller that knows no graph references
+        the cached constants any more calls release_consts()."""
         host = torch.as_tensor(values, dtype=torch.int32).contiguous()
         key = (tuple(host.shape), host.numpy().tobytes())
         t = self._consts.get(key)
         if t is None:
-            if len(self._consts) >= 64:
-                self._consts.clear()
+            if len(self._consts) >= self.MAX_CONSTS:
+                raise RuntimeError(f"Engine.device_const_i32: {self.MAX_CONSTS} distinct constants cached; call "
+                                   "release_consts() once no captured graph references them")
             t = self._consts[key] = host.to(self.device)
         return t
+
+    def release_consts(self) -> None:
+        """Drop the cached device constants (ROI offsets, row-QP schedules).  Only safe when no
+        captured HIP graph that used them will be replayed again."""
+        self._consts.clear()
 
     def fme_workspace(self, nref: int) -> torch.Tensor:
         """Phase planes of the references' frac frames (rebuilt by every FME call)."""
@@ -337,6 +351,16 @@ class Engine:
         if n:
             ws[RUN_TIMEOUT_WORD].zero_()
             raise RuntimeError(f"p_run_kernel: {n} dependency wait(s) timed out; the GOP's symbols are unreliable")
+
+    def take_fallback_count(self) -> int:
+        """Blocks of the persistent runs since the last call whose exact SEA search took the
+        dense fallback (SO_P_RUN_FALLBACK_WORD); clears the count.  Synchronises."""
+        ws = getattr(self, "_run_ws", None)
+        if ws is None:
+            return 0
+        n = int(ws[RUN_FALLBACK_WORD].item())
+        ws[RUN_FALLBACK_WORD].zero_()
+        return n
 
     def encode_i_rows(self, cur, by0: int, by1: int, qp_rd: int, out: FrameSymbols,
                       qp_row_dev: torch.Tensor | None = None, qp_map_dev: torch.Tensor | None = None,

@@ -309,7 +309,8 @@ def fpipe_plan(world: int, rank: int, nframes: int) -> dict:
     run: the P-frames of its persistent launch (rank 0's frame 0 is the I-frame); slot0: the
     slot of run[0] (its reference, frame run[0] - 1, arrives in that landing slot); push: per
     run frame f, where frame f's reconstruction goes -- slot (f + 1) // world of rank
-    fpipe_rank_of(f + 1), coded slot * 2 + (0: the next rank, 1: the previous rank)."""
+    fpipe_rank_of(f + 1), coded slot * 2 + (0: the next rank, 1: the previous rank), or -1 for
+    the GOP's last frame (nothing reads it: no push over the link)."""
     nblocks = -(-nframes // world)
     frames = []
     for k in range(nblocks):
@@ -319,6 +320,9 @@ def fpipe_plan(world: int, rank: int, nframes: int) -> dict:
     run = [k for k in frames if k > 0]
     push = []
     for f in run:
+        if f + 1 >= nframes:      # the GOP's last frame: no rank reads its reconstruction
+            push.append(-1)
+            continue
         r = fpipe_rank_of(world, f + 1)
         if r not in ((rank + 1) % world, (rank - 1) % world):
             raise AssertionError("fpipe_plan: frame f + 1 is not on a ring neighbour")
@@ -449,8 +453,8 @@ class FramePipeRank:
                 arr([s.qtc.data_ptr() for s in ss]), arr([s.tokens.data_ptr() for s in ss]),
                 arr([s.mae_num.data_ptr() for s in ss]), arr([s.recon.data_ptr() for s in ss]),
                 arr([s.sse.data_ptr() for s in ss]), self._ws.data_ptr(), self._planes.value, self._flags.value,
-                slot0, pplanes, pflags, p2planes, p2flags, (ctypes.c_int32 * n)(*plan["push"]), self.stride, ep,
-                int(self.max_wg), st), "so_encode_p_run_fpipe2")
+                slot0, pplanes, pflags, p2planes, p2flags, (ctypes.c_int32 * n)(*plan["push"]), self.nslots,
+                self.stride, ep, int(self.max_wg), st), "so_encode_p_run_fpipe2")
             for s in ss:
                 s.frame_type, s.qp_rd = 1, int(qp)
         return syms
@@ -496,9 +500,15 @@ class FramePipelineGOPEncoder:
         while the other ranks finish this GOP's last frames -- the pipeline fill is paid once
         per stream, not once per GOP.  GOP k+1 may start on a rank as soon as its own GOP k
         launch is done: every landing slot it overwrites was last read by a frame that its
-        own GOP k frames depend on."""
-        syms = self.r.encode(frames, intra_dur, qp) if syms is None else syms
+        own GOP k frames depend on.  That needs every rank to hold a frame
+        after its first, i.e. nframes > world: with nframes <= world rank 0 has only the
+        I-frame, and its next push into rank 1's slot 0 would race rank 1's read of it, so
+        reduce=False is refused there (the all_reduce orders the GOPs instead)."""
         nf = frames.shape[0]
+        if not reduce and nf <= self.world:
+            raise ValueError(f"encode(reduce=False) needs more frames than ranks ({nf} <= {self.world}): "
+                             "back-to-back GOPs would race on rank 1's first landing slot")
+        syms = self.r.encode(frames, intra_dur, qp) if syms is None else syms
         return {"symbols": syms, "sse": self.sse(syms, nf) if reduce else None,
                 "frame_type": [0 if k == 0 else 1 for k in range(nf)]}
 

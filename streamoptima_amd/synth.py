@@ -14,6 +14,13 @@ i.e. 8x8 random cells plus fixed per-pixel texture noise, moving with a global m
 of (+2, +1) px per frame (inside the +-16 search range), plus +-2 temporal noise so
 P-frame residuals are not identically zero.  h() is splitmix64 of the packed
 coordinates xor the seed.
+
+Content variants (`content=`, the bench's content-dependence records): the exact SEA search's
+speed depends on how well 4x4-cell sums separate candidates, the reference's exhaustive scan
+(Encoder.py:688-715) does not.  Only the base texture changes; motion and temporal noise stay:
+  "bench"   the texture above (8x8 cells, +-8 pixel noise);
+  "lowtex"  32x32 flat cells, +-1 pixel noise: inside a cell every candidate's 4x4 sums agree;
+  "noise"   128 + per-pixel noise in [-8, 8], no cells: 4x4 sums of noise barely differ.
 """
 from __future__ import annotations
 
@@ -34,13 +41,22 @@ def _h(x: np.ndarray, y: np.ndarray, seed: int) -> np.ndarray:
     return _splitmix64(key ^ np.uint64(seed & 0xFFFFFFFFFFFFFFFF))
 
 
-def base_texture(height: int, width: int, seed: int) -> np.ndarray:
+CONTENTS = ("bench", "lowtex", "noise")
+# per content: (cell size log2 or None for no cells, pixel-noise modulus)
+_CONTENT = {"bench": (3, 17), "lowtex": (5, 3), "noise": (None, 17)}
+
+
+def base_texture(height: int, width: int, seed: int, content: str = "bench") -> np.ndarray:
+    cl, nm = _CONTENT[content]
     with np.errstate(over="ignore"):
         ys, xs = np.meshgrid(np.arange(height, dtype=np.uint64),
                              np.arange(width, dtype=np.uint64), indexing="ij")
-        cell = _h(xs >> np.uint64(3), ys >> np.uint64(3), seed) & np.uint64(255)
-        noise = _h(xs, ys, seed ^ 0x9E37) % np.uint64(17)
-    v = cell.astype(np.int64) + noise.astype(np.int64) - 8
+        if cl is None:
+            cell = np.full(xs.shape, 128, np.uint64)
+        else:
+            cell = _h(xs >> np.uint64(cl), ys >> np.uint64(cl), seed) & np.uint64(255)
+        noise = _h(xs, ys, seed ^ 0x9E37) % np.uint64(nm)
+    v = cell.astype(np.int64) + noise.astype(np.int64) - nm // 2
     return np.clip(v, 0, 255).astype(np.uint8)
 
 
@@ -56,9 +72,9 @@ def synth_frame(base: np.ndarray, t: int, seed: int) -> np.ndarray:
     return np.clip(moved + tn.astype(np.int64) - 2, 0, 255).astype(np.uint8)
 
 
-def synth_sequence(frames: int, height: int, width: int, seed: int = 0) -> np.ndarray:
+def synth_sequence(frames: int, height: int, width: int, seed: int = 0, content: str = "bench") -> np.ndarray:
     """uint8 array [frames, height, width] (the reference's y_only_frame_arr, Encoder.py:93)."""
-    base = base_texture(height, width, seed)
+    base = base_texture(height, width, seed, content)
     out = np.empty((frames, height, width), dtype=np.uint8)
     for t in range(frames):
         out[t] = synth_frame(base, t, seed)
@@ -102,14 +118,16 @@ def _t_h(x, y, seed: int):
     return _t_splitmix64(((y << 32) | x) ^ _s64(seed & 0xFFFFFFFFFFFFFFFF))
 
 
-def synth_sequence_torch(frames: int, height: int, width: int, seed: int = 0, device="cuda"):
+def synth_sequence_torch(frames: int, height: int, width: int, seed: int = 0, device="cuda",
+                         content: str = "bench"):
     """torch.uint8 [frames, height, width] on `device`, equal to synth_sequence()."""
     import torch
+    cl, nm = _CONTENT[content]
     ys = torch.arange(height, dtype=torch.int64, device=device)[:, None].expand(height, width)
     xs = torch.arange(width, dtype=torch.int64, device=device)[None, :].expand(height, width)
-    cell = _t_h(xs >> 3, ys >> 3, seed) & 255
-    noise = _t_umod(_t_h(xs, ys, seed ^ 0x9E37), 17)
-    base = (cell + noise - 8).clamp_(0, 255)
+    cell = torch.full_like(xs, 128) if cl is None else _t_h(xs >> cl, ys >> cl, seed) & 255
+    noise = _t_umod(_t_h(xs, ys, seed ^ 0x9E37), nm)
+    base = (cell + noise - nm // 2).clamp_(0, 255)
     out = torch.empty((frames, height, width), dtype=torch.uint8, device=device)
     for t in range(frames):
         yy = torch.clamp(torch.arange(height, device=device) + t, max=height - 1)

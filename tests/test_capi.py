@@ -89,7 +89,8 @@ def test_p_runs_validation_without_gpu():
 def test_two_pass_run_and_frame_pipe_validation_without_gpu():
     """so_encode_p_run_2pass and so_encode_p_run_fpipe2 reject unsupported geometry, a bad QP
     clamp, a reconstruction aliasing the reference or lying in the landing planes, a short
-    landing stride and a negative push code -- on the host, before any launch."""
+    landing stride, a push code below -1 or past the peers' slots and a run past the landing
+    slots -- on the host, before any launch."""
     from streamoptima_amd import _lib
     lib = _lib.load()
     n, H, W = 2, 64, 128
@@ -116,15 +117,19 @@ def test_two_pass_run_and_frame_pipe_validation_without_gpu():
     stride = H * W
     land0, land_flags = 0x4000000, ctypes.c_void_p(0x5000000)
 
-    def fpipe(recon, push, stride=stride, slot0=0):
+    def fpipe(recon, push, stride=stride, slot0=0, nslots=3):
         return lib.so_encode_p_run_fpipe2(cur, n, H, W, 16, 16, 4, None, outs[0], outs[1], outs[2], outs[3], outs[4],
                                           recon, None, ws, ctypes.c_void_p(land0), land_flags, slot0, fake[14],
-                                          fake[15], fake[14], fake[15], (ctypes.c_int32 * n)(*push), stride, 1, 0,
-                                          None)
+                                          fake[15], fake[14], fake[15], (ctypes.c_int32 * n)(*push), nslots, stride,
+                                          1, 0, None)
     assert fpipe(recon, [0, 2], stride=stride - 1) == _lib.SO_E_INVALID
     assert fpipe(recon, [0, 2], slot0=-1) == _lib.SO_E_INVALID
-    assert fpipe(recon, [0, -1]) == _lib.SO_E_INVALID
+    assert fpipe(recon, [0, -2]) == _lib.SO_E_INVALID
     assert b"push_to[1]" in lib.so_last_error()
+    assert fpipe(recon, [0, 6]) == _lib.SO_E_INVALID            # slot 3 of a peer with 3 slots
+    assert b"push_to[1]" in lib.so_last_error()
+    assert fpipe(recon, [0, 2], slot0=2) == _lib.SO_E_INVALID   # slots 2, 3 of 3
+    assert b"nslots" in lib.so_last_error()
     assert fpipe(arr(fake[10], ctypes.c_void_p(land0 + stride)), [0, 2]) == _lib.SO_E_INVALID
     assert b"landing planes" in lib.so_last_error()
 

@@ -23,11 +23,14 @@ def test_reference_slots_match(world, nframes):
             assert slot == k // world and slot < p["nslots"]
             # where this frame's reconstruction goes: the rank of frame k + 1, its slot
             code = p["push"][i]
+            if k == nframes - 1:                       # nothing follows the GOP's last frame
+                assert code == -1
+                continue
             dst = (g + 1) % world if code % 2 == 0 else (g - 1) % world
             assert dst == fpipe_rank_of(world, k + 1) and code // 2 == (k + 1) // world
             assert code // 2 < plans[dst]["nslots"]
     if world > 2 and nframes >= 2 * world:   # both ring directions carry frames
-        codes = [c % 2 for p in plans for c in p["push"]]
+        codes = [c % 2 for p in plans for c in p["push"] if c >= 0]
         assert 0 < sum(codes) < len(codes)
 
 

@@ -1,6 +1,8 @@
 """GPU parity at the BENCHMARKED workloads: every frame of the 4K x 30 (configs[2]),
 1080p -> 1088 x 30 (configs[1]), 4K x 120 seed 1 (configs[3]) and 4K ROI + two-pass RC
-seed 2 (configs[4]) GOPs, bit-exact against the C oracle's per-frame digests
+seed 2 (configs[4]) GOPs, and of their variants at the same sizes (VBS-on 4K and 1080p,
+1080p FME / fast_me ParallelMode 0 and 2, 4K on low-texture and noise-only content),
+bit-exact against the C oracle's per-frame digests
 (tests/golden/large_gops.json, tests/golden/make_large_fixtures.py; the oracle itself is
 pinned to the reference's 2-frame 1088p / 4K hashes by tests/test_oracle_golden.py)."""
 import json
@@ -19,13 +21,13 @@ FIX = json.load(open(os.path.join(GOLDEN, "large_gops.json")))
 
 def _codec(name, dev, **over):
     from streamoptima_amd.Encoder import Y_Video_codec
-    from streamoptima_amd.workloads import RC_TABLES, WORKLOADS
+    from streamoptima_amd.workloads import ME_KW, RC_TABLES, WORKLOADS
     cfg = dict(WORKLOADS[name], **over)
-    kw = {}
+    kw = dict(ME_KW[cfg.get("me", "full")])
     if cfg.get("rc"):
-        kw = dict(RCFlag=cfg["rc"], targetBR=cfg["target"], qp_rate_tables=RC_TABLES, roi=cfg.get("roi"))
-    return cfg, Y_Video_codec(cfg["h"], cfg["w"], cfg["frames"], 16, 16, cfg["qp"], cfg["intra_dur"], 0, 0.015, False,
-                              device=dev, **kw)
+        kw.update(RCFlag=cfg["rc"], targetBR=cfg["target"], qp_rate_tables=RC_TABLES, roi=cfg.get("roi"))
+    return cfg, Y_Video_codec(cfg["h"], cfg["w"], cfg["frames"], 16, 16, cfg["qp"], cfg["intra_dur"], 0, 0.015,
+                              bool(cfg.get("vbs")), device=dev, **kw)
 
 
 def _frames(cfg, dev):
@@ -34,7 +36,8 @@ def _frames(cfg, dev):
     from streamoptima_amd.workloads import padded
     h, w, f = cfg["h"], cfg["w"], cfg["frames"]
     fr = alloc_planes(f, padded(h), padded(w), dev, fill=128)
-    fr[:, :h, :w].copy_(synth_sequence_torch(f, h, w, seed=cfg["seed"], device=dev))
+    fr[:, :h, :w].copy_(synth_sequence_torch(f, h, w, seed=cfg["seed"], device=dev,
+                                             content=cfg.get("content", "bench")))
     return fr
 
 
@@ -48,7 +51,8 @@ def _check(name, syms, psnr=None):
         np.testing.assert_allclose(psnr, fx["psnr"], rtol=0, atol=1e-9)
 
 
-@pytest.mark.parametrize("name", ["4k", "1080p", "4k120", "4k_rc2pass"])
+@pytest.mark.parametrize("name", ["4k", "1080p", "4k120", "4k_rc2pass", "4k_vbs", "1080p_vbs", "1080p_fme",
+                                  "1080p_fast", "1080p_fastpar", "4k_lowtex", "4k_noise"])
 def test_benchmarked_gop_bit_exact(gpu, name):
     cfg, codec = _codec(name, gpu)
     frames = _frames(cfg, gpu)
@@ -241,23 +245,3 @@ def test_fast_me_chain_speculation_matches_serial_walk(gpu, monkeypatch, vbs, fm
     monkeypatch.setenv("SO_FASTME_WARM", "0")
     monkeypatch.setenv("SO_FASTME_K", "8")
     assert run() == exp
-
-
-def test_vbs_sea_matches_dense_search(gpu, monkeypatch):
-    """VBSEnable: the block + sub-block SEA (me_sea2_vbs_kernel, SO_ME_IMPL=sea_vbs) against the dense wave search
-    (SO_ME_IMPL=dense, me_wave_kernel<16, true>) frame by frame on a 1920x1088 GOP -- block
-    and sub-block MVs, split decisions, QTC, reconstruction (Encoder.py:512-578)."""
-    from streamoptima_amd.Encoder import Y_Video_codec
-    from streamoptima_amd.digest import symbols_digest
-    from streamoptima_amd.engine import alloc_planes
-    from streamoptima_amd.synth import synth_sequence_torch
-    h, w, f = 1088, 1920, 4
-    codec = Y_Video_codec(h, w, f, 16, 16, 4, f, 0, 0.015, True, device=gpu)
-    fr = alloc_planes(f, h, w, gpu)
-    fr.copy_(synth_sequence_torch(f, h, w, seed=13, device=gpu))
-    monkeypatch.setenv("SO_ME_IMPL", "dense")
-    exp = [symbols_digest(s) for s in codec.encode_device(fr, f)["symbols"]]
-    monkeypatch.setenv("SO_ME_IMPL", "sea_vbs")   # opt-in: slower than the dense search
-    got = codec.encode_device(fr, f)
-    assert [symbols_digest(s) for s in got["symbols"]] == exp
-    assert int(sum(int(s.split.sum()) for s in got["symbols"][1:])) > 0   # some blocks split

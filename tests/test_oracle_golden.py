@@ -177,7 +177,9 @@ def test_gop_me_variants(name, cfg):
     assert (g["decoded"] == g["recon"]).all()
 
 
-@pytest.mark.parametrize("name,n", [("1080p", 3), ("4k", 2), ("4k120", 2), ("4k_rc2pass", 2)])
+@pytest.mark.parametrize("name,n", [("1080p", 3), ("4k", 2), ("4k120", 2), ("4k_rc2pass", 2), ("4k_vbs", 2),
+                                    ("1080p_vbs", 2), ("1080p_fme", 2), ("1080p_fast", 3), ("1080p_fastpar", 2),
+                                    ("4k_lowtex", 2), ("4k_noise", 2)])
 def test_large_gop_fixture_head_reproduces(name, n):
     """tests/golden/large_gops.json (the digests the -m gpu tests and bench.py check the HIP
     path against) is reproducible: the oracle's first frames of each benchmarked workload
@@ -190,10 +192,12 @@ def test_large_gop_fixture_head_reproduces(name, n):
     assert len(fx["frame_sha256"]) == cfg["frames"] and fx["config"]["seed"] == cfg["seed"]
     h, w = cfg["h"], cfg["w"]
     fr = np.full((n, padded(h), padded(w)), 128, np.uint8)
-    fr[:, :h, :w] = synth_sequence(n, h, w, seed=cfg["seed"])
+    fr[:, :h, :w] = synth_sequence(n, h, w, seed=cfg["seed"], content=cfg.get("content", "bench"))
     rc = cfg.get("rc")
+    me = cfg.get("me", "full")
     out = encode_gop(fr, cfg["qp"], cfg["intra_dur"], rc=rc, target=cfg.get("target"), tables=RC_TABLES if rc else None,
-                     roi=roi_offsets(cfg.get("roi"), h, w, 16))
+                     roi=roi_offsets(cfg.get("roi"), h, w, 16), vbs=bool(cfg.get("vbs")), lam=0.015, fme=me == "fme",
+                     fast_me=me in ("fast", "fastpar"), parallel_mode=2 if me == "fastpar" else 0)
     for i, r in enumerate(out):
         arrs = {k: r[k] for k in ("split", "mv", "qtc", "tokens", "mae_num", "recon")}
         if r.get("qp_map") is not None:

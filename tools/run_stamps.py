@@ -67,7 +67,6 @@ def main():
     ap.add_argument("--heights", default="272,1088,2160")
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--frames", type=int, default=24)
-    ap.add_argument("--tpx", type=int, default=128, help="tile width (SO_RUN_TPX)")
     a = ap.parse_args()
     from streamoptima_amd import _lib
     from streamoptima_amd.engine import Engine, alloc_planes
@@ -85,8 +84,7 @@ def main():
         i0 = eng.encode_i(fr[0], 4)
         outs = [eng.new_symbols(1) for _ in range(nf - 1)]
         curs = [fr[i] for i in range(1, nf)]
-        os.environ["SO_RUN_TPX"] = str(a.tpx)
-        tiles_x, ntr = -(-(w // 16) // (a.tpx // 16)), -(-(h // 16) // 2)
+        tiles_x, ntr = -(-(w // 16) // 8), -(-(h // 16) // 2)
         stamps = torch.zeros(((nf - 1) * tiles_x * ntr, 16), dtype=torch.int64, device=dev)
         eng.encode_p_run(curs, i0.recon, 4, outs)                 # warm
         assert lib.so_debug_set_run_stamps(stamps.data_ptr()) == 0
