@@ -685,6 +685,20 @@ def p2p_encoder(eng, frames, cfg, senc, world, max_wg=0):
     return penc, "in-launch p2p over xGMI (uncached landing planes, IPC), self-checked"
 
 
+def fpipe_rc_kw(codec) -> dict:
+    """FramePipeRank.encode's rate-control keywords for the codec's RC / ROI settings (the
+    row-QP schedule; RCFlag 3: two-pass with the ROI offsets and the QP clamp)."""
+    eng = codec.engine()
+    if not codec._rc_on():
+        return {}
+    kw = {"qp_row": codec.row_qp_schedule(eng.nby)}
+    if codec.RCFlag >= 3:
+        roi = codec.roi_block_offsets()
+        kw.update(two_pass=True, roi_dev=eng.device_const_i32(roi) if roi is not None else None,
+                  qp_clamp=tuple(codec.qp_clamp))
+    return kw
+
+
 def fpipe_encoder(codec, frames, cfg, world, max_wg=0):
     """The frame pipeline (streamoptima_amd/pipeline.py FramePipelineGOPEncoder), self-checked
     before timing: the first 2N+1 frames through it must give, on every rank, the digests of
@@ -708,7 +722,7 @@ def fpipe_encoder(codec, frames, cfg, world, max_wg=0):
     k = min(2 * world + 1, cfg["frames"])
     ok, why = 1, ""
     try:                      # this rank's launches only: a failure here must not strand the
-        a = penc.encode_local(frames[:k], k, cfg["qp"])     # other ranks in a collective
+        a = penc.encode_local(frames[:k], k, cfg["qp"], **fpipe_rc_kw(codec))   # other ranks in a collective
         torch.cuda.synchronize()
         ref = [symbols_digest(s) for s in codec.encode_device(frames[:k], k)["symbols"]]
     except Exception as e:   # noqa: BLE001
@@ -818,8 +832,11 @@ def main(argv=None):
         rc = cfg.get("rc")
         cap = 768 // (2 * world) if args.share_gpu else 0
         plain = not rc and plain_cfg and eng.pipelined_ok(1)
+        # the frame pipeline covers the plain GOP and two-pass RC / ROI (configs[4]): a rank
+        # owns whole frames, so the row-local QP statistics never cross ranks
+        fp_ok = plain_cfg and eng.pipelined_ok(1) and (not rc or (rc >= 3 and codec.intra_thresh is None))
         fpipe_note = ""
-        if args.shard == "fpipe" and plain:
+        if args.shard == "fpipe" and fp_ok:
             fenc, fpipe_note = fpipe_encoder(codec, frames, cfg, world, max_wg=cap)
         if fenc is not None:
             mode_note = (f"frame pipeline x{world} (one frame per rank per block of N frames, ring direction "
@@ -829,9 +846,10 @@ def main(argv=None):
             # the SSE all_reduce runs once, after timing (pipeline.py encode), unless every rank
             # does not hold a P-frame (frames <= ranks): then it orders back-to-back GOPs
             b2b = f > world
+            rc_kw = fpipe_rc_kw(codec)
 
             def step():
-                return fenc.encode(frames, cfg["intra_dur"], cfg["qp"], reduce=not b2b)
+                return fenc.encode(frames, cfg["intra_dur"], cfg["qp"], reduce=not b2b, **rc_kw)
         else:
             if args.exchange == "p2p" and plain:
                 penc, exchange_note = p2p_encoder(eng, frames, cfg, senc, world, max_wg=cap)
@@ -904,8 +922,7 @@ def main(argv=None):
                 full = [senc.gather_symbols(s) for s in res["symbols"]]
             if rank == 0:
                 hosts = [{k: (v.cpu().numpy() if torch.is_tensor(v) else v) for k, v in g.items()} for g in full]
-                parity = parity_of(hosts, name, cfg, sse=res["sse"]) if not cfg.get("rc") else {
-                    "bit_exact": None, "note": "per-block QP maps are stripe-local; checked by tests/test_gpu_large.py"}
+                parity = parity_of(hosts, name, cfg, sse=res["sse"])
         elif rank == 0 or world == 1:
             def redo():
                 poison(pre)

@@ -139,10 +139,10 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
  * acquire before reading the reference rows.
  */
 #define SO_P_RUN_TIMEOUT_WORD 32
-/* Word 40: the number of blocks whose exact SEA search took the dense fallback (more than 192
+/* Word 64: the number of blocks whose exact SEA search took the dense fallback (more than 192
  * candidates survived the 4x4-cell bound: flat or noise-like content), summed over launches
  * like the timeout count until the caller clears it (a content statistic, not an error). */
-#define SO_P_RUN_FALLBACK_WORD 40
+#define SO_P_RUN_FALLBACK_WORD 64
 size_t so_p_run_workspace_elems(int H, int W);
 int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W,
                     int bs, int sr, int qp_rd, const int32_t* qp_row, uint8_t* const* out_split,
@@ -258,6 +258,26 @@ int so_encode_p_run_fpipe2(const uint8_t* const* curs, int nframes, int H, int W
                            uint32_t* peer_flags, uint8_t* peer2_land0, uint32_t* peer2_flags,
                            const int32_t* push_to, int nslots, long long stride, uint32_t epoch,
                            int max_wg, void* stream);
+/*
+ * The frame pipeline with two-pass rate control and ROI (BASELINE configs[4] across GPUs;
+ * build extension): each of the rank's frames runs pass 1, the per-block
+ * QP map and pass 2 exactly as so_encode_p_run_2pass (roi, qp_lo, qp_hi, out_qp_map as there),
+ * tile by tile inside ONE persistent launch (a tile's pass 2 starts once its tile row finished
+ * pass 1), and pass 2 pushes the final reconstruction into the next frame's rank as
+ * so_encode_p_run_fpipe2 does (same landing planes, flags, push codes, nslots and epochs).
+ * A rank owns whole frames, so the row-local QP statistics never cross ranks.  The symbols
+ * and QP maps are those of the one-GPU two-pass sequence over the same frames.
+ */
+int so_encode_p_run_fpipe_2pass(const uint8_t* const* curs, int nframes, int H, int W, int bs, int sr,
+                                int qp_rd, const int32_t* qp_row, const int32_t* roi, int qp_lo,
+                                int qp_hi, uint8_t* const* out_split, int16_t* const* out_mv,
+                                int16_t* const* out_qtc, int32_t* const* out_tokens,
+                                int32_t* const* out_mae_num, uint8_t* const* out_recon,
+                                int32_t* const* out_sse, int32_t* const* out_qp_map, uint32_t* workspace,
+                                const uint8_t* land0, const uint32_t* land_flags, int slot0,
+                                uint8_t* peer_land0, uint32_t* peer_flags, uint8_t* peer2_land0,
+                                uint32_t* peer2_flags, const int32_t* push_to, int nslots, long long stride,
+                                uint32_t epoch, int max_wg, void* stream);
 int so_frame_push(const uint8_t* plane, int H, int W, uint8_t* peer_plane, uint32_t* peer_flags,
                   uint32_t epoch, void* stream);
 

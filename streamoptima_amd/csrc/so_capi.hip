@@ -573,20 +573,25 @@ int so_stripe_halo_push(const uint8_t* plane, int H, int W, int by0, int by1, in
 }
 
 // ---- one GOP across GPUs: consecutive frames on consecutive ranks (so_me.hip kRunFPipe) -----
-int so_encode_p_run_fpipe2(const uint8_t* const* curs, int nframes, int H, int W, int bs, int sr, int qp_rd,
-                           const int32_t* qp_row, uint8_t* const* out_split, int16_t* const* out_mv,
-                           int16_t* const* out_qtc, int32_t* const* out_tokens, int32_t* const* out_mae_num,
-                           uint8_t* const* out_recon, int32_t* const* out_sse, uint32_t* workspace,
-                           const uint8_t* land0, const uint32_t* land_flags, int slot0, uint8_t* peer_land0,
-                           uint32_t* peer_flags, uint8_t* peer2_land0, uint32_t* peer2_flags, const int32_t* push_to,
-                           int nslots, long long stride, uint32_t epoch, int max_wg, void* stream) {
-    const char* fn = "so_encode_p_run_fpipe2";
+// The frame pipeline's argument checks and launch, with (two_pass) or without two-pass RC.
+static int fpipe_run(const char* fn, bool two_pass, const uint8_t* const* curs, int nframes, int H, int W, int bs,
+                     int sr, int qp_rd, const int32_t* qp_row, const int32_t* roi, int qp_lo, int qp_hi,
+                     uint8_t* const* out_split, int16_t* const* out_mv, int16_t* const* out_qtc,
+                     int32_t* const* out_tokens, int32_t* const* out_mae_num, uint8_t* const* out_recon,
+                     int32_t* const* out_sse, int32_t* const* out_qp_map, uint32_t* workspace, const uint8_t* land0,
+                     const uint32_t* land_flags, int slot0, uint8_t* peer_land0, uint32_t* peer_flags,
+                     uint8_t* peer2_land0, uint32_t* peer2_flags, const int32_t* push_to, int nslots, long long stride,
+                     uint32_t epoch, int max_wg, void* stream) {
     SO_TRY(check_geom(fn, H, W, bs, 0));
     SO_TRY(check_sr(fn, sr));
     SO_TRY(check_qp(fn, qp_rd));
-    if (bs != 16 || sr != 16 || W % 128 != 0) {
-        set_error("%s: covers bs 16 / sr 16 / W %% 128 == 0", fn);
+    if (bs != 16 || sr != 16 || W % 128 != 0 || (two_pass && W > 8192)) {
+        set_error("%s: covers bs 16 / sr 16 / W %% 128 == 0%s", fn, two_pass ? ", W <= 8192" : "");
         return SO_E_UNSUPPORTED;
+    }
+    if (two_pass && (qp_lo < 0 || qp_hi > 20 || qp_lo > qp_hi)) {
+        set_error("%s: QP clamp [%d, %d] outside [0, 20]", fn, qp_lo, qp_hi);
+        return SO_E_INVALID;
     }
     // every rank owns `nslots` landing slots: this run reads slots [slot0, slot0 + nframes) and
     // writes (system scope, over xGMI) only slots below nslots of its peers
@@ -599,12 +604,14 @@ int so_encode_p_run_fpipe2(const uint8_t* const* curs, int nframes, int H, int W
     SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn); SO_NEED(workspace, fn); SO_NEED(land0, fn);
     SO_NEED(land_flags, fn); SO_NEED(peer_land0, fn); SO_NEED(peer_flags, fn); SO_NEED(peer2_land0, fn);
     SO_NEED(peer2_flags, fn); SO_NEED(push_to, fn);
+    if (two_pass) SO_NEED(out_qp_map, fn);
     std::vector<PFrameOut> outs((size_t)nframes);
     std::vector<int> push((size_t)nframes);
     const uint8_t* land_end = land0 + (long long)(slot0 + nframes) * stride;
     for (int i = 0; i < nframes; ++i) {
         SO_NEED(curs[i], fn); SO_NEED(out_split[i], fn); SO_NEED(out_mv[i], fn); SO_NEED(out_qtc[i], fn);
         SO_NEED(out_tokens[i], fn); SO_NEED(out_mae_num[i], fn); SO_NEED(out_recon[i], fn);
+        if (two_pass) SO_NEED(out_qp_map[i], fn);
         if (out_recon[i] >= land0 && out_recon[i] < land_end) {
             set_error("%s: out_recon[%d] lies in the landing planes", fn, i);
             return SO_E_INVALID;
@@ -615,12 +622,47 @@ int so_encode_p_run_fpipe2(const uint8_t* const* curs, int nframes, int H, int W
         }
         push[(size_t)i] = push_to[i];
         outs[i] = PFrameOut{out_split[i], out_mv[i], out_qtc[i], out_tokens[i], out_mae_num[i], out_recon[i],
-                            out_sse ? out_sse[i] : nullptr};
+                            out_sse ? out_sse[i] : nullptr, two_pass ? out_qp_map[i] : nullptr};
     }
     PRunStripe sp{0, H / 16, peer2_land0, peer_land0, stride, nullptr, land_flags, peer2_flags, peer_flags,
                   epoch, slot0, land0};
+    if (two_pass) {
+        sp.roi = roi;
+        sp.qp_lo = qp_lo;
+        sp.qp_hi = qp_hi;
+        return p_run_fpipe_2pass_launch(curs, nframes, H, W, qp_rd, qp_row, outs.data(), workspace, sp, max_wg,
+                                        (hipStream_t)stream, push.data());
+    }
     return p_run_fpipe_launch(curs, nframes, H, W, qp_rd, qp_row, outs.data(), workspace, sp, max_wg,
                               (hipStream_t)stream, push.data());
+}
+
+int so_encode_p_run_fpipe2(const uint8_t* const* curs, int nframes, int H, int W, int bs, int sr, int qp_rd,
+                           const int32_t* qp_row, uint8_t* const* out_split, int16_t* const* out_mv,
+                           int16_t* const* out_qtc, int32_t* const* out_tokens, int32_t* const* out_mae_num,
+                           uint8_t* const* out_recon, int32_t* const* out_sse, uint32_t* workspace,
+                           const uint8_t* land0, const uint32_t* land_flags, int slot0, uint8_t* peer_land0,
+                           uint32_t* peer_flags, uint8_t* peer2_land0, uint32_t* peer2_flags, const int32_t* push_to,
+                           int nslots, long long stride, uint32_t epoch, int max_wg, void* stream) {
+    return fpipe_run("so_encode_p_run_fpipe2", false, curs, nframes, H, W, bs, sr, qp_rd, qp_row, nullptr, 0, 0,
+                     out_split, out_mv, out_qtc, out_tokens, out_mae_num, out_recon, out_sse, nullptr, workspace, land0,
+                     land_flags, slot0, peer_land0, peer_flags, peer2_land0, peer2_flags, push_to, nslots, stride, epoch,
+                     max_wg, stream);
+}
+
+int so_encode_p_run_fpipe_2pass(const uint8_t* const* curs, int nframes, int H, int W, int bs, int sr, int qp_rd,
+                                const int32_t* qp_row, const int32_t* roi, int qp_lo, int qp_hi,
+                                uint8_t* const* out_split, int16_t* const* out_mv, int16_t* const* out_qtc,
+                                int32_t* const* out_tokens, int32_t* const* out_mae_num, uint8_t* const* out_recon,
+                                int32_t* const* out_sse, int32_t* const* out_qp_map, uint32_t* workspace,
+                                const uint8_t* land0, const uint32_t* land_flags, int slot0, uint8_t* peer_land0,
+                                uint32_t* peer_flags, uint8_t* peer2_land0, uint32_t* peer2_flags,
+                                const int32_t* push_to, int nslots, long long stride, uint32_t epoch, int max_wg,
+                                void* stream) {
+    return fpipe_run("so_encode_p_run_fpipe_2pass", true, curs, nframes, H, W, bs, sr, qp_rd, qp_row, roi, qp_lo, qp_hi,
+                     out_split, out_mv, out_qtc, out_tokens, out_mae_num, out_recon, out_sse, out_qp_map, workspace,
+                     land0, land_flags, slot0, peer_land0, peer_flags, peer2_land0, peer2_flags, push_to, nslots, stride,
+                     epoch, max_wg, stream);
 }
 
 int so_frame_push(const uint8_t* plane, int H, int W, uint8_t* peer_plane, uint32_t* peer_flags, uint32_t epoch,

@@ -1390,7 +1390,7 @@ template <class G>
 SO_DEV void tq16_pass2(PTileLds<G>& S, int g, int l, double* scratch, int bx0, int byt0, int nbx, int by1, int W,
                        int qp_rd, const int32_t* __restrict__ qp_row, const int32_t* __restrict__ roi, int qp_lo,
                        int qp_hi, const uint8_t* __restrict__ cur, const uint8_t* ref, const PFrameOut& o,
-                       const int32_t* __restrict__ t1) {
+                       const int32_t* __restrict__ t1, uint8_t* push = nullptr) {
     constexpr int TBX = G::TBX;
     const int bxl = g % TBX, byl = g / TBX;
     const int gbx = bx0 + bxl, gby = byt0 + byl;
@@ -1447,6 +1447,10 @@ SO_DEV void tq16_pass2(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
                    ((uint32_t)(rec[4 * k + 2] & 255) << 16) | ((uint32_t)(rec[4 * k + 3] & 255) << 24);
         uint8_t* rp = o.recon + (size_t)(y + l) * W + x;
         asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(rp), "v"(v) : "memory");
+        if (push) {   // frame pipeline: the next rank's landing plane (system scope, over xGMI)
+            uint8_t* q = push + (size_t)(y + l) * W + x;
+            asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(q), "v"(v) : "memory");
+        }
         int sse = 0;
         if (o.sse) {
             uint32_t cw[4];
@@ -1541,16 +1545,20 @@ struct PRunArgs {
 #define SO_RUN_TIMEOUT_WORD 32
 #endif
 #ifndef SO_RUN_DONE_BASE
-#define SO_RUN_DONE_BASE 64
+#define SO_RUN_DONE_BASE 96
 #endif
 // the task counter (hammered by every workgroup's dequeue), the timeout count and the done
 // flags live on separate 128-byte lines
 constexpr int kRunTimeoutWord = SO_RUN_TIMEOUT_WORD, kRunDoneBase = SO_RUN_DONE_BASE;
-// [1], [2] on the task counter's line: touched once per workgroup.  [40] (the timeout word's
-// line, written rarely): blocks whose SEA search took the dense fallback, summed over launches
-// until the caller clears it (SO_P_RUN_FALLBACK_WORD)
-constexpr int kRunExitWord = 1, kRunEpochWord = 2, kRunFallbackWord = 40;
-constexpr int kRunSingle = 0, kRunStripe = 1, kRunFPipe = 2, kRunTwoPass = 3;
+// [1], [2] on the task counter's line: touched once per workgroup.  [64] (a line of its own):
+// blocks whose SEA search took the dense fallback, summed over launches until the caller clears
+// it (SO_P_RUN_FALLBACK_WORD); each workgroup adds its total once, on its way out.  (Adding per
+// tile on the timeout word's line, which every waiting workgroup reads, cost +17 % per frame.)
+constexpr int kRunExitWord = 1, kRunEpochWord = 2, kRunFallbackWord = 64;
+// kRunFPipe2P: the frame pipeline with two-pass RC (each tile a pass-1 and a pass-2 task as
+// kRunTwoPass; the reference arrives in the landing planes as kRunFPipe, and pass 2 pushes
+// the final reconstruction on to the rank encoding the next frame)
+constexpr int kRunSingle = 0, kRunStripe = 1, kRunFPipe = 2, kRunTwoPass = 3, kRunFPipe2P = 4;
 // SO_RUN_PROFILE builds (tools/rc2p_ab.py): per-phase shader cycles >> 10 accumulated by wave 0
 // into workspace words 48.. (48 pass-1 task, 49 pass-2 task, 50 pass-2 row wait, 51 reference
 // wait); A/B diagnostics only
@@ -1571,7 +1579,8 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     __shared__ int s_task;
     const int tid = threadIdx.x;
     const int nbx = W / 16;
-    constexpr bool STRIPE = MODE == kRunStripe, FPIPE = MODE == kRunFPipe, TWOP = MODE == kRunTwoPass;
+    constexpr bool STRIPE = MODE == kRunStripe, FPIPE = MODE == kRunFPipe || MODE == kRunFPipe2P;
+    constexpr bool TWOP = MODE == kRunTwoPass || MODE == kRunFPipe2P;
     const int by0 = STRIPE ? sp.by0 : 0, by1 = STRIPE ? sp.by1 : H / 16;
     const int tiles_x = (nbx + G::TBX - 1) / G::TBX, ntr = (by1 - by0 + G::TBY - 1) / G::TBY;
     const int ntiles = tiles_x * ntr;
@@ -1587,6 +1596,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lane = tid & 63;
     const uint32_t one = lane == 0 ? 1u : 0u;
+    uint32_t fbsum = 0;   // wave 0: this workgroup's dense-fallback blocks over its tasks
     // this launch's epoch: ws[2] + 1 (ws[2] = the last finished launch's; written by that
     // launch's last workgroup, so every workgroup here reads it before it can change).  Done
     // flags hold the epoch of the launch that set them: nothing is zeroed between launches.
@@ -1631,7 +1641,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
         const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
         const bool first_row = ty == 0, last_row = ty == ntr - 1;
         // in-launch reference frame, or -1
-        const int dep = (MODE == kRunSingle || TWOP) ? a.dep[f] : f - 1;
+        const int dep = (MODE == kRunSingle || MODE == kRunTwoPass) ? a.dep[f] : f - 1;
         // the 3x3 tiles of frame f-1 around this one (the window's +-16 px), one flag per lane,
         // all polled in one round trip by wave 0 once the current tile is staged (ptile_body's
         // `pre`; the barrier after it releases the other waves).  Stripe: lanes 9-11 (12-14)
@@ -1747,7 +1757,9 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                         const bool v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ep;
                         if (__builtin_amdgcn_ballot_w64(lane < tiles_x && !v) == 0) break;
                         __builtin_amdgcn_s_sleep(1);
-                        if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
+                        // 50 ms; 2 s in the frame pipeline, whose pass-1 tasks may wait that long on
+                        // another rank's reconstruction
+                        if (__builtin_amdgcn_s_memrealtime() - t0 > (FPIPE ? 200000000ull : 5000000ull)) {
                             __hip_atomic_fetch_add(&ws[kRunTimeoutWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             break;
                         }
@@ -1766,14 +1778,23 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                     if (lane == 0) S.msum[wave] = (int32_t)sum;
                 }
                 __syncthreads();
+                // frame pipeline: where the final reconstruction goes (kRunFPipe's push code)
+                const int code = FPIPE ? a.dep[f] : -1;
+                uint8_t* const push = code >= 0 ? ((code & 1) ? sp.peer_up0 : sp.peer_dn0) +
+                                                      (long long)(code >> 1) * sp.stride : nullptr;
                 const int t2 = opaque_tid(), ln = t2 & 63, gq = (t2 >> 6) * G::TQ_BPW + (ln >> 4);
                 if (ln < 16 * G::TQ_BPW && gq < G::NBLK)
                     tq16_pass2<G>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by1, W, qp_rd, qp_row, sp.roi,
-                                  sp.qp_lo, sp.qp_hi, a.cur[f], ref, a.out[f], t1);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                                  sp.qp_lo, sp.qp_hi, a.cur[f], ref, a.out[f], t1, push);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // local and remote stores retired
                 __syncthreads();
-                if (wave == 0)
+                if (wave == 0) {
                     __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (lane == 0 && code >= 0)
+                        __hip_atomic_store(((code & 1) ? sp.peer_up_flags : sp.peer_dn_flags) +
+                                               (size_t)(code >> 1) * ntiles + tile,
+                                           sp.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
                 SO_RUN_PROF(49, __builtin_amdgcn_s_memtime() - pt0);
             }
         } else if constexpr (FPIPE) {
@@ -1833,12 +1854,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
         }
-#ifndef SO_RUN_FALLBACK_COUNT
-#define SO_RUN_FALLBACK_COUNT 1
-#endif
-        if (SO_RUN_FALLBACK_COUNT && pass == 1 && wave == 0 && S.st[0] != 0u)   // this tile's dense-fallback blocks
-            __hip_atomic_fetch_add(&ws[kRunFallbackWord], lane == 0 ? S.st[0] : 0u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+        if (pass == 1 && wave == 0) fbsum += S.st[0];   // this tile's dense-fallback blocks
 #ifdef SO_STAMPS
         if (tid == 0 && rec) {
             uint32_t hw, xcc;
@@ -1851,6 +1867,9 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 #endif
     }
     // the last workgroup out resets the task and exit counters and publishes the epoch
+    if (wave == 0 && fbsum != 0u)
+        __hip_atomic_fetch_add(&ws[kRunFallbackWord], lane == 0 ? fbsum : 0u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     if (wave == 0) {
         const uint32_t o = __builtin_amdgcn_readfirstlane(
             __hip_atomic_fetch_add(&ws[kRunExitWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -1909,7 +1928,7 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
             const int d = deps ? deps[g] : g - 1;
             a.cur[i] = curs[g];
             a.out[i] = outs[g];
-            if (MODE == kRunFPipe) {   // deps = the per-frame push codes (slot * 2 + peer)
+            if (MODE == kRunFPipe || MODE == kRunFPipe2P) {   // deps = the per-frame push codes (slot * 2 + peer)
                 a.ref[i] = nullptr;
                 a.dep[i] = deps ? deps[g] : -1;
                 continue;
@@ -1934,7 +1953,7 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
         if (max_wg > 0 && grid > max_wg) grid = max_wg;
         PRunStripe sp = sp0;
         sp.gbase = sp0.gbase + f0;
-        if (MODE == kRunTwoPass) {   // pass 2 of a row about one grid's worth of tasks after its pass 1
+        if (MODE == kRunTwoPass || MODE == kRunFPipe2P) {   // pass 2 of a row about one grid's worth of tasks after its pass 1
             const int tiles_x = (nbx + G::TBX - 1) / G::TBX, ntr = (rows + G::TBY - 1) / G::TBY;
             int lag = (int)((grid + tiles_x - 1) / tiles_x);
             if (const char* e = getenv("SO_P2LAG")) lag = atoi(e);   // A/B only
@@ -2005,6 +2024,18 @@ int p_run_fpipe_launch(const uint8_t* const* curs, int nframes, int H, int W, in
                        const int* push) {
     return p_run_launch_t<kRunFPipe>(curs, nframes, nullptr, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st,
                                           nullptr, push);
+}
+
+// The frame pipeline with two-pass RC (kRunFPipe2P): sp as p_run_fpipe_launch plus the ROI / QP
+// clamp; the pass-1 flags and token counts live in the workspace as in p_run_2pass_launch.
+int p_run_fpipe_2pass_launch(const uint8_t* const* curs, int nframes, int H, int W, int qp_rd, const int32_t* qp_row,
+                             const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp0, int max_wg, hipStream_t st,
+                             const int* push) {
+    PRunStripe sp = sp0;
+    sp.p1done = ws + kRunDoneBase + (size_t)kRunMax * run_tiles(H, W, Sea2Geo::TBX, Sea2Geo::TBY);
+    sp.t1 = reinterpret_cast<int32_t*>(sp.p1done + (size_t)kRunMax * run_tiles(H, W, Sea2Geo::TBX, Sea2Geo::TBY));
+    return p_run_launch_t<kRunFPipe2P>(curs, nframes, nullptr, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st,
+                                           nullptr, push, 2);
 }
 
 // The I-frame's hand-off (the P-frame run's frame 0 reads its boundary rows): copy the

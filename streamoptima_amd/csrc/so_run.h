@@ -75,5 +75,8 @@ int p_run_stripe_launch(const uint8_t* const* curs, int nframes, const uint8_t* 
 int p_run_fpipe_launch(const uint8_t* const* curs, int nframes, int H, int W, int qp_rd, const int32_t* qp_row,
                        const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg, hipStream_t st,
                        const int* push);
+int p_run_fpipe_2pass_launch(const uint8_t* const* curs, int nframes, int H, int W, int qp_rd, const int32_t* qp_row,
+                             const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg, hipStream_t st,
+                             const int* push);
 
 }  // namespace so

@@ -170,6 +170,19 @@ class StripeGOPEncoder:
             else:
                 full = pad
             out[name] = full[: e.nby * nbx]
+        qm = sym.extra.get("qp_map") if sym.extra else None
+        if qm is not None:
+            # ROI / two-pass RC: each rank's map is valid on its own block rows only; the
+            # frame's map is their rank-order concatenation, like every other symbol
+            pad = torch.zeros(self.rps * nbx, dtype=torch.int32, device=qm.device)
+            nrow = max(self.by1 - self.by0, 0) * nbx
+            pad[:nrow].copy_(qm[self.by0 * nbx:self.by0 * nbx + nrow])
+            full = torch.empty(self.world * self.rps * nbx, dtype=torch.int32, device=qm.device)
+            if self.world > 1:
+                dist.all_gather_into_tensor(full.view(torch.uint8), pad.view(torch.uint8), group=self.group)
+            else:
+                full.copy_(pad)
+            out["qp_map"] = full[: e.nby * nbx]
         out["recon"] = sym.recon
         out["frame_type"] = sym.frame_type
         return out

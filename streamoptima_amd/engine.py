@@ -18,7 +18,7 @@ from . import _lib
 
 SLACK = 64  # bytes readable past every plane (kernels read aligned words at row ends)
 RUN_TIMEOUT_WORD = 32   # so_encode_p_run workspace: the timeout count (include/streamoptima.h)
-RUN_FALLBACK_WORD = 40  # ... and the count of blocks whose SEA search took the dense fallback
+RUN_FALLBACK_WORD = 64  # ... and the count of blocks whose SEA search took the dense fallback
 
 
 def alloc_planes(n: int, h: int, w: int, device, fill: int | None = None) -> torch.Tensor:

@@ -28,6 +28,7 @@ front end (handles exchanged with all_gather_object; SSE summed with one all_red
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 
 import torch
@@ -413,30 +414,48 @@ class FramePipeRank:
                 self.lib.so_free_device(p)
         self._planes, self._flags = ctypes.c_void_p(), ctypes.c_void_p()
 
-    def encode(self, frames: torch.Tensor, intra_dur: int, qp: int) -> dict:
+    def encode(self, frames: torch.Tensor, intra_dur: int, qp: int, qp_row=None, roi_dev=None,
+               two_pass: bool = False, qp_clamp=(0, 12)) -> dict:
         """This rank's frames of the GOP {global index: FrameSymbols} (whole-frame symbols,
-        local reconstructions).  Asynchronous on the rank's stream."""
+        local reconstructions).  Asynchronous on the rank's stream.
+
+        Rate control (Y_Video_codec's RCFlag >= 1 without a P->I switch): qp_row = the per-row
+        QP schedule (content-independent, Encoder.py:1599-1609, so every rank computes it);
+        two_pass = RCFlag 3 (pass 1, the per-block QP map from the row's pass-1 tokens, pass 2;
+        roi_dev: int32 [nb] ROI offsets, qp_clamp: the map's clamp) -- configs[4].  A rank owns
+        whole frames, so the row-local statistics never cross ranks.  ROI without two-pass is
+        not covered here (the stripes are)."""
         e, lib = self.eng, self.lib
         nf = frames.shape[0]
         if nf > self.max_frames or intra_dur < nf:
             raise ValueError("the frame pipeline runs one GOP of <= max_frames frames with its only I-frame first")
         if self.peer is None:
             raise RuntimeError("connect() first")
+        if roi_dev is not None and not two_pass:
+            raise ValueError("the frame pipeline covers ROI with two-pass RC only")
         self.epoch += 1
         ep, st = self.epoch, self._st()
         mine = self.frames_of(nf)
         if self._syms is None or len(self._syms) != len(mine):
             self._syms = {k: e.new_symbols(0 if k == 0 else 1) for k in mine}
         syms = self._syms
+        qrd = e.qp_row_tensor(qp_row) if qp_row is not None else None
+        if two_pass:
+            for s in syms.values():
+                if "qp_map" not in s.extra:
+                    s.extra["qp_map"] = torch.empty(e.nb, dtype=torch.int32, device=e.device)
         pplanes, pflags = self.peer
         ks = mine
         if self.rank == 0:
             s0 = syms[0]
-            _lib.check(lib.so_encode_i_rows_ex(
-                frames[0].data_ptr(), e.h, e.w, e.bs, e.sr, 0, e.nby, int(qp), None, None, 0, 0.0,
-                s0.split.data_ptr(), s0.mv.data_ptr(), s0.qtc.data_ptr(), s0.tokens.data_ptr(), s0.mae_num.data_ptr(),
-                s0.recon.data_ptr(), s0.sse.data_ptr(), e.scratch.data_ptr(), st), "so_encode_i_rows_ex")
-            s0.frame_type, s0.qp_rd = 0, int(qp)
+            # the I-frame as encode_device's frame(): pass 1, the QP map, pass 2 (two-pass RC);
+            # the engine launches on the current stream, i.e. the rank's
+            with torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext():
+                e.encode_i(frames[0], qp, qp_row, out=s0, qp_row_dev=qrd)
+                if two_pass:
+                    qm = s0.extra["qp_map"]
+                    e.qp_map(s0.tokens, qp, qrd, roi_dev, qm, qp_lo=qp_clamp[0], qp_hi=qp_clamp[1])
+                    e.encode_i(frames[0], qp, qp_row, out=s0, qp_row_dev=qrd, qp_map_dev=qm)
             if nf > 1:   # frame 1 is rank 1's slot 0
                 _lib.check(lib.so_frame_push(s0.recon.data_ptr(), e.h, e.w, pplanes, pflags, ep, st), "so_frame_push")
             ks = mine[1:]
@@ -447,16 +466,25 @@ class FramePipeRank:
             arr = lambda xs: (ctypes.c_void_p * n)(*xs)  # noqa: E731
             ss = [syms[k] for k in ks]
             p2planes, p2flags = self.peer2
-            _lib.check(lib.so_encode_p_run_fpipe2(
-                arr([frames[k].data_ptr() for k in ks]), n, e.h, e.w, e.bs, e.sr, int(qp), None,
-                arr([s.split.data_ptr() for s in ss]), arr([s.mv.data_ptr() for s in ss]),
-                arr([s.qtc.data_ptr() for s in ss]), arr([s.tokens.data_ptr() for s in ss]),
-                arr([s.mae_num.data_ptr() for s in ss]), arr([s.recon.data_ptr() for s in ss]),
-                arr([s.sse.data_ptr() for s in ss]), self._ws.data_ptr(), self._planes.value, self._flags.value,
-                slot0, pplanes, pflags, p2planes, p2flags, (ctypes.c_int32 * n)(*plan["push"]), self.nslots,
-                self.stride, ep, int(self.max_wg), st), "so_encode_p_run_fpipe2")
+            outs = (arr([s.split.data_ptr() for s in ss]), arr([s.mv.data_ptr() for s in ss]),
+                    arr([s.qtc.data_ptr() for s in ss]), arr([s.tokens.data_ptr() for s in ss]),
+                    arr([s.mae_num.data_ptr() for s in ss]), arr([s.recon.data_ptr() for s in ss]),
+                    arr([s.sse.data_ptr() for s in ss]))
+            land = (self._planes.value, self._flags.value, slot0, pplanes, pflags, p2planes, p2flags,
+                    (ctypes.c_int32 * n)(*plan["push"]), self.nslots, self.stride, ep, int(self.max_wg), st)
+            curs = arr([frames[k].data_ptr() for k in ks])
+            if two_pass:
+                _lib.check(lib.so_encode_p_run_fpipe_2pass(
+                    curs, n, e.h, e.w, e.bs, e.sr, int(qp), _lib.ptr(qrd), _lib.ptr(roi_dev), int(qp_clamp[0]),
+                    int(qp_clamp[1]), *outs, arr([s.extra["qp_map"].data_ptr() for s in ss]), self._ws.data_ptr(),
+                    *land), "so_encode_p_run_fpipe_2pass")
+            else:
+                _lib.check(lib.so_encode_p_run_fpipe2(curs, n, e.h, e.w, e.bs, e.sr, int(qp), _lib.ptr(qrd), *outs,
+                                                      self._ws.data_ptr(), *land), "so_encode_p_run_fpipe2")
             for s in ss:
                 s.frame_type, s.qp_rd = 1, int(qp)
+        for s in syms.values():
+            s.qp_row = None if qp_row is None else list(qp_row)
         return syms
 
     def timed_out(self) -> bool:
@@ -488,11 +516,12 @@ class FramePipelineGOPEncoder:
         self.r.connect(nxt, prv)
         dist.barrier(group=group)
 
-    def encode_local(self, frames, intra_dur: int, qp: int) -> dict:
-        """This rank's launches only (no collective): {frame index: FrameSymbols}."""
-        return self.r.encode(frames, intra_dur, qp)
+    def encode_local(self, frames, intra_dur: int, qp: int, **rc) -> dict:
+        """This rank's launches only (no collective): {frame index: FrameSymbols}.  rc: the
+        FramePipeRank.encode rate-control keywords."""
+        return self.r.encode(frames, intra_dur, qp, **rc)
 
-    def encode(self, frames, intra_dur: int, qp: int, syms: dict | None = None, reduce: bool = True) -> dict:
+    def encode(self, frames, intra_dur: int, qp: int, syms: dict | None = None, reduce: bool = True, **rc) -> dict:
         """encode_local (unless its result is passed in) + one all_reduce of the per-frame SSE.
 
         reduce=False leaves "sse" None (sse() computes it later): no collective then joins
@@ -508,7 +537,7 @@ class FramePipelineGOPEncoder:
         if not reduce and nf <= self.world:
             raise ValueError(f"encode(reduce=False) needs more frames than ranks ({nf} <= {self.world}): "
                              "back-to-back GOPs would race on rank 1's first landing slot")
-        syms = self.r.encode(frames, intra_dur, qp) if syms is None else syms
+        syms = self.r.encode(frames, intra_dur, qp, **rc) if syms is None else syms
         return {"symbols": syms, "sse": self.sse(syms, nf) if reduce else None,
                 "frame_type": [0 if k == 0 else 1 for k in range(nf)]}
 

@@ -34,6 +34,30 @@ def test_library_exports_every_declared_symbol():
         assert re.search(rf"\bT {n}\b", out), n
 
 
+def test_ctypes_signatures_match_the_header():
+    """Every ctypes signature in _lib._SIGS has the header declaration's parameter count and
+    pointer / integer / floating kinds (a shifted argument would pass a size as a pointer)."""
+    from streamoptima_amd import _lib
+    hdr = open(os.path.join(ROOT, "include", "streamoptima.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    ptr_types = (ctypes.c_void_p, ctypes.c_char_p) + tuple(t for t in vars(ctypes).values()
+                                                         if isinstance(t, type) and t.__name__.startswith("LP_"))
+    for name, (args, _) in _lib._SIGS.items():
+        m = re.search(r"^\s*(?:int|size_t|const char\*)\s+" + name + r"\(([^;]*?)\);", hdr, re.M | re.S)
+        assert m, name
+        params = [p.strip() for p in m.group(1).split(",") if p.strip() and p.strip() != "void"]
+        assert len(params) == len(args), (name, len(params), len(args))
+        for i, (p, a) in enumerate(zip(params, args)):
+            is_ptr = "*" in p
+            if is_ptr:
+                assert a in ptr_types or issubclass(a, ctypes._Pointer), (name, i, p, a)
+            elif "double" in p:
+                assert a is ctypes.c_double, (name, i, p, a)
+            else:
+                assert a in (ctypes.c_int, ctypes.c_uint32, ctypes.c_int64, ctypes.c_longlong, ctypes.c_size_t,
+                             ctypes.c_ulonglong, ctypes.c_int32), (name, i, p, a)
+
+
 def test_code_object_is_gfx950():
     from streamoptima_amd import build
     blob = open(build.LIB_PATH, "rb").read()

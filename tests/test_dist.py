@@ -182,5 +182,9 @@ def test_stripe_gop_matches_single_process_oracle(tmp_path, world, case_name):
         for k in ("split", "mv", "qtc", "tokens", "mae_num", "recon"):
             np.testing.assert_array_equal(got[f"{k}_{i}"], np.asarray(r[k]).astype(got[f"{k}_{i}"].dtype),
                                           err_msg=f"frame {i} {k}")
+        if r.get("qp_map") is not None:      # ROI / two-pass: the gathered per-block QP map
+            np.testing.assert_array_equal(got[f"qp_map_{i}"], np.asarray(r["qp_map"]), err_msg=f"frame {i} qp_map")
+        else:
+            assert f"qp_map_{i}" not in got.files
         d = _frames()[i].astype(np.int64) - r["recon"].astype(np.int64)
         assert int(got["sse"][i]) == int((d * d).sum())

@@ -140,12 +140,93 @@ def test_stripe_run_two_processes_ipc(gpu, tmp_path):
     np.testing.assert_allclose(psnr, FIX["1080p"]["psnr"][:n], rtol=0, atol=1e-9)
 
 
+def _rc_codec(dev, n, rc, thresh):
+    from streamoptima_amd.Encoder import Y_Video_codec
+    from streamoptima_amd.workloads import RC_TABLES, WORKLOADS
+    cfg = WORKLOADS["4k_rc2pass"]
+    return Y_Video_codec(cfg["h"], cfg["w"], n, 16, 16, cfg["qp"], n, 0, 0.015, False, RCFlag=rc,
+                         targetBR=cfg["target"], qp_rate_tables=RC_TABLES, roi=cfg["roi"], intra_thresh=thresh,
+                         device=dev)
+
+
+def _rc_stripe_worker(rank, world, port, n, rc, thresh, outdir):
+    """dist.StripeGOPEncoder on the HIP engine: RC / ROI / two-pass GOPs as block-row stripes
+    with one RCCL-style all_gather (gloo here) per reconstruction."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from streamoptima_amd.digest import frame_digest
+        from streamoptima_amd.dist import StripeGOPEncoder
+        dev = torch.device("cuda:0")
+        cfg, fr = _frames("4k_rc2pass", dev, n)
+        codec = _rc_codec(dev, n, rc, thresh)
+        eng = codec.engine()
+        enc = StripeGOPEncoder(eng)
+        res = enc.encode(fr, n, cfg["qp"], qp_sched=codec.row_qp_schedule(eng.nby), rc_flag=rc, intra_thresh=thresh,
+                         roi=codec.roi_block_offsets())
+        digs = []
+        for s in res["symbols"]:
+            g = enc.gather_symbols(s)
+            digs.append(frame_digest(g["frame_type"], {k: (v.cpu().numpy() if torch.is_tensor(v) else v)
+                                                        for k, v in g.items()}))
+        if rank == 0:
+            with open(os.path.join(outdir, "digests.json"), "w") as fh:
+                json.dump({"digests": digs, "ftypes": res["frame_type"], "sse": res["sse"].cpu().tolist()}, fh)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rc_roi_stripes_two_processes(gpu, tmp_path):
+    """configs[4] across ranks (dist.StripeGOPEncoder with the HIP Engine, 2 processes on one
+    GPU): the 4K ROI + two-pass RC GOP head equals the oracle digests (QP maps gathered across
+    the stripes), and an RCFlag 2 GOP with ROI whose intra_thresh makes some P-frames switch to
+    intra (the all_reduce of the residual size, Encoder.py:1851-1856) equals the one-GPU encode."""
+    import torch.multiprocessing as mp
+    from streamoptima_amd.digest import symbols_digest
+    n = 6
+    mp.start_processes(_rc_stripe_worker, args=(2, _free_port(), n, 3, None, str(tmp_path)), nprocs=2,
+                       start_method="spawn")
+    got = json.load(open(tmp_path / "digests.json"))
+    assert got["digests"] == FIX["4k_rc2pass"]["frame_sha256"][:n]
+    psnr = [10 * np.log10(255 ** 2 / (s / (2160 * 3840))) for s in got["sse"]]
+    np.testing.assert_allclose(psnr, FIX["4k_rc2pass"]["psnr"][:n], rtol=0, atol=1e-9)
+    # RCFlag 2: a threshold between the P-frames' residual sizes, so the switch fires for some
+    _, fr = _frames("4k_rc2pass", gpu, n)
+    probe = _rc_codec(gpu, n, 2, 10 ** 12).encode_device(fr, n)
+    sizes = sorted(int(s.tokens.sum()) for s in probe["symbols"][1:])
+    thresh = (sizes[0] + sizes[-1]) // 2 if sizes[0] < sizes[-1] else sizes[0] - 1
+    exp = _rc_codec(gpu, n, 2, thresh).encode_device(fr, n)
+    assert 0 in exp["frame_type"][1:], "the threshold should switch a P-frame to intra"
+    exp_d = [symbols_digest(s) for s in exp["symbols"]]
+    mp.start_processes(_rc_stripe_worker, args=(2, _free_port(), n, 2, thresh, str(tmp_path)), nprocs=2,
+                       start_method="spawn")
+    got = json.load(open(tmp_path / "digests.json"))
+    assert got["ftypes"] == exp["frame_type"]
+    assert got["digests"] == exp_d
+    assert got["sse"] == exp["sse"].cpu().tolist()
+
+
 # ---- frame pipeline (consecutive frames on consecutive ranks, so_encode_p_run_fpipe) -------------
-@pytest.mark.parametrize("name,world,nframes", [("4k", 2, 12), ("4k", 3, 13), ("1080p", 2, 30)])
+def _fpipe_rc_kw(name, eng, nframes):
+    """FramePipeRank.encode's RC keywords of a workload (configs[4]: the row-QP schedule, two-pass,
+    the ROI offsets), from the drop-in codec's own settings."""
+    from streamoptima_amd.workloads import WORKLOADS
+    if not WORKLOADS[name].get("rc"):
+        return {}
+    codec = _rc_codec(eng.device, nframes, 3, None)
+    return dict(qp_row=codec.row_qp_schedule(eng.nby), two_pass=True,
+                roi_dev=eng.device_const_i32(codec.roi_block_offsets()), qp_clamp=tuple(codec.qp_clamp))
+
+
+@pytest.mark.parametrize("name,world,nframes", [("4k", 2, 12), ("4k", 3, 13), ("1080p", 2, 30), ("4k_rc2pass", 2, 8),
+                                                ("4k_rc2pass", 3, 10)])
 def test_frame_pipeline_in_process_matches_one_gpu(gpu, name, world, nframes):
     """Rank g encodes frames g, g+N, ...; each frame's reference arrives tile by tile from the
     previous rank.  Whole-frame symbols and local reconstructions of every frame must equal
-    the one-GPU GOP (oracle digests), twice in a row (epoch 2 over epoch 1's planes)."""
+    the one-GPU GOP (oracle digests), twice in a row (epoch 2 over epoch 1's planes).
+    4k_rc2pass: configs[4] (ROI + two-pass RC) on the frame pipeline, QP maps included."""
     from streamoptima_amd.digest import symbols_digest
     from streamoptima_amd.engine import Engine
     from streamoptima_amd.pipeline import FramePipeRank
@@ -158,11 +239,12 @@ def test_frame_pipeline_in_process_matches_one_gpu(gpu, name, world, nframes):
     torch.cuda.synchronize()
     for r in range(world):
         ranks[r].connect(ranks[(r + 1) % world].info(), ranks[(r - 1) % world].info())
+    rc_kw = [_fpipe_rc_kw(name, engines[r], nframes) for r in range(world)]
     for rep in range(2):
         syms = {}
         for r in range(world):
             with torch.cuda.stream(streams[r]):
-                syms.update(ranks[r].encode(fr, nframes, cfg["qp"]))
+                syms.update(ranks[r].encode(fr, nframes, cfg["qp"], **rc_kw[r]))
         torch.cuda.synchronize()
         for r in ranks:
             r.check()
