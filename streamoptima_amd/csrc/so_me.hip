@@ -789,6 +789,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
         }
         __syncthreads();
         if (r == 0) SO_SEA_STAMP(3, __builtin_amdgcn_s_memtime());
+        if (probe == 5) continue;   // phase-attribution builds (SO_PROF_PHASE=2): no search at all
         // 4x4 byte sums B4(row, c) = (sum of the 4x4 window block at (row, c)) >> 4, stored at
         // b4[row * B4P + (c & 3) * WD + (c >> 2)] (a candidate's four sums of one 4x4 row --
         // columns c, c+4, c+8, c+12 -- are then consecutive bytes).  Thread = (dword column m:
@@ -1267,7 +1268,10 @@ SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur
     const Sea2Lds L{S.win, b4w, S.curt, S.a4, list, S.lcount, S.keys, S.st};
     RefSet refs{};
     refs.p[0] = ref;
-    sea2_tile<G>(L, tile, cur, refs, 1, H, W, by0, by1, 0, pre);   // ends with a barrier
+#ifndef SO_PROF_PHASE   // phase-attribution A/B builds only (tools/prun_phase.py): 1 = no transforms
+#define SO_PROF_PHASE 0  // (the tile's current rows stored as its reconstruction), 2 = no search
+#endif                   // (window staged, every block at mv (0, 0))
+    sea2_tile<G>(L, tile, cur, refs, 1, H, W, by0, by1, SO_PROF_PHASE == 2 ? 5 : 0, pre);   // ends with a barrier
 
     const int tid = opaque_tid();
     SO_SEA_STAMP(5, __builtin_amdgcn_s_memtime());
@@ -1289,7 +1293,18 @@ SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur
         // 67.2 us per frame, 1088p 30.7 / 31.7 vs 28.7)
         const int ln = tid & 63, w = tid >> 6;
         const int gq = w * G::TQ_BPW + (ln >> 4);
-        if (ln < 16 * G::TQ_BPW && gq < G::NBLK)
+        if (SO_PROF_PHASE == 1 && ln < 16 * G::TQ_BPW && gq < G::NBLK) {
+            // no transforms: the current rows stand in for the reconstruction, so the next
+            // frame searches realistic content
+            const int bxl = gq % G::TBX, byl = gq / G::TBX, l = ln & 15;
+            const int gbx = bx0 + bxl, gby = byt0 + byl;
+            if (gbx < nbx && gby < by1) {
+                const uint32_t* crow = S.curt + (byl * 16 + l) * G::CPD + bxl * 4;
+                so_v4u v;
+                for (int k = 0; k < 4; ++k) v[k] = crow[k];
+                *reinterpret_cast<so_v4u*>(o.recon + (size_t)(gby * 16 + l) * W + gbx * 16) = v;
+            }
+        } else if (ln < 16 * G::TQ_BPW && gq < G::NBLK)
             tq16_exact<G, SC1, HALO, TOK>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by0, by1, W, qp_rd, qp_row,
                                      qp_map, o, hl);
     }

@@ -59,6 +59,14 @@ def analyse(rec, nframes, tiles_x, ntr):
         "decode": float(np.median(cyc(5, 6))), "tq_wave0": float(np.median(cyc(6, 7))),
         "store_drain_wave0": float(np.median(cyc(7, 14))), "barrier_flag": float(np.median(cyc(14, 13))),
         "tq_store_flag": float(np.median(cyc(5, 13)))}
+    # the search phase's spread: a tile whose wave holds a dense-fallback block keeps its other
+    # waves at the barrier (mean vs median, p90 / p99)
+    sc = cyc(4, 5).ravel()
+    out["search_cycles_mean_p50_p90_p99"] = [round(float(sc.mean())), round(float(np.median(sc))),
+                                            round(float(np.percentile(sc, 90))), round(float(np.percentile(sc, 99)))]
+    tot = cyc(1, 13).ravel()
+    out["tile_cycles_mean_p50_p90"] = [round(float(tot.mean())), round(float(np.median(tot))),
+                                       round(float(np.percentile(tot, 90)))]
     return out
 
 
@@ -93,7 +101,7 @@ def main():
         assert lib.so_debug_set_run_stamps(None) == 0
         eng.check_run()
         res[h] = analyse(stamps.cpu().numpy(), nf - 1, tiles_x, ntr)
-        print(f"H={h} W={w} TPX={a.tpx}:", json.dumps(res[h]), flush=True)
+        print(f"H={h} W={w}:", json.dumps(res[h]), flush=True)
     print(json.dumps(res))
 
 
