@@ -831,10 +831,11 @@ def main(argv=None):
         senc = StripeGOPEncoder(eng)
         rc = cfg.get("rc")
         cap = 768 // (2 * world) if args.share_gpu else 0
-        plain = not rc and plain_cfg and eng.pipelined_ok(1)
-        # the frame pipeline covers the plain GOP and two-pass RC / ROI (configs[4]): a rank
-        # owns whole frames, so the row-local QP statistics never cross ranks
-        fp_ok = plain_cfg and eng.pipelined_ok(1) and (not rc or (rc >= 3 and codec.intra_thresh is None))
+        plain = not rc and plain_cfg and eng.pipelined_ok(1, vbs_ok=False)
+        # the frame pipeline covers the plain GOP, VBSEnable and two-pass RC / ROI (configs[4]):
+        # a rank owns whole frames, so the row-local QP statistics never cross ranks
+        fp_ok = cfg.get("me", "full") == "full" and eng.pipelined_ok(1) and (
+            not rc or (rc >= 3 and codec.intra_thresh is None and not cfg.get("vbs")))
         fpipe_note = ""
         if args.shard == "fpipe" and fp_ok:
             fenc, fpipe_note = fpipe_encoder(codec, frames, cfg, world, max_wg=cap)

@@ -118,9 +118,11 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
  * A run of consecutive P-frames (the GOP loop's P-frames between two I-frames,
  * Encoder.py:1839-1867 with nRefFrames 1): frame i predicts from frame i-1's
  * reconstruction (out_recon[i-1]), frame 0 from ref0.  Output is identical to
- * so_encode_p_frame called per frame.  Covers bs 16 / sr 16 / no VBS with W a multiple
- * of 128 (whole cache lines per tile row); anything else is SO_E_UNSUPPORTED (call
- * so_encode_p_frame per frame).
+ * so_encode_p_frame called per frame.  Covers bs 16 / sr 16 with W a multiple of 128 (whole
+ * cache lines per tile row); anything else is SO_E_UNSUPPORTED (call so_encode_p_frame per
+ * frame).  vbs / lam: VBSEnable and calculate_RD_cost's lambda (Encoder.py:512-578,
+ * :1133-1158) -- the block and sub-block search and the RD split run inside the launch
+ * (vbs 0: lam unused).
  *
  * One persistent launch per 32 frames: workgroups take (frame, tile) tasks in frame-major
  * raster order, and a tile of frame i starts once the 3x3 tiles of frame i-1 its +-16 px
@@ -145,7 +147,8 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
 #define SO_P_RUN_FALLBACK_WORD 64
 size_t so_p_run_workspace_elems(int H, int W);
 int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W,
-                    int bs, int sr, int qp_rd, const int32_t* qp_row, uint8_t* const* out_split,
+                    int bs, int sr, int qp_rd, const int32_t* qp_row, int vbs, double lam,
+                    uint8_t* const* out_split,
                     int16_t* const* out_mv, int16_t* const* out_qtc, int32_t* const* out_tokens,
                     int32_t* const* out_mae_num, uint8_t* const* out_recon, int32_t* const* out_sse,
                     uint32_t* workspace, void* stream);
@@ -189,7 +192,8 @@ int so_encode_p_run_2pass(const uint8_t* const* curs, int nframes, const uint8_t
  */
 int so_encode_p_runs(const uint8_t* const* curs, int nframes, const uint8_t* const* refs,
                      const int32_t* ref_frame, int H, int W, int bs, int sr, int qp_rd,
-                     const int32_t* qp_row, uint8_t* const* out_split, int16_t* const* out_mv,
+                     const int32_t* qp_row, int vbs, double lam, uint8_t* const* out_split,
+                     int16_t* const* out_mv,
                      int16_t* const* out_qtc, int32_t* const* out_tokens, int32_t* const* out_mae_num,
                      uint8_t* const* out_recon, int32_t* const* out_sse, uint32_t* workspace,
                      void* stream);
@@ -250,7 +254,8 @@ int so_stripe_halo_push(const uint8_t* plane, int H, int W, int by0, int by1, in
  * (the I-frame) the same way.  workspace: so_p_run_workspace_elems(H, W), as so_encode_p_run.
  */
 int so_encode_p_run_fpipe2(const uint8_t* const* curs, int nframes, int H, int W, int bs, int sr,
-                           int qp_rd, const int32_t* qp_row, uint8_t* const* out_split,
+                           int qp_rd, const int32_t* qp_row, int vbs, double lam,
+                           uint8_t* const* out_split,
                            int16_t* const* out_mv, int16_t* const* out_qtc, int32_t* const* out_tokens,
                            int32_t* const* out_mae_num, uint8_t* const* out_recon,
                            int32_t* const* out_sse, uint32_t* workspace, const uint8_t* land0,

@@ -410,7 +410,8 @@ class Y_Video_codec(BlockAPI):
         # so_encode_p_run_2pass call -- the per-frame kernel sequence enqueued by the library
         # (same GPU time as this loop, a third of its host time, but a synchronous GOP measured
         # 0.6 ms slower) or, with SO_RUN_2PASS_FUSED=1, both passes in one persistent launch
-        pipelined2 = run_ok and two_pass and os.environ.get("SO_RUN_2PASS", "0") == "1"
+        pipelined2 = (run_ok and two_pass and eng.pipelined_ok(1, vbs_ok=False)
+                      and os.environ.get("SO_RUN_2PASS", "0") == "1")
         if pipelined and chunk is None and intra_dur < nframes - 1 and wait_input_default and on_output_default:
             # several P-runs between I-frames: independent chains, interleaved in one launch
             return self.encode_gops_device([frames_dev], intra_dur, symbols=[symbols] if symbols else None,

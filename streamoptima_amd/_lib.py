@@ -39,11 +39,12 @@ _SIGS = {
     "so_encode_p_rows": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _d, _vp, _vp, _vp, _vp,
                           _vp, _vp, _vp, _vp, _vp], _i),
     "so_p_run_workspace_elems": ([_i, _i], _sz),
-    "so_encode_p_run": ([_vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
+    "so_encode_p_run": ([_vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _i, _d, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+                        _i),
     "so_encode_p_run_2pass": ([_vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                _vp, _vp, _vp], _i),
-    "so_encode_p_runs": ([_vp, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
-                         _i),
+    "so_encode_p_runs": ([_vp, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _i, _d, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                          _vp], _i),
     "so_i_frame_scratch_elems": ([_i, _i, _i], _sz),
     "so_encode_i_frame": ([_vp, _i, _i, _i, _i, _i, _vp, _i, _d, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                            _vp, _vp], _i),
@@ -66,10 +67,10 @@ _SIGS = {
     "so_pack_bound": ([_i, _i], _sz),
     "so_sum_i32_rows": ([_vp, _i, _i, _vp, _vp], _i),
     "so_unpack_frames": ([_i, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp], _i),
-    "so_encode_p_run_fpipe2": ([_vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _i, ctypes.c_longlong, ctypes.c_uint32, _i,
-                                _vp],
-                               _i),
+    "so_encode_p_run_fpipe2": ([_vp, _i, _i, _i, _i, _i, _i, _vp, _i, _d,                 # .. vbs, lam
+                                _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,                    # outs, workspace
+                                _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _i,                 # landing .. nslots
+                                ctypes.c_longlong, ctypes.c_uint32, _i, _vp], _i),
     "so_encode_p_run_fpipe_2pass": ([_vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _i,          # .. qp_hi
                                      _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,             # outs, qp maps, ws
                                      _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _i,               # landing .. nslots

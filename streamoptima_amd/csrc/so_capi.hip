@@ -92,6 +92,19 @@ int intra_recon_launch(int H, int W, int bs, int sr, int qp, const int32_t* qp_r
                        hipStream_t st);
 
 // ---- validation ------------------------------------------------------------------------------
+// VBSEnable flag and calculate_RD_cost's lambda (Encoder.py:1133-1158)
+static int check_vbs(const char* fn, int vbs, double lam) {
+    if (vbs != 0 && vbs != 1) {
+        set_error("%s: vbs must be 0 or 1", fn);
+        return SO_E_INVALID;
+    }
+    if (vbs && !(lam >= 0.0 && lam < 1e300)) {
+        set_error("%s: lambda %g (VBSEnable needs a finite lambda >= 0)", fn, lam);
+        return SO_E_INVALID;
+    }
+    return SO_OK;
+}
+
 static int check_geom(const char* fn, int H, int W, int bs, int vbs) {
     if (bs != 16 && bs != 8) {
         set_error("%s: block_size %d not built (gfx950 kernels exist for 16 and 8)", fn, bs);
@@ -379,11 +392,13 @@ size_t so_p_run_workspace_elems(int H, int W) {
 }
 
 int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int bs, int sr,
-                    int qp_rd, const int32_t* qp_row, uint8_t* const* out_split, int16_t* const* out_mv,
-                    int16_t* const* out_qtc, int32_t* const* out_tokens, int32_t* const* out_mae_num,
-                    uint8_t* const* out_recon, int32_t* const* out_sse, uint32_t* workspace, void* stream) {
+                    int qp_rd, const int32_t* qp_row, int vbs, double lam, uint8_t* const* out_split,
+                    int16_t* const* out_mv, int16_t* const* out_qtc, int32_t* const* out_tokens,
+                    int32_t* const* out_mae_num, uint8_t* const* out_recon, int32_t* const* out_sse,
+                    uint32_t* workspace, void* stream) {
     const char* fn = "so_encode_p_run";
-    SO_TRY(check_geom(fn, H, W, bs, 0));
+    SO_TRY(check_geom(fn, H, W, bs, vbs));
+    SO_TRY(check_vbs(fn, vbs, lam));
     SO_TRY(check_sr(fn, sr));
     SO_TRY(check_qp(fn, qp_rd));
     if (bs != 16 || sr != 16 || W % 128 != 0) {
@@ -405,16 +420,18 @@ int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0
         outs[i] = PFrameOut{out_split[i], out_mv[i], out_qtc[i], out_tokens[i], out_mae_num[i], out_recon[i],
                             out_sse ? out_sse[i] : nullptr};
     }
-    return p_run_launch(curs, nframes, ref0, H, W, qp_rd, qp_row, outs.data(), workspace, (hipStream_t)stream);
+    return p_run_launch(curs, nframes, ref0, H, W, qp_rd, qp_row, vbs, lam, outs.data(), workspace,
+                        (hipStream_t)stream);
 }
 
 int so_encode_p_runs(const uint8_t* const* curs, int nframes, const uint8_t* const* refs, const int32_t* ref_frame,
-                     int H, int W, int bs, int sr, int qp_rd, const int32_t* qp_row, uint8_t* const* out_split,
-                     int16_t* const* out_mv, int16_t* const* out_qtc, int32_t* const* out_tokens,
-                     int32_t* const* out_mae_num, uint8_t* const* out_recon, int32_t* const* out_sse,
-                     uint32_t* workspace, void* stream) {
+                     int H, int W, int bs, int sr, int qp_rd, const int32_t* qp_row, int vbs, double lam,
+                     uint8_t* const* out_split, int16_t* const* out_mv, int16_t* const* out_qtc,
+                     int32_t* const* out_tokens, int32_t* const* out_mae_num, uint8_t* const* out_recon,
+                     int32_t* const* out_sse, uint32_t* workspace, void* stream) {
     const char* fn = "so_encode_p_runs";
-    SO_TRY(check_geom(fn, H, W, bs, 0));
+    SO_TRY(check_geom(fn, H, W, bs, vbs));
+    SO_TRY(check_vbs(fn, vbs, lam));
     SO_TRY(check_sr(fn, sr));
     SO_TRY(check_qp(fn, qp_rd));
     if (bs != 16 || sr != 16 || W % 128 != 0) {
@@ -449,7 +466,7 @@ int so_encode_p_runs(const uint8_t* const* curs, int nframes, const uint8_t* con
         outs[(size_t)i] = PFrameOut{out_split[i], out_mv[i], out_qtc[i], out_tokens[i], out_mae_num[i], out_recon[i],
                                     out_sse ? out_sse[i] : nullptr};
     }
-    return p_runs_launch(curs, nframes, refs, deps.data(), conc, H, W, qp_rd, qp_row, outs.data(), workspace,
+    return p_runs_launch(curs, nframes, refs, deps.data(), conc, H, W, qp_rd, qp_row, vbs, lam, outs.data(), workspace,
                          (hipStream_t)stream);
 }
 
@@ -575,16 +592,22 @@ int so_stripe_halo_push(const uint8_t* plane, int H, int W, int by0, int by1, in
 // ---- one GOP across GPUs: consecutive frames on consecutive ranks (so_me.hip kRunFPipe) -----
 // The frame pipeline's argument checks and launch, with (two_pass) or without two-pass RC.
 static int fpipe_run(const char* fn, bool two_pass, const uint8_t* const* curs, int nframes, int H, int W, int bs,
-                     int sr, int qp_rd, const int32_t* qp_row, const int32_t* roi, int qp_lo, int qp_hi,
+                     int sr, int qp_rd, const int32_t* qp_row, int vbs, double lam, const int32_t* roi, int qp_lo,
+                     int qp_hi,
                      uint8_t* const* out_split, int16_t* const* out_mv, int16_t* const* out_qtc,
                      int32_t* const* out_tokens, int32_t* const* out_mae_num, uint8_t* const* out_recon,
                      int32_t* const* out_sse, int32_t* const* out_qp_map, uint32_t* workspace, const uint8_t* land0,
                      const uint32_t* land_flags, int slot0, uint8_t* peer_land0, uint32_t* peer_flags,
                      uint8_t* peer2_land0, uint32_t* peer2_flags, const int32_t* push_to, int nslots, long long stride,
                      uint32_t epoch, int max_wg, void* stream) {
-    SO_TRY(check_geom(fn, H, W, bs, 0));
+    SO_TRY(check_geom(fn, H, W, bs, vbs));
+    SO_TRY(check_vbs(fn, vbs, lam));
     SO_TRY(check_sr(fn, sr));
     SO_TRY(check_qp(fn, qp_rd));
+    if (two_pass && vbs) {
+        set_error("%s: two-pass RC with VBSEnable is not built for the frame pipeline", fn);
+        return SO_E_UNSUPPORTED;
+    }
     if (bs != 16 || sr != 16 || W % 128 != 0 || (two_pass && W > 8192)) {
         set_error("%s: covers bs 16 / sr 16 / W %% 128 == 0%s", fn, two_pass ? ", W <= 8192" : "");
         return SO_E_UNSUPPORTED;
@@ -633,18 +656,18 @@ static int fpipe_run(const char* fn, bool two_pass, const uint8_t* const* curs, 
         return p_run_fpipe_2pass_launch(curs, nframes, H, W, qp_rd, qp_row, outs.data(), workspace, sp, max_wg,
                                         (hipStream_t)stream, push.data());
     }
-    return p_run_fpipe_launch(curs, nframes, H, W, qp_rd, qp_row, outs.data(), workspace, sp, max_wg,
+    return p_run_fpipe_launch(curs, nframes, H, W, qp_rd, qp_row, vbs, lam, outs.data(), workspace, sp, max_wg,
                               (hipStream_t)stream, push.data());
 }
 
 int so_encode_p_run_fpipe2(const uint8_t* const* curs, int nframes, int H, int W, int bs, int sr, int qp_rd,
-                           const int32_t* qp_row, uint8_t* const* out_split, int16_t* const* out_mv,
+                           const int32_t* qp_row, int vbs, double lam, uint8_t* const* out_split, int16_t* const* out_mv,
                            int16_t* const* out_qtc, int32_t* const* out_tokens, int32_t* const* out_mae_num,
                            uint8_t* const* out_recon, int32_t* const* out_sse, uint32_t* workspace,
                            const uint8_t* land0, const uint32_t* land_flags, int slot0, uint8_t* peer_land0,
                            uint32_t* peer_flags, uint8_t* peer2_land0, uint32_t* peer2_flags, const int32_t* push_to,
                            int nslots, long long stride, uint32_t epoch, int max_wg, void* stream) {
-    return fpipe_run("so_encode_p_run_fpipe2", false, curs, nframes, H, W, bs, sr, qp_rd, qp_row, nullptr, 0, 0,
+    return fpipe_run("so_encode_p_run_fpipe2", false, curs, nframes, H, W, bs, sr, qp_rd, qp_row, vbs, lam, nullptr, 0, 0,
                      out_split, out_mv, out_qtc, out_tokens, out_mae_num, out_recon, out_sse, nullptr, workspace, land0,
                      land_flags, slot0, peer_land0, peer_flags, peer2_land0, peer2_flags, push_to, nslots, stride, epoch,
                      max_wg, stream);
@@ -659,7 +682,8 @@ int so_encode_p_run_fpipe_2pass(const uint8_t* const* curs, int nframes, int H, 
                                 uint32_t* peer_flags, uint8_t* peer2_land0, uint32_t* peer2_flags,
                                 const int32_t* push_to, int nslots, long long stride, uint32_t epoch, int max_wg,
                                 void* stream) {
-    return fpipe_run("so_encode_p_run_fpipe_2pass", true, curs, nframes, H, W, bs, sr, qp_rd, qp_row, roi, qp_lo, qp_hi,
+    return fpipe_run("so_encode_p_run_fpipe_2pass", true, curs, nframes, H, W, bs, sr, qp_rd, qp_row, 0, 0.0, roi, qp_lo,
+                     qp_hi,
                      out_split, out_mv, out_qtc, out_tokens, out_mae_num, out_recon, out_sse, out_qp_map, workspace,
                      land0, land_flags, slot0, peer_land0, peer_flags, peer2_land0, peer2_flags, push_to, nslots, stride,
                      epoch, max_wg, stream);

@@ -681,7 +681,233 @@ struct NoPre {
 // `pre` runs (on every wave) after the current tile is staged and before the first
 // reference's window is read: p_run_kernel waits there for the reference's tiles, so the
 // current-tile staging overlaps that wait.
-template <class G, class Pre = NoPre>
+// ---- VBSEnable: exact SEA for a block and its four 8x8 sub-blocks (sea_vbs_block) ----------
+// The block search of find_best_match plus the sub-block searches of inter_prediction
+// (Encoder.py:512-544: find_best_match of each 8x8 sub-block over its own +-16 window), for a
+// block with x != 0, y != 0 away from the right / bottom frame edge (x, y <= W - 48, H - 48):
+// there every one of the 1089 candidates is valid for the block AND for each sub-block (the
+// sub-blocks' larger valid ranges only differ within 32 px of those edges; such blocks take the
+// dense search), so all five minima run over the same candidate set.
+//   1. One pass over the 4x4 byte sums gives, per candidate, the four sub-block bounds packed
+//      in two dwords (TL | TR << 16, BL | BR << 16: v_sad_u8 / v_sad_hi_u8 on the cell-sum
+//      dwords masked to the sub-block's two cells); the block bound is their sum.
+//      SAD_j >= 16 sum_j |dq| - 60, SAD >= 16 sum |dq| - 240 (q = 4x4 sum >> 4).
+//   2. A: U = the SAD of the smallest-bound candidate; every candidate with block bound <= U
+//      is evaluated exactly (four lanes per candidate), giving the block minimum and, from the
+//      same SADs split by quadrant, U_j = the smallest sub-block SAD seen.
+//   3. B: every remaining candidate with some sub-block bound <= U_j is evaluated exactly.
+// Any other candidate has SAD > U >= min (block) and SAD_j > U_j >= min_j for every j, so the
+// five lexicographic minima (SAD, |dx|+|dy|, ref, scan) are exactly the full searches'.  More
+// than CAP survivors in A or B: returns false and the caller runs the dense search.
+template <class G>
+SO_DEV void vbs_eval_list(const Sea2Lds& L, const uint16_t* list, uint32_t n, int cs, int bxl, int byl, int lane,
+                          uint64_t& bestB, uint64_t& best0, uint64_t& best1) {
+    constexpr int RP = G::RP, CPD = G::CPD;
+    const int sidx = lane >> 2, q = lane & 3;
+    const int crow0 = byl * 16 * CPD + bxl * 4;
+    uint32_t cr[4][4];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cr[rr][k] = L.curt[crow0 + (4 * q + rr) * CPD + k];
+#pragma unroll 1
+    for (uint32_t s0 = 0; s0 < n; s0 += 16) {
+        const bool act = s0 + (uint32_t)sidx < n;
+        const int cand = act ? (int)list[s0 + sidx] : cs;
+        const int dxi = cand / 33, di = cand - dxi * 33;
+        const int col = bxl * 16 + dxi;
+        const uint32_t sh = (uint32_t)(col & 3);
+        int wo = (byl * 16 + di + 4 * q) * RP + (col >> 2);
+        asm volatile("" : "+v"(wo));
+        uint32_t sl = 0, srr = 0;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            lds_vu32p p = (lds_vu32p)(L.win + wo + rr * RP);
+            const uint32_t q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4];
+            sl = __builtin_amdgcn_sad_u8(cr[rr][0], __builtin_amdgcn_alignbyte(q1, q0, sh), sl);
+            sl = __builtin_amdgcn_sad_u8(cr[rr][1], __builtin_amdgcn_alignbyte(q2, q1, sh), sl);
+            srr = __builtin_amdgcn_sad_u8(cr[rr][2], __builtin_amdgcn_alignbyte(q3, q2, sh), srr);
+            srr = __builtin_amdgcn_sad_u8(cr[rr][3], __builtin_amdgcn_alignbyte(q4, q3, sh), srr);
+        }
+        // quad lanes q = 0, 1 hold rows 0-7 (top sub-blocks), 2, 3 rows 8-15: pair them up
+        uint32_t v = sl | (srr << 16);
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppQuad1032, 0xF, 0xF, false);   // (L | R << 16) of the half
+        uint32_t hb = __builtin_amdgcn_sad_u16(v, 0u, 0u);                                       // the half's SAD
+        hb += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hb, kDppQuad2301, 0xF, 0xF, false);  // the block's
+        const int dx = dxi - 16, dy = di - 16;
+        const uint64_t tail = ((uint64_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)) << 24) | (uint64_t)cand;
+        const uint64_t kb = ((uint64_t)hb << 32) | tail;
+        const uint64_t k0 = ((uint64_t)(v & 0xFFFFu) << 32) | tail, k1 = ((uint64_t)(v >> 16) << 32) | tail;
+        bestB = (act && kb < bestB) ? kb : bestB;
+        best0 = (act && k0 < best0) ? k0 : best0;
+        best1 = (act && k1 < best1) ? k1 : best1;
+    }
+}
+
+template <class G>
+SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
+    constexpr int NT = G::NT, B4P = G::B4P, CAP = G::CAP, RP = G::RP, CPD = G::CPD;
+    int lane = tid & 63;
+    asm volatile("" : "+v"(lane));
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int xi = lane & 31, hh = lane >> 5;
+    const int d2 = lane < 33 ? lane : 32;
+    uint32_t AL[4], AR[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t a = L.a4[u * 4 + j];
+        AL[j] = a & 0xFFFFu;
+        AR[j] = a & 0xFFFF0000u;
+    }
+    // ---- 1. packed sub-block bounds ----------------------------------------------------------
+    const int cB = bxl * 16 + xi;
+    const int lb0 = (byl * 16 + 16 * hh) * B4P + (cB & 3) * G::WD + (cB >> 2);   // byte offset
+    const uint32_t bsh = (uint32_t)lb0 & 3;
+    int lo1 = lb0 >> 2;
+    asm volatile("" : "+v"(lo1));
+    lds_vu32p p1 = (lds_vu32p)(L.b4w + lo1);
+    uint32_t T[NT], Bt[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) { T[t] = 0; Bt[t] = 0; }
+    constexpr int PD = 2;
+    uint32_t n0[PD], n1[PD];
+#pragma unroll
+    for (int k = 0; k < PD; ++k) { n0[k] = p1[k * (B4P / 4)]; n1[k] = p1[k * (B4P / 4) + 1]; }
+#pragma unroll
+    for (int sr_ = 0; sr_ < NT + 12; ++sr_) {
+        const uint32_t w0 = n0[sr_ % PD], w1 = n1[sr_ % PD];
+        if (sr_ + PD < NT + 12) {
+            n0[sr_ % PD] = p1[(sr_ + PD) * (B4P / 4)];
+            n1[sr_ % PD] = p1[(sr_ + PD) * (B4P / 4) + 1];
+        }
+        const uint32_t P = __builtin_amdgcn_alignbyte(w1, w0, bsh);
+        const uint32_t PL = P & 0xFFFFu, PR = P & 0xFFFF0000u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int t = sr_ - 4 * j;
+            if (t >= 0 && t < NT) {
+                uint32_t& acc = j < 2 ? T[t] : Bt[t];
+                acc = __builtin_amdgcn_sad_hi_u8(AR[j], PR, __builtin_amdgcn_sad_u8(AL[j], PL, acc));
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+            if (t <= sr_) asm volatile("" : "+v"(T[t]), "+v"(Bt[t]) : : "memory");
+    }
+    uint32_t l2T = 0, l2B = 0;   // the dx = +16 column (lanes < 33: dy index d2)
+    {
+        int lo2 = ((byl * 16 + d2) * B4P + ((bxl * 16 + 32) >> 2)) >> 2;
+        asm volatile("" : "+v"(lo2));
+        lds_vu32p p2 = (lds_vu32p)(L.b4w + lo2);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t qv = p2[4 * j * (B4P / 4)];
+            uint32_t& acc = j < 2 ? l2T : l2B;
+            acc = __builtin_amdgcn_sad_hi_u8(AR[j], qv & 0xFFFF0000u, __builtin_amdgcn_sad_u8(AL[j], qv & 0xFFFFu, acc));
+        }
+    }
+    // block bound keys (LBq << 16) | t: the four sub-block bounds summed
+    uint32_t lb[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+        lb[t] = (__builtin_amdgcn_sad_u16(T[t], 0u, __builtin_amdgcn_sad_u16(Bt[t], 0u, 0u)) << 16) | (uint32_t)t;
+    const uint32_t lb2 = __builtin_amdgcn_sad_u16(l2T, 0u, __builtin_amdgcn_sad_u16(l2B, 0u, 0u));
+    const bool ok2 = lane < 33;
+    // ---- 2. U and the block survivors (A) -------------------------------------------------------
+    uint32_t kt = lb[0];
+#pragma unroll
+    for (int t = 1; t < NT; ++t) kt = lb[t] < kt ? lb[t] : kt;
+    uint32_t kl = ((kt >> 16) << 11) | (uint32_t)(xi * 33 + 16 * hh + (kt & 31));
+    {
+        const uint32_t k2 = (lb2 << 11) | (uint32_t)(32 * 33 + d2);
+        kl = (ok2 && k2 < kl) ? k2 : kl;
+    }
+    const uint32_t kmin = wave_min_u32(kl);
+    const int cs = (int)(kmin & 2047), cdx = cs / 33, cdi = cs - cdx * 33;
+    const int crow0 = byl * 16 * CPD + bxl * 4;
+    uint32_t U;
+    {
+        const int row = lane >> 2, kk = lane & 3;
+        const uint32_t w = win_u32<RP>(L.win, byl * 16 + cdi + row, bxl * 16 + cdx + 4 * kk);
+        U = wave_sum_u32(__builtin_amdgcn_sad_u8(L.curt[crow0 + row * CPD + kk], w, 0u));
+    }
+    const uint32_t qU = (U + 240) >> 4;
+    int thr = (int)((qU << 16) | 0xFFFFu);
+    asm volatile("" : "+v"(thr));
+    uint16_t* const mylist = L.list + wave * CAP;
+    const int cbase = xi * 33 + 16 * hh;
+    uint32_t nA = 0;
+#pragma unroll
+    for (int t = 0; t <= NT; ++t) {
+        const bool pass = t < NT ? (int)lb[t] <= thr : (ok2 && lb2 <= qU);
+        const uint64_t bal = __builtin_amdgcn_ballot_w64(pass);
+        if (bal) {
+            const uint32_t pos = nA + lane_prefix(bal);
+            if (pass && pos < (uint32_t)CAP) mylist[pos] = (uint16_t)(t < NT ? cbase + t : 32 * 33 + d2);
+            nA += (uint32_t)__builtin_popcountll(bal);
+        }
+    }
+    if (nA > (uint32_t)CAP) return false;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint64_t bestB = kNoKey, best0 = kNoKey, best1 = kNoKey;
+    vbs_eval_list<G>(L, mylist, nA, cs, bxl, byl, lane, bestB, best0, best1);
+    // U_j: the smallest sub-block SADs among the evaluated candidates (quad lanes 0, 1: top)
+    const bool top = (lane & 2) == 0;
+    const uint32_t uTL = wave_min_u32(top ? (uint32_t)(best0 >> 32) : ~0u);
+    const uint32_t uTR = wave_min_u32(top ? (uint32_t)(best1 >> 32) : ~0u);
+    const uint32_t uBL = wave_min_u32(top ? ~0u : (uint32_t)(best0 >> 32));
+    const uint32_t uBR = wave_min_u32(top ? ~0u : (uint32_t)(best1 >> 32));
+    // ---- 3. the sub-block survivors (B): some sub-block bound <= its U_j, not evaluated in A ----
+    typedef short so_v2i16 __attribute__((ext_vector_type(2)));
+    const uint32_t thT = (((uTL + 60) >> 4) + 1) | ((((uTR + 60) >> 4) + 1) << 16);
+    const uint32_t thB = (((uBL + 60) >> 4) + 1) | ((((uBR + 60) >> 4) + 1) << 16);
+    const auto any_sub = [&](uint32_t tv, uint32_t bv) {   // a 16-bit half of (bound - (thr + 1)) < 0
+        const so_v2i16 dt = __builtin_bit_cast(so_v2i16, tv) - __builtin_bit_cast(so_v2i16, thT);
+        const so_v2i16 db = __builtin_bit_cast(so_v2i16, bv) - __builtin_bit_cast(so_v2i16, thB);
+        return ((__builtin_bit_cast(uint32_t, dt) | __builtin_bit_cast(uint32_t, db)) & 0x80008000u) != 0u;
+    };
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // list A read before it is overwritten
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t nB = 0;
+#pragma unroll
+    for (int t = 0; t <= NT; ++t) {
+        const bool pass = t < NT ? (any_sub(T[t], Bt[t]) && !((int)lb[t] <= thr))
+                                 : (ok2 && any_sub(l2T, l2B) && !(lb2 <= qU));
+        const uint64_t bal = __builtin_amdgcn_ballot_w64(pass);
+        if (bal) {
+            const uint32_t pos = nB + lane_prefix(bal);
+            if (pass && pos < (uint32_t)CAP) mylist[pos] = (uint16_t)(t < NT ? cbase + t : 32 * 33 + d2);
+            nB += (uint32_t)__builtin_popcountll(bal);
+        }
+    }
+    if (nB > (uint32_t)CAP) return false;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    vbs_eval_list<G>(L, mylist, nB, cs, bxl, byl, lane, bestB, best0, best1);
+    const uint64_t kb = wave_min_u64_dpp(bestB);
+    const uint64_t kTL = wave_min_u64_dpp(top ? best0 : kNoKey), kTR = wave_min_u64_dpp(top ? best1 : kNoKey);
+    const uint64_t kBL = wave_min_u64_dpp(top ? kNoKey : best0), kBR = wave_min_u64_dpp(top ? kNoKey : best1);
+    if (lane == 0) {
+        unsigned long long* const ks = L.keys;
+        if (kb < ks[u]) ks[u] = kb;
+        unsigned long long* const sk = ks + G::NBLK + 4 * u;
+        if (kTL < sk[0]) sk[0] = kTL;
+        if (kTR < sk[1]) sk[1] = kTR;
+        if (kBL < sk[2]) sk[2] = kBL;
+        if (kBR < sk[3]) sk[3] = kBR;
+    }
+    return true;
+}
+
+// VBS: blocks with a sub-block search (x != 0 and y != 0, Encoder.py:512) take sea_vbs_block
+// (the block and its four 8x8 sub-blocks, keys [NBLK + 4u + j]) or, within 32 px of the right /
+// bottom edge or past CAP survivors, the dense wave search, whose v_sad_u8 work yields the
+// sub-block SADs with the block's; the other blocks the block's exact SEA.
+template <class G, class Pre = NoPre, bool VBS = false>
 SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cur, const RefSet& refs, int nref,
                       int H, int W, int by0, int by1, int probe, const Pre& pre = Pre()) {
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RP = G::RP, NT = G::NT;
@@ -712,7 +938,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
     SO_SEA_STAMP(1, __builtin_amdgcn_s_memtime());
 #endif
 
-    for (int i = tid; i < G::NBLK; i += G::NTHREADS) keys[i] = kNoKey;
+    for (int i = tid; i < G::NBLK * (VBS ? 5 : 1); i += G::NTHREADS) keys[i] = kNoKey;
     // interior window (uniform): thread = (row, column phase) with immediate per-dword offsets
     constexpr int WTPR = G::NTHREADS / G::WR, WNPT = (RP + WTPR - 1) / WTPR;
     static_assert(G::NTHREADS % G::WR == 0, "window staging");
@@ -836,6 +1062,19 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             const int bxl = u % TBX, byl = u / TBX;
             if (bx0 + bxl >= nbx || byt0 + byl >= by1) continue;   // wave-uniform
             const int x = x0 + bxl * 16, y = y0 + byl * 16;
+            if constexpr (VBS) {
+                if (x != 0 && y != 0) {   // uniform: block + sub-block search
+#ifndef SO_VBS_DENSE_ONLY   // A/B builds: every sub-searched block dense
+                    if (x + 48 <= W && y + 48 <= H && sea_vbs_block<G>(L, u, bxl, byl, tid)) continue;
+#endif
+                    if ((tid & 63) == 0) atomicAdd(&st_fb, 1u);   // counted as a dense fallback
+#ifndef SO_TEST_NODENSE
+                    wave_dense_block<16, true, RP, 0, false, true>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u,
+                                                                   tid, r);
+#endif
+                    continue;
+                }
+            }
             int lane = tid & 63;
             asm volatile("" : "+v"(lane));
             const int xi = lane & 31, hh = lane >> 5;
@@ -1107,6 +1346,15 @@ struct PTileGeo {
     static constexpr int TQD = G::NBLK * kTqScratch;                  // doubles
     static constexpr int U64 = ((B4 + LIST + 1) / 2 > TQD) ? (B4 + LIST + 1) / 2 : TQD;
 };
+// VBSEnable (tq16_vbs): 16 x 18 doubles per block (the 16 x 17 transpose of the block, or the
+// four 8 x 9 of its sub-blocks) + 256 bytes of sub-block token flags
+constexpr int kTqScratchVbs = 288;
+template <class G>
+struct PTileGeoVbs {
+    static constexpr int TQD = G::NBLK * kTqScratchVbs + G::NBLK * 256 / 8;
+    static constexpr int U64 = ((PTileGeo<G>::B4 + PTileGeo<G>::LIST + 1) / 2 > TQD)
+                                   ? (PTileGeo<G>::B4 + PTileGeo<G>::LIST + 1) / 2 : TQD;
+};
 
 // 16 bytes of window row `row` from byte column `col`, as 4 dwords (5 aligned ds_read_b32
 // + v_alignbyte: misaligned wide DS reads are replayed on gfx950)
@@ -1124,17 +1372,19 @@ SO_DEV void win_row16(const uint32_t* win, int row, int col, uint32_t (&w)[4]) {
 typedef uint32_t so_v4u __attribute__((ext_vector_type(4)));
 
 // The LDS of one fused tile.
-template <class G>
+// VBS: keys / mer hold the 16 blocks' records, then the 4 sub-blocks of each (NBLK + 4 g + j).
+template <class G, bool VBS = false>
 struct PTileLds {
+    static constexpr int NU = G::NBLK * (VBS ? 5 : 1);
     uint32_t win[G::WR * G::RP + 4];
     uint32_t curt[G::TPY * G::CPD];
     uint32_t a4[G::NBLK * 4];
     uint32_t lcount[G::NW];
-    unsigned long long keys[G::NBLK];
+    unsigned long long keys[NU];
     uint32_t st[2];
-    int32_t mer[G::NBLK][4];               // decoded ME records (dx, dy, ref, sad)
+    int32_t mer[NU][4];                    // decoded ME records (dx, dy, ref, sad)
     int32_t msum[G::TBY];                  // two-pass runs: pass-1 token sum of each block row
-    double un[PTileGeo<G>::U64];           // byte sums + survivor lists | FP64 transposes
+    double un[VBS ? PTileGeoVbs<G>::U64 : PTileGeo<G>::U64];   // byte sums + survivor lists | FP64 transposes
 };
 
 // Boundary rows of a rank's stripe that the neighbouring ranks read (so_encode_p_run_stripe):
@@ -1252,15 +1502,286 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
     }
 }
 
+// 8 bytes of window row `row` from byte column `col`, as 2 dwords (3 aligned ds_read_b32 +
+// v_alignbyte)
+template <int RP>
+SO_DEV void win_row8(const uint32_t* win, int row, int col, uint32_t (&w)[2]) {
+    lds_vu32p p = (lds_vu32p)(win + row * RP + (col >> 2));
+    const uint32_t sh = (uint32_t)(col & 3);
+    const uint32_t q0 = p[0], q1 = p[1], q2 = p[2];
+    w[0] = __builtin_amdgcn_alignbyte(q1, q0, sh);
+    w[1] = __builtin_amdgcn_alignbyte(q2, q1, sh);
+}
+
+// One 16-byte (or 8-byte) reconstruction row: local store write-through (sc1) and, for the
+// multi-GPU hand-off, the same bytes into a neighbour's landing plane (system scope).
+template <bool SC1, bool HALO>
+SO_DEV void store_rec_row(const PFrameOut& o, const PHalo& hl, int W, int x, int yy, const int* rec, int n) {
+    uint8_t* rp = o.recon + (size_t)yy * W + x;
+    if (n == 16) {
+        so_v4u v;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            v[k] = (uint32_t)(rec[4 * k] & 255) | ((uint32_t)(rec[4 * k + 1] & 255) << 8) |
+                   ((uint32_t)(rec[4 * k + 2] & 255) << 16) | ((uint32_t)(rec[4 * k + 3] & 255) << 24);
+        if constexpr (SC1) {
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(rp), "v"(v) : "memory");
+            if constexpr (HALO) {
+                if (hl.up && yy < hl.up_end) {
+                    uint8_t* q = hl.up + (size_t)yy * W + x;
+                    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(q), "v"(v) : "memory");
+                }
+                if (hl.dn && yy >= hl.dn_begin) {
+                    uint8_t* q = hl.dn + (size_t)yy * W + x;
+                    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(q), "v"(v) : "memory");
+                }
+            }
+        } else {
+            *reinterpret_cast<so_v4u*>(rp) = v;
+        }
+    } else {
+        typedef uint32_t so_v2u __attribute__((ext_vector_type(2)));
+        so_v2u v;
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            v[k] = (uint32_t)(rec[4 * k] & 255) | ((uint32_t)(rec[4 * k + 1] & 255) << 8) |
+                   ((uint32_t)(rec[4 * k + 2] & 255) << 16) | ((uint32_t)(rec[4 * k + 3] & 255) << 24);
+        if constexpr (SC1) {
+            asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(rp), "v"(v) : "memory");
+            if constexpr (HALO) {
+                if (hl.up && yy < hl.up_end) {
+                    uint8_t* q = hl.up + (size_t)yy * W + x;
+                    asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(q), "v"(v) : "memory");
+                }
+                if (hl.dn && yy >= hl.dn_begin) {
+                    uint8_t* q = hl.dn + (size_t)yy * W + x;
+                    asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(q), "v"(v) : "memory");
+                }
+            }
+        } else {
+            *reinterpret_cast<so_v2u*>(rp) = v;
+        }
+    }
+}
+
+// The VBSEnable transform path of one block inside the fused tile: the arithmetic of
+// inter_tq_kernel<16, true, false> (so_tq.hip) -- DCT of the block at the RD QP, the four 8x8
+// sub-blocks at max(QP - 1, 0) when x != 0 and y != 0, calculate_RD_cost of both and the
+// split decision !(cost_bs < cost_vbs) (Encoder.py:512-578, :1133-1158), then the chosen
+// path's requantisation at the block's final QP, IDCT and reconstruction -- with every pixel
+// read from the LDS tile (current rows) and window (predictions: block and sub-block MVs lie
+// inside the window's +-16 px, zero outside the frame as handle_boundary_conditions).
+// 16 lanes (l = row); `scratch` 288 doubles, `flags` 256 bytes of LDS owned by the lanes.
+// int16 pairs: the transform coefficients and quantised levels (|v| <= 4080) that must survive
+// the RD decision live packed, two per VGPR (the VBS tile kernel is register-bound)
+template <int N>
+SO_DEV void pack_i16(const int* v, uint32_t* p) {
+#pragma unroll
+    for (int k = 0; k < N / 2; ++k) p[k] = ((uint32_t)v[2 * k] & 0xFFFFu) | ((uint32_t)v[2 * k + 1] << 16);
+}
+template <int N>
+SO_DEV void unpack_i16(const uint32_t* p, int* v) {
+#pragma unroll
+    for (int k = 0; k < N / 2; ++k) {
+        v[2 * k] = (int)(int16_t)(p[k] & 0xFFFFu);
+        v[2 * k + 1] = (int)p[k] >> 16;
+    }
+}
+
+template <class G, bool SC1, bool HALO = false>
+SO_DEV void tq16_vbs(PTileLds<G, true>& S, int g, int l, double* scratch, uint8_t* flags, int bx0, int byt0, int nbx,
+                     int by0, int by1, int W, int qp_rd, const int32_t* __restrict__ qp_row,
+                     const int32_t* __restrict__ qp_map, double lam, const PFrameOut& o, const PHalo& hl = PHalo{}) {
+    constexpr int SR = G::SR, TBX = G::TBX;
+    const int bxl = g % TBX, byl = g / TBX;
+    const int gbx = bx0 + bxl, gby = byt0 + byl;
+    if (gbx >= nbx || gby >= by1) return;   // uniform over the block's 16 lanes
+    const size_t b = (size_t)(gby - by0) * nbx + gbx;
+    const int x = gbx * 16, y = gby * 16;
+    const int qpr = qp_map ? qp_map[(size_t)gby * nbx + gbx] : (qp_row ? qp_row[gby] : qp_rd);
+    const int dx = S.mer[g][0], dy = S.mer[g][1], rf = S.mer[g][2], sad = S.mer[g][3];
+    const int prow = byl * 16 + SR + dy + l, pcol = bxl * 16 + SR + dx;   // window coordinates
+    const uint32_t* crow = S.curt + (byl * 16 + l) * G::CPD + bxl * 4;
+    uint32_t tcp[8], qp8[8];   // the block's coefficients and its levels at the RD QP, packed
+    int tok_b = 0;
+    {
+        int res[16];
+        uint32_t pw[4];
+        win_row16<G::RP>(S.win, prow, pcol, pw);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t cw = crow[k];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) res[4 * k + e] = (int)((cw >> (8 * e)) & 255) - (int)((pw[k] >> (8 * e)) & 255);
+        }
+        double tcr[16];
+        xform2d_rows<16, false>(scratch, l, res, tcr);
+        int tc[16], q[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) tc[c] = (int)__builtin_rint(tcr[c]);
+        quant_row_i<16>(tc, l, qp_rd, q);
+        if (x != 0 && y != 0) tok_b = block_tokens<16>(nullptr, l, q);   // uniform
+        pack_i16<16>(tc, tcp);
+        pack_i16<16>(q, qp8);
+    }
+    bool split = false;
+    int mae_num = sad;
+    const int j = l >> 2, r0 = l & 3;
+    int sdx = 0, sdy = 0, sref = 0;
+    uint32_t stcp[8], qsp[8];   // the sub-blocks' coefficients and levels at max(QP_rd - 1, 0), packed
+    const int sxl = bxl * 16 + (j & 1) * 8, syl = byl * 16 + (j >> 1) * 8;   // sub-block in the tile (px)
+    const int qpm1_rd = qp_rd > 0 ? qp_rd - 1 : qp_rd;
+    if (x != 0 && y != 0) {   // uniform
+        const int32_t* sm = S.mer[G::NBLK + 4 * g + j];
+        sdx = sm[0]; sdy = sm[1]; sref = sm[2];
+        int sres[2][8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int row = r0 + 4 * h;
+            uint32_t pw[2];
+            win_row8<G::RP>(S.win, syl + SR + sdy + row, sxl + SR + sdx, pw);
+            const uint32_t* cr = S.curt + (syl + row) * G::CPD + (sxl >> 2);
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t cw = cr[k];
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    sres[h][4 * k + e] = (int)((cw >> (8 * e)) & 255) - (int)((pw[k] >> (8 * e)) & 255);
+            }
+        }
+        double std_[2][8];
+        xform2d_sub<false>(scratch, l, sres, std_);
+        int stc[2][8], qs[2][8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) stc[h][c] = (int)__builtin_rint(std_[h][c]);
+            quant_row_i<8>(stc[h], r0 + 4 * h, qpm1_rd, qs[h]);
+        }
+        const int tok_v = sub_tokens(flags, l, qs);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            pack_i16<8>(stc[h], stcp + 4 * h);
+            pack_i16<8>(qs[h], qsp + 4 * h);
+        }
+        int ssum = 0;
+        bool vinf = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int sk = S.mer[G::NBLK + 4 * g + k][3];
+            vinf |= sk < 0;
+            ssum += sk;
+        }
+        const double mae_b = sad < 0 ? __builtin_inf() : (double)sad / 256.0;
+        const double mae_v = vinf ? __builtin_inf() : (double)ssum / 256.0;
+        const double c_v = rd_cost(lam, 64 + 8 * tok_v, mae_v);
+        const double c_b = rd_cost(lam, 16 + 8 * tok_b, mae_b);
+        split = !(c_b < c_v);
+        mae_num = vinf ? -1 : ssum;
+    }
+    int tok, sse = 0;
+    if (!split) {
+        int q[16];
+        if (qpr != qp_rd) {
+            int tc[16];
+            unpack_i16<16>(tcp, tc);
+            quant_row_i<16>(tc, l, qpr, q);
+        } else {
+            unpack_i16<16>(qp8, q);
+        }
+        tok = block_tokens<16>(nullptr, l, q);
+        store_row_i16<16>(o.qtc + b * 256 + l * 16, q);
+        double dq[16], rd[16];
+        dequant_row_i<16>(q, l, qpr, dq);
+        xform2d_rows<16, true>(scratch, l, dq, rd);
+        int rec[16];
+        {
+            uint32_t pw[4];
+            win_row16<G::RP>(S.win, prow, pcol, pw);
+#pragma unroll
+            for (int c = 0; c < 16; ++c)
+                rec[c] = (int)((pw[c >> 2] >> (8 * (c & 3))) & 255) + (int)__builtin_rint(rd[c]);
+        }
+        store_rec_row<SC1, HALO>(o, hl, W, x, y + l, rec, 16);
+        if (o.sse) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t cw = crow[k];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int d = (int)((cw >> (8 * e)) & 255) - (rec[4 * k + e] & 255);
+                    sse += d * d;
+                }
+            }
+        }
+        if (l < 12) o.mv[b * 12 + l] = (int16_t)(l == 0 ? dx : l == 1 ? dy : l == 2 ? rf : 0);
+    } else {
+        const int qpm1 = qpr > 0 ? qpr - 1 : qpr;
+        int qs[2][8];
+        if (qpm1 != qpm1_rd) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                int stc[8];
+                unpack_i16<8>(stcp + 4 * h, stc);
+                quant_row_i<8>(stc, r0 + 4 * h, qpm1, qs[h]);
+            }
+        } else {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) unpack_i16<8>(qsp + 4 * h, qs[h]);
+        }
+        tok = sub_tokens(flags, l, qs);
+        double sdq[2][8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            store_row_i16<8>(o.qtc + b * 256 + j * 64 + (r0 + 4 * h) * 8, qs[h]);
+            dequant_row_i<8>(qs[h], r0 + 4 * h, qpm1, sdq[h]);
+        }
+        double srd[2][8];
+        xform2d_sub<true>(scratch, l, sdq, srd);
+        const int xs = x + (j & 1) * 8, ys = y + (j >> 1) * 8;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int row = r0 + 4 * h;
+            uint32_t pw[2];
+            win_row8<G::RP>(S.win, syl + SR + sdy + row, sxl + SR + sdx, pw);
+            int rec[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                rec[c] = (int)((pw[c >> 2] >> (8 * (c & 3))) & 255) + (int)__builtin_rint(srd[h][c]);
+            store_rec_row<SC1, HALO>(o, hl, W, xs, ys + row, rec, 8);
+            if (o.sse) {
+                const uint32_t* cr = S.curt + (syl + row) * G::CPD + (sxl >> 2);
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const uint32_t cw = cr[k];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int d = (int)((cw >> (8 * e)) & 255) - (rec[4 * k + e] & 255);
+                        sse += d * d;
+                    }
+                }
+            }
+        }
+        if (r0 < 3) o.mv[b * 12 + 3 * j + r0] = (int16_t)(r0 == 0 ? sdx : r0 == 1 ? sdy : sref);
+    }
+    if (o.sse) sse = group_sum<16>(sse);
+    if (l == 0) {
+        o.split[b] = (uint8_t)split;
+        o.tokens[b] = tok;
+        o.mae[b] = mae_num;
+        if (o.sse) o.sse[b] = sse;
+    }
+}
+
 // Search + transforms of tile `tile` of one frame.  SC1: the reconstruction rows are stored
 // write-through (global_store sc1), so another XCD that later reads them (p_run_kernel's
 // next frame) gets them from memory without a release fence.  Ends with every wave's
 // stores retired (s_waitcnt vmcnt(0)) and a workgroup barrier.  `pre`: as sea2_tile's.
-template <class G, bool SC1, class Pre = NoPre, bool HALO = false, bool TOK = false>
-SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur, const uint8_t* ref, int H, int W,
+template <class G, bool SC1, class Pre = NoPre, bool HALO = false, bool TOK = false, bool VBS = false>
+SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict__ cur, const uint8_t* ref, int H, int W,
                        int by0, int by1, int qp_rd, const int32_t* __restrict__ qp_row,
                        const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best, const PFrameOut& o,
-                       const Pre& pre = Pre(), const PHalo& hl = PHalo{}) {
+                       const Pre& pre = Pre(), const PHalo& hl = PHalo{}, double lam = 0.0) {
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY;
     using P = PTileGeo<G>;
     uint32_t* const b4w = reinterpret_cast<uint32_t*>(S.un);
@@ -1271,17 +1792,17 @@ SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur
 #ifndef SO_PROF_PHASE   // phase-attribution A/B builds only (tools/prun_phase.py): 1 = no transforms
 #define SO_PROF_PHASE 0  // (the tile's current rows stored as its reconstruction), 2 = no search
 #endif                   // (window staged, every block at mv (0, 0))
-    sea2_tile<G>(L, tile, cur, refs, 1, H, W, by0, by1, SO_PROF_PHASE == 2 ? 5 : 0, pre);   // ends with a barrier
+    sea2_tile<G, Pre, VBS>(L, tile, cur, refs, 1, H, W, by0, by1, SO_PROF_PHASE == 2 ? 5 : 0, pre);   // ends with a barrier
 
     const int tid = opaque_tid();
     SO_SEA_STAMP(5, __builtin_amdgcn_s_memtime());
     const int nbx = W / 16;
     const int tiles_x = (nbx + TBX - 1) / TBX;
     const int bx0 = (tile % tiles_x) * TBX, byt0 = by0 + (tile / tiles_x) * TBY;
-    for (int i = tid; i < G::NBLK; i += G::NTHREADS) {
+    for (int i = tid; i < PTileLds<G, VBS>::NU; i += G::NTHREADS) {
         decode_key(S.keys[i], SR, S.mer[i]);
         const int gbx = bx0 + i % TBX, gby = byt0 + i / TBX;
-        if (out_best && gbx < nbx && gby < by1) {
+        if (out_best && i < G::NBLK && gbx < nbx && gby < by1) {
             int32_t* ob = out_best + ((size_t)(gby - by0) * nbx + gbx) * 4;
             ob[0] = S.mer[i][0]; ob[1] = S.mer[i][1]; ob[2] = S.mer[i][2]; ob[3] = S.mer[i][3];
         }
@@ -1304,9 +1825,15 @@ SO_DEV void ptile_body(PTileLds<G>& S, int tile, const uint8_t* __restrict__ cur
                 for (int k = 0; k < 4; ++k) v[k] = crow[k];
                 *reinterpret_cast<so_v4u*>(o.recon + (size_t)(gby * 16 + l) * W + gbx * 16) = v;
             }
-        } else if (ln < 16 * G::TQ_BPW && gq < G::NBLK)
-            tq16_exact<G, SC1, HALO, TOK>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by0, by1, W, qp_rd, qp_row,
-                                     qp_map, o, hl);
+        } else if (ln < 16 * G::TQ_BPW && gq < G::NBLK) {
+            if constexpr (VBS)
+                tq16_vbs<G, SC1, HALO>(S, gq, ln & 15, S.un + gq * kTqScratchVbs,
+                                       reinterpret_cast<uint8_t*>(S.un + G::NBLK * kTqScratchVbs) + gq * 256, bx0,
+                                       byt0, nbx, by0, by1, W, qp_rd, qp_row, qp_map, lam, o, hl);
+            else
+                tq16_exact<G, SC1, HALO, TOK>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by0, by1, W, qp_rd,
+                                              qp_row, qp_map, o, hl);
+        }
     }
     SO_SEA_STAMP(7, __builtin_amdgcn_s_memtime());
     if constexpr (SC1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
@@ -1584,18 +2111,21 @@ constexpr int kRunSingle = 0, kRunStripe = 1, kRunFPipe = 2, kRunTwoPass = 3, kR
 #define SO_RUN_PROF(word, cyc) do { } while (0)
 #endif
 
-template <int NW, int MODE>
-__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE)))
+// VBS: VBSEnable (the block + sub-block dense search, tq16_vbs; ~128 VGPRs, 4 waves per SIMD)
+template <int NW, int MODE, bool VBS = false>
+__global__ void __launch_bounds__(NW * 64)
+__attribute__((amdgpu_waves_per_eu(VBS ? 4 : (NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE))))
 p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, int H, int W,
              int qp_rd, const int32_t* __restrict__ qp_row, uint32_t* __restrict__ ws, int ws_stamp_base,
-             const PRunStripe sp) {
+             const PRunStripe sp, double lam) {
     using G = Sea2GeoT<NW>;
-    __shared__ PTileLds<G> S;
+    __shared__ PTileLds<G, VBS> S;
     __shared__ int s_task;
     const int tid = threadIdx.x;
     const int nbx = W / 16;
     constexpr bool STRIPE = MODE == kRunStripe, FPIPE = MODE == kRunFPipe || MODE == kRunFPipe2P;
     constexpr bool TWOP = MODE == kRunTwoPass || MODE == kRunFPipe2P;
+    static_assert(!(VBS && (TWOP || MODE == kRunStripe)), "VBS runs: one GPU and the frame pipeline");
     const int by0 = STRIPE ? sp.by0 : 0, by1 = STRIPE ? sp.by1 : H / 16;
     const int tiles_x = (nbx + G::TBX - 1) / G::TBX, ntr = (by1 - by0 + G::TBY - 1) / G::TBY;
     const int ntiles = tiles_x * ntr;
@@ -1823,8 +2353,9 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             PHalo hl{};
             hl.dn = code >= 0 ? pbase + (long long)slot * sp.stride : nullptr;   // every row of the tile
             hl.dn_begin = 0;
-            ptile_body<G, true, decltype(wait_ref), true>(S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd, qp_row,
-                                                          nullptr, nullptr, a.out[f], wait_ref, hl);
+            ptile_body<G, true, decltype(wait_ref), true, false, VBS>(S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd,
+                                                                      qp_row, nullptr, nullptr, a.out[f], wait_ref, hl,
+                                                                      lam);
             // ptile_body ended with every wave's stores (local and remote) retired and a barrier
             if (wave == 0) {
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
@@ -1861,8 +2392,9 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 #ifdef SO_RUN_PROFILE
             const unsigned long long pt0 = __builtin_amdgcn_s_memtime();
 #endif
-            ptile_body<G, true>(S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd, qp_row, nullptr, nullptr, a.out[f],
-                                wait_ref);
+            ptile_body<G, true, decltype(wait_ref), false, false, VBS>(S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd,
+                                                                       qp_row, nullptr, nullptr, a.out[f], wait_ref,
+                                                                       PHalo{}, lam);
             SO_RUN_PROF(52, __builtin_amdgcn_s_memtime() - pt0);
             // ptile_body ended with every wave's write-through stores retired and a barrier
             if (wave == 0)
@@ -1919,16 +2451,16 @@ static void device_shape(int* ncu) {
 // refs / deps (may be null: one run, frame g predicting from g - 1 and frame 0 from ref0): frame g
 // predicts from outs[deps[g]].recon when deps[g] >= 0 (0 <= deps[g] < g), else from refs[g].
 // conc: independent runs interleaved in the list (their tiles are in flight together).
-template <int MODE>
+template <int MODE, bool VBS = false>
 static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                           const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp0,
                           int max_wg, hipStream_t st, const uint8_t* const* refs = nullptr,
-                          const int* deps = nullptr, int conc = 1) {
+                          const int* deps = nullptr, int conc = 1, double lam = 0.0) {
     using G = Sea2GeoT<SO_PTILE_NW>;
     static int ncu = 0, per_cu = 0;
     if (ncu == 0) {
         device_shape(&ncu);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p_run_kernel<SO_PTILE_NW, MODE>,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p_run_kernel<SO_PTILE_NW, MODE, VBS>,
                                                          SO_PTILE_NW * 64, 0) != hipSuccess || per_cu <= 0)
             per_cu = 1;
     }
@@ -1974,8 +2506,8 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
             if (const char* e = getenv("SO_P2LAG")) lag = atoi(e);   // A/B only
             sp.p2lag = lag < 1 ? 1 : (lag > ntr ? ntr : lag);
         }
-        hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, MODE>), dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), 0, st, a, n,
-                           f0 ? outs[f0 - 1].recon : ref0, H, W, qp_rd, qp_row, ws, (int)(f0 * ntiles), sp);
+        hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, MODE, VBS>), dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), 0, st, a, n,
+                           f0 ? outs[f0 - 1].recon : ref0, H, W, qp_rd, qp_row, ws, (int)(f0 * ntiles), sp, lam);
         const int rc = check_launch("p_run_kernel");
         if (rc != SO_OK) return rc;
     }
@@ -1986,21 +2518,27 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
 // faster where a frame has fewer tiles than resident workgroups, 1088p 29.5 vs 28.3 us per
 // frame, and 1.56x slower at 4K: removed).
 int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
-                 const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, hipStream_t st) {
+                 const int32_t* qp_row, int vbs, double lam, const PFrameOut* outs, uint32_t* ws, hipStream_t st) {
     PRunStripe sp{};
     sp.by0 = 0;
     sp.by1 = H / 16;
+    if (vbs)
+        return p_run_launch_t<kRunSingle, true>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, 0, st, nullptr,
+                                                nullptr, 1, lam);
     return p_run_launch_t<kRunSingle>(curs, nframes, ref0, H, W, qp_rd, qp_row, outs, ws, sp, 0, st);
 }
 
 // Several independent runs in one list (so_encode_p_runs): frame g predicts from
 // outs[deps[g]].recon (deps[g] < g) or, with deps[g] < 0, from refs[g].
 int p_runs_launch(const uint8_t* const* curs, int nframes, const uint8_t* const* refs, const int* deps, int conc,
-                  int H, int W, int qp_rd, const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws,
-                  hipStream_t st) {
+                  int H, int W, int qp_rd, const int32_t* qp_row, int vbs, double lam, const PFrameOut* outs,
+                  uint32_t* ws, hipStream_t st) {
     PRunStripe sp{};
     sp.by0 = 0;
     sp.by1 = H / 16;
+    if (vbs)
+        return p_run_launch_t<kRunSingle, true>(curs, nframes, nullptr, H, W, qp_rd, qp_row, outs, ws, sp, 0, st, refs,
+                                                deps, conc, lam);
     return p_run_launch_t<kRunSingle>(curs, nframes, nullptr, H, W, qp_rd, qp_row, outs, ws, sp, 0, st, refs, deps,
                                            conc);
 }
@@ -2035,8 +2573,11 @@ int p_run_stripe_launch(const uint8_t* const* curs, int nframes, const uint8_t* 
 }
 
 int p_run_fpipe_launch(const uint8_t* const* curs, int nframes, int H, int W, int qp_rd, const int32_t* qp_row,
-                       const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg, hipStream_t st,
-                       const int* push) {
+                       int vbs, double lam, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg,
+                       hipStream_t st, const int* push) {
+    if (vbs)
+        return p_run_launch_t<kRunFPipe, true>(curs, nframes, nullptr, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st,
+                                               nullptr, push, 1, lam);
     return p_run_launch_t<kRunFPipe>(curs, nframes, nullptr, H, W, qp_rd, qp_row, outs, ws, sp, max_wg, st,
                                           nullptr, push);
 }

@@ -61,11 +61,12 @@ struct PRunStripe {
 
 size_t p_run_workspace_words(int H, int W);
 int32_t* p_run_t1_region(uint32_t* ws, int H, int W);
+// vbs / lam: VBSEnable (the block + sub-block search and the RD split inside the run)
 int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
-                 const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, hipStream_t st);
+                 const int32_t* qp_row, int vbs, double lam, const PFrameOut* outs, uint32_t* ws, hipStream_t st);
 int p_runs_launch(const uint8_t* const* curs, int nframes, const uint8_t* const* refs, const int* deps, int conc,
-                  int H, int W, int qp_rd, const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws,
-                  hipStream_t st);
+                  int H, int W, int qp_rd, const int32_t* qp_row, int vbs, double lam, const PFrameOut* outs,
+                  uint32_t* ws, hipStream_t st);
 int p_run_2pass_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                        const int32_t* qp_row, const int32_t* roi, int qp_lo, int qp_hi, const PFrameOut* outs,
                        uint32_t* ws, hipStream_t st);
@@ -73,8 +74,8 @@ int p_run_stripe_launch(const uint8_t* const* curs, int nframes, const uint8_t* 
                         const int32_t* qp_row, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg,
                         hipStream_t st);
 int p_run_fpipe_launch(const uint8_t* const* curs, int nframes, int H, int W, int qp_rd, const int32_t* qp_row,
-                       const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg, hipStream_t st,
-                       const int* push);
+                       int vbs, double lam, const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg,
+                       hipStream_t st, const int* push);
 int p_run_fpipe_2pass_launch(const uint8_t* const* curs, int nframes, int H, int W, int qp_rd, const int32_t* qp_row,
                              const PFrameOut* outs, uint32_t* ws, const PRunStripe& sp, int max_wg, hipStream_t st,
                              const int* push);

@@ -215,11 +215,12 @@ class Engine:
         return out
 
     # ---- P-frame runs (one persistent launch) ----------------------------------------------
-    def pipelined_ok(self, nref: int = 1) -> bool:
+    def pipelined_ok(self, nref: int = 1, vbs_ok: bool = True) -> bool:
         """The configurations encode_p_run covers: the fused search + transform kernel
-        (bs 16, sr 16, full search, no VBS / FME, one reference) on whole 128-byte rows."""
-        return (self.bs == 16 and self.sr == 16 and self.me_mode == _lib.ME_FULL and not self.fme and not self.vbs
-                and nref == 1 and self.w % 128 == 0)
+        (bs 16, sr 16, full search, no FME, one reference) on whole 128-byte rows; VBSEnable
+        too unless vbs_ok is False (the two-pass RC run and the stripe hand-off)."""
+        return (self.bs == 16 and self.sr == 16 and self.me_mode == _lib.ME_FULL and not self.fme
+                and (vbs_ok or not self.vbs) and nref == 1 and self.w % 128 == 0)
 
     def encode_p_run(self, curs: list, ref0: torch.Tensor, qp_rd: int, outs: list, qp_row=None,
                      qp_row_dev: torch.Tensor | None = None) -> list:
@@ -229,7 +230,7 @@ class Engine:
         only the run's last frame has a launch tail.  Symbols identical to per-frame
         encode_p; asynchronous."""
         if not self.pipelined_ok():
-            raise ValueError("encode_p_run covers bs 16 / sr 16 / full search / no VBS, FME / W % 128 == 0")
+            raise ValueError("encode_p_run covers bs 16 / sr 16 / full search / no FME / W % 128 == 0")
         n = len(curs)
         if n == 0:
             return []
@@ -245,6 +246,7 @@ class Engine:
             return (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
         rc = self.lib.so_encode_p_run(
             arr(curs), n, ref0.data_ptr(), self.h, self.w, self.bs, self.sr, int(qp_rd), _lib.ptr(qrd),
+            int(self.vbs), self.lam,
             arr([o.split for o in outs]), arr([o.mv for o in outs]), arr([o.qtc for o in outs]),
             arr([o.tokens for o in outs]), arr([o.mae_num for o in outs]), arr([o.recon for o in outs]),
             arr([o.sse for o in outs]), self._run_ws.data_ptr(), _lib.stream_handle(self.device))
@@ -262,7 +264,7 @@ class Engine:
         those QPs on pass 1's motion vectors) as ONE persistent launch.  qp_maps[i] (int32
         [nb]) receives frame i's QPs.  Symbols identical to encode_p + qp_map + encode_p
         (reuse_me) per frame; asynchronous."""
-        if not self.pipelined_ok():
+        if not self.pipelined_ok(vbs_ok=False):
             raise ValueError("encode_p_run_2pass covers bs 16 / sr 16 / full search / no VBS, FME / W % 128 == 0")
         n = len(curs)
         if n == 0:
@@ -299,7 +301,7 @@ class Engine:
         of every run is in flight at once.  Each run's symbols are identical to encode_p_run
         of that run alone; asynchronous."""
         if not self.pipelined_ok():
-            raise ValueError("encode_p_runs covers bs 16 / sr 16 / full search / no VBS, FME / W % 128 == 0")
+            raise ValueError("encode_p_runs covers bs 16 / sr 16 / full search / no FME / W % 128 == 0")
         qrd = qp_row_dev if qp_row_dev is not None else self.qp_row_tensor(qp_row)
         curs, refs, ref_frame, outs, last = [], [], [], [], {}
         for k in range(max((len(r[0]) for r in runs), default=0)):
@@ -326,7 +328,7 @@ class Engine:
             return (ctypes.c_void_p * n)(*[0 if t is None else t.data_ptr() for t in ts])
         rc = self.lib.so_encode_p_runs(
             arr(curs), n, arr(refs), (ctypes.c_int32 * n)(*ref_frame), self.h, self.w, self.bs, self.sr, int(qp_rd),
-            _lib.ptr(qrd), arr([o.split for o in outs]), arr([o.mv for o in outs]), arr([o.qtc for o in outs]),
+            _lib.ptr(qrd), int(self.vbs), self.lam, arr([o.split for o in outs]), arr([o.mv for o in outs]), arr([o.qtc for o in outs]),
             arr([o.tokens for o in outs]), arr([o.mae_num for o in outs]), arr([o.recon for o in outs]),
             arr([o.sse for o in outs]), self._run_ws.data_ptr(), _lib.stream_handle(self.device))
         _lib.check(rc, "so_encode_p_runs")

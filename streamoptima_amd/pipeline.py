@@ -45,7 +45,7 @@ class StripeRunRank:
 
     def __init__(self, engine, world: int, rank: int, max_frames: int, stream=None, max_wg: int = 0):
         e = engine
-        if not e.pipelined_ok(1):
+        if not e.pipelined_ok(1, vbs_ok=False):
             raise ValueError("the stripe run covers bs 16 / sr 16 / full search / no VBS, FME / W % 128 == 0")
         self.eng, self.world, self.rank = e, world, rank
         self.by0, self.by1, self.rps = stripe_rows(e.nby, world, rank)
@@ -349,7 +349,7 @@ class FramePipeRank:
         if world < 2:
             raise ValueError("the frame pipeline needs at least 2 ranks")
         if not e.pipelined_ok(1):
-            raise ValueError("the frame pipeline covers bs 16 / sr 16 / full search / no VBS, FME / W % 128 == 0")
+            raise ValueError("the frame pipeline covers bs 16 / sr 16 / full search / no FME / W % 128 == 0")
         self.eng, self.world, self.rank, self.max_frames = e, world, rank, max_frames
         self.stream, self.max_wg = stream, max_wg
         lib = self.lib = _lib.load()
@@ -433,6 +433,8 @@ class FramePipeRank:
             raise RuntimeError("connect() first")
         if roi_dev is not None and not two_pass:
             raise ValueError("the frame pipeline covers ROI with two-pass RC only")
+        if two_pass and e.vbs:
+            raise ValueError("the frame pipeline's two-pass RC runs without VBSEnable")
         self.epoch += 1
         ep, st = self.epoch, self._st()
         mine = self.frames_of(nf)
@@ -479,8 +481,8 @@ class FramePipeRank:
                     int(qp_clamp[1]), *outs, arr([s.extra["qp_map"].data_ptr() for s in ss]), self._ws.data_ptr(),
                     *land), "so_encode_p_run_fpipe_2pass")
             else:
-                _lib.check(lib.so_encode_p_run_fpipe2(curs, n, e.h, e.w, e.bs, e.sr, int(qp), _lib.ptr(qrd), *outs,
-                                                      self._ws.data_ptr(), *land), "so_encode_p_run_fpipe2")
+                _lib.check(lib.so_encode_p_run_fpipe2(curs, n, e.h, e.w, e.bs, e.sr, int(qp), _lib.ptr(qrd), int(e.vbs),
+                                                      e.lam, *outs, self._ws.data_ptr(), *land), "so_encode_p_run_fpipe2")
             for s in ss:
                 s.frame_type, s.qp_rd = 1, int(qp)
         for s in syms.values():

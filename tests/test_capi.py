@@ -95,9 +95,9 @@ def test_p_runs_validation_without_gpu():
     cur = arr(fake[0], fake[1])
     outs = [arr(fake[2 + 2 * k], fake[3 + 2 * k]) for k in range(5)]
 
-    def call(refs, ref_frame, recon):
-        return lib.so_encode_p_runs(cur, n, refs, (ctypes.c_int32 * n)(*ref_frame), 64, 128, 16, 16, 4, None,
-                                    outs[0], outs[1], outs[2], outs[3], outs[4], recon, None,
+    def call(refs, ref_frame, recon, vbs=0, lam=0.0):
+        return lib.so_encode_p_runs(cur, n, refs, (ctypes.c_int32 * n)(*ref_frame), 64, 128, 16, 16, 4, None, vbs,
+                                    lam, outs[0], outs[1], outs[2], outs[3], outs[4], recon, None,
                                     ctypes.c_void_p(0x9000), None)
     recon = arr(fake[10], fake[11])
     assert call(arr(fake[8], fake[9]), [-1, 1], recon) == _lib.SO_E_INVALID
@@ -105,8 +105,11 @@ def test_p_runs_validation_without_gpu():
     assert call(arr(fake[8], None), [-1, -1], recon) == _lib.SO_E_INVALID
     assert call(arr(fake[10], None), [-1, 0], recon) == _lib.SO_E_INVALID
     assert b"aliases" in lib.so_last_error()
-    assert lib.so_encode_p_runs(cur, n, arr(fake[8], None), (ctypes.c_int32 * n)(-1, 0), 64, 96, 16, 16, 4, None,
-                                outs[0], outs[1], outs[2], outs[3], outs[4], recon, None, ctypes.c_void_p(0x9000),
+    assert call(arr(fake[8], None), [-1, 0], recon, vbs=2) == _lib.SO_E_INVALID
+    assert call(arr(fake[8], None), [-1, 0], recon, vbs=1, lam=float("nan")) == _lib.SO_E_INVALID
+    assert b"lambda" in lib.so_last_error()
+    assert lib.so_encode_p_runs(cur, n, arr(fake[8], None), (ctypes.c_int32 * n)(-1, 0), 64, 96, 16, 16, 4, None, 0,
+                                0.0, outs[0], outs[1], outs[2], outs[3], outs[4], recon, None, ctypes.c_void_p(0x9000),
                                 None) == _lib.SO_E_UNSUPPORTED
 
 
@@ -142,7 +145,8 @@ def test_two_pass_run_and_frame_pipe_validation_without_gpu():
     land0, land_flags = 0x4000000, ctypes.c_void_p(0x5000000)
 
     def fpipe(recon, push, stride=stride, slot0=0, nslots=3):
-        return lib.so_encode_p_run_fpipe2(cur, n, H, W, 16, 16, 4, None, outs[0], outs[1], outs[2], outs[3], outs[4],
+        return lib.so_encode_p_run_fpipe2(cur, n, H, W, 16, 16, 4, None, 0, 0.0, outs[0], outs[1], outs[2], outs[3],
+                                          outs[4],
                                           recon, None, ws, ctypes.c_void_p(land0), land_flags, slot0, fake[14],
                                           fake[15], fake[14], fake[15], (ctypes.c_int32 * n)(*push), nslots, stride,
                                           1, 0, None)

@@ -220,6 +220,37 @@ def test_4k120_poisoned_outputs(gpu):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("h,w,intra_dur", [(272, 640, 5), (1088, 1920, 4)])
+def test_vbs_run_matches_per_frame(gpu, monkeypatch, h, w, intra_dur):
+    """VBSEnable in the persistent run (p_run_kernel<8, 0, true>: the block + sub-block dense
+    search on the tile's LDS window and tq16_vbs's RD split) against the per-frame kernels
+    (SO_PIPELINE=0: me_wave_kernel<16, true> + inter_tq_kernel<16, true>), frame by frame, on
+    frames with edge tiles (640 = 5 tiles, 272 rows: a half tile row), several I-frames, and
+    through encode_gops_device (runs of two GOPs interleaved in one launch)."""
+    from streamoptima_amd.Encoder import Y_Video_codec
+    from streamoptima_amd.digest import symbols_digest
+    from streamoptima_amd.engine import alloc_planes
+    from streamoptima_amd.synth import synth_sequence_torch
+    f = 9
+    codec = Y_Video_codec(h, w, f, 16, 16, 4, intra_dur, 0, 0.015, True, device=gpu)
+    assert codec.engine().pipelined_ok(1)
+    fa = alloc_planes(f, h, w, gpu)
+    fa.copy_(synth_sequence_torch(f, h, w, seed=21, device=gpu))
+    fb = alloc_planes(f, h, w, gpu)
+    fb.copy_(fa.flip(0))
+    monkeypatch.setenv("SO_PIPELINE", "0")
+    exp = [[symbols_digest(s) for s in codec.encode_device(g, intra_dur)["symbols"]] for g in (fa, fb)]
+    monkeypatch.delenv("SO_PIPELINE")
+    got = codec.encode_device(fa, intra_dur)
+    torch.cuda.synchronize()
+    assert [symbols_digest(s) for s in got["symbols"]] == exp[0]
+    assert int(sum(int(s.split.sum()) for s in got["symbols"][1:])) > 0   # some blocks split
+    res = codec.encode_gops_device([fa, fb], intra_dur)
+    torch.cuda.synchronize()
+    for g in range(2):
+        assert [symbols_digest(s) for s in res[g]["symbols"]] == exp[g], g
+
+
 @pytest.mark.parametrize("vbs,fme", [(False, False), (True, False), (False, True), (True, True)])
 def test_fast_me_chain_speculation_matches_serial_walk(gpu, monkeypatch, vbs, fme):
     """fast_me mode 0 (Encoder.py:719-742, the predictor chain of :462-585): the segmented

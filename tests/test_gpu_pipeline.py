@@ -221,18 +221,19 @@ def _fpipe_rc_kw(name, eng, nframes):
 
 
 @pytest.mark.parametrize("name,world,nframes", [("4k", 2, 12), ("4k", 3, 13), ("1080p", 2, 30), ("4k_rc2pass", 2, 8),
-                                                ("4k_rc2pass", 3, 10)])
+                                                ("4k_rc2pass", 3, 10), ("4k_vbs", 2, 8), ("1080p_vbs", 3, 10)])
 def test_frame_pipeline_in_process_matches_one_gpu(gpu, name, world, nframes):
     """Rank g encodes frames g, g+N, ...; each frame's reference arrives tile by tile from the
     previous rank.  Whole-frame symbols and local reconstructions of every frame must equal
     the one-GPU GOP (oracle digests), twice in a row (epoch 2 over epoch 1's planes).
-    4k_rc2pass: configs[4] (ROI + two-pass RC) on the frame pipeline, QP maps included."""
+    4k_rc2pass: configs[4] (ROI + two-pass RC) on the frame pipeline, QP maps included; *_vbs:
+    VBSEnable (block + sub-block search and the RD split inside the launch)."""
     from streamoptima_amd.digest import symbols_digest
     from streamoptima_amd.engine import Engine
     from streamoptima_amd.pipeline import FramePipeRank
     cfg, fr = _frames(name, gpu, nframes)
     h, w = fr.shape[1:]
-    engines = [Engine(h, w, 16, 16, False, 0.015, gpu) for _ in range(world)]
+    engines = [Engine(h, w, 16, 16, bool(cfg.get("vbs")), 0.015, gpu) for _ in range(world)]
     streams = _streams(gpu)[:world]
     cap = 768 // (2 * world)
     ranks = [FramePipeRank(engines[r], world, r, nframes, stream=streams[r], max_wg=cap) for r in range(world)]

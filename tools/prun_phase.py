@@ -19,12 +19,13 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--h", type=int, default=2160)
     ap.add_argument("--w", type=int, default=3840)
+    ap.add_argument("--vbs", action="store_true", help="VBSEnable (p_run_kernel<8, 0, true>)")
     a = ap.parse_args()
     from streamoptima_amd.engine import Engine, alloc_planes
     from streamoptima_amd.synth import synth_sequence_torch
     dev = torch.device("cuda:0")
     f = 30
-    eng = Engine(a.h, a.w, 16, 16, False, 0.015, dev)
+    eng = Engine(a.h, a.w, 16, 16, a.vbs, 0.015, dev)
     fr = alloc_planes(f, a.h, a.w, dev)
     fr.copy_(synth_sequence_torch(f, a.h, a.w, seed=0, device=dev))
     i0 = eng.encode_i(fr[0], 4)
@@ -43,7 +44,7 @@ def main():
         ts.append(e0.elapsed_time(e1) * 1e3)
     eng.check_run()
     ts.sort()
-    print(json.dumps({"lib": os.environ.get("SO_LIB_PATH", "default"), "frames": f - 1,
+    print(json.dumps({"lib": os.environ.get("SO_LIB_PATH", "default"), "vbs": a.vbs, "frames": f - 1,
                       "launch_us_min": round(ts[0], 1), "launch_us_median": round(ts[len(ts) // 2], 1),
                       "us_per_frame_median": round(ts[len(ts) // 2] / (f - 1), 2)}), flush=True)
 
