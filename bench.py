@@ -591,8 +591,9 @@ def record_single(name: str, args, dev) -> dict:
     p_blocks = (cfg["frames"] - -(-cfg["frames"] // cfg["intra_dur"])) * eng.nb
     fb = eng.take_fallback_count()
     rec["sea_dense_fallback"] = {"blocks": fb, "p_blocks": p_blocks, "frac": round(fb / p_blocks, 5),
-                                 "note": "P-frame blocks whose 4x4-cell bound left more than 192 survivors "
-                                         "(SO_P_RUN_FALLBACK_WORD, one GOP)"}
+                                 "note": "P-frame blocks searched dense: the 4x4-cell bound left more than 192 "
+                                         "survivors, or the tile searched dense from the start because the same tile "
+                                         "of the previous frame mostly overflowed (SO_P_RUN_FALLBACK_WORD, one GOP)"}
     if not args.no_parity:
         def redo():
             poison(pre)

@@ -907,9 +907,14 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
 // (the block and its four 8x8 sub-blocks, keys [NBLK + 4u + j]) or, within 32 px of the right /
 // bottom edge or past CAP survivors, the dense wave search, whose v_sad_u8 work yields the
 // sub-block SADs with the block's; the other blocks the block's exact SEA.
+// dense_flag (LDS, read after `pre`): nonzero = every block of the tile takes the dense search
+// directly (p_run_kernel sets it when the same tile of the previous frame had most of its
+// blocks overflow the SEA bound: flat or noise-like content, where computing the bound only to
+// fall back costs more than it saves).
 template <class G, class Pre = NoPre, bool VBS = false>
 SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cur, const RefSet& refs, int nref,
-                      int H, int W, int by0, int by1, int probe, const Pre& pre = Pre()) {
+                      int H, int W, int by0, int by1, int probe, const Pre& pre = Pre(),
+                      const int* dense_flag = nullptr) {
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RP = G::RP, NT = G::NT;
     constexpr int B4P = G::B4P, CAP = G::CAP, CP = G::TPX;
     uint32_t* const win = L.win;
@@ -1016,6 +1021,22 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
         __syncthreads();
         if (r == 0) SO_SEA_STAMP(3, __builtin_amdgcn_s_memtime());
         if (probe == 5) continue;   // phase-attribution builds (SO_PROF_PHASE=2): no search at all
+        if (dense_flag && __builtin_amdgcn_readfirstlane(*dense_flag)) {   // uniform: the whole tile dense
+#pragma unroll 1
+            for (int u = wave; u < G::NBLK; u += G::NW) {
+                const int bxl = u % TBX, byl = u / TBX;
+                if (bx0 + bxl >= nbx || byt0 + byl >= by1) continue;   // wave-uniform
+                const int x = x0 + bxl * 16, y = y0 + byl * 16;
+                if (VBS && x != 0 && y != 0)
+                    wave_dense_block<16, true, RP, 0, false, true>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u,
+                                                                   tid, r);
+                else
+                    wave_dense_block<16, false, RP, 0, false, true>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u,
+                                                                    tid, r);
+                if ((tid & 63) == 0) atomicAdd(&st_fb, 1u);
+            }
+            continue;
+        }
         // 4x4 byte sums B4(row, c) = (sum of the 4x4 window block at (row, c)) >> 4, stored at
         // b4[row * B4P + (c & 3) * WD + (c >> 2)] (a candidate's four sums of one 4x4 row --
         // columns c, c+4, c+8, c+12 -- are then consecutive bytes).  Thread = (dword column m:
@@ -1777,11 +1798,20 @@ SO_DEV void tq16_vbs(PTileLds<G, true>& S, int g, int l, double* scratch, uint8_
 // write-through (global_store sc1), so another XCD that later reads them (p_run_kernel's
 // next frame) gets them from memory without a release fence.  Ends with every wave's
 // stores retired (s_waitcnt vmcnt(0)) and a workgroup barrier.  `pre`: as sea2_tile's.
+// write-through (sc1) stores: the value is in memory once the store retires
+SO_DEV void store_sc1_i16(int16_t* p, int v) {
+    asm volatile("global_store_short %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+SO_DEV void store_sc1_i32(int32_t* p, int v) {
+    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
 template <class G, bool SC1, class Pre = NoPre, bool HALO = false, bool TOK = false, bool VBS = false>
 SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict__ cur, const uint8_t* ref, int H, int W,
                        int by0, int by1, int qp_rd, const int32_t* __restrict__ qp_row,
                        const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best, const PFrameOut& o,
-                       const Pre& pre = Pre(), const PHalo& hl = PHalo{}, double lam = 0.0) {
+                       const Pre& pre = Pre(), const PHalo& hl = PHalo{}, double lam = 0.0,
+                       const int* dense_flag = nullptr, int32_t* fb_out = nullptr) {
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY;
     using P = PTileGeo<G>;
     uint32_t* const b4w = reinterpret_cast<uint32_t*>(S.un);
@@ -1792,7 +1822,8 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
 #ifndef SO_PROF_PHASE   // phase-attribution A/B builds only (tools/prun_phase.py): 1 = no transforms
 #define SO_PROF_PHASE 0  // (the tile's current rows stored as its reconstruction), 2 = no search
 #endif                   // (window staged, every block at mv (0, 0))
-    sea2_tile<G, Pre, VBS>(L, tile, cur, refs, 1, H, W, by0, by1, SO_PROF_PHASE == 2 ? 5 : 0, pre);   // ends with a barrier
+    sea2_tile<G, Pre, VBS>(L, tile, cur, refs, 1, H, W, by0, by1, SO_PROF_PHASE == 2 ? 5 : 0, pre,
+                           dense_flag);   // ends with a barrier
 
     const int tid = opaque_tid();
     SO_SEA_STAMP(5, __builtin_amdgcn_s_memtime());
@@ -1807,6 +1838,9 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
             ob[0] = S.mer[i][0]; ob[1] = S.mer[i][1]; ob[2] = S.mer[i][2]; ob[3] = S.mer[i][3];
         }
     }
+    // the tile's dense-block count (p_run_kernel: the next frame's same tile reads it), stored
+    // write-through now so that the drain below covers it
+    if (fb_out != nullptr && tid == 0) store_sc1_i32(fb_out, (int)S.st[0]);
     __syncthreads();
     SO_SEA_STAMP(6, __builtin_amdgcn_s_memtime());
     {   // block g = wave * TQ_BPW + (lane >> 4) on lanes [0, 16 * TQ_BPW) of waves 0..NBLK/TQ_BPW-1
@@ -1851,12 +1885,6 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
 // pass 2 (the transforms at the block QPs, from the ME records pass 1 stored); a pass-2 task
 // starts once every tile of its tile row finished pass 1 (the row sums).
 
-SO_DEV void store_sc1_i16(int16_t* p, int v) {
-    asm volatile("global_store_short %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-SO_DEV void store_sc1_i32(int32_t* p, int v) {
-    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
 
 // pass 1 of one block (16 lanes, l = row): residual from the LDS window / tile as tq16_exact,
 // the forward transform, quantisation at the row QP and the token count.  Stores the ME
@@ -2121,6 +2149,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     using G = Sea2GeoT<NW>;
     __shared__ PTileLds<G, VBS> S;
     __shared__ int s_task;
+    __shared__ int s_dense;   // kRunSingle: this tile searches dense (sea2_tile's dense_flag)
     const int tid = threadIdx.x;
     const int nbx = W / 16;
     constexpr bool STRIPE = MODE == kRunStripe, FPIPE = MODE == kRunFPipe || MODE == kRunFPipe2P;
@@ -2134,6 +2163,9 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     // on tasks earlier in the queue
     const int per_frame = TWOP ? 2 * ntiles : ntiles, ntasks = per_frame * nframes;
     uint32_t* const done = ws + kRunDoneBase;
+    // kRunSingle: per (frame, tile) the count of blocks that searched dense (after the done
+    // flags, the pass-1 flags and token counts: p_run_workspace_words)
+    uint32_t* const tilefb = ws + kRunDoneBase + 2 * (size_t)kRunMax * ntiles + (size_t)kRunMax * nbx * (H / 16);
     // Every queue / flag access is made by ALL lanes of wave 0 under a wave-uniform branch
     // (lane 0 adds 1, the others 0): a `tid == 0` branch ahead of a barrier inside this loop
     // gets structurised into a divergent inner loop that never re-runs the dequeue (a hang;
@@ -2141,7 +2173,8 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lane = tid & 63;
     const uint32_t one = lane == 0 ? 1u : 0u;
-    uint32_t fbsum = 0;   // wave 0: this workgroup's dense-fallback blocks over its tasks
+    __shared__ uint32_t s_fbsum;   // this workgroup's dense-searched blocks over its tasks (LDS: a
+    if (tid == 0) s_fbsum = 0;     // register kept live across the loop cost spills)
     // this launch's epoch: ws[2] + 1 (ws[2] = the last finished launch's; written by that
     // launch's last workgroup, so every workgroup here reads it before it can change).  Done
     // flags hold the epoch of the launch that set them: nothing is zeroed between launches.
@@ -2152,6 +2185,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             const int t = (int)__builtin_amdgcn_readfirstlane(
                 __hip_atomic_fetch_add(&ws[0], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             s_task = t;
+            s_dense = 0;
         }
         __syncthreads();
         const int task = __builtin_amdgcn_readfirstlane(s_task);
@@ -2232,13 +2266,21 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             // enqueue its launch late (a rank's kernel can start waiting on a neighbour whose
             // process is descheduled, e.g. several ranks time-sharing one GPU)
             constexpr unsigned long long kWaitLimit = (STRIPE || FPIPE) ? 200000000ull : 5000000ull;
+            // one GPU: lane 9 reads, in the same round trips, the dense-block count of the same tile
+            // of the reference frame (a heuristic only -- dense and SEA searches are both exact --
+            // so it is read unordered with the flags)
+            const bool fbl = MODE == kRunSingle && lane == 9 && dep >= 0;
+            if (fbl) c = tilefb + (size_t)dep * ntiles + tile;
+            uint32_t raw = 0;
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
             for (;;) {
                 uint32_t v;
-                if ((STRIPE || FPIPE) && rneed)
+                if ((STRIPE || FPIPE) && rneed) {
                     v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == sp.epoch ? 1u : 0u;
-                else
-                    v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ep ? 1u : 0u;
+                } else {
+                    raw = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    v = raw == ep ? 1u : 0u;
+                }
                 if (__builtin_amdgcn_ballot_w64((need || rneed) && v == 0u) == 0) break;
                 __builtin_amdgcn_s_sleep(1);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitLimit) {
@@ -2258,6 +2300,13 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
+            // the same tile of the reference frame had most of its blocks overflow the SEA bound
+            // -> this one searches dense from the start, except every 4th frame, which probes
+            // the bound again
+            if (MODE == kRunSingle && dep >= 0 && (f & 3) != 0) {
+                const uint32_t fb = (uint32_t)__builtin_amdgcn_readlane((int)raw, 9);
+                if (lane == 0) s_dense = fb >= 8u ? 1 : 0;
+            }
         };
         const uint8_t* ref = FPIPE ? sp.land0 + (long long)(sp.gbase + f) * sp.stride
                                    : (MODE == kRunSingle || TWOP) ? a.ref[f] : (f ? a.out[f - 1].recon : ref0);
@@ -2394,14 +2443,16 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 #endif
             ptile_body<G, true, decltype(wait_ref), false, false, VBS>(S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd,
                                                                        qp_row, nullptr, nullptr, a.out[f], wait_ref,
-                                                                       PHalo{}, lam);
+                                                                       PHalo{}, lam, &s_dense,
+                                                                       reinterpret_cast<int32_t*>(tilefb) +
+                                                                           (size_t)f * ntiles + tile);
             SO_RUN_PROF(52, __builtin_amdgcn_s_memtime() - pt0);
             // ptile_body ended with every wave's write-through stores retired and a barrier
             if (wave == 0)
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (pass == 1 && wave == 0) fbsum += S.st[0];   // this tile's dense-fallback blocks
+        if (pass == 1 && tid == 0) s_fbsum += S.st[0];   // this tile's dense-searched blocks
 #ifdef SO_STAMPS
         if (tid == 0 && rec) {
             uint32_t hw, xcc;
@@ -2414,9 +2465,12 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 #endif
     }
     // the last workgroup out resets the task and exit counters and publishes the epoch
-    if (wave == 0 && fbsum != 0u)
-        __hip_atomic_fetch_add(&ws[kRunFallbackWord], lane == 0 ? fbsum : 0u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+    if (wave == 0) {
+        const uint32_t fbsum = __builtin_amdgcn_readfirstlane(s_fbsum);
+        if (fbsum != 0u)
+            __hip_atomic_fetch_add(&ws[kRunFallbackWord], lane == 0 ? fbsum : 0u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (wave == 0) {
         const uint32_t o = __builtin_amdgcn_readfirstlane(
             __hip_atomic_fetch_add(&ws[kRunExitWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -2435,8 +2489,8 @@ static size_t run_tiles(int H, int W, int tbx, int tby) {
 }
 size_t p_run_workspace_words(int H, int W) {
     using G = Sea2Geo;
-    return (size_t)kRunDoneBase + 2 * (size_t)kRunMax * run_tiles(H, W, G::TBX, G::TBY) +
-           (size_t)kRunMax * (W / 16) * (H / 16);
+    return (size_t)kRunDoneBase + 3 * (size_t)kRunMax * run_tiles(H, W, G::TBX, G::TBY) +
+           (size_t)kRunMax * (W / 16) * (H / 16);   // + the per-tile dense counts
 }
 
 // Launch the run in <= kRunMax-frame launches.  max_wg > 0 caps the resident grid (several
