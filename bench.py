@@ -282,7 +282,7 @@ def pmc_record(config: str):
     except (ValueError, OSError):
         return {}
     for k, v in ks.items():
-        if k.startswith("so::p_run_kernel<8"):      # p_run_kernel<8, 0, 128> (one GPU, full frame)
+        if k.startswith("so::p_run_kernel<8, 0"):   # p_run_kernel<8, 0, false> (one GPU, full frame)
             return v
     return {}
 
@@ -308,7 +308,7 @@ def roofline_of(rl: dict, config: str) -> dict:
                 "kernel_cycles": round(cyc), "effective_clock_ghz": round(cyc / launch_s / 1e9, 3),
                 "source": "profiles/pmc_me_traffic.json (rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES "
                           "GRBM_GUI_ACTIVE ..., tools/gpu_traffic.sh)"}
-    return {"bound": "hbm", "kernel": "p_run_kernel<8, 0, 128>", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
+    return {"bound": "hbm", "kernel": "p_run_kernel<8, 0, false>", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
             "traffic_note": "HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE x 2, the "
                             "factor measured for 4-B and 16-B coalesced reads (tools/ubench_fetch.cpp)",
@@ -569,6 +569,20 @@ def time_steps_median(step, args, dev):
     return elapsed, res, [round(e / args.steps * 1e3, 3) for e, _ in runs]
 
 
+def dense_fallback_of(eng, cfg, step) -> dict:
+    """The fraction of one GOP's P-frame blocks whose exact SEA search took the dense path
+    (one extra, untimed step; the persistent run's fallback word)."""
+    eng.take_fallback_count()
+    step()
+    eng.check_run()
+    p_blocks = (cfg["frames"] - -(-cfg["frames"] // cfg["intra_dur"])) * eng.nb
+    fb = eng.take_fallback_count()
+    return {"blocks": fb, "p_blocks": p_blocks, "frac": round(fb / p_blocks, 5),
+            "note": "P-frame blocks searched dense: the 4x4-cell bound left more than 192 survivors, or the tile "
+                    "searched dense from the start because the same tile of the previous frame mostly overflowed "
+                    "(SO_P_RUN_FALLBACK_WORD, one GOP)"}
+
+
 def record_single(name: str, args, dev) -> dict:
     """Another workload measured like the headline (one GOP per step, median of
     --record-repeats timed runs, parity-checked): configs[1] (1080p) and the content-dependence
@@ -585,15 +599,7 @@ def record_single(name: str, args, dev) -> dict:
            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "ms_per_step_runs": runs, "width": cfg["w"],
            "height": cfg["h"], "encoded_height": padded(cfg["h"]), "frames": cfg["frames"],
            "content": cfg.get("content", "bench")}
-    eng.take_fallback_count()
-    step()
-    eng.check_run()
-    p_blocks = (cfg["frames"] - -(-cfg["frames"] // cfg["intra_dur"])) * eng.nb
-    fb = eng.take_fallback_count()
-    rec["sea_dense_fallback"] = {"blocks": fb, "p_blocks": p_blocks, "frac": round(fb / p_blocks, 5),
-                                 "note": "P-frame blocks searched dense: the 4x4-cell bound left more than 192 "
-                                         "survivors, or the tile searched dense from the start because the same tile "
-                                         "of the previous frame mostly overflowed (SO_P_RUN_FALLBACK_WORD, one GOP)"}
+    rec["sea_dense_fallback"] = dense_fallback_of(eng, cfg, step)
     if not args.no_parity:
         def redo():
             poison(pre)
@@ -934,6 +940,11 @@ def main(argv=None):
             parity = parity_of(res["symbols"], name, cfg, redo, sse=res["sse"])
     barrier(world)
 
+    fallback = None
+    if (world == 1 and not args.cpu_plumbing and codec is not None and cfg.get("me", "full") == "full"
+            and not cfg.get("rc") and codec.engine().pipelined_ok(1)):
+        fallback = dense_fallback_of(codec.engine(), cfg, step)
+
     psnr_mean = None
     if "sse" in res:
         hp = -(-h // 16) * 16
@@ -984,6 +995,8 @@ def main(argv=None):
         "psnr_mean_db": round(psnr_mean, 4) if psnr_mean is not None else None,
         "psnr_delta_db": parity.get("psnr_delta_db") if parity else None,
     }
+    if fallback:
+        line["sea_dense_fallback"] = fallback
     if world > 1:
         # dependency waits of the in-launch hand-off that passed their bound during the timed
         # run, summed over ranks (nonzero: that run was discarded and the stripes timed instead)

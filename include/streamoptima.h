@@ -247,11 +247,15 @@ int so_stripe_halo_push(const uint8_t* plane, int H, int W, int by0, int by1, in
  * tile by tile == epoch as it arrives.  The persistent run of the rank's frames [slot0,
  * slot0 + nframes) waits per tile for the 3x3 arrived tiles of its reference, and stores every
  * tile's reconstruction both into out_recon[i] (local) and, system-scope write-through over
- * xGMI, into the next rank's plane peer_land0 + (slot + peer_slot_off) * stride (peer_slot_off
- * = 1 on rank N-1, whose frames feed rank 0's next slot; 0 otherwise) before setting that
- * rank's flag to epoch.  Epochs are never reset (a new GOP uses a new epoch).  The symbols
- * are those of so_encode_p_run over the same frames.  so_frame_push sends a finished frame
- * (the I-frame) the same way.  workspace: so_p_run_workspace_elems(H, W), as so_encode_p_run.
+ * xGMI, into the landing plane its push code names before setting that rank's flag to epoch:
+ * push_to[i] = 2 * slot + peer puts frame i's reconstruction into slot `slot` of peer_land0
+ * (peer 0, flags peer_flags) or of peer2_land0 (peer 1, flags peer2_flags) -- the two ring
+ * neighbours, so the ring direction can alternate per block of N frames -- and -1 pushes
+ * nothing (the GOP's last frame).  Slots at or past nslots (every rank's slot count) are
+ * rejected, as is slot0 + nframes > nslots.  Epochs are never reset (a new GOP uses a new
+ * epoch).  vbs / lam as so_encode_p_run.  The symbols are those of so_encode_p_run over the
+ * same frames.  so_frame_push sends a finished frame (the I-frame) the same way.  workspace:
+ * so_p_run_workspace_elems(H, W), as so_encode_p_run.  max_wg > 0 caps the grid.
  */
 int so_encode_p_run_fpipe2(const uint8_t* const* curs, int nframes, int H, int W, int bs, int sr,
                            int qp_rd, const int32_t* qp_row, int vbs, double lam,
@@ -271,7 +275,10 @@ int so_encode_p_run_fpipe2(const uint8_t* const* curs, int nframes, int H, int W
  * pass 1), and pass 2 pushes the final reconstruction into the next frame's rank as
  * so_encode_p_run_fpipe2 does (same landing planes, flags, push codes, nslots and epochs).
  * A rank owns whole frames, so the row-local QP statistics never cross ranks.  The symbols
- * and QP maps are those of the one-GPU two-pass sequence over the same frames.
+ * and QP maps are those of the one-GPU two-pass sequence over the same frames.  A tile row's
+ * pass-2 tasks are queued about one grid's worth of tile rows after its pass-1 tasks; p2lag > 0
+ * caps that lag (consecutive frames across ranks trail each other by ~lag + 2 tile rows, so
+ * more ranks want a shorter one: pipeline.fpipe_p2lag); 0 = no cap.
  */
 int so_encode_p_run_fpipe_2pass(const uint8_t* const* curs, int nframes, int H, int W, int bs, int sr,
                                 int qp_rd, const int32_t* qp_row, const int32_t* roi, int qp_lo,
@@ -282,7 +289,7 @@ int so_encode_p_run_fpipe_2pass(const uint8_t* const* curs, int nframes, int H, 
                                 const uint8_t* land0, const uint32_t* land_flags, int slot0,
                                 uint8_t* peer_land0, uint32_t* peer_flags, uint8_t* peer2_land0,
                                 uint32_t* peer2_flags, const int32_t* push_to, int nslots, long long stride,
-                                uint32_t epoch, int max_wg, void* stream);
+                                uint32_t epoch, int max_wg, int p2lag, void* stream);
 int so_frame_push(const uint8_t* plane, int H, int W, uint8_t* peer_plane, uint32_t* peer_flags,
                   uint32_t epoch, void* stream);
 

@@ -74,7 +74,7 @@ _SIGS = {
     "so_encode_p_run_fpipe_2pass": ([_vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _i,          # .. qp_hi
                                      _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,             # outs, qp maps, ws
                                      _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _i,               # landing .. nslots
-                                     ctypes.c_longlong, ctypes.c_uint32, _i, _vp], _i),
+                                     ctypes.c_longlong, ctypes.c_uint32, _i, _i, _vp], _i),   # .. max_wg p2lag stream
     "so_frame_push": ([_vp, _i, _i, _vp, _vp, ctypes.c_uint32, _vp], _i),
     "so_pack_frames": ([_i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, ctypes.c_ulonglong, _vp], _i),
     "so_fme_plane_stride": ([_i, _i], _sz),

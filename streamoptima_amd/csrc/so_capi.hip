@@ -599,7 +599,7 @@ static int fpipe_run(const char* fn, bool two_pass, const uint8_t* const* curs, 
                      int32_t* const* out_sse, int32_t* const* out_qp_map, uint32_t* workspace, const uint8_t* land0,
                      const uint32_t* land_flags, int slot0, uint8_t* peer_land0, uint32_t* peer_flags,
                      uint8_t* peer2_land0, uint32_t* peer2_flags, const int32_t* push_to, int nslots, long long stride,
-                     uint32_t epoch, int max_wg, void* stream) {
+                     uint32_t epoch, int max_wg, int p2lag, void* stream) {
     SO_TRY(check_geom(fn, H, W, bs, vbs));
     SO_TRY(check_vbs(fn, vbs, lam));
     SO_TRY(check_sr(fn, sr));
@@ -618,6 +618,10 @@ static int fpipe_run(const char* fn, bool two_pass, const uint8_t* const* curs, 
     }
     // every rank owns `nslots` landing slots: this run reads slots [slot0, slot0 + nframes) and
     // writes (system scope, over xGMI) only slots below nslots of its peers
+    if (p2lag < 0) {
+        set_error("%s: p2lag %d < 0", fn, p2lag);
+        return SO_E_INVALID;
+    }
     if (slot0 < 0 || nslots < 1 || slot0 + nframes > nslots || stride < (long long)H * W) {
         set_error("%s: slot0 %d + %d frames / nslots %d / stride %lld", fn, slot0, nframes, nslots, stride);
         return SO_E_INVALID;
@@ -653,6 +657,7 @@ static int fpipe_run(const char* fn, bool two_pass, const uint8_t* const* curs, 
         sp.roi = roi;
         sp.qp_lo = qp_lo;
         sp.qp_hi = qp_hi;
+        sp.p2lag = p2lag;
         return p_run_fpipe_2pass_launch(curs, nframes, H, W, qp_rd, qp_row, outs.data(), workspace, sp, max_wg,
                                         (hipStream_t)stream, push.data());
     }
@@ -670,7 +675,7 @@ int so_encode_p_run_fpipe2(const uint8_t* const* curs, int nframes, int H, int W
     return fpipe_run("so_encode_p_run_fpipe2", false, curs, nframes, H, W, bs, sr, qp_rd, qp_row, vbs, lam, nullptr, 0, 0,
                      out_split, out_mv, out_qtc, out_tokens, out_mae_num, out_recon, out_sse, nullptr, workspace, land0,
                      land_flags, slot0, peer_land0, peer_flags, peer2_land0, peer2_flags, push_to, nslots, stride, epoch,
-                     max_wg, stream);
+                     max_wg, 0, stream);
 }
 
 int so_encode_p_run_fpipe_2pass(const uint8_t* const* curs, int nframes, int H, int W, int bs, int sr, int qp_rd,
@@ -681,12 +686,12 @@ int so_encode_p_run_fpipe_2pass(const uint8_t* const* curs, int nframes, int H, 
                                 const uint8_t* land0, const uint32_t* land_flags, int slot0, uint8_t* peer_land0,
                                 uint32_t* peer_flags, uint8_t* peer2_land0, uint32_t* peer2_flags,
                                 const int32_t* push_to, int nslots, long long stride, uint32_t epoch, int max_wg,
-                                void* stream) {
+                                int p2lag, void* stream) {
     return fpipe_run("so_encode_p_run_fpipe_2pass", true, curs, nframes, H, W, bs, sr, qp_rd, qp_row, 0, 0.0, roi, qp_lo,
                      qp_hi,
                      out_split, out_mv, out_qtc, out_tokens, out_mae_num, out_recon, out_sse, out_qp_map, workspace,
                      land0, land_flags, slot0, peer_land0, peer_flags, peer2_land0, peer2_flags, push_to, nslots, stride,
-                     epoch, max_wg, stream);
+                     epoch, max_wg, p2lag, stream);
 }
 
 int so_frame_push(const uint8_t* plane, int H, int W, uint8_t* peer_plane, uint32_t* peer_flags, uint32_t epoch,

@@ -2556,7 +2556,11 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
         sp.gbase = sp0.gbase + f0;
         if (MODE == kRunTwoPass || MODE == kRunFPipe2P) {   // pass 2 of a row about one grid's worth of tasks after its pass 1
             const int tiles_x = (nbx + G::TBX - 1) / G::TBX, ntr = (rows + G::TBY - 1) / G::TBY;
+            // about one grid's worth of tile rows (a pass-2 task then rarely waits holding its
+            // slot), capped by the caller's lag (the frame pipeline: consecutive frames on
+            // different ranks trail each other by ~lag + 2 rows, so more ranks want less)
             int lag = (int)((grid + tiles_x - 1) / tiles_x);
+            if (sp0.p2lag > 0 && sp0.p2lag < lag) lag = sp0.p2lag;
             if (const char* e = getenv("SO_P2LAG")) lag = atoi(e);   // A/B only
             sp.p2lag = lag < 1 ? 1 : (lag > ntr ? ntr : lag);
         }

@@ -43,7 +43,8 @@ HALO_TOP, HALO_BOT = 16, 32       # landing-plane rows above / below the stripe
 class StripeRunRank:
     """Buffers and launches of one rank of a GOP split into block-row stripes."""
 
-    def __init__(self, engine, world: int, rank: int, max_frames: int, stream=None, max_wg: int = 0):
+    def __init__(self, engine, world: int, rank: int, max_frames: int, stream=None, max_wg: int = 0,
+                 p2lag=None):
         e = engine
         if not e.pipelined_ok(1, vbs_ok=False):
             raise ValueError("the stripe run covers bs 16 / sr 16 / full search / no VBS, FME / W % 128 == 0")
@@ -332,6 +333,21 @@ def fpipe_plan(world: int, rank: int, nframes: int) -> dict:
             "nslots": nblocks + 1}
 
 
+def fpipe_p2lag(world: int, ntr: int) -> int:
+    """Cap on the pass-2 lag (tile rows) of the two-pass frame pipeline, 0 = no cap.  The
+    library queues a tile row's pass-2 tasks about one grid's worth of rows after its pass 1
+    (~26 at 4K on a whole MI355X: fewer and a pass-2 task waits holding its slot).  Frame
+    k+1's tile row r waits for frame k's pass 2 of rows r-1..r+1, so consecutive frames trail
+    each other by ~lag + 2 rows and the GOP's chain takes ~F (lag + 2) row-times, against
+    F ntr / N row-times of work per rank: past N (lag + 2) > ntr the chain, not the CUs, sets
+    the pace, hence lag <= ntr / N - 2 (4K: 20 at N = 3, 6 at N = 8).  Measured on one GPU with
+    in-process ranks (tools/fpipe2p_probe.py, profiles/r03/fpipe2p_half.log): 3 ranks, 4K ROI +
+    two-pass GOP, lag 26 / 12 / 5 -> 6.87 / 6.04 / 5.70 ms.  DESIGN.md section 6.1."""
+    if world <= 2:
+        return 0
+    return max(3, ntr // world - 2)
+
+
 class FramePipeRank:
     """One rank of a GOP whose frames are dealt round-robin over the ranks:
     rank g encodes one frame of every block of N consecutive frames (fpipe_plan: ranks 0..N-1
@@ -344,7 +360,8 @@ class FramePipeRank:
     ahead, so N ranks encode N frames at once; the only traffic is each reconstruction,
     once, over the xGMI link to the next rank."""
 
-    def __init__(self, engine, world: int, rank: int, max_frames: int, stream=None, max_wg: int = 0):
+    def __init__(self, engine, world: int, rank: int, max_frames: int, stream=None, max_wg: int = 0,
+                 p2lag=None):
         e = engine
         if world < 2:
             raise ValueError("the frame pipeline needs at least 2 ranks")
@@ -355,6 +372,7 @@ class FramePipeRank:
         lib = self.lib = _lib.load()
         self.tiles_x, self.ntr = e.w // 128, -(-e.nby // 2)
         self.ntiles = self.tiles_x * self.ntr
+        self.p2lag = fpipe_p2lag(world, self.ntr) if p2lag is None else int(p2lag)
         self.nslots = fpipe_plan(world, rank, max_frames)["nslots"]
         self.stride = -(-(e.h * e.w + 256) // 256) * 256
         self._planes, self._flags = ctypes.c_void_p(), ctypes.c_void_p()
@@ -473,16 +491,17 @@ class FramePipeRank:
                     arr([s.mae_num.data_ptr() for s in ss]), arr([s.recon.data_ptr() for s in ss]),
                     arr([s.sse.data_ptr() for s in ss]))
             land = (self._planes.value, self._flags.value, slot0, pplanes, pflags, p2planes, p2flags,
-                    (ctypes.c_int32 * n)(*plan["push"]), self.nslots, self.stride, ep, int(self.max_wg), st)
+                    (ctypes.c_int32 * n)(*plan["push"]), self.nslots, self.stride, ep, int(self.max_wg))
             curs = arr([frames[k].data_ptr() for k in ks])
             if two_pass:
                 _lib.check(lib.so_encode_p_run_fpipe_2pass(
                     curs, n, e.h, e.w, e.bs, e.sr, int(qp), _lib.ptr(qrd), _lib.ptr(roi_dev), int(qp_clamp[0]),
                     int(qp_clamp[1]), *outs, arr([s.extra["qp_map"].data_ptr() for s in ss]), self._ws.data_ptr(),
-                    *land), "so_encode_p_run_fpipe_2pass")
+                    *land, self.p2lag, st), "so_encode_p_run_fpipe_2pass")
             else:
                 _lib.check(lib.so_encode_p_run_fpipe2(curs, n, e.h, e.w, e.bs, e.sr, int(qp), _lib.ptr(qrd), int(e.vbs),
-                                                      e.lam, *outs, self._ws.data_ptr(), *land), "so_encode_p_run_fpipe2")
+                                                      e.lam, *outs, self._ws.data_ptr(), *land, st),
+                           "so_encode_p_run_fpipe2")
             for s in ss:
                 s.frame_type, s.qp_rd = 1, int(qp)
         for s in syms.values():

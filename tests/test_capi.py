@@ -161,6 +161,17 @@ def test_two_pass_run_and_frame_pipe_validation_without_gpu():
     assert fpipe(arr(fake[10], ctypes.c_void_p(land0 + stride)), [0, 2]) == _lib.SO_E_INVALID
     assert b"landing planes" in lib.so_last_error()
 
+    def fpipe2p(push, p2lag=0, lo=0, hi=12):
+        return lib.so_encode_p_run_fpipe_2pass(cur, n, H, W, 16, 16, 4, None, None, lo, hi, outs[0], outs[1], outs[2],
+                                               outs[3], outs[4], recon, None, qmap, ws, ctypes.c_void_p(land0),
+                                               land_flags, 0, fake[14], fake[15], fake[14], fake[15],
+                                               (ctypes.c_int32 * n)(*push), 3, stride, 1, 0, p2lag, None)
+    assert fpipe2p([0, 2], p2lag=-1) == _lib.SO_E_INVALID
+    assert b"p2lag" in lib.so_last_error()
+    assert fpipe2p([0, 2], lo=7, hi=3) == _lib.SO_E_INVALID
+    assert fpipe2p([0, 8]) == _lib.SO_E_INVALID
+    assert b"push_to[1]" in lib.so_last_error()
+
 
 def test_product_never_imports_the_oracle():
     pkg = os.path.join(ROOT, "streamoptima_amd")

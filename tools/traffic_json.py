@@ -71,7 +71,8 @@ doc["_note"] = ("per launch: hbm_bytes = calib_b32 * FETCH_SIZE * 1024 + WRITE_S
                 "bytes read / FETCH_SIZE bytes measured by tools/ubench_fetch.cpp; sq_* / grbm_* = SQ issue counters "
                 "per launch from one more pass")
 doc["_fetch_calibration"] = {"bytes_over_fetch_size": calib, "source": f"{base}/{tag}_calib"}
-doc[cfg] = {"source": f"{base}/{tag}_{cfg}_*", "kernels": per}
+keep = {k: v for k, v in doc.get(cfg, {}).items() if k not in ("source", "kernels")}   # e.g. phase splits
+doc[cfg] = {"source": f"{base}/{tag}_{cfg}_*", "kernels": per, **keep}
 json.dump(doc, open(out, "w"), indent=1, sort_keys=True)
 print("calibration", calib)
 for k, v in per.items():
