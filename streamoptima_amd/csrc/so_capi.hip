@@ -85,10 +85,10 @@ int inter_recon_launch(const RefSet& refs, const uint8_t* planes, size_t pstride
 int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int by0, int by1, int qp_rd,
                         const int32_t* qp_row, const int32_t* qp_map, int vbs, double lam, uint8_t* out_split, int16_t* out_mv,
                         int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon,
-                        int32_t* out_sse, int32_t* idres, hipStream_t st);
+                        int32_t* out_sse, uint8_t* idres, hipStream_t st);
 int intra_recon_launch(int H, int W, int bs, int sr, int qp, const int32_t* qp_row, const int32_t* qp_map,
                        const uint8_t* split,
-                       const int16_t* mv, const int16_t* qtc, uint8_t* out_recon, int32_t* idres,
+                       const int16_t* mv, const int16_t* qtc, uint8_t* out_recon, uint8_t* idres,
                        hipStream_t st);
 
 // ---- validation ------------------------------------------------------------------------------
@@ -811,7 +811,8 @@ int so_encode_i_rows(const uint8_t* cur, int H, int W, int bs, int sr, int by0, 
     SO_NEED(cur, fn); SO_NEED(out_split, fn); SO_NEED(out_mv, fn); SO_NEED(out_qtc, fn);
     SO_NEED(out_tokens, fn); SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn); SO_NEED(scratch, fn);
     return intra_encode_launch(cur, H, W, bs, sr, by0, by1, qp_rd, qp_row, nullptr, vbs, lam, out_split, out_mv, out_qtc,
-                               out_tokens, out_mae_num, out_recon, out_sse, scratch, (hipStream_t)stream);
+                               out_tokens, out_mae_num, out_recon, out_sse, reinterpret_cast<uint8_t*>(scratch),
+                               (hipStream_t)stream);
 }
 
 int so_encode_i_frame(const uint8_t* cur, int H, int W, int bs, int sr, int qp_rd, const int32_t* qp_row,
@@ -846,8 +847,8 @@ int so_intra_recon(int H, int W, int bs, int qp, const int32_t* qp_row, const ui
     SO_TRY(check_qp(fn, qp));
     SO_NEED(split, fn); SO_NEED(mv, fn); SO_NEED(qtc, fn); SO_NEED(out_recon, fn); SO_NEED(scratch, fn);
     // the recon kernel only needs sr to size its ring: the largest reachable offset is 64
-    return intra_recon_launch(H, W, bs, 64, qp, qp_row, nullptr, split, mv, qtc, out_recon, scratch,
-                              (hipStream_t)stream);
+    return intra_recon_launch(H, W, bs, 64, qp, qp_row, nullptr, split, mv, qtc, out_recon,
+                              reinterpret_cast<uint8_t*>(scratch), (hipStream_t)stream);
 }
 
 size_t so_fme_plane_stride(int H, int W) {
@@ -1001,7 +1002,8 @@ int so_encode_i_rows_ex(const uint8_t* cur, int H, int W, int bs, int sr, int by
     SO_NEED(cur, fn); SO_NEED(out_split, fn); SO_NEED(out_mv, fn); SO_NEED(out_qtc, fn);
     SO_NEED(out_tokens, fn); SO_NEED(out_mae_num, fn); SO_NEED(out_recon, fn); SO_NEED(scratch, fn);
     return intra_encode_launch(cur, H, W, bs, sr, by0, by1, qp_rd, qp_row, qp_map, vbs, lam, out_split, out_mv,
-                               out_qtc, out_tokens, out_mae_num, out_recon, out_sse, scratch, (hipStream_t)stream);
+                               out_qtc, out_tokens, out_mae_num, out_recon, out_sse, reinterpret_cast<uint8_t*>(scratch),
+                               (hipStream_t)stream);
 }
 
 int so_intra_recon_ex(int H, int W, int bs, int qp, const int32_t* qp_row, const int32_t* qp_map,
@@ -1012,8 +1014,8 @@ int so_intra_recon_ex(int H, int W, int bs, int qp, const int32_t* qp_row, const
     SO_TRY(check_intra_width(fn, W));
     SO_TRY(check_qp(fn, qp));
     SO_NEED(split, fn); SO_NEED(mv, fn); SO_NEED(qtc, fn); SO_NEED(out_recon, fn); SO_NEED(scratch, fn);
-    return intra_recon_launch(H, W, bs, 64, qp, qp_row, qp_map, split, mv, qtc, out_recon, scratch,
-                              (hipStream_t)stream);
+    return intra_recon_launch(H, W, bs, 64, qp, qp_row, qp_map, split, mv, qtc, out_recon,
+                              reinterpret_cast<uint8_t*>(scratch), (hipStream_t)stream);
 }
 
 int so_qp_map(const int32_t* tokens, int H, int W, int bs, int by0, int by1, int qp_rd, const int32_t* qp_row,

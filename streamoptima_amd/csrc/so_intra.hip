@@ -37,7 +37,7 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int by0, int nrow
                 uint8_t* __restrict__ out_split,
                 int16_t* __restrict__ out_mv, int16_t* __restrict__ out_qtc,
                 int32_t* __restrict__ out_tokens, int32_t* __restrict__ out_mae,
-                int32_t* __restrict__ idres) {
+                uint8_t* __restrict__ idres) {
     constexpr int G = BS, BPW = 256 / G, SB = BS / 2;
     constexpr int LDS_D = VBS ? 288 : BS * (BS + 1);
     __shared__ double ldsd[BPW * LDS_D];
@@ -225,7 +225,7 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int by0, int nrow
     }
 
     int tok;
-    int32_t* rb = idres + (size_t)b * BS * BS;
+    uint8_t* rb = idres + (size_t)b * BS * BS;
     if (!split) {
         if (qpr != qp_rd) quant_row_i<BS>(tc, l, qpr, q);
         tok = block_tokens<BS>(fl, l, q);
@@ -234,8 +234,11 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int by0, int nrow
         dequant_row_i<BS>(q, l, qpr, dq);
         double rd[BS];
         xform2d_rows<BS, true>(dl, l, dq, rd);
+        // residuals mod 256 (the reconstruction wraps to uint8: only the low byte matters)
+        int rr[BS];
 #pragma unroll
-        for (int c = 0; c < BS; ++c) rb[l * BS + c] = (int)__builtin_rint(rd[c]);
+        for (int c = 0; c < BS; ++c) rr[c] = (int)__builtin_rint(rd[c]);
+        store_row_u8<BS>(rb, BS, 0, l, rr);
         for (int k = l; k < 4; k += G) out_mv[(size_t)b * 4 + k] = (int16_t)(k == 0 ? mv : 0);
     } else {
         if constexpr (VBS) {
@@ -255,10 +258,12 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int by0, int nrow
             xform2d_sub<true>(dl, l, sdq, srd);
             // idres is row-major bs x bs for every block (intra_recon_kernel indexes pixels)
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
+            for (int h = 0; h < 2; ++h) {
+                int rr[SB];
 #pragma unroll
-                for (int c = 0; c < 8; ++c)
-                    rb[((j >> 1) * SB + r0 + 4 * h) * BS + (j & 1) * SB + c] = (int)__builtin_rint(srd[h][c]);
+                for (int c = 0; c < SB; ++c) rr[c] = (int)__builtin_rint(srd[h][c]);
+                store_row_u8<SB>(rb, BS, (j & 1) * SB, (j >> 1) * SB + r0 + 4 * h, rr);
+            }
             if (r0 == 0) out_mv[(size_t)b * 4 + j] = (int16_t)smv;
         } else {
             tok = 0;
@@ -276,7 +281,7 @@ template <int BS, bool VBS>
 __global__ void __launch_bounds__(256)
 dequant_idct_kernel(int H, int W, int qp, const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map,
                     const uint8_t* __restrict__ split, const int16_t* __restrict__ qtc,
-                    int32_t* __restrict__ idres) {
+                    uint8_t* __restrict__ idres) {
     constexpr int G = BS, BPW = 256 / G;
     constexpr int LDS_D = VBS ? 288 : BS * (BS + 1);
     __shared__ double ldsd[BPW * LDS_D];
@@ -287,15 +292,17 @@ dequant_idct_kernel(int H, int W, int qp, const int32_t* __restrict__ qp_row, co
     double* dl = ldsd + g * LDS_D;
     const int by = b / nbx;
     const int qpr = qp_map ? qp_map[b] : (qp_row ? qp_row[by] : qp);
-    int32_t* rb = idres + (size_t)b * BS * BS;
+    uint8_t* rb = idres + (size_t)b * BS * BS;
     if (!VBS || !split[b]) {
         int q[BS], dq[BS];
         load_row_i16<BS>(qtc + (size_t)b * BS * BS + l * BS, q);
         dequant_row<BS>(q, l, qpr, dq);
         double rd[BS];
         xform2d_rows<BS, true>(dl, l, dq, rd);
+        int rr[BS];   // mod 256, as intra_tq_kernel
 #pragma unroll
-        for (int c = 0; c < BS; ++c) rb[l * BS + c] = (int)__builtin_rint(rd[c]);
+        for (int c = 0; c < BS; ++c) rr[c] = (int)__builtin_rint(rd[c]);
+        store_row_u8<BS>(rb, BS, 0, l, rr);
     } else if constexpr (VBS) {
         const int j = l >> 2, r0 = l & 3;
         const int qpm1 = qpr > 0 ? qpr - 1 : qpr;
@@ -309,10 +316,12 @@ dequant_idct_kernel(int H, int W, int qp, const int32_t* __restrict__ qp_row, co
         double srd[2][8];
         xform2d_sub<true>(dl, l, sdq, srd);
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < 2; ++h) {
+            int rr[8];
 #pragma unroll
-            for (int c = 0; c < 8; ++c)
-                rb[((j >> 1) * 8 + r0 + 4 * h) * BS + (j & 1) * 8 + c] = (int)__builtin_rint(srd[h][c]);
+            for (int c = 0; c < 8; ++c) rr[c] = (int)__builtin_rint(srd[h][c]);
+            store_row_u8<8>(rb, BS, (j & 1) * 8, (j >> 1) * 8 + r0 + 4 * h, rr);
+        }
     }
 }
 
@@ -327,7 +336,7 @@ dequant_idct_kernel(int H, int W, int qp, const int32_t* __restrict__ qp_row, co
 template <int BS>
 __global__ void __launch_bounds__(256)
 intra_recon_kernel(int H, int W, int by0, const uint8_t* __restrict__ split, const int16_t* __restrict__ mv,
-                   const int32_t* __restrict__ idres, const uint8_t* __restrict__ cur,
+                   const uint8_t* __restrict__ idres, const uint8_t* __restrict__ cur,
                    uint8_t* __restrict__ out_recon, int32_t* __restrict__ out_sse) {
     constexpr int SB = BS / 2, NT = 256;
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];   // 12 * W bytes
@@ -394,7 +403,7 @@ intra_recon_kernel(int H, int W, int by0, const uint8_t* __restrict__ split, con
 template <int BS, bool NEAR>
 __global__ void __launch_bounds__(256)
 intra_recon_seq_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict__ split, const int16_t* __restrict__ mv,
-                       const int32_t* __restrict__ idres, const uint8_t* __restrict__ cur,
+                       const uint8_t* __restrict__ idres, const uint8_t* __restrict__ cur,
                        uint8_t* __restrict__ out_recon, int32_t* __restrict__ out_sse) {
     constexpr int SB = BS / 2, RPW = 64 / BS, RING = 128;
     __shared__ int ring[4 * RPW][RING];
@@ -495,7 +504,7 @@ intra_recon_seq_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict__
 
 // rows [0, nrows_px) of the stripe starting at block row by0: sequential kernel for sr <= 64
 static int intra_recon_rows(int W, int bs, int sr, int by0, int nrows_px, const uint8_t* split, const int16_t* mv,
-                            const int32_t* idres, const uint8_t* cur, uint8_t* out_recon, int32_t* out_sse, int H,
+                            const uint8_t* idres, const uint8_t* cur, uint8_t* out_recon, int32_t* out_sse, int H,
                             hipStream_t st) {
     if (nrows_px <= 0) return SO_OK;
     if (sr <= 64) {
@@ -526,7 +535,7 @@ static int intra_recon_rows(int W, int bs, int sr, int by0, int nrows_px, const 
 int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int by0, int by1, int qp_rd,
                         const int32_t* qp_row, const int32_t* qp_map, int vbs, double lam, uint8_t* out_split, int16_t* out_mv,
                         int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon,
-                        int32_t* out_sse, int32_t* idres, hipStream_t st) {
+                        int32_t* out_sse, uint8_t* idres, hipStream_t st) {
     const int nrows = by1 - by0;
     if (nrows <= 0) return SO_OK;
     const int nb = (W / bs) * nrows;
@@ -554,7 +563,7 @@ int intra_encode_launch(const uint8_t* cur, int H, int W, int bs, int sr, int by
 
 int intra_recon_launch(int H, int W, int bs, int sr, int qp, const int32_t* qp_row, const int32_t* qp_map,
                        const uint8_t* split,
-                       const int16_t* mv, const int16_t* qtc, uint8_t* out_recon, int32_t* idres,
+                       const int16_t* mv, const int16_t* qtc, uint8_t* out_recon, uint8_t* idres,
                        hipStream_t st) {
     const int nb = (W / bs) * (H / bs);
     const int bpw = 256 / bs;

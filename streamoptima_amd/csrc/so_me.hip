@@ -596,6 +596,10 @@ int me_fme_launch(const uint8_t* cur, const uint8_t* planes, size_t pstride, int
 #ifndef SO_SEA_CAP   // survivors per block evaluated from the list; more take the dense fallback
 #define SO_SEA_CAP 192
 #endif
+#ifndef SO_SEA_CAP_VBS   // the same for a VBS block's block / sub-block lists (sea_vbs_block): looser
+#define SO_SEA_CAP_VBS 384   // sub-block bounds leave more survivors (4K VBS P-run 161.5 -> 158.8 us,
+                             // dense blocks 8.9 -> 3.8 %; 768: 161.5, profiles/r03/r03n/vbs_ab.log)
+#endif
 #ifndef SO_PTILE_WPE16   // waves per SIMD of the 16-wave fused tile kernels (A/B builds only)
 #define SO_PTILE_WPE16 8
 #endif
@@ -618,7 +622,8 @@ struct Sea2GeoT {
     static constexpr int B4RS = B4NB * B4BAND;            // stored rows: whole bands, no bounds tests
     static constexpr int NBLK = TBX * TBY;
     static constexpr int NW = NW_, NTHREADS = NW * 64;
-    static constexpr int CAP = SO_SEA_CAP;
+    static constexpr int CAP = SO_SEA_CAP, CAPV = SO_SEA_CAP_VBS;
+    static constexpr int CAPL = CAP > CAPV ? CAP : CAPV;   // list entries per wave
     static constexpr int CPD = TPX / 4 + 1;               // current-tile pitch in dwords: 16 rows of
                                                           // one block column land on 16 banks
     static_assert(WD * B4NB <= NTHREADS, "byte-sum threads");
@@ -746,7 +751,7 @@ SO_DEV void vbs_eval_list(const Sea2Lds& L, const uint16_t* list, uint32_t n, in
 
 template <class G>
 SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
-    constexpr int NT = G::NT, B4P = G::B4P, CAP = G::CAP, RP = G::RP, CPD = G::CPD;
+    constexpr int NT = G::NT, B4P = G::B4P, CAP = G::CAPV, RP = G::RP, CPD = G::CPD;
     int lane = tid & 63;
     asm volatile("" : "+v"(lane));
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -834,7 +839,7 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
     const uint32_t qU = (U + 240) >> 4;
     int thr = (int)((qU << 16) | 0xFFFFu);
     asm volatile("" : "+v"(thr));
-    uint16_t* const mylist = L.list + wave * CAP;
+    uint16_t* const mylist = L.list + wave * G::CAPL;
     const int cbase = xi * 33 + 16 * hh;
     uint32_t nA = 0;
 #pragma unroll
@@ -1197,7 +1202,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             // write their candidates at the running count + the lane's rank in the ballot (no
             // per-lane bit loops, no LDS atomics).  Writes past CAP are dropped: that block
             // takes the dense fallback below.
-            uint16_t* mylist = list + wave * CAP;
+            uint16_t* mylist = list + wave * G::CAPL;
             const int cbase = xi * 33 + 16 * hh;
             uint32_t nsur = 0;
 #pragma unroll
@@ -1222,6 +1227,16 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
                 continue;
             }
             if (probe == 4) continue;
+            if (nsur == 1) {
+                // the smallest-bound candidate cs always survives (16 LBq(cs) - 240 <= SAD(cs) = U),
+                // so a lone survivor IS cs and its SAD is U: no second evaluation (the median
+                // block on textured content)
+                const int dx = cdx - 16, dy = cdi - 16;
+                const uint64_t key = me_key(U, (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)), (uint32_t)r,
+                                            (uint32_t)cs);
+                if (lane == 0 && key < keys[u]) keys[u] = key;
+                continue;
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1301,7 +1316,7 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
     __shared__ uint32_t b4w[(G::B4RS * B4P + 4) / 4];
     __shared__ uint32_t curt[G::TPY * G::CPD];
     __shared__ uint32_t a4[G::NBLK * 4];
-    __shared__ uint16_t list[G::NW * G::CAP];
+    __shared__ uint16_t list[G::NW * G::CAPL];
     __shared__ uint32_t lcount[G::NW];
     __shared__ unsigned long long keys[G::NBLK];
     __shared__ uint32_t st[2];
@@ -1363,7 +1378,7 @@ constexpr int kTqScratch = 16 * 17;
 template <class G>
 struct PTileGeo {
     static constexpr int B4 = (G::B4RS * G::B4P + 4) / 4;             // dwords
-    static constexpr int LIST = G::NW * G::CAP / 2;                   // dwords
+    static constexpr int LIST = G::NW * G::CAPL / 2;                  // dwords
     static constexpr int TQD = G::NBLK * kTqScratch;                  // doubles
     static constexpr int U64 = ((B4 + LIST + 1) / 2 > TQD) ? (B4 + LIST + 1) / 2 : TQD;
 };
