@@ -55,19 +55,36 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, de
     if out is None and not defines and not force and not _stale():
         return LIB_PATH
     tlib = _torch_lib_dir()
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
-           *[f"-D{d}" for d in defines],
-           "-I", os.path.join(os.path.dirname(PKG), "include"),
-           "-o", target + ".tmp", *sources(),
-           f"-L{tlib}", "-lamdhip64", f"-Wl,-rpath,{tlib}"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-6000:]}")
-    if verbose and r.stderr:
-        print(r.stderr[-4000:], file=sys.stderr)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+             "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
+             *[f"-D{d}" for d in defines],
+             "-I", os.path.join(os.path.dirname(PKG), "include")]
+    # one object per translation unit, compiled side by side (each .hip is self-contained:
+    # device code is shared only through headers), then one link
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+    srcs = sources()
+    with tempfile.TemporaryDirectory(prefix="so_build_") as tmp:
+        objs = [os.path.join(tmp, os.path.basename(s) + ".o") for s in srcs]
+        cmds = [[_hipcc(), *flags, "-c", s, "-o", o] for s, o in zip(srcs, objs)]
+        cmds.append([_hipcc(), f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", target + ".tmp", *objs,
+                     f"-L{tlib}", "-lamdhip64", f"-Wl,-rpath,{tlib}"])
+        jobs = max(1, min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+
+        def run(cmd):
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            return subprocess.run(cmd, capture_output=True, text=True)
+
+        with ThreadPoolExecutor(jobs) as ex:
+            results = list(ex.map(run, cmds[:-1]))
+        results.append(run(cmds[-1]) if all(r.returncode == 0 for r in results) else None)
+        for cmd, r in zip(cmds, results):
+            if r is not None and r.returncode != 0:
+                raise RuntimeError(f"hipcc failed ({r.returncode}) on {cmd[-3] if '-c' in cmd else 'link'}:\n"
+                                   f"{r.stderr[-6000:]}")
+            if verbose and r is not None and r.stderr:
+                print(r.stderr[-4000:], file=sys.stderr)
     os.replace(target + ".tmp", target)
     return target
 
