@@ -993,9 +993,25 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
         for (int q = 0; q < 4; ++q) sum = __builtin_amdgcn_sad_u8(curt[(rr + q) * G::CPD + m], 0u, sum);
         reinterpret_cast<uint8_t*>(a4)[i] = (uint8_t)(sum >> 4);
     }
+    // Blocks of the tile go to waves dynamically: wave w starts with block w, then takes the
+    // next unclaimed one (an LDS counter), so a wave stuck on a many-survivor or dense-fallback
+    // block no longer holds a second block back while the others wait at the barrier.
+    // (SO_SEA_STATIC: the fixed u = w, w + NW assignment, A/B builds only.)
+    uint32_t* const grab = L.lcount;
+    const auto next_block = [&](int u) -> int {
+#ifdef SO_SEA_STATIC
+        return u + G::NW;
+#else
+        (void)u;
+        uint32_t nx = 0;
+        if ((tid & 63) == 0) nx = __hip_atomic_fetch_add(grab, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return (int)__builtin_amdgcn_readfirstlane(nx);
+#endif
+    };
     for (int r = 0; r < nref; ++r) {
         const uint8_t* ref = refs.p[r];
         if (r == 0) pre();
+        if (tid == 0) *grab = (uint32_t)G::NW;   // read after the barrier below
         __syncthreads();
         if (r == 0) SO_SEA_STAMP(2, __builtin_amdgcn_s_memtime());
         if (win_int) {   // all loads first, then the LDS stores
@@ -1028,7 +1044,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
         if (probe == 5) continue;   // phase-attribution builds (SO_PROF_PHASE=2): no search at all
         if (dense_flag && __builtin_amdgcn_readfirstlane(*dense_flag)) {   // uniform: the whole tile dense
 #pragma unroll 1
-            for (int u = wave; u < G::NBLK; u += G::NW) {
+            for (int u = wave; u < G::NBLK; u = next_block(u)) {
                 const int bxl = u % TBX, byl = u / TBX;
                 if (bx0 + bxl >= nbx || byt0 + byl >= by1) continue;   // wave-uniform
                 const int x = x0 + bxl * 16, y = y0 + byl * 16;
@@ -1084,7 +1100,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
         if (r == 0) SO_SEA_STAMP(4, __builtin_amdgcn_s_memtime());
         if (probe == 1) continue;   // timing probe (tools/me_ab2.py): staging + byte sums only
 #pragma unroll 1
-        for (int u = wave; u < G::NBLK; u += G::NW) {
+        for (int u = wave; u < G::NBLK; u = next_block(u)) {
             const int bxl = u % TBX, byl = u / TBX;
             if (bx0 + bxl >= nbx || byt0 + byl >= by1) continue;   // wave-uniform
             const int x = x0 + bxl * 16, y = y0 + byl * 16;

@@ -7,7 +7,7 @@ import subprocess
 import sys
 
 CHILD = r'''
-import json, sys, time, torch
+import json, os, sys, time, torch
 sys.path.insert(0, ".")
 from streamoptima_amd.engine import Engine, alloc_planes
 from streamoptima_amd.synth import synth_sequence_torch
@@ -17,7 +17,7 @@ for h, w in ((2160, 3840), (1088, 1920), (272, 3840)):
     f = 30
     eng = Engine(h, w, 16, 16, False, 0.015, dev)
     fr = alloc_planes(f, h, w, dev)
-    fr.copy_(synth_sequence_torch(f, h, w, seed=0, device=dev))
+    fr.copy_(synth_sequence_torch(f, h, w, seed=0, device=dev, content=os.environ.get("SO_AB_CONTENT", "bench")))
     i0 = eng.encode_i(fr[0], 4)
     outs = [eng.new_symbols(1) for _ in range(f - 1)]
     ts = []
