@@ -15,7 +15,7 @@ dev = torch.device("cuda:0")
 out = {}
 for h, w in ((2160, 3840), (1088, 1920), (272, 3840)):
     f = 30
-    eng = Engine(h, w, 16, 16, False, 0.015, dev)
+    eng = Engine(h, w, 16, 16, os.environ.get("SO_AB_VBS") == "1", 0.015, dev)
     fr = alloc_planes(f, h, w, dev)
     fr.copy_(synth_sequence_torch(f, h, w, seed=0, device=dev, content=os.environ.get("SO_AB_CONTENT", "bench")))
     i0 = eng.encode_i(fr[0], 4)
