@@ -164,16 +164,31 @@ SO_DEV void load_row_i16(const int16_t* __restrict__ p, int* v) {
 // ---- 2-D transforms through LDS --------------------------------------------------------------
 // N x N transform of one block by N lanes (lane l owns row l on input and output).
 // lds: N rows of pitch N+1 doubles owned by this lane group.
+// Integer rows (T = int, N = 16: residuals forward, dequantised coefficients inverse) go through
+// the scratch as int32 and take dct2_16_i / dct3_16_i on axis 0: half the first transpose's
+// LDS bytes and the exact integer steps on the 2-cycle pipe.
 template <int N, bool INVERSE, class T>
 SO_DEV void xform2d_rows(double* lds, int l, const T* in_row, double* out_row) {
     constexpr int P = N + 1;
-#pragma unroll
-    for (int c = 0; c < N; ++c) lds[l * P + c] = (double)in_row[c];
-    wave_sync();
     double v[N];
+    if constexpr (N == 16 && __is_same(T, int)) {
+        int* const li = reinterpret_cast<int*>(lds);
 #pragma unroll
-    for (int r = 0; r < N; ++r) v[r] = lds[r * P + l];
-    if constexpr (INVERSE) dct::dct3<N>(v); else dct::dct2<N>(v);   // axis 0 (columns)
+        for (int c = 0; c < N; ++c) li[l * P + c] = in_row[c];
+        wave_sync();
+        int x[N];
+#pragma unroll
+        for (int r = 0; r < N; ++r) x[r] = li[r * P + l];
+        wave_sync();   // every lane's int reads before the doubles below overwrite them
+        if constexpr (INVERSE) dct::dct3_16_i(x, v); else dct::dct2_16_i(x, v);   // axis 0 (columns)
+    } else {
+#pragma unroll
+        for (int c = 0; c < N; ++c) lds[l * P + c] = (double)in_row[c];
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < N; ++r) v[r] = lds[r * P + l];
+        if constexpr (INVERSE) dct::dct3<N>(v); else dct::dct2<N>(v);   // axis 0 (columns)
+    }
 #pragma unroll
     for (int r = 0; r < N; ++r) lds[r * P + l] = v[r];
     wave_sync();
@@ -309,6 +324,13 @@ template <int N>
 SO_DEV void dequant_row_i(const int* q, int row, int qp, double* dq) {
 #pragma unroll
     for (int c = 0; c < N; ++c) dq[c] = __builtin_amdgcn_ldexp((double)q[c], q_exp_fast<N>(row, c, qp));
+}
+
+// QTC * Q as int32 (xform2d_rows' integer inverse path): |q| 2^k <= |TC| + 2^(k-1)
+template <int N>
+SO_DEV void dequant_row_int(const int* q, int row, int qp, int* dq) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) dq[c] = (int)((uint32_t)q[c] << q_exp_fast<N>(row, c, qp));
 }
 
 // Token count of an N x N block (N lanes, lane l owns row l) = nnz + number of maximal

@@ -306,6 +306,124 @@ SO_DEV void dct3(double* c) {
     }
 }
 
+// ---- integer inputs (the first pass of a 2-D transform) ------------------------------------
+// dct2<16> / dct3<16> of a vector of integers (residuals; dequantised coefficients).  An FP64
+// add, subtract or doubling of integers below 2^24 is exact, so every such step of the sequence
+// above is done in int32 (a 2-cycle VALU op on gfx950 against 4 for FP64) and its value
+// converted where it first meets a twiddle: the same doubles bit for bit, with as many
+// conversions as loading the 16 inputs as doubles took.  54 of dct2's FP64 ops and 14 of
+// dct3's move to the integer pipe.
+SO_DEV void dct2_16_i(const int (&x)[16], double (&c)[16]) {
+    using TW = TW16;
+    int y[16];   // T_dcst23 type-2 prelude
+    y[0] = 2 * x[0];
+    y[15] = 2 * x[15];
+#pragma unroll
+    for (int k = 1; k < 15; k += 2) {
+        y[k + 1] = x[k + 1] - x[k];
+        y[k] = x[k] + x[k + 1];
+    }
+    // radb4<4, 1>: CC(a, 0, c) = y[a + 4 c], CH(a, 0, c) = h[a + 4 c]; ih = the integer entries
+    int ih0, ih1, ih2, ih3, ih4, ih8, ih11, ih12;
+    double h5, h6, h7, h9, h10, h13, h14, h15;
+    {
+        const int tr2 = y[0] + y[15], tr1 = y[0] - y[15];
+        ih0 = tr2 + 2 * y[7];
+        ih8 = tr2 - 2 * y[7];
+        ih12 = tr1 + 2 * y[8];
+        ih4 = tr1 - 2 * y[8];
+    }
+    {
+        const int ti1 = y[12] + y[4], ti2 = y[12] - y[4];
+        const int tr2 = y[3] + y[11], tr1 = y[3] - y[11];
+        ih3 = tr2 + tr2;
+        h7 = kSqrt2 * (double)(tr1 - ti1);
+        ih11 = ti2 + ti2;
+        h15 = -kSqrt2 * (double)(tr1 + ti1);
+    }
+    {
+        const int tr2 = y[1] + y[13], tr1 = y[1] - y[13];
+        const int ti1 = y[2] + y[14], ti2 = y[2] - y[14];
+        const int tr4 = y[10] + y[6], ti3 = y[10] - y[6];
+        const int tr3 = y[9] + y[5], ti4 = y[9] - y[5];
+        ih1 = tr2 + tr3;
+        const double cr3 = (double)(tr2 - tr3);
+        ih2 = ti2 + ti3;
+        const double ci3 = (double)(ti2 - ti3);
+        const double cr4 = (double)(tr1 + tr4), cr2 = (double)(tr1 - tr4);
+        const double ci2 = (double)(ti1 + ti4), ci4 = (double)(ti1 - ti4);
+        h6 = TW::rf(0) * ci2 + TW::rf(1) * cr2;
+        h5 = TW::rf(0) * cr2 - TW::rf(1) * ci2;
+        h10 = TW::rf(3) * ci3 + TW::rf(4) * cr3;
+        h9 = TW::rf(3) * cr3 - TW::rf(4) * ci3;
+        h14 = TW::rf(6) * ci4 + TW::rf(7) * cr4;
+        h13 = TW::rf(6) * cr4 - TW::rf(7) * ci4;
+    }
+    // radb4<1, 4>: CC(0, b, k) = h[b + 4 k], CH(0, k, j) = c[k + 4 j]
+    {   // k = 0: all four inputs integers
+        const int tr2 = ih0 + ih3, tr1 = ih0 - ih3;
+        c[0] = (double)(tr2 + 2 * ih1);
+        c[8] = (double)(tr2 - 2 * ih1);
+        c[12] = (double)(tr1 + 2 * ih2);
+        c[4] = (double)(tr1 - 2 * ih2);
+    }
+    {   // k = 1
+        const double a = (double)ih4, tr2 = a + h7, tr1 = a - h7;
+        c[1] = __builtin_fma(2.0, h5, tr2);
+        c[9] = __builtin_fma(-2.0, h5, tr2);
+        c[13] = __builtin_fma(2.0, h6, tr1);
+        c[5] = __builtin_fma(-2.0, h6, tr1);
+    }
+    {   // k = 2
+        const double tr2 = (double)(ih8 + ih11), tr1 = (double)(ih8 - ih11);
+        c[2] = __builtin_fma(2.0, h9, tr2);
+        c[10] = __builtin_fma(-2.0, h9, tr2);
+        c[14] = __builtin_fma(2.0, h10, tr1);
+        c[6] = __builtin_fma(-2.0, h10, tr1);
+    }
+    {   // k = 3
+        const double a = (double)ih12, tr2 = a + h15, tr1 = a - h15;
+        c[3] = __builtin_fma(2.0, h13, tr2);
+        c[11] = __builtin_fma(-2.0, h13, tr2);
+        c[15] = __builtin_fma(2.0, h14, tr1);
+        c[7] = __builtin_fma(-2.0, h14, tr1);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) c[i] *= TW::fct;
+    // dct2's post-twiddles, unchanged
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+        const int kc = 16 - k;
+        const double ha = 0.5 * TW::dct(k - 1), hb = 0.5 * TW::dct(kc - 1);
+        double t1 = ha * c[kc] + hb * c[k];
+        double t2 = ha * c[k] - hb * c[kc];
+        c[k] = t1 + t2;
+        c[kc] = t1 - t2;
+    }
+    c[8] *= TW::dct(7);
+    c[0] *= kSqrt2 * 0.5;
+}
+
+SO_DEV void dct3_16_i(const int (&x)[16], double (&c)[16]) {
+    using TW = TW16;
+    c[0] = (double)x[0] * kSqrt2;
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+        const int kc = 16 - k;
+        const double t1 = (double)(x[k] + x[kc]), t2 = (double)(x[k] - x[kc]);
+        c[k] = TW::dct(k - 1) * t2 + TW::dct(kc - 1) * t1;
+        c[kc] = TW::dct(k - 1) * t1 - TW::dct(kc - 1) * t2;
+    }
+    c[8] = (double)x[8] * (2 * TW::dct(7));
+    Rfft<16>::forward(c);
+#pragma unroll
+    for (int k = 1; k < 15; k += 2) {
+        double t = c[k];
+        c[k] -= c[k + 1];
+        c[k + 1] += t;
+    }
+}
+
 #undef SO_PM
 #undef SO_MULPM
 

@@ -230,8 +230,8 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int by0, int nrow
         if (qpr != qp_rd) quant_row_i<BS>(tc, l, qpr, q);
         tok = block_tokens<BS>(fl, l, q);
         store_row_i16<BS>(out_qtc + (size_t)b * BS * BS + l * BS, q);
-        double dq[BS];
-        dequant_row_i<BS>(q, l, qpr, dq);
+        int dq[BS];
+        dequant_row_int<BS>(q, l, qpr, dq);
         double rd[BS];
         xform2d_rows<BS, true>(dl, l, dq, rd);
         // residuals mod 256 (the reconstruction wraps to uint8: only the low byte matters)

@@ -1496,8 +1496,9 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
             return;
         }
         store_row_i16<16>(o.qtc + b * 256 + l * 16, q);
-        double dq[16], rd[16];
-        dequant_row_i<16>(q, l, qpr, dq);
+        int dq[16];
+        double rd[16];
+        dequant_row_int<16>(q, l, qpr, dq);
         xform2d_rows<16, true>(dl, l, dq, rd);
         int rec[16];
         {
@@ -1743,8 +1744,9 @@ SO_DEV void tq16_vbs(PTileLds<G, true>& S, int g, int l, double* scratch, uint8_
         }
         tok = block_tokens<16>(nullptr, l, q);
         store_row_i16<16>(o.qtc + b * 256 + l * 16, q);
-        double dq[16], rd[16];
-        dequant_row_i<16>(q, l, qpr, dq);
+        int dq[16];
+        double rd[16];
+        dequant_row_int<16>(q, l, qpr, dq);
         xform2d_rows<16, true>(scratch, l, dq, rd);
         int rec[16];
         {
@@ -2029,8 +2031,9 @@ SO_DEV void tq16_pass2(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
                 uint64_t, __builtin_amdgcn_ldexp(__builtin_rint(tcr[c]), -q_exp_fast<16>(l, c, qpr)) + kRne);
         const int tok = block_tokens<16>(nullptr, l, q);
         store_row_i16<16>(o.qtc + b * 256 + l * 16, q);
-        double dq[16], rd[16];
-        dequant_row_i<16>(q, l, qpr, dq);
+        int dq[16];
+        double rd[16];
+        dequant_row_int<16>(q, l, qpr, dq);
         xform2d_rows<16, true>(scratch, l, dq, rd);
         int rec[16];
         {

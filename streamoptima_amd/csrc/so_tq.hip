@@ -126,9 +126,9 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, const uint8_t* __r
         tok = block_tokens<BS>(fl, l, q);
         store_row_i16<BS>(out_qtc + (size_t)b * BS * BS + l * BS, q);
         int rec[BS];
-        double dq[BS], rd[BS];
-        if constexpr (VBS) dequant_row_i<BS>(q, l, qpr, dq);
-        else dequant_row_d<BS>(qd, l, qpr, dq);
+        int dq[BS];
+        double rd[BS];
+        dequant_row_int<BS>(q, l, qpr, dq);
         xform2d_rows<BS, true>(dl, l, dq, rd);
 #pragma unroll
         for (int c = 0; c < BS; ++c) rec[c] = pred[c] + (int)__builtin_rint(rd[c]);
