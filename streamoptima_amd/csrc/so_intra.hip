@@ -502,11 +502,155 @@ intra_recon_seq_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict__
     }
 }
 
+// The same recurrence for sr <= BS as a chunked scan: one wave per pixel row, the row's nbx
+// blocks in K = 64 / BS chunks of L blocks, chunk k on lanes [k BS, (k + 1) BS).  Block j maps
+// the previous block's values to its own, v_j[c] = res_j[c] + (use_j[c] ? v_{j-1}[src_j(c)]
+// : 128), and such maps compose: over a chunk, v[c] = A[c] + (S[c] ? e[S[c] - 1] : 0) with e
+// the values entering the chunk (A mod 256 in bits 0-7, S in bits 8-12 of a 16-bit word).
+//   0. lane = block (64 blocks per pass, one row load of each): every pixel's (res, use, src)
+//      packed into the LDS slot of (block, column);
+//   1. each chunk composes its blocks' maps left to right, one ds_bpermute per block, and
+//      leaves the prefix map after every block in its slot;
+//   2. the chunks' end values, in order (K - 1 dependent ds_bpermutes);
+//   3. every block applies its prefix map to the values entering its chunk (independent),
+//      into an LDS copy of the pixel row;
+//   4. the row out in 16-byte stores, its SSE from 16-byte loads of the current row.
+// L + K dependent steps instead of nbx (4K: 64 instead of 240); arithmetic mod 256 as above.
+template <int BS>
+__global__ void __launch_bounds__(64)
+intra_recon_scan_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict__ split, const int16_t* __restrict__ mv,
+                        const uint8_t* __restrict__ idres, const uint8_t* __restrict__ cur,
+                        uint8_t* __restrict__ out_recon, int32_t* __restrict__ out_sse) {
+    constexpr int K = 64 / BS, SB = BS / 2, ND = BS / 4, TU = 4;
+    extern __shared__ __attribute__((aligned(16))) uint16_t slot[];   // [L][64], then the pixel row
+    const int lane = threadIdx.x;
+    const int k = lane / BS, c = lane - k * BS;
+    const int yl = blockIdx.x;
+    const int yy = by0 * BS + yl, byl = yl / BS, i = yl - byl * BS, nbx = W / BS;
+    const int L = (nbx + K - 1) / K, j0 = k * L;
+    const bool lower = i >= SB;
+    uint8_t* const rowb = reinterpret_cast<uint8_t*>(slot + (size_t)L * 64);
+    // ---- 0. inputs, a block per lane -------------------------------------------------------
+    for (int t0 = 0; t0 * 64 < nbx; t0 += TU) {
+        uint32_t rw[TU][ND], mw[TU][2], sp[TU];
+#pragma unroll
+        for (int t = 0; t < TU; ++t) {
+            int jb = (t0 + t) * 64 + lane;
+            jb = jb < nbx ? jb : nbx - 1;
+            const size_t b = (size_t)byl * nbx + jb;
+            const uint32_t* rp = reinterpret_cast<const uint32_t*>(idres + b * BS * BS + i * BS);
+#pragma unroll
+            for (int d = 0; d < ND; ++d) rw[t][d] = rp[d];
+            const uint2 m4 = *reinterpret_cast<const uint2*>(mv + b * 4);
+            mw[t][0] = m4.x;
+            mw[t][1] = m4.y;
+            sp[t] = split[b];
+        }
+#pragma unroll
+        for (int t = 0; t < TU; ++t) {
+            const int jb = (t0 + t) * 64 + lane;
+            if (jb < nbx) {
+                // dx of the left / right half of this pixel row (the block's, or its sub-blocks')
+                const uint32_t wl = (sp[t] && lower) ? mw[t][1] : mw[t][0];
+                const int dxl = (int)(int16_t)(wl & 0xFFFF);
+                const int dxr = sp[t] ? (int)(int16_t)(wl >> 16) : dxl;
+                const int kq = jb / L, s = jb - kq * L;
+                uint32_t pk[BS / 2];
+#pragma unroll
+                for (int cc = 0; cc < BS; ++cc) {
+                    const int rel = cc + (cc >= SB ? dxr : dxl);
+                    const bool use = jb != 0 && rel < 0;
+                    const uint32_t v = ((rw[t][cc >> 2] >> (8 * (cc & 3))) & 255u) | (use ? 256u : 0u) |
+                                       ((uint32_t)((rel + BS) & (BS - 1)) << 9);
+                    pk[cc >> 1] = (cc & 1) ? (pk[cc >> 1] | (v << 16)) : v;
+                }
+                uint4* dst = reinterpret_cast<uint4*>(slot + (size_t)s * 64 + kq * BS);
+#pragma unroll
+                for (int q = 0; q < BS / 8; ++q) dst[q] = make_uint4(pk[4 * q], pk[4 * q + 1], pk[4 * q + 2], pk[4 * q + 3]);
+            }
+        }
+    }
+    __syncthreads();
+    // ---- 1. prefix maps per chunk ------------------------------------------------------------
+    // (slots past nbx hold stale words: they compose too, but `wl` keeps the map after the
+    // chunk's last valid block and step 3 stores nothing for them)
+    const int gbase = lane & ~(BS - 1);
+    uint32_t w = (uint32_t)(c + 1) << 8;   // identity: A = 0, S = c + 1
+    uint32_t wl = w;
+    const int nvalid = nbx - j0 < L ? (nbx - j0 > 0 ? nbx - j0 : 0) : L;
+    uint32_t in = slot[lane];
+    for (int s = 0; s < nvalid; ++s) {
+        const uint32_t cin = in;
+        if (s + 1 < nvalid) in = slot[(s + 1) * 64 + lane];
+        const uint32_t g = (uint32_t)__builtin_amdgcn_ds_bpermute((gbase + (int)(cin >> 9)) << 2, (int)w);
+        const bool use = (cin & 256u) != 0u;
+        w = ((cin + (use ? g : 128u)) & 255u) | (use ? (g & 0x1F00u) : 0u);
+        slot[s * 64 + lane] = (uint16_t)w;
+    }
+    wl = w;
+    // ---- 2. values leaving each chunk ----------------------------------------------------------
+    // chunk 0 starts at block 0, where nothing has a source: its maps are constants
+    uint32_t cv = wl & 255u;
+#pragma unroll
+    for (int kk = 1; kk < K; ++kk) {
+        const uint32_t si = (wl >> 8) & 31u;
+        const int addr = ((kk - 1) * BS + (int)(si ? si - 1 : 0)) << 2;
+        const uint32_t g = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)cv);
+        if (k == kk && si) cv = ((wl & 255u) + g) & 255u;
+    }
+    // ---- 3. every pixel, into the LDS row ------------------------------------------------------
+    const int ebase = (k > 0 ? k - 1 : 0) * BS;
+    for (int s = 0; s < nvalid; ++s) {
+        const uint32_t m = slot[s * 64 + lane];
+        const uint32_t si = (m >> 8) & 31u;
+        const uint32_t e = (uint32_t)__builtin_amdgcn_ds_bpermute((ebase + (int)(si ? si - 1 : 0)) << 2, (int)cv);
+        rowb[(j0 + s) * BS + c] = (uint8_t)((m + (si ? e : 0u)) & 255u);
+    }
+    __syncthreads();
+    // ---- 4. the row out, its SSE ----------------------------------------------------------------
+    const uint8_t* crow = cur ? cur + (size_t)yy * W : nullptr;
+    uint8_t* orow = out_recon + (size_t)yy * W;
+    int sse = 0;
+    for (int x0 = lane * 16; x0 < W; x0 += 64 * 16) {
+        const uint4 r = *reinterpret_cast<const uint4*>(rowb + x0);
+        *reinterpret_cast<uint4*>(orow + x0) = r;
+        if (crow) {
+            const uint4 q = *reinterpret_cast<const uint4*>(crow + x0);
+            const uint32_t rr[4] = {r.x, r.y, r.z, r.w}, qq[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int d = 0; d < 4; ++d)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int df = (int)((qq[d] >> (8 * e)) & 255u) - (int)((rr[d] >> (8 * e)) & 255u);
+                    sse += df * df;
+                }
+        }
+    }
+    if (out_sse) {
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) sse += __shfl_xor(sse, m, 64);
+        if (lane == 0) out_sse[yl] = sse;
+    }
+}
+
 // rows [0, nrows_px) of the stripe starting at block row by0: sequential kernel for sr <= 64
 static int intra_recon_rows(int W, int bs, int sr, int by0, int nrows_px, const uint8_t* split, const int16_t* mv,
                             const uint8_t* idres, const uint8_t* cur, uint8_t* out_recon, int32_t* out_sse, int H,
                             hipStream_t st) {
     if (nrows_px <= 0) return SO_OK;
+#ifndef SO_IRS_SEQ   // A/B builds: the sequential walk for sr <= bs too
+    if (sr <= bs && W % 16 == 0) {   // (16-byte row stores)
+        const int k = 64 / bs, nbx = W / bs, L = (nbx + k - 1) / k;
+        const size_t lds = (size_t)L * 64 * sizeof(uint16_t) + (size_t)W;
+        if (bs == 16)
+            hipLaunchKernelGGL(intra_recon_scan_kernel<16>, dim3(nrows_px), dim3(64), lds, st, W, nrows_px, by0, split,
+                               mv, idres, cur, out_recon, out_sse);
+        else
+            hipLaunchKernelGGL(intra_recon_scan_kernel<8>, dim3(nrows_px), dim3(64), lds, st, W, nrows_px, by0, split,
+                               mv, idres, cur, out_recon, out_sse);
+        return check_launch("intra_recon_scan_kernel");
+    }
+#endif
     if (sr <= 64) {
         // SO_IRS_WPB waves per workgroup (the kernel is a latency chain per wave; 1 spreads
         // the 4K I-frame's 540 waves over all 256 CUs instead of 135)
