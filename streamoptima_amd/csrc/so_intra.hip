@@ -502,40 +502,45 @@ intra_recon_seq_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict__
     }
 }
 
-// The same recurrence for sr <= BS as a chunked scan: one wave per pixel row, the row's nbx
-// blocks in K = 64 / BS chunks of L blocks, chunk k on lanes [k BS, (k + 1) BS).  Block j maps
-// the previous block's values to its own, v_j[c] = res_j[c] + (use_j[c] ? v_{j-1}[src_j(c)]
-// : 128), and such maps compose: over a chunk, v[c] = A[c] + (S[c] ? e[S[c] - 1] : 0) with e
-// the values entering the chunk (A mod 256 in bits 0-7, S in bits 8-12 of a 16-bit word).
-//   0. lane = block (64 blocks per pass, one row load of each): every pixel's (res, use, src)
-//      packed into the LDS slot of (block, column);
+// The same recurrence for sr <= BS as a chunked scan: WPR waves per pixel row, the row's nbx
+// blocks in K = 64 WPR / BS chunks of L blocks, chunk k on threads [k BS, (k + 1) BS).  Block j
+// maps the previous block's values to its own, v_j[c] = res_j[c] + (use_j[c] ?
+// v_{j-1}[src_j(c)] : 128), and such maps compose: over a chunk, v[c] = A[c] + (S[c] ?
+// e[S[c] - 1] : 0) with e the values entering the chunk (A mod 256 in bits 0-7, S in bits 8-12
+// of a 16-bit word).
+//   0. thread = block (64 WPR blocks per pass, one row load of each): every pixel's
+//      (res, use, src) packed into the LDS slot of (block, column);
 //   1. each chunk composes its blocks' maps left to right, one ds_bpermute per block, and
 //      leaves the prefix map after every block in its slot;
-//   2. the chunks' end values, in order (K - 1 dependent ds_bpermutes);
+//   2. the chunk maps composed over each wave's chunks (GPW - 1 ds_bpermute steps), then the
+//      waves' end values in order through LDS (WPR - 1 barriers): the values leaving every chunk;
 //   3. every block applies its prefix map to the values entering its chunk (independent),
 //      into an LDS copy of the pixel row;
 //   4. the row out in 16-byte stores, its SSE from 16-byte loads of the current row.
-// L + K dependent steps instead of nbx (4K: 64 instead of 240); arithmetic mod 256 as above.
-template <int BS>
-__global__ void __launch_bounds__(64)
+// L + GPW + WPR dependent steps instead of nbx (4K, WPR 2: 30 + 4 + 2 instead of 240);
+// arithmetic mod 256 as above.
+template <int BS, int WPR>
+__global__ void __launch_bounds__(64 * WPR)
 intra_recon_scan_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict__ split, const int16_t* __restrict__ mv,
                         const uint8_t* __restrict__ idres, const uint8_t* __restrict__ cur,
                         uint8_t* __restrict__ out_recon, int32_t* __restrict__ out_sse) {
-    constexpr int K = 64 / BS, SB = BS / 2, ND = BS / 4, TU = 4;
-    extern __shared__ __attribute__((aligned(16))) uint16_t slot[];   // [L][64], then the pixel row
-    const int lane = threadIdx.x;
-    const int k = lane / BS, c = lane - k * BS;
+    constexpr int NT = 64 * WPR, K = NT / BS, GPW = 64 / BS, SB = BS / 2, ND = BS / 4, TU = 4, U3 = 4;
+    extern __shared__ __attribute__((aligned(16))) uint16_t slot[];   // [L][NT], ev[NT], the pixel row
+    __shared__ int ssum[WPR];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int k = tid / BS, c = tid - k * BS, g = k - wv * GPW;
     const int yl = blockIdx.x;
     const int yy = by0 * BS + yl, byl = yl / BS, i = yl - byl * BS, nbx = W / BS;
     const int L = (nbx + K - 1) / K, j0 = k * L;
     const bool lower = i >= SB;
-    uint8_t* const rowb = reinterpret_cast<uint8_t*>(slot + (size_t)L * 64);
-    // ---- 0. inputs, a block per lane -------------------------------------------------------
-    for (int t0 = 0; t0 * 64 < nbx; t0 += TU) {
+    uint32_t* const ev = reinterpret_cast<uint32_t*>(slot + (size_t)L * NT);
+    uint8_t* const rowb = reinterpret_cast<uint8_t*>(ev + NT);
+    // ---- 0. inputs, a block per thread ------------------------------------------------------
+    for (int t0 = 0; t0 * NT < nbx; t0 += TU) {
         uint32_t rw[TU][ND], mw[TU][2], sp[TU];
 #pragma unroll
         for (int t = 0; t < TU; ++t) {
-            int jb = (t0 + t) * 64 + lane;
+            int jb = (t0 + t) * NT + tid;
             jb = jb < nbx ? jb : nbx - 1;
             const size_t b = (size_t)byl * nbx + jb;
             const uint32_t* rp = reinterpret_cast<const uint32_t*>(idres + b * BS * BS + i * BS);
@@ -548,12 +553,12 @@ intra_recon_scan_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict_
         }
 #pragma unroll
         for (int t = 0; t < TU; ++t) {
-            const int jb = (t0 + t) * 64 + lane;
+            const int jb = (t0 + t) * NT + tid;
             if (jb < nbx) {
                 // dx of the left / right half of this pixel row (the block's, or its sub-blocks')
-                const uint32_t wl = (sp[t] && lower) ? mw[t][1] : mw[t][0];
-                const int dxl = (int)(int16_t)(wl & 0xFFFF);
-                const int dxr = sp[t] ? (int)(int16_t)(wl >> 16) : dxl;
+                const uint32_t wlr = (sp[t] && lower) ? mw[t][1] : mw[t][0];
+                const int dxl = (int)(int16_t)(wlr & 0xFFFF);
+                const int dxr = sp[t] ? (int)(int16_t)(wlr >> 16) : dxl;
                 const int kq = jb / L, s = jb - kq * L;
                 uint32_t pk[BS / 2];
 #pragma unroll
@@ -564,7 +569,7 @@ intra_recon_scan_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict_
                                        ((uint32_t)((rel + BS) & (BS - 1)) << 9);
                     pk[cc >> 1] = (cc & 1) ? (pk[cc >> 1] | (v << 16)) : v;
                 }
-                uint4* dst = reinterpret_cast<uint4*>(slot + (size_t)s * 64 + kq * BS);
+                uint4* dst = reinterpret_cast<uint4*>(slot + (size_t)s * NT + kq * BS);
 #pragma unroll
                 for (int q = 0; q < BS / 8; ++q) dst[q] = make_uint4(pk[4 * q], pk[4 * q + 1], pk[4 * q + 2], pk[4 * q + 3]);
             }
@@ -572,46 +577,58 @@ intra_recon_scan_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict_
     }
     __syncthreads();
     // ---- 1. prefix maps per chunk ------------------------------------------------------------
-    // (slots past nbx hold stale words: they compose too, but `wl` keeps the map after the
-    // chunk's last valid block and step 3 stores nothing for them)
     const int gbase = lane & ~(BS - 1);
-    uint32_t w = (uint32_t)(c + 1) << 8;   // identity: A = 0, S = c + 1
-    uint32_t wl = w;
     const int nvalid = nbx - j0 < L ? (nbx - j0 > 0 ? nbx - j0 : 0) : L;
-    uint32_t in = slot[lane];
+    uint32_t w = (uint32_t)(c + 1) << 8;   // identity: A = 0, S = c + 1
+    uint32_t in = slot[tid];
     for (int s = 0; s < nvalid; ++s) {
         const uint32_t cin = in;
-        if (s + 1 < nvalid) in = slot[(s + 1) * 64 + lane];
-        const uint32_t g = (uint32_t)__builtin_amdgcn_ds_bpermute((gbase + (int)(cin >> 9)) << 2, (int)w);
+        if (s + 1 < nvalid) in = slot[(s + 1) * NT + tid];
+        const uint32_t gv = (uint32_t)__builtin_amdgcn_ds_bpermute((gbase + (int)(cin >> 9)) << 2, (int)w);
         const bool use = (cin & 256u) != 0u;
-        w = ((cin + (use ? g : 128u)) & 255u) | (use ? (g & 0x1F00u) : 0u);
-        slot[s * 64 + lane] = (uint16_t)w;
+        w = ((cin + (use ? gv : 128u)) & 255u) | (use ? (gv & 0x1F00u) : 0u);
+        slot[s * NT + tid] = (uint16_t)w;
     }
-    wl = w;
     // ---- 2. values leaving each chunk ----------------------------------------------------------
-    // chunk 0 starts at block 0, where nothing has a source: its maps are constants
-    uint32_t cv = wl & 255u;
+    // the chunk maps composed over the wave's groups: P maps the values entering the wave's
+    // first chunk to those leaving this one
+    uint32_t P = w;
 #pragma unroll
-    for (int kk = 1; kk < K; ++kk) {
-        const uint32_t si = (wl >> 8) & 31u;
-        const int addr = ((kk - 1) * BS + (int)(si ? si - 1 : 0)) << 2;
-        const uint32_t g = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)cv);
-        if (k == kk && si) cv = ((wl & 255u) + g) & 255u;
+    for (int gg = 1; gg < GPW; ++gg) {
+        const uint32_t si = (w >> 8) & 31u;
+        const uint32_t pg = (uint32_t)__builtin_amdgcn_ds_bpermute(((gg - 1) * BS + (int)(si ? si - 1 : 0)) << 2, (int)P);
+        if (g == gg) P = ((w + (si ? pg : 0u)) & 255u) | (si ? (pg & 0x1F00u) : 0u);
+    }
+    // wave 0 starts at block 0, where nothing has a source: its P are constants; wave ww takes
+    // the values leaving wave ww-1's last chunk
+#pragma unroll
+    for (int ww = 0; ww < WPR; ++ww) {
+        if (wv == ww) {
+            const uint32_t si = (P >> 8) & 31u;
+            const uint32_t e = (ww > 0 && si) ? ev[(ww * GPW - 1) * BS + si - 1] : 0u;
+            ev[tid] = (P + e) & 255u;
+        }
+        __syncthreads();
     }
     // ---- 3. every pixel, into the LDS row ------------------------------------------------------
-    const int ebase = (k > 0 ? k - 1 : 0) * BS;
-    for (int s = 0; s < nvalid; ++s) {
-        const uint32_t m = slot[s * 64 + lane];
-        const uint32_t si = (m >> 8) & 31u;
-        const uint32_t e = (uint32_t)__builtin_amdgcn_ds_bpermute((ebase + (int)(si ? si - 1 : 0)) << 2, (int)cv);
-        rowb[(j0 + s) * BS + c] = (uint8_t)((m + (si ? e : 0u)) & 255u);
+    const uint32_t* const ein = ev + (k > 0 ? k - 1 : 0) * BS - 1;
+    for (int s0 = 0; s0 < nvalid; s0 += U3) {
+        uint32_t m[U3];
+#pragma unroll
+        for (int u = 0; u < U3; ++u) m[u] = s0 + u < nvalid ? slot[(s0 + u) * NT + tid] : 0u;
+#pragma unroll
+        for (int u = 0; u < U3; ++u) {
+            const uint32_t si = (m[u] >> 8) & 31u;
+            const uint32_t e = si ? ein[si] : 0u;
+            if (s0 + u < nvalid) rowb[(j0 + s0 + u) * BS + c] = (uint8_t)((m[u] + e) & 255u);
+        }
     }
     __syncthreads();
     // ---- 4. the row out, its SSE ----------------------------------------------------------------
     const uint8_t* crow = cur ? cur + (size_t)yy * W : nullptr;
     uint8_t* orow = out_recon + (size_t)yy * W;
     int sse = 0;
-    for (int x0 = lane * 16; x0 < W; x0 += 64 * 16) {
+    for (int x0 = tid * 16; x0 < W; x0 += NT * 16) {
         const uint4 r = *reinterpret_cast<const uint4*>(rowb + x0);
         *reinterpret_cast<uint4*>(orow + x0) = r;
         if (crow) {
@@ -629,7 +646,14 @@ intra_recon_scan_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict_
     if (out_sse) {
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) sse += __shfl_xor(sse, m, 64);
-        if (lane == 0) out_sse[yl] = sse;
+        if (lane == 0) ssum[wv] = sse;
+        __syncthreads();
+        if (tid == 0) {
+            int t = 0;
+#pragma unroll
+            for (int ww = 0; ww < WPR; ++ww) t += ssum[ww];
+            out_sse[yl] = t;
+        }
     }
 }
 
@@ -640,14 +664,18 @@ static int intra_recon_rows(int W, int bs, int sr, int by0, int nrows_px, const 
     if (nrows_px <= 0) return SO_OK;
 #ifndef SO_IRS_SEQ   // A/B builds: the sequential walk for sr <= bs too
     if (sr <= bs && W % 16 == 0) {   // (16-byte row stores)
-        const int k = 64 / bs, nbx = W / bs, L = (nbx + k - 1) / k;
-        const size_t lds = (size_t)L * 64 * sizeof(uint16_t) + (size_t)W;
+#ifndef SO_IRS_WPR   // waves per pixel row of the scan
+#define SO_IRS_WPR 4
+#endif
+        constexpr int WPR = SO_IRS_WPR, NT = 64 * WPR;
+        const int k = NT / bs, nbx = W / bs, L = (nbx + k - 1) / k;
+        const size_t lds = (size_t)L * NT * sizeof(uint16_t) + NT * sizeof(uint32_t) + (size_t)W;
         if (bs == 16)
-            hipLaunchKernelGGL(intra_recon_scan_kernel<16>, dim3(nrows_px), dim3(64), lds, st, W, nrows_px, by0, split,
-                               mv, idres, cur, out_recon, out_sse);
+            hipLaunchKernelGGL((intra_recon_scan_kernel<16, WPR>), dim3(nrows_px), dim3(NT), lds, st, W, nrows_px, by0,
+                               split, mv, idres, cur, out_recon, out_sse);
         else
-            hipLaunchKernelGGL(intra_recon_scan_kernel<8>, dim3(nrows_px), dim3(64), lds, st, W, nrows_px, by0, split,
-                               mv, idres, cur, out_recon, out_sse);
+            hipLaunchKernelGGL((intra_recon_scan_kernel<8, WPR>), dim3(nrows_px), dim3(NT), lds, st, W, nrows_px, by0,
+                               split, mv, idres, cur, out_recon, out_sse);
         return check_launch("intra_recon_scan_kernel");
     }
 #endif
