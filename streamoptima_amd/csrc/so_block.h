@@ -237,24 +237,48 @@ SO_DEV void xform2d_rows_half(double* lds, int l, const T* in_row, double* out_r
 
 // Four 8x8 sub-blocks by 16 lanes: lane l owns sub-block j = l >> 2 and rows
 // (l & 3), (l & 3) + 4 on input and output.  lds: 4 x 8 x 9 doubles.
+// Integer rows (T = int) go through the scratch as int32 and take dct2_8_i / dct3_8_i on the
+// column pass, as xform2d_rows<16> does.
 template <bool INVERSE, class T>
 SO_DEV void xform2d_sub(double* lds, int l, const T (&in)[2][8], double (&out)[2][8]) {
     const int j = l >> 2, r0 = l & 3;
     double* s = lds + j * 72;
+    if constexpr (__is_same(T, int)) {
+        int* const si = reinterpret_cast<int*>(s);
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int c = 0; c < 8; ++c) s[(r0 + 4 * h) * 9 + c] = (double)in[h][c];
-    wave_sync();
+            for (int c = 0; c < 8; ++c) si[(r0 + 4 * h) * 9 + c] = in[h][c];
+        wave_sync();
+        int x[2][8];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        double v[8];
-        const int col = r0 + 4 * h;
+        for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int r = 0; r < 8; ++r) v[r] = s[r * 9 + col];
-        if constexpr (INVERSE) dct::dct3<8>(v); else dct::dct2<8>(v);
+            for (int r = 0; r < 8; ++r) x[h][r] = si[r * 9 + r0 + 4 * h];
+        wave_sync();   // every lane's int reads before the doubles below overwrite them
 #pragma unroll
-        for (int r = 0; r < 8; ++r) s[r * 9 + col] = v[r];
+        for (int h = 0; h < 2; ++h) {
+            double v[8];
+            if constexpr (INVERSE) dct::dct3_8_i(x[h], v); else dct::dct2_8_i(x[h], v);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) s[r * 9 + r0 + 4 * h] = v[r];
+        }
+    } else {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int c = 0; c < 8; ++c) s[(r0 + 4 * h) * 9 + c] = (double)in[h][c];
+        wave_sync();
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            double v[8];
+            const int col = r0 + 4 * h;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = s[r * 9 + col];
+            if constexpr (INVERSE) dct::dct3<8>(v); else dct::dct2<8>(v);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) s[r * 9 + col] = v[r];
+        }
     }
     wave_sync();
 #pragma unroll

@@ -424,6 +424,75 @@ SO_DEV void dct3_16_i(const int (&x)[16], double (&c)[16]) {
     }
 }
 
+// The same for N = 8 (the VBS sub-blocks): rfftp [2, 4]; 24 of dct2<8>'s FP64 ops and 6 of
+// dct3<8>'s move to int32.
+SO_DEV void dct2_8_i(const int (&x)[8], double (&c)[8]) {
+    using TW = TW8;
+    int y[8];
+    y[0] = 2 * x[0];
+    y[7] = 2 * x[7];
+#pragma unroll
+    for (int k = 1; k < 7; k += 2) {
+        y[k + 1] = x[k + 1] - x[k];
+        y[k] = x[k] + x[k + 1];
+    }
+    // radb2<4, 1>: CC(a, b, 0) = y[a + 4 b], CH(a, 0, c) = h[a + 4 c]
+    const int ih0 = y[0] + y[7], ih4 = y[0] - y[7];
+    const int ih3 = 2 * y[3], ih7 = -2 * y[4];
+    const int ih1 = y[1] + y[5], tr2 = y[1] - y[5];
+    const int ti2 = y[2] + y[6], ih2 = y[2] - y[6];
+    const double h6 = TW::rf(0) * (double)ti2 + TW::rf(1) * (double)tr2;
+    const double h5 = TW::rf(0) * (double)tr2 - TW::rf(1) * (double)ti2;
+    // radb4<1, 2>: CC(0, b, k) = h[b + 4 k], CH(0, k, j) = c[k + 2 j]
+    {   // k = 0: all four inputs integers
+        const int t2 = ih0 + ih3, t1 = ih0 - ih3;
+        c[0] = (double)(t2 + 2 * ih1);
+        c[4] = (double)(t2 - 2 * ih1);
+        c[6] = (double)(t1 + 2 * ih2);
+        c[2] = (double)(t1 - 2 * ih2);
+    }
+    {   // k = 1: h[4], h[7] integers, h[5], h[6] not
+        const double t2 = (double)(ih4 + ih7), t1 = (double)(ih4 - ih7);
+        c[1] = __builtin_fma(2.0, h5, t2);
+        c[5] = __builtin_fma(-2.0, h5, t2);
+        c[7] = __builtin_fma(2.0, h6, t1);
+        c[3] = __builtin_fma(-2.0, h6, t1);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c[i] *= TW::fct;
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+        const int kc = 8 - k;
+        const double ha = 0.5 * TW::dct(k - 1), hb = 0.5 * TW::dct(kc - 1);
+        double t1 = ha * c[kc] + hb * c[k];
+        double t2 = ha * c[k] - hb * c[kc];
+        c[k] = t1 + t2;
+        c[kc] = t1 - t2;
+    }
+    c[4] *= TW::dct(3);
+    c[0] *= kSqrt2 * 0.5;
+}
+
+SO_DEV void dct3_8_i(const int (&x)[8], double (&c)[8]) {
+    using TW = TW8;
+    c[0] = (double)x[0] * kSqrt2;
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+        const int kc = 8 - k;
+        const double t1 = (double)(x[k] + x[kc]), t2 = (double)(x[k] - x[kc]);
+        c[k] = TW::dct(k - 1) * t2 + TW::dct(kc - 1) * t1;
+        c[kc] = TW::dct(k - 1) * t1 - TW::dct(kc - 1) * t2;
+    }
+    c[4] = (double)x[4] * (2 * TW::dct(3));
+    Rfft<8>::forward(c);
+#pragma unroll
+    for (int k = 1; k < 7; k += 2) {
+        double t = c[k];
+        c[k] -= c[k + 1];
+        c[k + 1] += t;
+    }
+}
+
 #undef SO_PM
 #undef SO_MULPM
 

@@ -1784,11 +1784,11 @@ SO_DEV void tq16_vbs(PTileLds<G, true>& S, int g, int l, double* scratch, uint8_
             for (int h = 0; h < 2; ++h) unpack_i16<8>(qsp + 4 * h, qs[h]);
         }
         tok = sub_tokens(flags, l, qs);
-        double sdq[2][8];
+        int sdq[2][8];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             store_row_i16<8>(o.qtc + b * 256 + j * 64 + (r0 + 4 * h) * 8, qs[h]);
-            dequant_row_i<8>(qs[h], r0 + 4 * h, qpm1, sdq[h]);
+            dequant_row_int<8>(qs[h], r0 + 4 * h, qpm1, sdq[h]);
         }
         double srd[2][8];
         xform2d_sub<true>(scratch, l, sdq, srd);

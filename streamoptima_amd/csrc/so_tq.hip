@@ -148,11 +148,11 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, const uint8_t* __r
 #pragma unroll
                 for (int h = 0; h < 2; ++h) quant_row_i<8>(stc[h], r0 + 4 * h, qpm1, qs[h]);
             tok = sub_tokens(fl, l, qs);
-            double sdq[2][8];
+            int sdq[2][8];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 store_row_i16<8>(out_qtc + (size_t)b * BS * BS + j * 64 + (r0 + 4 * h) * 8, qs[h]);
-                dequant_row_i<8>(qs[h], r0 + 4 * h, qpm1, sdq[h]);
+                dequant_row_int<8>(qs[h], r0 + 4 * h, qpm1, sdq[h]);
             }
             double srd[2][8];
             xform2d_sub<true>(dl, l, sdq, srd);

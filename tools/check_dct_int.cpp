@@ -1,4 +1,4 @@
-// Host check: dct2_16_i / dct3_16_i (so_dct.h) against dct2<16> / dct3<16> on the same
+// Host check: dct2_16_i / dct3_16_i / dct2_8_i / dct3_8_i (so_dct.h) against dct2<N> / dct3<N> on the same
 // integers converted to double -- bit for bit.
 //   hipcc -O2 -ffp-contract=off -DSO_DEV=inline tools/check_dct_int.cpp -o /tmp/check_dct_int && /tmp/check_dct_int
 #include <cstdio>
@@ -29,6 +29,17 @@ int main() {
         so::dct::dct3<16>(a);
         so::dct::dct3_16_i(x, b);
         if (std::memcmp(a, b, sizeof a)) ++bad3;
+        int x8[8];
+        for (int i = 0; i < 8; ++i) x8[i] = x[i] + x[i + 8];
+        double a8[8], b8[8];
+        for (int i = 0; i < 8; ++i) a8[i] = (double)x8[i];
+        so::dct::dct2<8>(a8);
+        so::dct::dct2_8_i(x8, b8);
+        if (std::memcmp(a8, b8, sizeof a8)) ++bad2;
+        for (int i = 0; i < 8; ++i) a8[i] = (double)x8[i];
+        so::dct::dct3<8>(a8);
+        so::dct::dct3_8_i(x8, b8);
+        if (std::memcmp(a8, b8, sizeof a8)) ++bad3;
         ++n;
     }
     std::printf("vectors %ld  dct2 mismatches %ld  dct3 mismatches %ld\n", n, bad2, bad3);
