@@ -1437,6 +1437,10 @@ struct PTileLds {
     int32_t mer[NU][4];                    // decoded ME records (dx, dy, ref, sad)
     int32_t msum[G::TBY];                  // two-pass runs: pass-1 token sum of each block row
     double un[VBS ? PTileGeoVbs<G>::U64 : PTileGeo<G>::U64];   // byte sums + survivor lists | FP64 transposes
+    // VBS: the chosen levels of each block (16 lanes x 8 packed int16 pairs) and its split state
+    // (0 block, 1 split, 2 none) between tq16_vbs_fwd and tq16_vbs_inv
+    uint32_t lev[VBS ? G::NBLK * 16 * 8 : 1];
+    uint8_t vsp[VBS ? G::NBLK : 1];
 };
 
 // Boundary rows of a rank's stripe that the neighbouring ranks read (so_encode_p_run_stripe):
@@ -1642,13 +1646,16 @@ SO_DEV void unpack_i16(const uint32_t* p, int* v) {
 }
 
 template <class G, bool SC1, bool HALO = false>
-SO_DEV void tq16_vbs(PTileLds<G, true>& S, int g, int l, double* scratch, uint8_t* flags, int bx0, int byt0, int nbx,
+SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, uint8_t* flags, int bx0, int byt0, int nbx,
                      int by0, int by1, int W, int qp_rd, const int32_t* __restrict__ qp_row,
-                     const int32_t* __restrict__ qp_map, double lam, const PFrameOut& o, const PHalo& hl = PHalo{}) {
+                         const int32_t* __restrict__ qp_map, double lam, const PFrameOut& o) {
     constexpr int SR = G::SR, TBX = G::TBX;
     const int bxl = g % TBX, byl = g / TBX;
     const int gbx = bx0 + bxl, gby = byt0 + byl;
-    if (gbx >= nbx || gby >= by1) return;   // uniform over the block's 16 lanes
+    if (gbx >= nbx || gby >= by1) {   // uniform over the block's 16 lanes
+        if (l == 0) S.vsp[g] = 2;        // no block: no inverse
+        return;
+    }
     const size_t b = (size_t)(gby - by0) * nbx + gbx;
     const int x = gbx * 16, y = gby * 16;
     const int qpr = qp_map ? qp_map[(size_t)gby * nbx + gbx] : (qp_row ? qp_row[gby] : qp_rd);
@@ -1732,7 +1739,10 @@ SO_DEV void tq16_vbs(PTileLds<G, true>& S, int g, int l, double* scratch, uint8_
         split = !(c_b < c_v);
         mae_num = vinf ? -1 : ssum;
     }
-    int tok, sse = 0;
+    // the chosen levels at the block's final QP: QTC, tokens and the block records now; the
+    // levels to LDS for tq16_vbs_inv (after the tile's barrier, in split-sorted order)
+    uint32_t* const lv = S.lev + (g * 16 + l) * 8;
+    int tok;
     if (!split) {
         int q[16];
         if (qpr != qp_rd) {
@@ -1744,30 +1754,7 @@ SO_DEV void tq16_vbs(PTileLds<G, true>& S, int g, int l, double* scratch, uint8_
         }
         tok = block_tokens<16>(nullptr, l, q);
         store_row_i16<16>(o.qtc + b * 256 + l * 16, q);
-        int dq[16];
-        double rd[16];
-        dequant_row_int<16>(q, l, qpr, dq);
-        xform2d_rows<16, true>(scratch, l, dq, rd);
-        int rec[16];
-        {
-            uint32_t pw[4];
-            win_row16<G::RP>(S.win, prow, pcol, pw);
-#pragma unroll
-            for (int c = 0; c < 16; ++c)
-                rec[c] = (int)((pw[c >> 2] >> (8 * (c & 3))) & 255) + (int)__builtin_rint(rd[c]);
-        }
-        store_rec_row<SC1, HALO>(o, hl, W, x, y + l, rec, 16);
-        if (o.sse) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t cw = crow[k];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int d = (int)((cw >> (8 * e)) & 255) - (rec[4 * k + e] & 255);
-                    sse += d * d;
-                }
-            }
-        }
+        pack_i16<16>(q, lv);
         if (l < 12) o.mv[b * 12 + l] = (int16_t)(l == 0 ? dx : l == 1 ? dy : l == 2 ? rf : 0);
     } else {
         const int qpm1 = qpr > 0 ? qpr - 1 : qpr;
@@ -1784,11 +1771,95 @@ SO_DEV void tq16_vbs(PTileLds<G, true>& S, int g, int l, double* scratch, uint8_
             for (int h = 0; h < 2; ++h) unpack_i16<8>(qsp + 4 * h, qs[h]);
         }
         tok = sub_tokens(flags, l, qs);
-        int sdq[2][8];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             store_row_i16<8>(o.qtc + b * 256 + j * 64 + (r0 + 4 * h) * 8, qs[h]);
-            dequant_row_int<8>(qs[h], r0 + 4 * h, qpm1, sdq[h]);
+            pack_i16<8>(qs[h], lv + 4 * h);
+        }
+        if (r0 < 3) o.mv[b * 12 + 3 * j + r0] = (int16_t)(r0 == 0 ? sdx : r0 == 1 ? sdy : sref);
+    }
+    if (l == 0) {
+        S.vsp[g] = (uint8_t)split;
+        o.split[b] = (uint8_t)split;
+        o.tokens[b] = tok;
+        o.mae[b] = mae_num;
+    }
+}
+
+// The inverse half of the VBS transform path, for slot k of the tile's blocks in split-sorted
+// order (unsplit blocks first, then split ones, then none): the four blocks of a wave then
+// take one of the two inverse paths -- a wave with both ran both (about two waves in three on
+// the bench content, split ~50 %), now at most one wave per tile does.  Reads the levels
+// tq16_vbs_fwd left in LDS; dequantisation, IDCT, reconstruction and SSE.
+template <class G, bool SC1, bool HALO = false>
+SO_DEV void tq16_vbs_inv(PTileLds<G, true>& S, int k, int l, double* scratch, int bx0, int byt0, int nbx,
+                         int by0, int by1, int W, int qp_rd, const int32_t* __restrict__ qp_row,
+                         const int32_t* __restrict__ qp_map, const PFrameOut& o, const PHalo& hl = PHalo{}) {
+    constexpr int SR = G::SR, TBX = G::TBX;
+    // slot k -> block g: the k-th unsplit block, else the (k - #unsplit)-th split one
+    uint32_t mns = 0, ms = 0;
+#pragma unroll
+    for (int i = 0; i < G::NBLK; ++i) {
+        const uint32_t v = S.vsp[i];
+        mns |= (v == 0 ? 1u : 0u) << i;
+        ms |= (v == 1 ? 1u : 0u) << i;
+    }
+    const int nns = __builtin_popcount(mns);
+    int kk = k < nns ? k : k - nns;
+    uint32_t m = k < nns ? mns : ms;
+    if (kk >= __builtin_popcount(m)) return;   // uniform over the 16 lanes: no block
+#pragma unroll 1
+    for (; kk > 0; --kk) m &= m - 1;           // drop the kk lowest set bits
+    const int g = __builtin_ctz(m);
+    const bool split = k >= nns;
+    const int bxl = g % TBX, byl = g / TBX;
+    const int gbx = bx0 + bxl, gby = byt0 + byl;
+    const size_t b = (size_t)(gby - by0) * nbx + gbx;
+    const int x = gbx * 16, y = gby * 16;
+    const int qpr = qp_map ? qp_map[(size_t)gby * nbx + gbx] : (qp_row ? qp_row[gby] : qp_rd);
+    const uint32_t* const lv = S.lev + (g * 16 + l) * 8;
+    const uint32_t* crow = S.curt + (byl * 16 + l) * G::CPD + bxl * 4;
+    const int j = l >> 2, r0 = l & 3;
+    int sse = 0;
+    if (!split) {
+        const int dx = S.mer[g][0], dy = S.mer[g][1];
+        const int prow = byl * 16 + SR + dy + l, pcol = bxl * 16 + SR + dx;   // window coordinates
+        int q[16], dq[16];
+        unpack_i16<16>(lv, q);
+        dequant_row_int<16>(q, l, qpr, dq);
+        double rd[16];
+        xform2d_rows<16, true>(scratch, l, dq, rd);
+        int rec[16];
+        {
+            uint32_t pw[4];
+            win_row16<G::RP>(S.win, prow, pcol, pw);
+#pragma unroll
+            for (int c = 0; c < 16; ++c)
+                rec[c] = (int)((pw[c >> 2] >> (8 * (c & 3))) & 255) + (int)__builtin_rint(rd[c]);
+        }
+        store_rec_row<SC1, HALO>(o, hl, W, x, y + l, rec, 16);
+        if (o.sse) {
+#pragma unroll
+            for (int kq = 0; kq < 4; ++kq) {
+                const uint32_t cw = crow[kq];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int d = (int)((cw >> (8 * e)) & 255) - (rec[4 * kq + e] & 255);
+                    sse += d * d;
+                }
+            }
+        }
+    } else {
+        const int qpm1 = qpr > 0 ? qpr - 1 : qpr;
+        const int32_t* sm = S.mer[G::NBLK + 4 * g + j];
+        const int sdx = sm[0], sdy = sm[1];
+        const int sxl = bxl * 16 + (j & 1) * 8, syl = byl * 16 + (j >> 1) * 8;   // sub-block in the tile (px)
+        int sdq[2][8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            int qs[8];
+            unpack_i16<8>(lv + 4 * h, qs);
+            dequant_row_int<8>(qs, r0 + 4 * h, qpm1, sdq[h]);
         }
         double srd[2][8];
         xform2d_sub<true>(scratch, l, sdq, srd);
@@ -1806,24 +1877,20 @@ SO_DEV void tq16_vbs(PTileLds<G, true>& S, int g, int l, double* scratch, uint8_
             if (o.sse) {
                 const uint32_t* cr = S.curt + (syl + row) * G::CPD + (sxl >> 2);
 #pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const uint32_t cw = cr[k];
+                for (int kq = 0; kq < 2; ++kq) {
+                    const uint32_t cw = cr[kq];
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        const int d = (int)((cw >> (8 * e)) & 255) - (rec[4 * k + e] & 255);
+                        const int d = (int)((cw >> (8 * e)) & 255) - (rec[4 * kq + e] & 255);
                         sse += d * d;
                     }
                 }
             }
         }
-        if (r0 < 3) o.mv[b * 12 + 3 * j + r0] = (int16_t)(r0 == 0 ? sdx : r0 == 1 ? sdy : sref);
     }
-    if (o.sse) sse = group_sum<16>(sse);
-    if (l == 0) {
-        o.split[b] = (uint8_t)split;
-        o.tokens[b] = tok;
-        o.mae[b] = mae_num;
-        if (o.sse) o.sse[b] = sse;
+    if (o.sse) {
+        sse = group_sum<16>(sse);
+        if (l == 0) o.sse[b] = sse;
     }
 }
 
@@ -1894,12 +1961,21 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
             }
         } else if (ln < 16 * G::TQ_BPW && gq < G::NBLK) {
             if constexpr (VBS)
-                tq16_vbs<G, SC1, HALO>(S, gq, ln & 15, S.un + gq * kTqScratchVbs,
-                                       reinterpret_cast<uint8_t*>(S.un + G::NBLK * kTqScratchVbs) + gq * 256, bx0,
-                                       byt0, nbx, by0, by1, W, qp_rd, qp_row, qp_map, lam, o, hl);
+                tq16_vbs_fwd<G, SC1, HALO>(S, gq, ln & 15, S.un + gq * kTqScratchVbs,
+                                           reinterpret_cast<uint8_t*>(S.un + G::NBLK * kTqScratchVbs) + gq * 256, bx0,
+                                           byt0, nbx, by0, by1, W, qp_rd, qp_row, qp_map, lam, o);
             else
                 tq16_exact<G, SC1, HALO, TOK>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by0, by1, W, qp_rd,
                                               qp_row, qp_map, o, hl);
+        }
+    }
+    if constexpr (VBS) {
+        if (SO_PROF_PHASE != 1) {
+            __syncthreads();   // every block's levels and split state in LDS
+            const int ln = tid & 63, gq = (tid >> 6) * G::TQ_BPW + (ln >> 4);
+            if (ln < 16 * G::TQ_BPW && gq < G::NBLK)
+                tq16_vbs_inv<G, SC1, HALO>(S, gq, ln & 15, S.un + gq * kTqScratchVbs, bx0, byt0, nbx, by0, by1, W, qp_rd,
+                                           qp_row, qp_map, o, hl);
         }
     }
     SO_SEA_STAMP(7, __builtin_amdgcn_s_memtime());

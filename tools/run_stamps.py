@@ -75,6 +75,7 @@ def main():
     ap.add_argument("--heights", default="272,1088,2160")
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--frames", type=int, default=24)
+    ap.add_argument("--vbs", action="store_true", help="VBSEnable (p_run_kernel<8, 0, true>)")
     a = ap.parse_args()
     from streamoptima_amd import _lib
     from streamoptima_amd.engine import Engine, alloc_planes
@@ -85,7 +86,7 @@ def main():
     res = {}
     for h in [int(x) for x in a.heights.split(",")]:
         w = a.width
-        eng = Engine(h, w, 16, 16, False, 0.015, dev)
+        eng = Engine(h, w, 16, 16, a.vbs, 0.015, dev)
         nf = a.frames + 1
         fr = alloc_planes(nf, h, w, dev)
         fr.copy_(synth_sequence_torch(nf, h, w, seed=0, device=dev))
