@@ -529,7 +529,13 @@ intra_recon_scan_kernel(int W, int nrows_px, int by0, const uint8_t* __restrict_
     __shared__ int ssum[WPR];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int k = tid / BS, c = tid - k * BS, g = k - wv * GPW;
-    const int yl = blockIdx.x;
+    // workgroup -> pixel row so that the BS rows of a block row share an XCD (workgroups are
+    // dealt round-robin over the 8 XCDs): each row reads BS bytes of every block's residual,
+    // and its neighbours' reads of the same lines then hit that XCD's L2 (one row per XCD in
+    // turn read every block's lines from memory 8 times over: 85 MB per 4K I-frame vs ~25)
+    const int xcd = blockIdx.x & 7, kx = blockIdx.x >> 3;
+    const int yl = (((kx / BS) << 3) + xcd) * BS + kx % BS;
+    if (yl >= nrows_px) return;   // uniform: the grid is rounded up to 8 block rows
     const int yy = by0 * BS + yl, byl = yl / BS, i = yl - byl * BS, nbx = W / BS;
     const int L = (nbx + K - 1) / K, j0 = k * L;
     const bool lower = i >= SB;
@@ -670,11 +676,12 @@ static int intra_recon_rows(int W, int bs, int sr, int by0, int nrows_px, const 
         constexpr int WPR = SO_IRS_WPR, NT = 64 * WPR;
         const int k = NT / bs, nbx = W / bs, L = (nbx + k - 1) / k;
         const size_t lds = (size_t)L * NT * sizeof(uint16_t) + NT * sizeof(uint32_t) + (size_t)W;
+        const int nbr = (nrows_px + bs - 1) / bs, grid = (nbr + 7) / 8 * 8 * bs;   // whole groups of 8 block rows
         if (bs == 16)
-            hipLaunchKernelGGL((intra_recon_scan_kernel<16, WPR>), dim3(nrows_px), dim3(NT), lds, st, W, nrows_px, by0,
+            hipLaunchKernelGGL((intra_recon_scan_kernel<16, WPR>), dim3(grid), dim3(NT), lds, st, W, nrows_px, by0,
                                split, mv, idres, cur, out_recon, out_sse);
         else
-            hipLaunchKernelGGL((intra_recon_scan_kernel<8, WPR>), dim3(nrows_px), dim3(NT), lds, st, W, nrows_px, by0,
+            hipLaunchKernelGGL((intra_recon_scan_kernel<8, WPR>), dim3(grid), dim3(NT), lds, st, W, nrows_px, by0,
                                split, mv, idres, cur, out_recon, out_sse);
         return check_launch("intra_recon_scan_kernel");
     }
