@@ -186,6 +186,10 @@ CASES = [
     (64, 64, 16, 7, False, 1, 4, "synth"),        # generic ME path (sr != 16)
     (64, 80, 16, 5, True, 2, 3, "tie"),
     (256, 272, 16, 16, True, 1, 4, "synth"),      # more than one ME tile
+    (64, 64, 8, 8, False, 1, 3, "synth"),         # 8x8 blocks, sr <= bs: the intra scan at BS 8
+    (48, 40, 8, 8, False, 1, 2, "tie"),           # W % 16 != 0: the sequential intra walk
+    (32, 1024, 8, 8, False, 1, 4, "synth"),       # 128 blocks a row: 32 chunks of 4 (intra scan)
+    (32, 2048, 16, 16, False, 1, 4, "tie"),       # 128 blocks a row: 16 chunks of 8 over 4 waves
 ]
 
 
