@@ -706,7 +706,7 @@ struct NoPre {
 // than CAP survivors in A or B: returns false and the caller runs the dense search.
 template <class G>
 SO_DEV void vbs_eval_list(const Sea2Lds& L, const uint16_t* list, uint32_t n, int cs, int bxl, int byl, int lane,
-                          uint64_t& bestB, uint64_t& best0, uint64_t& best1) {
+                          uint64_t& bestB, uint32_t& best0, uint32_t& best1) {
     constexpr int RP = G::RP, CPD = G::CPD;
     const int sidx = lane >> 2, q = lane & 3;
     const int crow0 = byl * 16 * CPD + bxl * 4;
@@ -740,9 +740,12 @@ SO_DEV void vbs_eval_list(const Sea2Lds& L, const uint16_t* list, uint32_t n, in
         uint32_t hb = __builtin_amdgcn_sad_u16(v, 0u, 0u);                                       // the half's SAD
         hb += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hb, kDppQuad2301, 0xF, 0xF, false);  // the block's
         const int dx = dxi - 16, dy = di - 16;
-        const uint64_t tail = ((uint64_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)) << 24) | (uint64_t)cand;
+        const uint32_t md = (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy));
+        const uint64_t tail = ((uint64_t)md << 24) | (uint64_t)cand;
         const uint64_t kb = ((uint64_t)hb << 32) | tail;
-        const uint64_t k0 = ((uint64_t)(v & 0xFFFFu) << 32) | tail, k1 = ((uint64_t)(v >> 16) << 32) | tail;
+        // sub-block keys in 32 bits: SAD_j < 2^14 (64 pixels), |dx| + |dy| <= 32, cand < 2^11
+        const uint32_t t32 = (md << 11) | (uint32_t)cand;
+        const uint32_t k0 = ((v & 0xFFFFu) << 17) | t32, k1 = ((v >> 16) << 17) | t32;
         bestB = (act && kb < bestB) ? kb : bestB;
         best0 = (act && k0 < best0) ? k0 : best0;
         best1 = (act && k1 < best1) ? k1 : best1;
@@ -856,14 +859,15 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    uint64_t bestB = kNoKey, best0 = kNoKey, best1 = kNoKey;
+    uint64_t bestB = kNoKey;
+    uint32_t best0 = ~0u, best1 = ~0u;
     vbs_eval_list<G>(L, mylist, nA, cs, bxl, byl, lane, bestB, best0, best1);
     // U_j: the smallest sub-block SADs among the evaluated candidates (quad lanes 0, 1: top)
     const bool top = (lane & 2) == 0;
-    const uint32_t uTL = wave_min_u32(top ? (uint32_t)(best0 >> 32) : ~0u);
-    const uint32_t uTR = wave_min_u32(top ? (uint32_t)(best1 >> 32) : ~0u);
-    const uint32_t uBL = wave_min_u32(top ? ~0u : (uint32_t)(best0 >> 32));
-    const uint32_t uBR = wave_min_u32(top ? ~0u : (uint32_t)(best1 >> 32));
+    const uint32_t uTL = wave_min_u32(top ? best0 : ~0u) >> 17;
+    const uint32_t uTR = wave_min_u32(top ? best1 : ~0u) >> 17;
+    const uint32_t uBL = wave_min_u32(top ? ~0u : best0) >> 17;
+    const uint32_t uBR = wave_min_u32(top ? ~0u : best1) >> 17;
     // ---- 3. the sub-block survivors (B): some sub-block bound <= its U_j, not evaluated in A ----
     typedef short so_v2i16 __attribute__((ext_vector_type(2)));
     const uint32_t thT = (((uTL + 60) >> 4) + 1) | ((((uTR + 60) >> 4) + 1) << 16);
@@ -894,8 +898,12 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     vbs_eval_list<G>(L, mylist, nB, cs, bxl, byl, lane, bestB, best0, best1);
     const uint64_t kb = wave_min_u64_dpp(bestB);
-    const uint64_t kTL = wave_min_u64_dpp(top ? best0 : kNoKey), kTR = wave_min_u64_dpp(top ? best1 : kNoKey);
-    const uint64_t kBL = wave_min_u64_dpp(top ? kNoKey : best0), kBR = wave_min_u64_dpp(top ? kNoKey : best1);
+    // the 32-bit sub-block keys widened to the 64-bit key layout (SAD << 32 | md << 24 | cand)
+    const auto widen = [](uint32_t k) {
+        return ((uint64_t)(k >> 17) << 32) | ((uint64_t)((k >> 11) & 63u) << 24) | (uint64_t)(k & 2047u);
+    };
+    const uint64_t kTL = widen(wave_min_u32(top ? best0 : ~0u)), kTR = widen(wave_min_u32(top ? best1 : ~0u));
+    const uint64_t kBL = widen(wave_min_u32(top ? ~0u : best0)), kBR = widen(wave_min_u32(top ? ~0u : best1));
     if (lane == 0) {
         unsigned long long* const ks = L.keys;
         if (kb < ks[u]) ks[u] = kb;
