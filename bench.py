@@ -64,7 +64,9 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 # v_sad_u8 issue limit measured on the box (tools/ubench_sad.cpp): 4.39 cycles per wave64
 # instruction at 8 waves/SIMD = 5.60e11 wave-instr/s = 1.434e14 |diffs|/s
 SAD_MEASURED_OPS = 5.603e11 * 256
+SAD_NOMINAL_OPS = 1.57e14      # 256 CUs x 2.4 GHz x 64 lanes x 4 bytes
 N_SIMD = 1024                  # 256 CUs x 4 SIMDs
+POOL_CAP = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)   # the GPU box's CPU share per GPU job
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 
 
@@ -109,6 +111,10 @@ def parse(argv=None):
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal on a one-GPU host: every rank on cuda:0, gloo collectives, each rank's persistent "
                          "grid capped to a 1/(2N) share of the GPU (numbers are not a scaling measurement)")
+    ap.add_argument("--inject-failure", default=None, metavar="WHAT",
+                    help="test mode: make the named secondary measurement (e.g. records.1080p, cpu_baseline; with "
+                         "--cpu-plumbing any name) raise, to check that the headline line still prints and the exit "
+                         "status is nonzero")
     ap.add_argument("--cpu-plumbing", action="store_true",
                     help="test mode: gloo + a trivial CPU stand-in engine (no encode, no GPU) to exercise the "
                          "rank launch, sharding, timing and JSON line on a CPU-only host")
@@ -204,7 +210,7 @@ def poison(syms):
 
 
 # ---- roofline ----------------------------------------------------------------------------------
-def kernel_roofline(codec, frames_dev, symbols, reps: int) -> dict:
+def kernel_roofline(codec, frames_dev, symbols, reps: int, components: bool = True) -> dict:
     """Average duration of p_run_kernel (the product path of a GOP's P-frames: one
     persistent launch per <= 32 frames, so_encode_p_run) measured with HIP events recorded
     on its launch stream, replaying the GOP's own P-frames against the reconstructions of
@@ -241,13 +247,19 @@ def kernel_roofline(codec, frames_dev, symbols, reps: int) -> dict:
         eng.encode_p_run([frames_dev[i] for i in range(1, nf)], symbols[0].recon, 4, run_outs)
 
     out = {}
+    sad_ops = None
     for name, fn in (("run", run), ("me", me), ("tq", tq)):
+        if name != "run" and not components:
+            continue
         # warm up for >= 0.2 s of GPU work: after an idle stretch the clock needs that long to
         # return to its working value (a 3-call warm-up read 15x too slow after the parity pass)
         t_end = time.perf_counter() + 0.2
         while time.perf_counter() < t_end:
             fn()
             torch.cuda.synchronize()
+        if name == "run":
+            eng.check_run()
+            eng.take_sad_ops()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         e0.record(stream)
@@ -257,6 +269,9 @@ def kernel_roofline(codec, frames_dev, symbols, reps: int) -> dict:
         e1.record(stream)
         torch.cuda.synchronize()
         out[name] = e0.elapsed_time(e1) / n_rep / 1e3  # seconds per call
+        if name == "run":
+            eng.check_run()
+            sad_ops = eng.take_sad_ops() / n_rep   # SO_P_RUN_SAD_OPS_WORD over the timed calls
     eng.check_run()
     nb = eng.nb
     # algorithmic work: SAD ops = valid candidates x bs^2
@@ -268,12 +283,14 @@ def kernel_roofline(codec, frames_dev, symbols, reps: int) -> dict:
     # one P-frame of the fused kernel: cur + ref read, recon + QTC int16 written (5 B/px), and
     # per block split 1 + mv 12 x int16 + tokens, mae, sse int32 (37 B)
     frame_bytes = 5 * h * w + 37 * nb
-    return {"me_s": out["me"], "tq_s": out["tq"], "run_s": out["run"], "run_frames": nf - 1,
+    return {"me_s": out.get("me"), "tq_s": out.get("tq"), "run_s": out["run"], "run_frames": nf - 1,
             "frame_bytes": frame_bytes, "me_bytes": 2 * h * w + 16 * nb, "tq_bytes": 5 * h * w + 8 * nb,
-            "sad_ops": cands * bs * bs, "cands": cands}
+            "sad_ops": cands * bs * bs, "cands": cands, "executed_sad_ops": sad_ops, "vbs": eng.vbs}
 
 
-def pmc_record(config: str):
+def pmc_record(config: str, kernel: str):
+    """The committed PMC summary of `kernel` (a name prefix) for workload `config`
+    (profiles/pmc_me_traffic.json, written by tools/traffic_json.py from rocprofv3 --pmc runs)."""
     p = os.path.join(ROOT, "profiles", "pmc_me_traffic.json")
     if not os.path.exists(p):
         return {}
@@ -282,17 +299,23 @@ def pmc_record(config: str):
     except (ValueError, OSError):
         return {}
     for k, v in ks.items():
-        if k.startswith("so::p_run_kernel<8, 0"):   # p_run_kernel<8, 0, false> (one GPU, full frame)
+        if k.startswith(kernel):
             return v
     return {}
 
 
 def roofline_of(rl: dict, config: str) -> dict:
+    """The dominant kernel's roofline line (task contract): p_run_kernel, the persistent fused
+    search + transform launch of the GOP's P-frames, timed live with HIP events; the HBM
+    fraction of its algorithmic bytes, the VALU busy fraction and HBM traffic from the
+    committed PMC counters of the same workload, and the SAD fraction of the searches'
+    EXECUTED v_sad byte operations (kernel-side count, SO_P_RUN_SAD_OPS_WORD)."""
+    kname = f"so::p_run_kernel<8, 0, {'true' if rl['vbs'] else 'false'}>"
     n_launch = -(-rl["run_frames"] // 32)       # so_encode_p_run: <= 32 frames per launch
     launch_s = rl["run_s"] / n_launch
     alg = rl["run_frames"] * rl["frame_bytes"] / n_launch
     gbs = alg / launch_s / 1e9
-    pm = pmc_record(config)
+    pm = pmc_record(config, kname)
     traffic = round(pm["hbm_bytes"]) if pm.get("hbm_bytes") else None
     valu = None
     if pm.get("sq_active_inst_valu") and pm.get("grbm_gui_active"):
@@ -306,28 +329,51 @@ def roofline_of(rl: dict, config: str) -> dict:
                 if pm.get("sq_insts_valu") else None,
                 "waves_per_simd": round(4 * pm["sq_wave_cycles"] / (cyc * N_SIMD), 2) if pm.get("sq_wave_cycles") else None,
                 "kernel_cycles": round(cyc), "effective_clock_ghz": round(cyc / launch_s / 1e9, 3),
-                "source": "profiles/pmc_me_traffic.json (rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES "
+                "source": f"profiles/pmc_me_traffic.json [{config}] (rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES "
                           "GRBM_GUI_ACTIVE ..., tools/gpu_traffic.sh)"}
-    return {"bound": "hbm", "kernel": "p_run_kernel<8, 0, false>", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
-            "traffic_note": "HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE x 2, the "
-                            "factor measured for 4-B and 16-B coalesced reads (tools/ubench_fetch.cpp)",
-            "algorithmic_bytes": round(alg), "launch_us": round(launch_s * 1e6, 2),
-            "frames_per_launch": round(rl["run_frames"] / n_launch, 2),
-            "per_frame_us": round(rl["run_s"] / rl["run_frames"] * 1e6, 2),
-            "binding_limit": "valu",
-            "valu": valu,
-            "note": "frac is the required HBM fraction (algorithmic bytes / launch time / 8 TB/s); the kernel is "
-                    "bound by VALU issue (SEA search + FP64 pocketfft-exact DCT), whose measured busy fraction is "
-                    "valu.valu_busy_frac",
-            "components": {
-                "me_search": {"kernel": "me_sea2_kernel", "launch_us": round(rl["me_s"] * 1e6, 2),
-                              "achieved_gbs": round(rl["me_bytes"] / rl["me_s"] / 1e9, 2),
-                              "dense_equivalent_sad_frac_of_measured_peak":
-                                  round(rl["sad_ops"] / rl["me_s"] / SAD_MEASURED_OPS, 4),
-                              "candidates": rl["cands"]},
-                "transform": {"kernel": "inter_tq_kernel<16, false, false>", "launch_us": round(rl["tq_s"] * 1e6, 2),
-                              "achieved_gbs": round(rl["tq_bytes"] / rl["tq_s"] / 1e9, 2)}}}
+    ex = rl.get("executed_sad_ops")
+    sad = {"executed_byte_ops_per_launch": round(ex / n_launch) if ex else None,
+           "executed_frac_of_measured_peak": round(ex / rl["run_s"] / SAD_MEASURED_OPS, 4) if ex else None,
+           "executed_frac_of_nominal_peak": round(ex / rl["run_s"] / SAD_NOMINAL_OPS, 4) if ex else None,
+           "dense_equivalent_byte_ops_per_launch": round(rl["sad_ops"] * rl["run_frames"] / n_launch),
+           "dense_equivalent_frac_of_nominal_peak": round(rl["sad_ops"] * rl["run_frames"] / rl["run_s"]
+                                                          / SAD_NOMINAL_OPS, 4),
+           "note": "executed = every v_sad_u8 / v_sad_hi_u8 lane instruction of the searches (byte sums, bounds, "
+                   "survivor and dense SADs) x 4 bytes, counted in the kernel; peaks: 1.434e14 |diff|/s measured "
+                   "(tools/ubench_sad.cpp), 1.57e14 nominal (BASELINE.md section 4). The dense-equivalent count is the "
+                   "reference's full scan (Encoder.py:688-715, valid candidates x 256), which the exact SEA search "
+                   "mostly skips, so its 'fraction' can exceed 1"}
+    out = {"bound": "hbm", "kernel": kname, "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
+           "traffic_note": "HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE x 2, the "
+                           "factor measured for 4-B and 16-B coalesced reads (tools/ubench_fetch.cpp)",
+           "algorithmic_bytes": round(alg), "launch_us": round(launch_s * 1e6, 2),
+           "frames_per_launch": round(rl["run_frames"] / n_launch, 2),
+           "per_frame_us": round(rl["run_s"] / rl["run_frames"] * 1e6, 2),
+           "binding_limit": "valu",
+           "valu": valu, "sad": sad,
+           "note": "frac is the required HBM fraction (algorithmic bytes / launch time / 8 TB/s); the kernel is "
+                   "bound by VALU issue (SEA search + FP64 pocketfft-exact DCT), whose measured busy fraction is "
+                   "valu.valu_busy_frac"}
+    if rl.get("me_s") and rl.get("tq_s"):
+        out["components"] = {
+            "me_search": {"kernel": "me_sea2_kernel", "launch_us": round(rl["me_s"] * 1e6, 2),
+                          "achieved_gbs": round(rl["me_bytes"] / rl["me_s"] / 1e9, 2), "candidates": rl["cands"]},
+            "transform": {"kernel": "inter_tq_kernel<16, false, false>", "launch_us": round(rl["tq_s"] * 1e6, 2),
+                          "achieved_gbs": round(rl["tq_bytes"] / rl["tq_s"] / 1e9, 2)}}
+    return out
+
+
+def gop_roofline(cfg, step_s: float, gops: int = 1) -> dict:
+    """Whole-step HBM fraction: every frame's algorithmic bytes (cur +
+    ref read, recon + int16 QTC written = 5 B/px, 37 B/block of symbols) over the measured step
+    time, for records whose step is more than the one persistent run (GOP streams, two-pass)."""
+    from streamoptima_amd.workloads import padded
+    h, w = padded(cfg["h"]), cfg["w"]
+    alg = gops * cfg["frames"] * (5 * h * w + 37 * (h // 16) * (w // 16))
+    gbs = alg / step_s / 1e9
+    return {"bound": "hbm", "scope": "whole step (every kernel of the GOP)", "achieved": round(gbs, 2),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5), "algorithmic_bytes": alg}
 
 
 # ---- CPU baseline --------------------------------------------------------------------------------
@@ -366,10 +412,15 @@ def cpu_baseline(cfg, rows: int, pool_rows: int) -> dict:
     intra_rows(cur, sample, qp=cfg["qp"])
     ti = (time.perf_counter() - t0) / len(sample)
     t_gop = nrows * (ti + (f - 1) * tp)
+    # BASELINE.md section 3 asks for Pool(os.cpu_count()).  os.cpu_count() on the GPU box is the
+    # whole host (256 threads), but one GPU's job is allotted 16 of them (the box's worker-pool
+    # rule: OMP_NUM_THREADS / MAX_JOBS are set to 16 there, and a pool sized to the host
+    # oversubscribes the job's share): the pool gets min(affinity, 16) workers and the line
+    # states both numbers.
     try:
-        procs = min(len(os.sched_getaffinity(0)), 16)   # the box's CPU share is 16
+        procs = min(len(os.sched_getaffinity(0)), POOL_CAP)
     except AttributeError:
-        procs = min(os.cpu_count() or 1, 16)
+        procs = min(os.cpu_count() or 1, POOL_CAP)
     t0 = time.perf_counter()
     inter_rows_pool(cur, ref, psample, procs, qp=cfg["qp"])
     tpp = (time.perf_counter() - t0) / len(psample)
@@ -386,6 +437,8 @@ def cpu_baseline(cfg, rows: int, pool_rows: int) -> dict:
                       f"extrapolated to {nrows} rows x (1 I + {f - 1} P); "
                       f"P {tp * nrows:.1f} s/frame, I {ti * nrows:.2f} s/frame",
             "pool": {"value": round(f * h * w / t_gop_pool / 1e6, 6), "unit": "Mpx/s", "cores": procs,
+                     "cores_note": f"Pool({procs}), not Pool(os.cpu_count() = {os.cpu_count()}): the GPU box allots "
+                                   f"{POOL_CAP} CPUs to one GPU's job",
                      "sample": f"{len(psample)} P-frame block rows (spread over the frame) over Pool({procs}), one row per task "
                                f"(ParallelMode-2 analogue); P {tpp * nrows:.2f} s/frame"},
             "host": cpu_model(), "os_cpu_count": os.cpu_count(), "calibration": calib}
@@ -530,7 +583,9 @@ def psnr_delta(sse, fx, hp: int, w: int) -> dict | None:
         return None
     vals = sse.cpu().numpy() if torch.is_tensor(sse) else np.asarray(sse)
     got = [float("inf") if s == 0 else 10 * np.log10(255 ** 2 / (float(s) / (hp * w))) for s in vals]
-    d = [abs(a - b) for a, b in zip(got, fx["psnr"]) if np.isfinite(a) and np.isfinite(b)]
+    # both inf (an exact frame on both sides): equal; one inf and one finite: a mismatch (inf)
+    d = [abs(a - b) if (np.isfinite(a) and np.isfinite(b)) else (0.0 if a == b else float("inf"))
+         for a, b in zip(got, fx["psnr"])]
     return {"psnr_delta_db_max": float(max(d)) if d else None, "frames": len(got),
             "psnr_mean_db": round(float(np.mean([g for g in got if np.isfinite(g)])), 4),
             "tolerance_db": 1e-4}
@@ -600,6 +655,9 @@ def record_single(name: str, args, dev) -> dict:
            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "ms_per_step_runs": runs, "width": cfg["w"],
            "height": cfg["h"], "encoded_height": padded(cfg["h"]), "frames": cfg["frames"],
            "content": cfg.get("content", "bench")}
+    if eng.pipelined_ok(1):   # right after timing, the GPU at its working clock
+        rec["roofline"] = roofline_of(kernel_roofline(codec, frames, res["symbols"], args.kernel_reps,
+                                                      components=False), name)
     rec["sea_dense_fallback"] = dense_fallback_of(eng, cfg, step)
     if not args.no_parity:
         def redo():
@@ -608,6 +666,8 @@ def record_single(name: str, args, dev) -> dict:
             eng.check_run()
             return r["symbols"]
         rec["parity"] = parity_of(res["symbols"], name, cfg, redo, sse=res["sse"])
+    rec["roofline_gop"] = gop_roofline(cfg, elapsed / args.steps)
+    rec["wait_health"] = eng.wait_health.as_dict()
     return rec
 
 
@@ -646,6 +706,8 @@ def record_gops_in_flight(name: str, ngops: int, args, dev) -> dict:
         per = [parity_of(r["symbols"], name, cfg, sse=r["sse"]) for r in res]
         rec["parity"] = {"bit_exact": all(p and p.get("bit_exact") for p in per),
                          "gops_checked": len(per), "fixture": per[0].get("fixture") if per[0] else None}
+    rec["roofline_gop"] = gop_roofline(cfg, elapsed / args.steps, ngops)
+    rec["wait_health"] = eng.wait_health.as_dict()
     return rec
 
 
@@ -744,7 +806,8 @@ def fpipe_encoder(codec, frames, cfg, world, max_wg=0):
     flag = torch.tensor([1 if good else 0], dtype=torch.int32, device=eng.device)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     if int(flag.item()) == 0:
-        penc.r._ws[32].zero_()
+        from streamoptima_amd import runhealth
+        runhealth.clear(penc.r._ws)
         return None, "self-check failed"
     return penc, "frame pipeline over xGMI (IPC-mapped uncached landing planes), self-checked"
 
@@ -888,12 +951,17 @@ def main(argv=None):
     if penc is not None or fenc is not None:
         # a lost hand-off anywhere voids the timed run: time the all_gather path instead
         import torch.distributed as dist
+        from streamoptima_amd import runhealth
         r_ = (penc or fenc).r
-        lost = torch.tensor([int(r_._ws[32].item())], dtype=torch.int32, device=dev)
+        h_ = runhealth.read(r_._ws)
+        if h_["record"]:
+            print(f"bench.py rank {rank}: hand-off wait timed out: {runhealth.describe(h_['record'])}",
+                  file=sys.stderr, flush=True)
+        lost = torch.tensor([h_["timeouts"]], dtype=torch.int32, device=dev)
         dist.all_reduce(lost, op=dist.ReduceOp.SUM)
         timeouts = int(lost.item())
         if timeouts:
-            r_._ws[32].zero_()
+            runhealth.clear(r_._ws)
             penc = fenc = None
             mode_note = f"stripe x{world} (block rows of one GOP; hand-off: {{}})"
             exchange_note = "all_gather (RCCL) per frame; the p2p run timed out a hand-off and was discarded"
@@ -904,11 +972,12 @@ def main(argv=None):
 
     # ---- right after timing (GPU still at its working clock): the dominant kernel's roofline ----
     rl = None
-    if rank == 0 and not args.cpu_plumbing and plain_cfg and codec.engine().pipelined_ok(1) and not cfg.get("rc"):
+    if (rank == 0 and not args.cpu_plumbing and cfg.get("me", "full") == "full" and codec.engine().pipelined_ok(1)
+            and not cfg.get("rc")):
         # stripe mode: the kernel is timed on rank 0's GPU alone over the full frame (a
         # one-GPU GOP supplies the reference reconstructions it replays)
         syms = res["symbols"] if not stripe else codec.encode_device(frames, cfg["intra_dur"])["symbols"]
-        rl = kernel_roofline(codec, frames, syms, args.kernel_reps)
+        rl = kernel_roofline(codec, frames, syms, args.kernel_reps, components=not cfg.get("vbs"))
 
     # ---- after timing: parity of the timed output ----
     parity = None
@@ -953,21 +1022,42 @@ def main(argv=None):
         vals = [10 * np.log10(255 ** 2 / (s / (hp * w))) for s in sse if s > 0]
         psnr_mean = float(np.mean(vals)) if vals else None
 
+    # ---- secondary measurements: each one's failure is recorded in the line (and makes the exit
+    # status nonzero) instead of voiding the headline measured above ----
+    failures = []
+
+    def guarded(what, fn):
+        try:
+            if args.inject_failure == what:
+                raise RuntimeError(f"--inject-failure {what}")
+            return fn()
+        except Exception as e:   # noqa: BLE001 -- reported, never swallowed: rc != 0 below
+            import traceback
+            failures.append(what)
+            print(f"bench.py: {what} failed:\n{traceback.format_exc()}", file=sys.stderr, flush=True)
+            return {"error": f"{type(e).__name__}: {e}"}
+
+    headline_health = None
+    if codec is not None and not stripe:
+        headline_health = codec.engine().wait_health.as_dict()
     records = None
     if rank == 0 and world == 1 and not args.cpu_plumbing and not args.no_records and name == "4k":
-        records = {"1080p": record_single("1080p", args, dev)}
+        records = {"1080p": guarded("records.1080p", lambda: record_single("1080p", args, dev))}
         for k in args.gops_in_flight:
             for nm in ("1080p", "4k"):
-                records[f"{nm}_x{k}gop"] = record_gops_in_flight(nm, k, args, dev)
+                records[f"{nm}_x{k}gop"] = guarded(f"records.{nm}_x{k}gop",
+                                                   lambda nm=nm, k=k: record_gops_in_flight(nm, k, args, dev))
         if not args.no_content_records:
             for nm in ("4k_lowtex", "4k_noise"):
-                records[nm] = record_single(nm, args, dev)
+                records[nm] = guarded(f"records.{nm}", lambda nm=nm: record_single(nm, args, dev))
+    if rank == 0 and args.cpu_plumbing and args.inject_failure:   # the mechanism, on a CPU-only host
+        records = {args.inject_failure: guarded(args.inject_failure, lambda: {"plumbing": True})}
     pcie = None
     if rank == 0 and world == 1 and not args.cpu_plumbing and not args.no_pcie and plain_cfg:
-        pcie = pcie_inclusive(codec, cfg, frames)
+        pcie = guarded("pcie_inclusive", lambda: pcie_inclusive(codec, cfg, frames))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.cpu_plumbing:
-        cpu = cpu_baseline(cfg, args.cpu_rows, args.cpu_pool_rows)
+        cpu = guarded("cpu_baseline", lambda: cpu_baseline(cfg, args.cpu_rows, args.cpu_pool_rows))
     if rank != 0:
         barrier(world)
         return
@@ -992,7 +1082,7 @@ def main(argv=None):
                    "launch": "hip-graph (one GOP per replay)" if args.graph else "host launches"},
         "parity": parity,
         "roofline": roofline_of(rl, name) if rl else None,
-        "cpu_baseline": cpu,
+        "cpu_baseline": cpu if (cpu is None or "error" not in cpu) else None,
         "psnr_mean_db": round(psnr_mean, 4) if psnr_mean is not None else None,
         "psnr_delta_db": parity.get("psnr_delta_db") if parity else None,
     }
@@ -1002,14 +1092,23 @@ def main(argv=None):
         # dependency waits of the in-launch hand-off that passed their bound during the timed
         # run, summed over ranks (nonzero: that run was discarded and the stripes timed instead)
         line["timeouts"] = timeouts
+    if headline_health is not None:
+        line["wait_health"] = headline_health
     if records:
         line["records"] = records
     if pcie:
         line["pcie_inclusive"] = pcie
-    if cpu:
+    if cpu and cpu.get("value"):
         line["gpu_over_cpu"] = round(mpx / cpu["value"], 1)
+    if cpu and "error" in cpu:
+        line["cpu_baseline_error"] = cpu["error"]
+    if failures:
+        line["failed"] = failures
     print(json.dumps(line), flush=True)
     barrier(world)
+    if failures:
+        sys.exit(f"bench.py: {len(failures)} secondary measurement(s) failed: {', '.join(failures)} "
+                 "(the headline line above is complete)")
 
 
 

@@ -115,6 +115,26 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
                      uint8_t* out_recon, int32_t* out_sse, int32_t* scratch, void* stream);
 
 /*
+ * Process-wide options of the library (explicit calls, not environment variables; the A/B
+ * knobs of the development tools exist only in -DSO_AB builds).  Set them before enqueueing
+ * the work they affect; they are read on the host when a call enqueues its launches.
+ *   SO_OPT_RUN_2PASS_FUSED   so_encode_p_run_2pass runs both passes of every frame in ONE
+ *                            persistent launch (1) instead of the per-frame kernel sequence
+ *                            (0, default; measured faster)
+ *   SO_OPT_FASTME_SERIAL     fast_me under ParallelMode 0: the one-wavefront serial walk of the
+ *                            predictor chain (1) instead of the speculated segments (0, default)
+ *   SO_OPT_FASTME_SEGMENT    blocks per speculated segment (default 32, >= 1)
+ *   SO_OPT_FASTME_WARMUP     blocks a segment's guess runs ahead of it (default 32, >= 0)
+ * so_set_option returns SO_E_INVALID for an unknown option or a value out of range.
+ */
+#define SO_OPT_RUN_2PASS_FUSED 1
+#define SO_OPT_FASTME_SERIAL 2
+#define SO_OPT_FASTME_SEGMENT 3
+#define SO_OPT_FASTME_WARMUP 4
+int so_set_option(int option, int value);
+int so_get_option(int option);
+
+/*
  * A run of consecutive P-frames (the GOP loop's P-frames between two I-frames,
  * Encoder.py:1839-1867 with nRefFrames 1): frame i predicts from frame i-1's
  * reconstruction (out_recon[i-1]), frame 0 from ref0.  Output is identical to
@@ -134,17 +154,40 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
  * at 0 and its epoch in the workspace (done flags are compared with the launch's epoch, so
  * nothing is reset between launches).  One workspace serves one stream at a time.  Word 32
  * (SO_P_RUN_TIMEOUT_WORD) is the timeout count: the caller reads it after the run (or after a
- * whole GOP of runs) and clears it.
- * Nonzero means a dependency wait passed 50 ms (2 s for another rank's flags) and the run's
- * symbols may be wrong; the
- * facade raises (Engine.check_run).  Consumers poll the flags and then take an agent-scope
- * acquire before reading the reference rows.
+ * whole GOP of runs) and clears it (with words 33..35 and the record at 96..127).
+ * Nonzero means a dependency wait polled for 50 ms (2 s for another rank's flags; intervals in
+ * which the waiting wave was descheduled are not counted) and the run's symbols may be wrong;
+ * the facade raises with the record of the first such wait (Engine.check_run).  Consumers poll
+ * the flags and then take an agent-scope acquire before reading the reference rows.
  */
 #define SO_P_RUN_TIMEOUT_WORD 32
 /* Word 64: the number of blocks whose exact SEA search took the dense fallback (more than 192
  * candidates survived the 4x4-cell bound: flat or noise-like content), summed over launches
  * like the timeout count until the caller clears it (a content statistic, not an error). */
 #define SO_P_RUN_FALLBACK_WORD 64
+/* Words 66..67 (uint64, little endian): SAD byte operations the searches executed (every
+ * v_sad_u8 / v_sad_hi_u8 lane instruction counts its 4 bytes: byte sums, bounds, survivor and
+ * dense SADs), summed like word 64.  The dense-equivalent count of the reference's full scan
+ * (Encoder.py:688-715) is (valid candidates) x 256 per P-frame; this is what ran. */
+#define SO_P_RUN_SAD_OPS_WORD 66
+/* Wait health, accumulated like the timeout count ("Waits"):
+ * word 33: waits whose relaxed flag polls kept missing a flag for 1 ms of polling that an
+ *          atomic read then found set (the wait completes with atomic reads; not an error);
+ * word 34: poll intervals longer than 1 ms (the waiting wave was descheduled: compute-queue
+ *          preemption), excluded from the wait's bound (not an error). */
+#define SO_P_RUN_STALE_WORD 33
+#define SO_P_RUN_GAP_WORD 34
+/* Words 96..127: the record of the first wait that timed out since word 35 was cleared (all
+ * zero: none).  [0] magic 0x534F0001, [1] task, [2] frame (in the launch), [3] dep frame,
+ * [4] tile, [5] the launch's epoch (local flags), [6] the GOP epoch (another rank's flags),
+ * [7] mode | vbs << 4 | pass << 8 | escalated << 12, [8] lanes waited on (bit l), [9] lanes
+ * polling another rank's flags, [10] polling time (100 MHz ticks, gaps excluded), [11] wall
+ * ticks, [12] longest poll gap, [13] polls, [14] ticks from the timeout until every awaited
+ * flag read set (0xFFFFFFFF: not within 50 ms more), [15] HW_ID, [16] XCC_ID, [17] blockIdx.x,
+ * [18] gridDim.x, [19] lanes whose flag an atomic read found set at the timeout,
+ * [20 + l] the last value lane l read (l < 12). */
+#define SO_P_RUN_DIAG_WORD 96
+#define SO_P_RUN_DIAG_MAGIC 0x534F0001u
 size_t so_p_run_workspace_elems(int H, int W);
 int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W,
                     int bs, int sr, int qp_rd, const int32_t* qp_row, int vbs, double lam,
@@ -163,8 +206,8 @@ int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0
  * so_encode_p_rows_ex (pass 1) + so_qp_map + so_encode_p_rows_ex(SO_REUSE_ME) (pass 2);
  * out_qp_map[i] (int32 [nb]) receives frame i's QPs.  roi: int32 [nb] offsets or NULL.  By
  * default the library enqueues that per-frame kernel sequence itself (pass 1 tokens-only, the
- * QP map, pass 2; the ME records kept in the workspace); with SO_RUN_2PASS_FUSED=1 in the
- * environment both passes run in ONE persistent launch instead (each tile two tasks, a pass-2
+ * QP map, pass 2; the ME records kept in the workspace); with so_set_option(
+ * SO_OPT_RUN_2PASS_FUSED, 1) both passes run in ONE persistent launch instead (each tile two tasks, a pass-2
  * task waiting for its tile row's pass 1; measured slower).  Frame i predicts from frame i-1's
  * pass-2 reconstruction, frame 0 from ref0.  Same coverage and workspace as so_encode_p_run
  * (W <= 8192).

@@ -88,12 +88,16 @@ _SIGS = {
                              _vp, _vp, _vp], _i),
     "so_intra_recon_ex": ([_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], _i),
     "so_qp_map": ([_vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp], _i),
+    "so_set_option": ([_i, _i], _i),
+    "so_get_option": ([_i], _i),
 }
 
 # ME modes (include/streamoptima.h)
 ME_FULL, ME_FAST, ME_FAST_PAR = 0, 1, 2
 REUSE_ME = 1   # so_encode_p_rows_ex flags
 TOKENS_ONLY = 2
+# so_set_option (include/streamoptima.h SO_OPT_*)
+OPT_RUN_2PASS_FUSED, OPT_FASTME_SERIAL, OPT_FASTME_SEGMENT, OPT_FASTME_WARMUP = 1, 2, 3, 4
 
 EXPORTED = tuple(_SIGS)
 
@@ -131,6 +135,29 @@ def check(rc: int, what: str) -> None:
         if rc == SO_E_UNSUPPORTED:
             raise NotImplementedError(f"{what}: {msg}")
         raise HipPathError(f"{what}: HIP error {rc}: {msg}")
+
+
+def set_option(opt: int, value: int) -> int:
+    """so_set_option; returns the previous value (raises ValueError on a bad option / value)."""
+    lib = load()
+    old = lib.so_get_option(opt)
+    check(lib.so_set_option(opt, int(value)), "so_set_option")
+    return old
+
+
+class option:
+    """Context manager: so_set_option for the duration of a block (tests, A/B tools)."""
+
+    def __init__(self, opt: int, value: int):
+        self.opt, self.value, self.old = opt, value, None
+
+    def __enter__(self):
+        self.old = set_option(self.opt, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        set_option(self.opt, self.old)
+        return False
 
 
 def ptr(t) -> int | None:

@@ -6,6 +6,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <vector>
 
 #include <hip/hip_ext.h>
@@ -22,6 +23,13 @@ void set_error(const char* fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(g_err, sizeof(g_err), fmt, ap);
     va_end(ap);
+}
+
+// so_set_option / so_get_option (SO_OPT_*): index = option id
+static std::atomic<int> g_opt[5] = {0, 0, 0, 32, 32};
+
+int option(int id) {
+    return (id > 0 && id < 5) ? g_opt[id].load(std::memory_order_relaxed) : 0;
 }
 
 int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, int bs, int sr, int by0, int by1,
@@ -69,10 +77,14 @@ int frame_push_launch(const uint8_t* plane, int H, int W, uint8_t* dst, uint32_t
 // SO_ME_IMPL A/B selection keeps the two-launch path (ME kernel + inter_tq_kernel).
 static bool use_fused(int bs, int sr, int vbs, int nref) {
     if (bs != 16 || sr != 16 || vbs || nref != 1) return false;
+#ifdef SO_AB   // A/B builds only
     const char* f = getenv("SO_FUSED");
     if (f && strcmp(f, "0") == 0) return false;
     const char* impl = getenv("SO_ME_IMPL");
     return impl == nullptr || impl[0] == 0;
+#else
+    return true;
+#endif
 }
 
 int inter_tq_launch(const uint8_t* cur, const RefSet& refs, const uint8_t* planes, size_t pstride, int H, int W,
@@ -299,6 +311,21 @@ extern "C" {
 
 int so_abi_version(void) { return SO_ABI_VERSION; }
 
+int so_set_option(int opt, int value) {
+    const bool ok = (opt == SO_OPT_RUN_2PASS_FUSED || opt == SO_OPT_FASTME_SERIAL) ? (value == 0 || value == 1)
+                    : opt == SO_OPT_FASTME_SEGMENT                               ? value >= 1
+                    : opt == SO_OPT_FASTME_WARMUP                                ? value >= 0
+                                                                                 : false;
+    if (!ok) {
+        set_error("so_set_option: option %d value %d is unknown or out of range", opt, value);
+        return SO_E_INVALID;
+    }
+    g_opt[opt].store(value, std::memory_order_relaxed);
+    return SO_OK;
+}
+
+int so_get_option(int opt) { return option(opt); }
+
 const char* so_last_error(void) { return g_err; }
 
 int so_me_full_search(const uint8_t* cur, const uint8_t* const* refs, int nref, int H, int W, int bs,
@@ -502,8 +529,7 @@ int so_encode_p_run_2pass(const uint8_t* const* curs, int nframes, const uint8_t
                                     out_sse ? out_sse[i] : nullptr, out_qp_map[i]};
     }
     hipStream_t st = (hipStream_t)stream;
-    const char* fused = getenv("SO_RUN_2PASS_FUSED");   // opt-in: both passes in one persistent launch
-    if (fused && atoi(fused) == 1)
+    if (option(SO_OPT_RUN_2PASS_FUSED) == 1)   // opt-in: both passes in one persistent launch
         return p_run_2pass_launch(curs, nframes, ref0, H, W, qp_rd, qp_row, roi, qp_lo, qp_hi, outs.data(), workspace,
                                   st);
     // default (faster): per frame, pass 1 (fused search + tokens only),

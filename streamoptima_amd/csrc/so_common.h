@@ -14,6 +14,9 @@ namespace so {
 // Thread-local last error message (so_last_error()).
 void set_error(const char* fmt, ...);
 
+// The current value of a process-wide option (so_set_option, SO_OPT_*).
+int option(int id);
+
 inline int check_launch(const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

@@ -339,11 +339,9 @@ int me_fastpred_launch(const uint8_t* cur, const uint8_t* const* ptrs, int nptr,
     for (int i = 0; i < nptr && i < 4 * kMaxRef; ++i) R.p[i] = ptrs[i];
     const int nb = (W / bs) * (by1 - by0);
     if (nb <= 0) return SO_OK;
-    const char* ser = getenv("SO_FASTME_SERIAL");   // A/B: the one-wavefront walk
-    if (serial && seg_ws && !(ser && atoi(ser) == 1)) {   // no workspace (so_me_search_ex): the walk
-        int K = 32, warm = 32;
-        if (const char* e = getenv("SO_FASTME_K")) K = atoi(e) > 0 ? atoi(e) : K;
-        if (const char* e = getenv("SO_FASTME_WARM")) warm = atoi(e) >= 0 ? atoi(e) : warm;
+    // SO_OPT_FASTME_SERIAL: the one-wavefront walk; no workspace (so_me_search_ex): the walk
+    if (serial && seg_ws && option(SO_OPT_FASTME_SERIAL) != 1) {
+        int K = option(SO_OPT_FASTME_SEGMENT), warm = option(SO_OPT_FASTME_WARMUP);
         if ((nb + K - 1) / K > kFastSegMax) K = (nb + kFastSegMax - 1) / kFastSegMax;
         const int nseg = (nb + K - 1) / K;
         int32_t* nfixed = nullptr;

@@ -669,7 +669,10 @@ static int intra_recon_rows(int W, int bs, int sr, int by0, int nrows_px, const 
                             hipStream_t st) {
     if (nrows_px <= 0) return SO_OK;
 #ifndef SO_IRS_SEQ   // A/B builds: the sequential walk for sr <= bs too
-    if (sr <= bs && W % 16 == 0) {   // (16-byte row stores)
+    // 16-byte row loads / stores of cur and out_recon: W % 16 == 0 and 16-byte aligned planes
+    // (the C-ABI takes any plane pointer; a misaligned one takes the sequential walk)
+    const bool a16 = ((reinterpret_cast<uintptr_t>(cur) | reinterpret_cast<uintptr_t>(out_recon)) & 15) == 0;
+    if (sr <= bs && W % 16 == 0 && a16) {
 #ifndef SO_IRS_WPR   // waves per pixel row of the scan
 #define SO_IRS_WPR 4
 #endif

@@ -19,6 +19,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "so_block.h"
 #include "so_common.h"
 #include "so_dpp.h"
@@ -30,6 +34,14 @@ SO_DEV uint64_t me_key(uint32_t sad, uint32_t l1, uint32_t ref, uint32_t scan) {
     return ((uint64_t)sad << 32) | ((uint64_t)l1 << 24) | ((uint64_t)ref << 16) | (uint64_t)scan;
 }
 constexpr uint64_t kNoKey = ~0ull;
+// SAD byte operations of one wave_dense_block at bs 16 (2 passes x (17 x 8 + 8) x 4 v_sad_u8
+// per lane, 64 lanes, 4 bytes each)
+constexpr uint32_t kDenseSadOps = 1152u * 256u;
+#ifdef SO_NO_OPS
+#define SO_OPS_ADD(p, v) ((void)0)
+#else
+#define SO_OPS_ADD(p, v) atomicAdd((p), (v))
+#endif
 
 SO_DEV void decode_key(uint64_t k, int sr, int32_t* out) {
     if (k == kNoKey) {
@@ -674,7 +686,7 @@ struct Sea2Lds {
     uint16_t* list;            // [NW * CAP] survivor lists
     uint32_t* lcount;          // [NW]
     unsigned long long* keys;  // [NBLK] packed best key per block
-    uint32_t* st;              // [2] SO_STAMPS only: fallback blocks, survivors
+    uint32_t* st;              // [3]: dense-fallback blocks, survivors (SO_STAMPS only), SAD byte ops
 };
 
 // Exact SEA full search of tile `tile` (16 blocks of 16x16) over nref references.  On
@@ -831,6 +843,8 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
         kl = (ok2 && k2 < kl) ? k2 : kl;
     }
     const uint32_t kmin = wave_min_u32(kl);
+    // SAD byte operations: the packed bounds (136 + 8 lane instructions), U (1)
+    if (lane == 0) SO_OPS_ADD(&L.st[2], 145u * 256u);
     const int cs = (int)(kmin & 2047), cdx = cs / 33, cdi = cs - cdx * 33;
     const int crow0 = byl * 16 * CPD + bxl * 4;
     uint32_t U;
@@ -856,6 +870,7 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
         }
     }
     if (nA > (uint32_t)CAP) return false;
+    if (lane == 0) SO_OPS_ADD(&L.st[2], 16u * ((nA + 15) / 16) * 256u);   // list A: 16 per 16 candidates
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -893,6 +908,7 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
         }
     }
     if (nB > (uint32_t)CAP) return false;
+    if (lane == 0) SO_OPS_ADD(&L.st[2], 16u * ((nB + 15) / 16) * 256u);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -949,6 +965,10 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
     // fallback count: the content-dependence records of bench.py)
     uint32_t& st_fb = L.st[0];
     if (tid == 0) st_fb = 0;
+    // st[2]: SAD byte operations executed for this tile (every v_sad_u8 / v_sad_hi_u8 lane
+    // instruction counts 4): the current tile's 4x4 sums, here
+    uint32_t& st_ops = L.st[2];
+    if (tid == 0) st_ops = G::NBLK * 16 * 4 * 4;
 #ifdef SO_STAMPS
     uint32_t& st_sur = L.st[1];
     if (tid == 0) st_sur = 0;
@@ -1062,7 +1082,10 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
                 else
                     wave_dense_block<16, false, RP, 0, false, true>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u,
                                                                     tid, r);
-                if ((tid & 63) == 0) atomicAdd(&st_fb, 1u);
+                if ((tid & 63) == 0) {
+                    atomicAdd(&st_fb, 1u);
+                    SO_OPS_ADD(&st_ops, kDenseSadOps);
+                }
             }
             continue;
         }
@@ -1070,6 +1093,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
         // b4[row * B4P + (c & 3) * WD + (c >> 2)] (a candidate's four sums of one 4x4 row --
         // columns c, c+4, c+8, c+12 -- are then consecutive bytes).  Thread = (dword column m:
         // columns 4m..4m+3, band of B4BAND output rows).
+        if (tid == 0) SO_OPS_ADD(&st_ops, (uint32_t)(G::WD * G::B4NB * (G::B4BAND + 3) * 4 * 4));
         if (tid < G::WD * G::B4NB) {
             const int m = tid % G::WD, band = tid / G::WD;
             const int r0 = band * G::B4BAND;
@@ -1117,7 +1141,10 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
 #ifndef SO_VBS_DENSE_ONLY   // A/B builds: every sub-searched block dense
                     if (x + 48 <= W && y + 48 <= H && sea_vbs_block<G>(L, u, bxl, byl, tid)) continue;
 #endif
-                    if ((tid & 63) == 0) atomicAdd(&st_fb, 1u);   // counted as a dense fallback
+                    if ((tid & 63) == 0) {
+                        atomicAdd(&st_fb, 1u);   // counted as a dense fallback
+                        SO_OPS_ADD(&st_ops, kDenseSadOps);
+                    }
 #ifndef SO_TEST_NODENSE
                     wave_dense_block<16, true, RP, 0, false, true>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u,
                                                                    tid, r);
@@ -1201,6 +1228,8 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
                 kl = (ok2 && k2 < kl) ? k2 : kl;
             }
             const uint32_t kmin = wave_min_u32(kl);
+            // the bound pass: 68 + 4 SAD lane instructions, the U evaluation: 1
+            if (lane == 0) SO_OPS_ADD(&st_ops, kmin == 0xFFFFFFFFu ? 72u * 256u : 73u * 256u);
             if (kmin == 0xFFFFFFFFu) continue;                 // no valid candidate: key stays none
             const int cs = (int)(kmin & 2047), cdx = cs / 33, cdi = cs - cdx * 33;
             const int crow0 = byl * 16 * G::CPD + bxl * 4;   // current block in curt (dwords)
@@ -1243,7 +1272,10 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             if (lane == 0) atomicAdd(&st_sur, nsur);
 #endif
             if (nsur > (uint32_t)CAP) {
-                if (lane == 0) atomicAdd(&st_fb, 1u);
+                if (lane == 0) {
+                    atomicAdd(&st_fb, 1u);
+                    SO_OPS_ADD(&st_ops, kDenseSadOps);
+                }
                 if (probe == 3) continue;
                 // fallback: the dense wave search on the single-copy window
                 wave_dense_block<16, false, RP, 0, false, true>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u, tid,
@@ -1261,6 +1293,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
                 if (lane == 0 && key < keys[u]) keys[u] = key;
                 continue;
             }
+            if (lane == 0) SO_OPS_ADD(&st_ops, (nsur <= 4 ? 4u : 16u * ((nsur + 15) / 16)) * 256u);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1343,7 +1376,7 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
     __shared__ uint16_t list[G::NW * G::CAPL];
     __shared__ uint32_t lcount[G::NW];
     __shared__ unsigned long long keys[G::NBLK];
-    __shared__ uint32_t st[2];
+    __shared__ uint32_t st[3];
     const Sea2Lds L{win, b4w, curt, a4, list, lcount, keys, st};
     SO_STAMP_REC_SET(g_sea_stamps ? g_sea_stamps + (size_t)blockIdx.x * 12 : nullptr);
     sea2_tile<Sea2Geo>(L, blockIdx.x, cur, refs, nref, H, W, by0, by1, probe);
@@ -1441,7 +1474,7 @@ struct PTileLds {
     uint32_t a4[G::NBLK * 4];
     uint32_t lcount[G::NW];
     unsigned long long keys[NU];
-    uint32_t st[2];
+    uint32_t st[3];
     int32_t mer[NU][4];                    // decoded ME records (dx, dy, ref, sad)
     int32_t msum[G::TBY];                  // two-pass runs: pass-1 token sum of each block row
     double un[VBS ? PTileGeoVbs<G>::U64 : PTileGeo<G>::U64];   // byte sums + survivor lists | FP64 transposes
@@ -2233,16 +2266,29 @@ struct PRunArgs {
 #define SO_RUN_TIMEOUT_WORD 32
 #endif
 #ifndef SO_RUN_DONE_BASE
-#define SO_RUN_DONE_BASE 96
+#define SO_RUN_DONE_BASE 128
 #endif
-// the task counter (hammered by every workgroup's dequeue), the timeout count and the done
-// flags live on separate 128-byte lines
+// the task counter (hammered by every workgroup's dequeue), the timeout count, the fallback and
+// SAD counts, the wait diagnostic record and the done flags live on separate 128-byte lines
 constexpr int kRunTimeoutWord = SO_RUN_TIMEOUT_WORD, kRunDoneBase = SO_RUN_DONE_BASE;
 // [1], [2] on the task counter's line: touched once per workgroup.  [64] (a line of its own):
 // blocks whose SEA search took the dense fallback, summed over launches until the caller clears
 // it (SO_P_RUN_FALLBACK_WORD); each workgroup adds its total once, on its way out.  (Adding per
 // tile on the timeout word's line, which every waiting workgroup reads, cost +17 % per frame.)
-constexpr int kRunExitWord = 1, kRunEpochWord = 2, kRunFallbackWord = 64;
+// [66..67] (same line, 64-bit): the search's executed SAD byte operations, added the same way.
+constexpr int kRunExitWord = 1, kRunEpochWord = 2, kRunFallbackWord = 64, kRunSadOpsWord = SO_P_RUN_SAD_OPS_WORD;
+// The waits' health words on the timeout word's line (written only when something unusual
+// happened, so the per-tile read of the timeout word stays a clean hit):
+//   [33] waits whose relaxed polls kept missing a flag that an atomic read then found set
+//        (evidence of a stale copy; the wait itself goes on with atomic reads and completes);
+//   [34] poll intervals of >= 1 ms (the wave was descheduled: queue preemption / CWSR), which
+//        do not count towards the wait's bound;
+//   [35] the diagnostic record's claim counter.
+// [96..127]: the record of the first wait that timed out (SO_P_RUN_DIAG_WORD, layout in
+// include/streamoptima.h; Engine.check_run prints it).
+constexpr int kRunStaleWord = SO_P_RUN_STALE_WORD, kRunGapWord = SO_P_RUN_GAP_WORD, kRunClaimWord = 35;
+constexpr int kRunDiagWord = SO_P_RUN_DIAG_WORD;
+static_assert(kRunDoneBase >= kRunDiagWord + 32, "the diagnostic record precedes the done flags");
 // kRunFPipe2P: the frame pipeline with two-pass RC (each tile a pass-1 and a pass-2 task as
 // kRunTwoPass; the reference arrives in the landing planes as kRunFPipe, and pass 2 pushes
 // the final reconstruction on to the rank encoding the next frame)
@@ -2256,6 +2302,122 @@ constexpr int kRunSingle = 0, kRunStripe = 1, kRunFPipe = 2, kRunTwoPass = 3, kR
 #else
 #define SO_RUN_PROF(word, cyc) do { } while (0)
 #endif
+
+// ---- dependency waits ---------------------------------------------------------------------------
+// What a wave polls for: lane l waits on *c (when need) until it reads `want` (agent-scope
+// flags of this GPU) or `sys_want` (sysl: another rank's flags, system scope).
+struct RunWait {
+    int task, f, dep, tile, mode;
+    uint32_t want, sys_want;
+    unsigned long long limit;   // polling time bound, 100 MHz s_memrealtime ticks
+};
+constexpr unsigned long long kRunGapTicks = 100000ull;        // 1 ms: a descheduled wave
+constexpr unsigned long long kRunEscalateTicks = 100000ull;   // 1 ms of polling: atomic reads
+
+SO_DEV uint32_t rmw_read(const uint32_t* c) {
+    return __hip_atomic_fetch_add(const_cast<uint32_t*>(c), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Called by every lane of ONE wave (wave-uniform control flow throughout: a lane-0 branch
+// around a loop with a barrier after it gets structurised into a hang, see p_run_kernel).
+// Relaxed polls with s_sleep; the elapsed time counts only poll-to-poll intervals shorter than
+// 1 ms, so a wave that was descheduled (queue preemption) is not mistaken for a lost flag;
+// after 1 ms of polling the awaited local flags are read with atomic RMWs instead (these cannot
+// be served from a stale cached copy; a first RMW that finds a flag the loads kept missing is
+// counted in ws[kRunStaleWord]).  Past `limit` the wave counts a timeout and, if it is the
+// first, writes the diagnostic record (ws[kRunDiagWord..+31]) and keeps reading the awaited
+// flags for up to 50 ms more to record when they arrive.  Returns the lane's last raw value.
+// (Durations in 32 bits of 100 MHz ticks: the wait state is a handful of SGPRs.)
+SO_DEV uint32_t run_poll(const uint32_t* c, bool need, bool sysl, uint32_t* ws, const RunWait& w) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t one = lane == 0 ? 1u : 0u;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t last = 0, susp = 0, raw = 0;   // ticks since t0 at the last poll; descheduled ticks
+    bool esc = false;
+    for (;;) {
+        if (sysl)
+            raw = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else if (esc && need)
+            raw = rmw_read(c);
+        else
+            raw = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool ok = raw == (sysl ? w.sys_want : w.want);
+        if (__builtin_amdgcn_ballot_w64(need && !ok) == 0) break;
+        __builtin_amdgcn_s_sleep(1);
+        const uint32_t now = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t0), gap = now - last;
+        last = now;
+        if (gap >= (uint32_t)kRunGapTicks) {
+            susp += gap;
+            __hip_atomic_fetch_add(&ws[kRunGapWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const uint32_t active = now - susp;
+        if (!esc && active > (uint32_t)kRunEscalateTicks) {
+            esc = true;
+            const uint32_t v2 = (need && !sysl) ? rmw_read(c) : raw;
+            if (__builtin_amdgcn_ballot_w64(need && !sysl && !ok && v2 == w.want) != 0)
+                __hip_atomic_fetch_add(&ws[kRunStaleWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (active > (uint32_t)w.limit) {
+            __hip_atomic_fetch_add(&ws[kRunTimeoutWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t claim = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_fetch_add(&ws[kRunClaimWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (claim == 0u) {   // uniform: the first timed-out wait of the workspace records itself
+                const uint32_t rv = (need && !sysl) ? rmw_read(c) : raw;
+                const uint64_t bneed = __builtin_amdgcn_ballot_w64(need);
+                const uint64_t bsys = __builtin_amdgcn_ballot_w64(need && sysl);
+                const uint64_t brmw = __builtin_amdgcn_ballot_w64(need && !sysl && rv == w.want);
+                const uint32_t other = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane - 20) & 63) << 2, (int)raw);
+                uint32_t hw, xcc;
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                uint32_t v = other;
+                v = lane == 1 ? (uint32_t)w.task : v;
+                v = lane == 2 ? (uint32_t)w.f : v;
+                v = lane == 3 ? (uint32_t)w.dep : v;
+                v = lane == 4 ? (uint32_t)w.tile : v;
+                v = lane == 5 ? w.want : v;
+                v = lane == 6 ? w.sys_want : v;
+                v = lane == 7 ? ((uint32_t)w.mode | (esc ? 1u << 12 : 0u)) : v;
+                v = lane == 8 ? (uint32_t)bneed : v;
+                v = lane == 9 ? (uint32_t)bsys : v;
+                v = lane == 10 ? active : v;
+                v = lane == 11 ? now : v;
+                v = lane == 12 ? susp : v;
+                v = lane == 13 ? 0u : v;
+                v = lane == 14 ? 0xFFFFFFFFu : v;
+                v = lane == 15 ? hw : v;
+                v = lane == 16 ? xcc : v;
+                v = lane == 17 ? (uint32_t)blockIdx.x : v;
+                v = lane == 18 ? (uint32_t)gridDim.x : v;
+                v = lane == 19 ? (uint32_t)brmw : v;
+                if (lane >= 1 && lane < 32)
+                    __hip_atomic_store(&ws[kRunDiagWord + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // keep reading the awaited flags (atomically) for up to 50 ms: when -- whether --
+                // they arrive tells a slow holder from a lost or unseen flag
+                const unsigned long long ta = __builtin_amdgcn_s_memrealtime();
+                uint32_t arrive = 0xFFFFFFFFu;
+                for (;;) {
+                    const uint32_t x = sysl ? __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                            : (need ? rmw_read(c) : 0u);
+                    const uint32_t el = (uint32_t)(__builtin_amdgcn_s_memrealtime() - ta);
+                    if (__builtin_amdgcn_ballot_w64(need && x != (sysl ? w.sys_want : w.want)) == 0) {
+                        arrive = el;
+                        break;
+                    }
+                    if (el > 5000000u) break;
+                    __builtin_amdgcn_s_sleep(8);
+                }
+                if (lane == 14)
+                    __hip_atomic_store(&ws[kRunDiagWord + 14], arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0)
+                    __hip_atomic_store(&ws[kRunDiagWord], SO_P_RUN_DIAG_MAGIC, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+            break;
+        }
+    }
+    return raw;
+}
 
 // VBS: VBSEnable (the block + sub-block dense search, tq16_vbs; ~128 VGPRs, 4 waves per SIMD)
 template <int NW, int MODE, bool VBS = false>
@@ -2292,7 +2454,11 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     const int lane = tid & 63;
     const uint32_t one = lane == 0 ? 1u : 0u;
     __shared__ uint32_t s_fbsum;   // this workgroup's dense-searched blocks over its tasks (LDS: a
-    if (tid == 0) s_fbsum = 0;     // register kept live across the loop cost spills)
+    __shared__ unsigned long long s_ops;   // register kept live across the loop cost spills)
+    if (tid == 0) {                        // and its SAD byte operations
+        s_fbsum = 0;
+        s_ops = 0;
+    }
     // this launch's epoch: ws[2] + 1 (ws[2] = the last finished launch's; written by that
     // launch's last workgroup, so every workgroup here reads it before it can change).  Done
     // flags hold the epoch of the launch that set them: nothing is zeroed between launches.
@@ -2380,32 +2546,20 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                     rneed = true;
                 }
             }
-            // 50 ms within one GPU; 2 s where the flags come from another rank, whose host may
-            // enqueue its launch late (a rank's kernel can start waiting on a neighbour whose
-            // process is descheduled, e.g. several ranks time-sharing one GPU)
+            // 50 ms of polling within one GPU; 2 s where the flags come from another rank, whose
+            // host may enqueue its launch late (a rank's kernel can start waiting on a neighbour
+            // whose process is descheduled, e.g. several ranks time-sharing one GPU)
             constexpr unsigned long long kWaitLimit = (STRIPE || FPIPE) ? 200000000ull : 5000000ull;
             // one GPU: lane 9 reads, in the same round trips, the dense-block count of the same tile
             // of the reference frame (a heuristic only -- dense and SEA searches are both exact --
             // so it is read unordered with the flags)
             const bool fbl = MODE == kRunSingle && lane == 9 && dep >= 0;
             if (fbl) c = tilefb + (size_t)dep * ntiles + tile;
-            uint32_t raw = 0;
+#ifdef SO_RUN_PROFILE
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            for (;;) {
-                uint32_t v;
-                if ((STRIPE || FPIPE) && rneed) {
-                    v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == sp.epoch ? 1u : 0u;
-                } else {
-                    raw = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    v = raw == ep ? 1u : 0u;
-                }
-                if (__builtin_amdgcn_ballot_w64((need || rneed) && v == 0u) == 0) break;
-                __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitLimit) {
-                    __hip_atomic_fetch_add(&ws[kRunTimeoutWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-            }
+#endif
+            const RunWait rw{task, f, dep, tile, MODE | (VBS ? 16 : 0) | (pass << 8), ep, sp.epoch, kWaitLimit};
+            const uint32_t raw = run_poll(c, need || rneed, (STRIPE || FPIPE) && rneed, ws, rw);
             SO_RUN_PROF(51, (__builtin_amdgcn_s_memrealtime() - t0) * 25);   // 100 MHz ticks -> ~2.5 GHz cycles
 #ifdef SO_STAMPS
             if (lane == 0 && rec) rec[10] = __builtin_amdgcn_s_memrealtime();
@@ -2458,24 +2612,16 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             } else {
                 if (wave == 0) {   // every tile of this tile row finished pass 1 (tiles_x <= 64)
                     const uint32_t* c = sp.p1done + (size_t)f * ntiles + ty * tiles_x + (lane < tiles_x ? lane : 0);
-                    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #if SO_RUN_ABORT_CHECK
                     const bool skip =
                         __hip_atomic_load(ws + kRunTimeoutWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
 #else
                     const bool skip = false;
 #endif
-                    while (!skip) {
-                        const bool v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ep;
-                        if (__builtin_amdgcn_ballot_w64(lane < tiles_x && !v) == 0) break;
-                        __builtin_amdgcn_s_sleep(1);
-                        // 50 ms; 2 s in the frame pipeline, whose pass-1 tasks may wait that long on
-                        // another rank's reconstruction
-                        if (__builtin_amdgcn_s_memrealtime() - t0 > (FPIPE ? 200000000ull : 5000000ull)) {
-                            __hip_atomic_fetch_add(&ws[kRunTimeoutWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            break;
-                        }
-                    }
+                    // 50 ms of polling; 2 s in the frame pipeline, whose pass-1 tasks may wait that
+                    // long on another rank's reconstruction
+                    const RunWait rw{task, f, -2, tile, MODE | (2 << 8), ep, sp.epoch, FPIPE ? 200000000ull : 5000000ull};
+                    if (!skip) run_poll(c, lane < tiles_x, false, ws, rw);
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     SO_RUN_PROF(50, __builtin_amdgcn_s_memtime() - pt0);
@@ -2570,7 +2716,10 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (pass == 1 && tid == 0) s_fbsum += S.st[0];   // this tile's dense-searched blocks
+        if (pass == 1 && tid == 0) {   // this tile's dense-searched blocks and SAD byte operations
+            s_fbsum += S.st[0];
+            s_ops += S.st[2];
+        }
 #ifdef SO_STAMPS
         if (tid == 0 && rec) {
             uint32_t hw, xcc;
@@ -2588,6 +2737,10 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
         if (fbsum != 0u)
             __hip_atomic_fetch_add(&ws[kRunFallbackWord], lane == 0 ? fbsum : 0u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long ops = s_ops;
+        if (ops != 0ull)
+            __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(ws + kRunSadOpsWord), lane == 0 ? ops : 0ull,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (wave == 0) {
         const uint32_t o = __builtin_amdgcn_readfirstlane(
@@ -2613,11 +2766,31 @@ size_t p_run_workspace_words(int H, int W) {
 
 // Launch the run in <= kRunMax-frame launches.  max_wg > 0 caps the resident grid (several
 // ranks sharing one GPU in the tests).
-static void device_shape(int* ncu) {
+// The calling thread's current device: its CU count and the kernel's resident workgroups per CU
+// (the occupancy API), cached per (device, kernel) under a mutex -- a process may drive several
+// devices from several host threads.  (The grid only sizes the run: a workgroup that is not
+// resident holds no task, so an over-estimate costs speed, never progress.)
+static int run_shape(const void* kernel, int* ncu, int* per_cu) {
+    static std::mutex mu;
+    static std::map<std::pair<int, const void*>, std::pair<int, int>> cache;
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || *ncu <= 0)
-        *ncu = 256;
+    const hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) {
+        set_error("p_run: hipGetDevice: %s", hipGetErrorString(e));
+        return (int)e;
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_pair(dev, kernel);
+    auto it = cache.find(key);
+    if (it == cache.end()) {
+        int n = 0, p = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&p, kernel, SO_PTILE_NW * 64, 0) != hipSuccess || p <= 0) p = 1;
+        it = cache.emplace(key, std::make_pair(n, p)).first;
+    }
+    *ncu = it->second.first;
+    *per_cu = it->second.second;
+    return SO_OK;
 }
 
 // refs / deps (may be null: one run, frame g predicting from g - 1 and frame 0 from ref0): frame g
@@ -2629,12 +2802,10 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
                           int max_wg, hipStream_t st, const uint8_t* const* refs = nullptr,
                           const int* deps = nullptr, int conc = 1, double lam = 0.0) {
     using G = Sea2GeoT<SO_PTILE_NW>;
-    static int ncu = 0, per_cu = 0;
-    if (ncu == 0) {
-        device_shape(&ncu);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, p_run_kernel<SO_PTILE_NW, MODE, VBS>,
-                                                         SO_PTILE_NW * 64, 0) != hipSuccess || per_cu <= 0)
-            per_cu = 1;
+    int ncu = 0, per_cu = 0;
+    {
+        const int rc = run_shape(reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS>), &ncu, &per_cu);
+        if (rc != SO_OK) return rc;
     }
     const int nbx = W / 16;
     const int rows = MODE == kRunStripe ? sp0.by1 - sp0.by0 : H / 16;
@@ -2663,10 +2834,12 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
         // wait on others -- a frame's time is its slowest tile's (1080p: 30 vs 33 us/frame).
         int pcu = (int)((ntiles * conc + ncu - 1) / ncu);
         if (pcu > per_cu) pcu = per_cu;
-        if (const char* e = getenv("SO_RUN_PER_CU")) {   // A/B only: resident workgroups per CU
+#ifdef SO_AB
+        if (const char* e = getenv("SO_RUN_PER_CU")) {   // A/B builds only: resident workgroups per CU
             const int v = atoi(e);
             if (v > 0 && v <= per_cu) pcu = v;
         }
+#endif
         long grid = (long)ncu * pcu;
         if (grid > ntiles * n) grid = ntiles * n;
         if (max_wg > 0 && grid > max_wg) grid = max_wg;
@@ -2679,7 +2852,9 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
             // different ranks trail each other by ~lag + 2 rows, so more ranks want less)
             int lag = (int)((grid + tiles_x - 1) / tiles_x);
             if (sp0.p2lag > 0 && sp0.p2lag < lag) lag = sp0.p2lag;
-            if (const char* e = getenv("SO_P2LAG")) lag = atoi(e);   // A/B only
+#ifdef SO_AB
+            if (const char* e = getenv("SO_P2LAG")) lag = atoi(e);   // A/B builds only
+#endif
             sp.p2lag = lag < 1 ? 1 : (lag > ntr ? ntr : lag);
         }
         hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, MODE, VBS>), dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), 0, st, a, n,
@@ -2905,12 +3080,16 @@ int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, in
     const int nbx = W / bs, nrows = by1 - by0;
     if (nrows <= 0) return SO_OK;
     if (sr == 16 && (bs == 16 || bs == 8) && (out_sub == nullptr || bs == 16)) {
-        // SO_ME_IMPL=dense selects the dense wave kernel where SEA would run (A/B, bench)
+#ifdef SO_AB   // A/B builds: SO_ME_IMPL=dense selects the dense wave kernel where SEA would run
         const char* impl = getenv("SO_ME_IMPL");
         const bool use_dense = impl && strcmp(impl, "dense") == 0;
+        const char* pr = getenv("SO_SEA_PROBE");   // timing probes only (tools/me_ab2.py)
+#else
+        const bool use_dense = false;
+        const char* pr = nullptr;
+#endif
         if (!use_dense && bs == 16 && out_sub == nullptr) {
             const dim3 sgrid(((nbx + Sea2Geo::TBX - 1) / Sea2Geo::TBX) * ((nrows + Sea2Geo::TBY - 1) / Sea2Geo::TBY));
-            const char* pr = getenv("SO_SEA_PROBE");   // timing probes only (tools/me_ab2.py)
             hipLaunchKernelGGL(me_sea2_kernel, sgrid, dim3(Sea2Geo::NTHREADS), 0, st, cur, refs, nref, H, W, by0, by1,
                                out_best, pr ? atoi(pr) : 0);
             return check_launch("me_sea2_kernel");

@@ -99,6 +99,8 @@ class StripeGOPEncoder:
         def stripe(cur, intra, qp_rd, plane):
             sym = e.new_stripe_symbols(0 if intra else 1, self.by0, self.by1, plane)
             if self.by1 <= self.by0:            # a rank past the last block row idles
+                if use_map:   # but joins the QP-map all_gather like every rank (gather_symbols)
+                    sym.extra["qp_map"] = torch.zeros(e.nb, dtype=torch.int32, device=e.device)
                 return sym
             qmap = torch.empty(e.nb, dtype=torch.int32, device=e.device) if use_map else None
 

@@ -8,17 +8,18 @@ these tensors only when asked.
 """
 from __future__ import annotations
 
+import collections
 from dataclasses import dataclass, field
 
 import ctypes
 
 import torch
 
-from . import _lib
+from . import _lib, runhealth
 
 SLACK = 64  # bytes readable past every plane (kernels read aligned words at row ends)
-RUN_TIMEOUT_WORD = 32   # so_encode_p_run workspace: the timeout count (include/streamoptima.h)
-RUN_FALLBACK_WORD = 64  # ... and the count of blocks whose SEA search took the dense fallback
+RUN_TIMEOUT_WORD = runhealth.TIMEOUT_WORD     # so_encode_p_run workspace (include/streamoptima.h)
+RUN_FALLBACK_WORD = runhealth.FALLBACK_WORD   # blocks whose SEA search took the dense fallback
 
 
 def alloc_planes(n: int, h: int, w: int, device, fill: int | None = None) -> torch.Tensor:
@@ -72,7 +73,9 @@ class Engine:
         self.me_mode = int(me_mode)
         self.fme = bool(fme)
         self._fme_ws = None
-        self._consts: dict = {}
+        self._consts: collections.OrderedDict = collections.OrderedDict()   # device_const_i32 (LRU)
+        self._pinned_consts: set = set()                                    # ... held by captured graphs
+        self.wait_health = runhealth.HealthLog()   # non-fatal wait counts of the persistent runs
 
     MAX_CONSTS = 4096
 
@@ -80,24 +83,32 @@ class Engine:
         """A read-only int32 device copy of `values`, uploaded once per distinct content, so
         a GOP replayed from a captured HIP graph issues no host->device copy.
 
-        Entries are never evicted behind the caller's back: a captured graph holds their raw
-        device pointers, so freeing one would make a later replay read freed memory.  Past
-        MAX_CONSTS distinct contents this raises; a caller that knows no graph references
-        the cached constants any more calls release_consts()."""
+        The cache is LRU-bounded at MAX_CONSTS entries, except that an entry looked up while
+        a HIP graph is being captured on this device is pinned: the graph holds its raw
+        device pointer, so evicting it would make a later replay read freed memory.  Pinned
+        entries are dropped only by release_consts(), which the owner of such a graph calls
+        once the graph is gone."""
         host = torch.as_tensor(values, dtype=torch.int32).contiguous()
         key = (tuple(host.shape), host.numpy().tobytes())
         t = self._consts.get(key)
         if t is None:
-            if len(self._consts) >= self.MAX_CONSTS:
-                raise RuntimeError(f"Engine.device_const_i32: {self.MAX_CONSTS} distinct constants cached; call "
-                                   "release_consts() once no captured graph references them")
             t = self._consts[key] = host.to(self.device)
+            if len(self._consts) > self.MAX_CONSTS:   # evict the least recently used unpinned entry
+                for k in self._consts:
+                    if k not in self._pinned_consts and k != key:
+                        del self._consts[k]
+                        break
+        else:
+            self._consts.move_to_end(key)
+        if self.device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            self._pinned_consts.add(key)
         return t
 
     def release_consts(self) -> None:
-        """Drop the cached device constants (ROI offsets, row-QP schedules).  Only safe when no
-        captured HIP graph that used them will be replayed again."""
+        """Drop the cached device constants (ROI offsets, row-QP schedules), pinned ones too.
+        Only safe when no captured HIP graph that used them will be replayed again."""
         self._consts.clear()
+        self._pinned_consts.clear()
 
     def fme_workspace(self, nref: int) -> torch.Tensor:
         """Phase planes of the references' frac frames (rebuilt by every FME call)."""
@@ -340,19 +351,20 @@ class Engine:
     def run_timed_out(self) -> bool:
         """True if a dependency wait of any encode_p_run since the last check_run timed out
         (never expected: the run's symbols would then be unreliable).  Synchronises."""
-        ws = getattr(self, "_run_ws", None)
-        return bool(ws is not None and int(ws[RUN_TIMEOUT_WORD].item()) != 0)
+        return runhealth.timed_out(getattr(self, "_run_ws", None))
 
     def check_run(self) -> None:
-        """Raise if any encode_p_run since the last check timed out, then clear the count.
-        Encoder.encode()/encode_device(check=True) and bench.py call it once per GOP."""
+        """Raise if any encode_p_run since the last check timed out -- naming the first such
+        wait from the workspace's diagnostic record (runhealth.describe) -- then clear the
+        count; the non-fatal wait counts go to self.wait_health.  Encoder.encode() /
+        encode_device(check=True) and bench.py call it once per GOP."""
+        runhealth.check(getattr(self, "_run_ws", None), self.wait_health, "p_run_kernel")
+
+    def take_sad_ops(self) -> int:
+        """SAD byte operations the persistent runs' searches executed since the last call
+        (SO_P_RUN_SAD_OPS_WORD); clears the count.  Synchronises."""
         ws = getattr(self, "_run_ws", None)
-        if ws is None:
-            return
-        n = int(ws[RUN_TIMEOUT_WORD].item())
-        if n:
-            ws[RUN_TIMEOUT_WORD].zero_()
-            raise RuntimeError(f"p_run_kernel: {n} dependency wait(s) timed out; the GOP's symbols are unreliable")
+        return 0 if ws is None else runhealth.take_u64(ws, runhealth.SAD_OPS_WORD)
 
     def take_fallback_count(self) -> int:
         """Blocks of the persistent runs since the last call whose exact SEA search took the

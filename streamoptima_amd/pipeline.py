@@ -33,7 +33,7 @@ import ctypes
 
 import torch
 
-from . import _lib
+from . import _lib, runhealth
 from .dist import stripe_rows
 from .engine import FrameSymbols
 
@@ -43,8 +43,7 @@ HALO_TOP, HALO_BOT = 16, 32       # landing-plane rows above / below the stripe
 class StripeRunRank:
     """Buffers and launches of one rank of a GOP split into block-row stripes."""
 
-    def __init__(self, engine, world: int, rank: int, max_frames: int, stream=None, max_wg: int = 0,
-                 p2lag=None):
+    def __init__(self, engine, world: int, rank: int, max_frames: int, stream=None, max_wg: int = 0):
         e = engine
         if not e.pipelined_ok(1, vbs_ok=False):
             raise ValueError("the stripe run covers bs 16 / sr 16 / full search / no VBS, FME / W % 128 == 0")
@@ -71,6 +70,7 @@ class StripeRunRank:
         self.peer_up = self.peer_dn = None      # (virtual base of frame 0, flags array to set)
         self._opened = []
         self._ws = torch.zeros(lib.so_p_run_workspace_elems(e.h, e.w), dtype=torch.int32, device=e.device)
+        self.wait_health = runhealth.HealthLog()
 
     # ---- addressing -----------------------------------------------------------------------
     def _st(self):
@@ -217,13 +217,12 @@ class StripeRunRank:
         return out
 
     def timed_out(self) -> bool:
-        return int(self._ws[32].item()) != 0
+        return runhealth.timed_out(self._ws)
 
     def check(self) -> None:
-        n = int(self._ws[32].item())
-        if n:
-            self._ws[32].zero_()
-            raise RuntimeError(f"p_run stripe: {n} dependency wait(s) timed out (lost hand-off); symbols unreliable")
+        """Raise (naming the first timed-out wait: peer flags, slot, epoch) if a hand-off wait
+        timed out since the last check; clear the counts."""
+        runhealth.check(self._ws, self.wait_health, "p_run stripe (hand-off)")
 
 
 class PipelinedStripeGOPEncoder:
@@ -384,6 +383,7 @@ class FramePipeRank:
         self.peer = self.peer2 = None
         self._opened = []
         self._ws = torch.zeros(lib.so_p_run_workspace_elems(e.h, e.w), dtype=torch.int32, device=e.device)
+        self.wait_health = runhealth.HealthLog()
         self._syms = None
 
     def _st(self):
@@ -509,13 +509,12 @@ class FramePipeRank:
         return syms
 
     def timed_out(self) -> bool:
-        return int(self._ws[32].item()) != 0
+        return runhealth.timed_out(self._ws)
 
     def check(self) -> None:
-        n = int(self._ws[32].item())
-        if n:
-            self._ws[32].zero_()
-            raise RuntimeError(f"p_run frame pipeline: {n} dependency wait(s) timed out; symbols unreliable")
+        """Raise (naming the first timed-out wait: landing slot, flags, GOP epoch) if a wait
+        timed out since the last check; clear the counts."""
+        runhealth.check(self._ws, self.wait_health, "p_run frame pipeline")
 
 
 class FramePipelineGOPEncoder:

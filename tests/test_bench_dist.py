@@ -74,3 +74,21 @@ def test_bench_gpus_mismatch_is_an_error():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-plumbing", "--gpus", "2"], env=env,
                          capture_output=True, text=True, timeout=120)
     assert out.returncode != 0 and "WORLD_SIZE 1" in out.stderr
+
+
+def test_bench_secondary_failure_keeps_the_headline_line():
+    """A failing secondary measurement (a record, the PCIe leg, the CPU baseline) is recorded in
+    the line as {"error": ...} and named in `failed`; the headline line is still printed, and the
+    exit status is nonzero so the failure stays visible (no retry, no silent pass)."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-plumbing", "--frames", "2",
+                          "--steps", "1", "--warmup", "0", "--inject-failure", "records.1080p_x2gop"], env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode != 0
+    line = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["value"] > 0 and line["failed"] == ["records.1080p_x2gop"]
+    assert "injected" in line["records"]["records.1080p_x2gop"]["error"] or \
+        "--inject-failure" in line["records"]["records.1080p_x2gop"]["error"]
+    assert "secondary measurement(s) failed" in out.stderr

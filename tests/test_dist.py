@@ -163,8 +163,10 @@ def _worker(rank, world, port, case_name, outdir):
 
 
 @pytest.mark.parametrize("world,case_name", [(2, "plain"), (2, "vbs_nref2"), (2, "rc2"), (4, "plain"),
-                                             (2, "rc3_roi"), (3, "roi_only")])
+                                             (2, "rc3_roi"), (3, "roi_only"), (4, "roi_only")])
 def test_stripe_gop_matches_single_process_oracle(tmp_path, world, case_name):
+    """(4, "roi_only"): 6 block rows over 4 ranks leave rank 3 idle; it must still join the
+    QP-map all_gather (an idle rank that skipped it hung the others)."""
     from oracle.gop import encode_gop
     mp.start_processes(_worker, args=(world, _free_port(), case_name, str(tmp_path)), nprocs=world,
                        start_method="spawn")

@@ -14,6 +14,8 @@ import torch
 
 from conftest import GOLDEN
 
+from streamoptima_amd import _lib
+
 pytestmark = pytest.mark.gpu
 
 FIX = json.load(open(os.path.join(GOLDEN, "large_gops.json")))
@@ -119,7 +121,7 @@ def test_interleaved_gops_ragged_runs(gpu, monkeypatch):
 @pytest.mark.parametrize("roi", [None, [(100, 40, 400, 200, -2), (0, 150, 260, 272, 3)]])
 def test_two_pass_run_matches_per_frame(gpu, monkeypatch, roi, fused):
     """so_encode_p_run_2pass -- the library-enqueued per-frame sequence (default) and both
-    passes of every P-frame in one persistent launch (SO_RUN_2PASS_FUSED=1) -- against the
+    passes of every P-frame in one persistent launch (SO_OPT_RUN_2PASS_FUSED) -- against the
     Python-driven per-frame sequence pass 1 -> so_qp_map -> pass 2 (SO_PIPELINE=0), frame by
     frame including the QP maps, on a 640x272 GOP (5 x 9 tiles: pass-2 tasks of the 5-tile rows
     waiting on their row's pass 1), with and without ROI, two runs (intra_dur 5 of 11)."""
@@ -138,8 +140,8 @@ def test_two_pass_run_matches_per_frame(gpu, monkeypatch, roi, fused):
     exp_d = [symbols_digest(s) for s in exp["symbols"]]
     monkeypatch.delenv("SO_PIPELINE")
     monkeypatch.setenv("SO_RUN_2PASS", "1")
-    monkeypatch.setenv("SO_RUN_2PASS_FUSED", fused)
-    got = codec.encode_device(fr, 5)
+    with _lib.option(_lib.OPT_RUN_2PASS_FUSED, int(fused)):
+        got = codec.encode_device(fr, 5)
     torch.cuda.synchronize()
     assert all("qp_map" in s.extra for s in got["symbols"])
     assert [symbols_digest(s) for s in got["symbols"]] == exp_d
@@ -255,7 +257,7 @@ def test_vbs_run_matches_per_frame(gpu, monkeypatch, h, w, intra_dur):
 def test_fast_me_chain_speculation_matches_serial_walk(gpu, monkeypatch, vbs, fme):
     """fast_me mode 0 (Encoder.py:719-742, the predictor chain of :462-585): the segmented
     speculative chain (one wavefront per 32-block segment, warm-up guess, in-order check and
-    redo) against the one-wavefront serial walk (SO_FASTME_SERIAL=1), frame by frame, on
+    redo) against the one-wavefront serial walk (SO_OPT_FASTME_SERIAL), frame by frame, on
     1920x1088 with and without VBS / FME -- and with no warm-up and 8-block segments, where
     nearly every guess is wrong and the redo path carries the result."""
     from streamoptima_amd.Encoder import Y_Video_codec
@@ -269,10 +271,8 @@ def test_fast_me_chain_speculation_matches_serial_walk(gpu, monkeypatch, vbs, fm
 
     def run():
         return [symbols_digest(s) for s in codec.encode_device(fr, f)["symbols"]]
-    monkeypatch.setenv("SO_FASTME_SERIAL", "1")
-    exp = run()
-    monkeypatch.delenv("SO_FASTME_SERIAL")
+    with _lib.option(_lib.OPT_FASTME_SERIAL, 1):
+        exp = run()
     assert run() == exp
-    monkeypatch.setenv("SO_FASTME_WARM", "0")
-    monkeypatch.setenv("SO_FASTME_K", "8")
-    assert run() == exp
+    with _lib.option(_lib.OPT_FASTME_WARMUP, 0), _lib.option(_lib.OPT_FASTME_SEGMENT, 8):
+        assert run() == exp
