@@ -189,6 +189,13 @@ int so_get_option(int option);
 #define SO_P_RUN_DIAG_WORD 96
 #define SO_P_RUN_DIAG_MAGIC 0x534F0001u
 size_t so_p_run_workspace_elems(int H, int W);
+/* The workgroups the persistent run kernel keeps resident on the calling thread's current
+ * device (CUs x workgroups per CU; vbs: the VBSEnable kernel): the grid of an uncapped launch.
+ * Several ranks' runs sharing ONE device (in-process tests, time-shared rehearsals) must keep
+ * the sum of their grids (max_wg of the stripe / frame-pipeline entry points) within it: a
+ * launch that cannot become resident would leave the others waiting on its tasks (DESIGN.md
+ * section 6, "Forward progress").  SO_E_INVALID if the device query fails. */
+int so_p_run_resident_workgroups(int vbs);
 int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W,
                     int bs, int sr, int qp_rd, const int32_t* qp_row, int vbs, double lam,
                     uint8_t* const* out_split,

@@ -39,6 +39,7 @@ _SIGS = {
     "so_encode_p_rows": ([_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _d, _vp, _vp, _vp, _vp,
                           _vp, _vp, _vp, _vp, _vp], _i),
     "so_p_run_workspace_elems": ([_i, _i], _sz),
+    "so_p_run_resident_workgroups": ([_i], _i),
     "so_encode_p_run": ([_vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _i, _d, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
                         _i),
     "so_encode_p_run_2pass": ([_vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -118,6 +119,8 @@ def load(path: str | None = None):
                 "There is no CPU fallback for the encode path.")
         lib = ctypes.CDLL(p)
         for name, (args, res) in _SIGS.items():
+            if p != LIB_PATH and not hasattr(lib, name):
+                continue   # an older A/B build (tools/) without a newer entry point
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = res

@@ -416,6 +416,15 @@ size_t so_p_run_workspace_elems(int H, int W) {
     return p_run_workspace_words(H, W);
 }
 
+int so_p_run_resident_workgroups(int vbs) {
+    const int n = p_run_capacity(vbs ? 1 : 0);
+    if (n <= 0) {
+        set_error("so_p_run_resident_workgroups: device query failed");
+        return SO_E_INVALID;
+    }
+    return n;
+}
+
 int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int bs, int sr,
                     int qp_rd, const int32_t* qp_row, int vbs, double lam, uint8_t* const* out_split,
                     int16_t* const* out_mv, int16_t* const* out_qtc, int32_t* const* out_tokens,

@@ -1165,7 +1165,12 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             const uint32_t bsh = (uint32_t)lb0 & 3;
             int lo1 = lb0 >> 2;
             asm volatile("" : "+v"(lo1));
+#ifdef SO_B4_READ2   // A/B: plain (mergeable into ds_read2_b32) reads of the byte-sum rows
+            typedef const __attribute__((address_space(3))) uint32_t* lds_u32p_;
+            lds_u32p_ p1 = (lds_u32p_)(b4w + lo1);
+#else
             lds_vu32p p1 = (lds_vu32p)(b4w + lo1);
+#endif
             // lb[t] = (LBq << 16) | t: v_sad_hi_u8 accumulates each sum << 16 onto the initial t
             // (an inline constant), so the smallest-bound key below needs no shifts or ORs
             // (LBq <= 16 * 255 < 2^16)
@@ -2329,6 +2334,25 @@ SO_DEV uint32_t rmw_read(const uint32_t* c) {
 // flags for up to 50 ms more to record when they arrive.  Returns the lane's last raw value.
 // (Durations in 32 bits of 100 MHz ticks: the wait state is a handful of SGPRs.)
 SO_DEV uint32_t run_poll(const uint32_t* c, bool need, bool sysl, uint32_t* ws, const RunWait& w) {
+#ifdef SO_WAIT_SIMPLE   // TEMP A/B: the round-3 loop
+    {
+        const uint32_t one = (threadIdx.x & 63) == 0 ? 1u : 0u;
+        uint32_t raw = 0;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            raw = sysl ? __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                       : __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool ok = raw == (sysl ? w.sys_want : w.want);
+            if (__builtin_amdgcn_ballot_w64(need && !ok) == 0) break;
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > w.limit) {
+                __hip_atomic_fetch_add(&ws[kRunTimeoutWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        return raw;
+    }
+#endif
     const int lane = threadIdx.x & 63;
     const uint32_t one = lane == 0 ? 1u : 0u;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -2791,6 +2815,15 @@ static int run_shape(const void* kernel, int* ncu, int* per_cu) {
     *ncu = it->second.first;
     *per_cu = it->second.second;
     return SO_OK;
+}
+
+// Resident workgroups of the persistent run kernel on the current device (so_p_run_resident_
+// workgroups): the grid a launch uses when nothing caps it.
+int p_run_capacity(int vbs) {
+    int ncu = 0, per_cu = 0;
+    const int rc = vbs ? run_shape(reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, kRunSingle, true>), &ncu, &per_cu)
+                       : run_shape(reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, kRunSingle, false>), &ncu, &per_cu);
+    return rc != SO_OK ? -rc : ncu * per_cu;
 }
 
 // refs / deps (may be null: one run, frame g predicting from g - 1 and frame 0 from ref0): frame g

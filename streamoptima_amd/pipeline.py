@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import weakref
 
 import torch
 
@@ -38,6 +39,56 @@ from .dist import stripe_rows
 from .engine import FrameSymbols
 
 HALO_TOP, HALO_BOT = 16, 32       # landing-plane rows above / below the stripe
+
+# Resident-slot claims of the ranks living in THIS process, per device (DESIGN.md section 6,
+# "Forward progress"): a rank's persistent launch may wait on another rank's tasks, which only
+# a resident workgroup of that rank's launch can take.  One rank per GPU always fits (each
+# launch's grid is at most its device's resident capacity).  Ranks sharing one device (the
+# in-process tests, --share-gpu rehearsals) must cap their grids (max_wg) so that every
+# launch can be resident at once -- in practice with a margin: three two-pass ranks whose grids
+# summed to exactly the device's capacity stalled (profiles/r03/fpipe2p_fullcap_w3.log), while
+# three quarters of it has always run -- so ranks sharing a device may together claim that.  A
+# rank whose claim would overflow it is refused here instead of stalling its peers until the
+# wait bound.
+_CLAIMS: dict = {}
+SHARED_LIMIT = 0.75
+
+
+def _claim_slots(owner, engine, max_wg: int, vbs: bool):
+    """Record this rank's resident-slot claim on its device (the fraction of the device's
+    resident workgroups its launch grid takes); refuse it if the device would be overcommitted."""
+    dev = engine.device.index if engine.device.index is not None else torch.cuda.current_device()
+    with torch.cuda.device(dev):
+        cap = _lib.load().so_p_run_resident_workgroups(int(vbs))
+    if cap <= 0:
+        _lib.check(cap, "so_p_run_resident_workgroups")
+    want = max_wg if 0 < max_wg <= cap else cap
+    frac = want / cap
+    live = _CLAIMS.setdefault(dev, {})
+
+    def limit():   # a lone rank: the whole device; ranks sharing it: SHARED_LIMIT of it together
+        return 1.0 if not live else SHARED_LIMIT
+    held = sum(live.values())
+    if held + frac > limit() + 1e-9:
+        import gc
+        gc.collect()   # ranks already dropped but held by a reference cycle release their claims
+        held = sum(live.values())
+    if held + frac > limit() + 1e-9:
+        raise ValueError(f"{type(owner).__name__}: {len(live)} rank(s) of this process already hold {held:.2f} of the "
+                         f"resident workgroups of cuda:{dev}; this rank's run needs {want} of {cap} (max_wg "
+                         f"{max_wg or 'uncapped'}). Ranks sharing one GPU must cap max_wg so that their launches "
+                         f"together use at most {SHARED_LIMIT:.0%} of it (DESIGN.md section 6, forward progress)")
+    key = id(owner)
+    live[key] = frac
+    owner._claim = (dev, key)
+    weakref.finalize(owner, live.pop, key, None)
+    return want
+
+
+def _release_slots(owner) -> None:
+    dev, key = getattr(owner, "_claim", (None, None))
+    if dev is not None:
+        _CLAIMS.get(dev, {}).pop(key, None)
 
 
 class StripeRunRank:
@@ -54,6 +105,7 @@ class StripeRunRank:
         self.max_frames = max_frames
         self.stream = stream
         self.max_wg = max_wg
+        self.resident = _claim_slots(self, e, max_wg, False)
         self.tiles_x = e.w // 128
         lib = self.lib = _lib.load()
         w = e.w
@@ -137,6 +189,7 @@ class StripeRunRank:
                 self.lib.so_free_device(p)
         self._planes = ctypes.c_void_p()
         self._flags = ctypes.c_void_p()
+        _release_slots(self)
 
     # ---- one GOP ---------------------------------------------------------------------------
     def new_symbols(self, frame_type: int) -> FrameSymbols:
@@ -368,6 +421,7 @@ class FramePipeRank:
             raise ValueError("the frame pipeline covers bs 16 / sr 16 / full search / no FME / W % 128 == 0")
         self.eng, self.world, self.rank, self.max_frames = e, world, rank, max_frames
         self.stream, self.max_wg = stream, max_wg
+        self.resident = _claim_slots(self, e, max_wg, e.vbs)
         lib = self.lib = _lib.load()
         self.tiles_x, self.ntr = e.w // 128, -(-e.nby // 2)
         self.ntiles = self.tiles_x * self.ntr
@@ -431,6 +485,7 @@ class FramePipeRank:
             if p.value:
                 self.lib.so_free_device(p)
         self._planes, self._flags = ctypes.c_void_p(), ctypes.c_void_p()
+        _release_slots(self)
 
     def encode(self, frames: torch.Tensor, intra_dur: int, qp: int, qp_row=None, roi_dev=None,
                two_pass: bool = False, qp_clamp=(0, 12)) -> dict:

@@ -340,3 +340,29 @@ def test_frame_pipeline_two_processes_ipc(gpu, tmp_path):
     assert got["digests"] == FIX["4k"]["frame_sha256"][:n]
     psnr = [10 * np.log10(255 ** 2 / (s / (2160 * 3840))) for s in got["sse"]]
     np.testing.assert_allclose(psnr, FIX["4k"]["psnr"][:n], rtol=0, atol=1e-9)
+
+
+def test_in_process_ranks_must_fit_one_gpu(gpu):
+    """Ranks sharing ONE GPU in a process (as these tests run them) can only make progress if
+    every rank's persistent launch is resident at once: a rank whose launch cannot become
+    resident would leave its peers polling for its tasks until the wait bound
+    (profiles/r03/fpipe2p_fullcap_w3.log: three uncapped-share two-pass ranks, 256 timeouts
+    each).  One rank per GPU always fits (its grid is its device's resident capacity; DESIGN.md
+    section 6).  So the library refuses an in-process rank whose claim overflows the device
+    (a lone rank: all of it; ranks sharing it: 3/4 of it together, the margin the time-shared
+    runs have always had), and accepts capped ranks within that."""
+    from streamoptima_amd import _lib
+    from streamoptima_amd.engine import Engine
+    from streamoptima_amd.pipeline import FramePipeRank
+    cap = _lib.load().so_p_run_resident_workgroups(0)
+    assert cap >= 256
+    engines = [Engine(272, 3840, 16, 16, False, 0.015, gpu) for _ in range(3)]
+    a = FramePipeRank(engines[0], 3, 0, 6, max_wg=0)            # uncapped: the whole device
+    with pytest.raises(ValueError, match="resident workgroups"):
+        FramePipeRank(engines[1], 3, 1, 6, max_wg=cap // 3)
+    a.close()
+    ranks = [FramePipeRank(engines[r], 3, r, 6, max_wg=cap // 4) for r in range(3)]   # 3/4 of the device, shared
+    with pytest.raises(ValueError, match="resident workgroups"):
+        FramePipeRank(engines[0], 3, 0, 6, max_wg=1)
+    for r in ranks:
+        r.close()
