@@ -257,9 +257,6 @@ def kernel_roofline(codec, frames_dev, symbols, reps: int, components: bool = Tr
         while time.perf_counter() < t_end:
             fn()
             torch.cuda.synchronize()
-        if name == "run":
-            eng.check_run()
-            eng.take_sad_ops()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         e0.record(stream)
@@ -270,8 +267,14 @@ def kernel_roofline(codec, frames_dev, symbols, reps: int, components: bool = Tr
         torch.cuda.synchronize()
         out[name] = e0.elapsed_time(e1) / n_rep / 1e3  # seconds per call
         if name == "run":
+            # the executed SAD operations of the same work: one more (untimed) replay with the
+            # kernel-side count on (SO_OPT_COUNT_SAD_OPS, words 66..67; off in timed runs)
             eng.check_run()
-            sad_ops = eng.take_sad_ops() / n_rep   # SO_P_RUN_SAD_OPS_WORD over the timed calls
+            eng.take_sad_ops()
+            with _lib.option(_lib.OPT_COUNT_SAD_OPS, 1):
+                fn()
+                torch.cuda.synchronize()
+            sad_ops = eng.take_sad_ops()
     eng.check_run()
     nb = eng.nb
     # algorithmic work: SAD ops = valid candidates x bs^2

@@ -125,12 +125,17 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
  *                            predictor chain (1) instead of the speculated segments (0, default)
  *   SO_OPT_FASTME_SEGMENT    blocks per speculated segment (default 32, >= 1)
  *   SO_OPT_FASTME_WARMUP     blocks a segment's guess runs ahead of it (default 32, >= 0)
+ *   SO_OPT_COUNT_SAD_OPS     the persistent runs count their searches' SAD byte operations into
+ *                            workspace words 66..67 (1; default 0: the count's LDS atomics cost
+ *                            ~1 % of the run, so only a measurement turns it on)
  * so_set_option returns SO_E_INVALID for an unknown option or a value out of range.
  */
 #define SO_OPT_RUN_2PASS_FUSED 1
 #define SO_OPT_FASTME_SERIAL 2
 #define SO_OPT_FASTME_SEGMENT 3
 #define SO_OPT_FASTME_WARMUP 4
+#define SO_OPT_COUNT_SAD_OPS 5
+#define SO_OPT_TEST_LOSE_FLAG 6
 int so_set_option(int option, int value);
 int so_get_option(int option);
 
@@ -165,7 +170,8 @@ int so_get_option(int option);
  * candidates survived the 4x4-cell bound: flat or noise-like content), summed over launches
  * like the timeout count until the caller clears it (a content statistic, not an error). */
 #define SO_P_RUN_FALLBACK_WORD 64
-/* Words 66..67 (uint64, little endian): SAD byte operations the searches executed (every
+/* Words 66..67 (uint64, little endian; with SO_OPT_COUNT_SAD_OPS set): SAD byte operations the
+ * searches executed (every
  * v_sad_u8 / v_sad_hi_u8 lane instruction counts its 4 bytes: byte sums, bounds, survivor and
  * dense SADs), summed like word 64.  The dense-equivalent count of the reference's full scan
  * (Encoder.py:688-715) is (valid candidates) x 256 per P-frame; this is what ran. */

@@ -26,10 +26,10 @@ void set_error(const char* fmt, ...) {
 }
 
 // so_set_option / so_get_option (SO_OPT_*): index = option id
-static std::atomic<int> g_opt[5] = {0, 0, 0, 32, 32};
+static std::atomic<int> g_opt[7] = {0, 0, 0, 32, 32, 0, 0};
 
 int option(int id) {
-    return (id > 0 && id < 5) ? g_opt[id].load(std::memory_order_relaxed) : 0;
+    return (id > 0 && id < 7) ? g_opt[id].load(std::memory_order_relaxed) : 0;
 }
 
 int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, int bs, int sr, int by0, int by1,
@@ -312,9 +312,10 @@ extern "C" {
 int so_abi_version(void) { return SO_ABI_VERSION; }
 
 int so_set_option(int opt, int value) {
-    const bool ok = (opt == SO_OPT_RUN_2PASS_FUSED || opt == SO_OPT_FASTME_SERIAL) ? (value == 0 || value == 1)
+    const bool ok = (opt == SO_OPT_RUN_2PASS_FUSED || opt == SO_OPT_FASTME_SERIAL || opt == SO_OPT_COUNT_SAD_OPS)
+                        ? (value == 0 || value == 1)
                     : opt == SO_OPT_FASTME_SEGMENT                               ? value >= 1
-                    : opt == SO_OPT_FASTME_WARMUP                                ? value >= 0
+                    : opt == SO_OPT_FASTME_WARMUP || opt == SO_OPT_TEST_LOSE_FLAG ? value >= 0
                                                                                  : false;
     if (!ok) {
         set_error("so_set_option: option %d value %d is unknown or out of range", opt, value);

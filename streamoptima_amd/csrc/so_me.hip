@@ -37,11 +37,9 @@ constexpr uint64_t kNoKey = ~0ull;
 // SAD byte operations of one wave_dense_block at bs 16 (2 passes x (17 x 8 + 8) x 4 v_sad_u8
 // per lane, 64 lanes, 4 bytes each)
 constexpr uint32_t kDenseSadOps = 1152u * 256u;
-#ifdef SO_NO_OPS
-#define SO_OPS_ADD(p, v) ((void)0)
-#else
-#define SO_OPS_ADD(p, v) atomicAdd((p), (v))
-#endif
+// only when the run counts (SO_OPT_COUNT_SAD_OPS: bench.py's roofline replay); a uniform
+// branch otherwise (the count's LDS atomics cost ~1 % of the P-run)
+#define SO_OPS_ADD(p, v) do { if (L.count_ops) atomicAdd((p), (v)); } while (0)
 
 SO_DEV void decode_key(uint64_t k, int sr, int32_t* out) {
     if (k == kNoKey) {
@@ -687,6 +685,7 @@ struct Sea2Lds {
     uint32_t* lcount;          // [NW]
     unsigned long long* keys;  // [NBLK] packed best key per block
     uint32_t* st;              // [3]: dense-fallback blocks, survivors (SO_STAMPS only), SAD byte ops
+    int count_ops;             // st[2] is counted (SO_OPT_COUNT_SAD_OPS)
 };
 
 // Exact SEA full search of tile `tile` (16 blocks of 16x16) over nref references.  On
@@ -1957,12 +1956,12 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
                        int by0, int by1, int qp_rd, const int32_t* __restrict__ qp_row,
                        const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best, const PFrameOut& o,
                        const Pre& pre = Pre(), const PHalo& hl = PHalo{}, double lam = 0.0,
-                       const int* dense_flag = nullptr, int32_t* fb_out = nullptr) {
+                       const int* dense_flag = nullptr, int32_t* fb_out = nullptr, int count_ops = 0) {
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY;
     using P = PTileGeo<G>;
     uint32_t* const b4w = reinterpret_cast<uint32_t*>(S.un);
     uint16_t* const list = reinterpret_cast<uint16_t*>(b4w + P::B4);
-    const Sea2Lds L{S.win, b4w, S.curt, S.a4, list, S.lcount, S.keys, S.st};
+    const Sea2Lds L{S.win, b4w, S.curt, S.a4, list, S.lcount, S.keys, S.st, count_ops};
     RefSet refs{};
     refs.p[0] = ref;
 #ifndef SO_PROF_PHASE   // phase-attribution A/B builds only (tools/prun_phase.py): 1 = no transforms
@@ -2333,7 +2332,7 @@ SO_DEV uint32_t rmw_read(const uint32_t* c) {
 // first, writes the diagnostic record (ws[kRunDiagWord..+31]) and keeps reading the awaited
 // flags for up to 50 ms more to record when they arrive.  Returns the lane's last raw value.
 // (Durations in 32 bits of 100 MHz ticks: the wait state is a handful of SGPRs.)
-SO_DEV uint32_t run_poll(const uint32_t* c, bool need, bool sysl, uint32_t* ws, const RunWait& w) {
+SO_DEV uint32_t run_poll_full(const uint32_t* c, bool need, bool sysl, uint32_t* ws, const RunWait& w) {
 #ifdef SO_WAIT_SIMPLE   // TEMP A/B: the round-3 loop
     {
         const uint32_t one = (threadIdx.x & 63) == 0 ? 1u : 0u;
@@ -2441,6 +2440,29 @@ SO_DEV uint32_t run_poll(const uint32_t* c, bool need, bool sysl, uint32_t* ws, 
         }
     }
     return raw;
+}
+
+#ifdef SO_WAIT_CALL   // TEMP A/B: the long wait out of line
+__device__ __attribute__((noinline)) uint32_t run_poll_slow(const uint32_t* c, bool need, bool sysl, uint32_t* ws,
+                                                            const RunWait& w) {
+    return run_poll_full(c, need, sysl, ws, w);
+}
+#endif
+
+SO_DEV uint32_t run_poll(const uint32_t* c, bool need, bool sysl, uint32_t* ws, const RunWait& w) {
+#ifdef SO_WAIT_CALL
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const uint32_t raw = sysl ? __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                  : __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__builtin_amdgcn_ballot_w64(need && raw != (sysl ? w.sys_want : w.want)) == 0) return raw;
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kRunEscalateTicks) break;
+    }
+    return run_poll_slow(c, need, sysl, ws, w);
+#else
+    return run_poll_full(c, need, sysl, ws, w);
+#endif
 }
 
 // VBS: VBSEnable (the block + sub-block dense search, tq16_vbs; ~128 VGPRs, 4 waves per SIMD)
@@ -2617,7 +2639,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 using P = PTileGeo<G>;
                 uint32_t* const b4w = reinterpret_cast<uint32_t*>(S.un);
                 const Sea2Lds L{S.win, b4w, S.curt, S.a4, reinterpret_cast<uint16_t*>(b4w + P::B4), S.lcount, S.keys,
-                                S.st};
+                                S.st, sp.count_ops};
                 RefSet refs{};
                 refs.p[0] = ref;
                 sea2_tile<G>(L, tile, a.cur[f], refs, 1, H, W, 0, by1, 0, wait_ref);   // ends with a barrier
@@ -2692,7 +2714,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             hl.dn_begin = 0;
             ptile_body<G, true, decltype(wait_ref), true, false, VBS>(S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd,
                                                                       qp_row, nullptr, nullptr, a.out[f], wait_ref, hl,
-                                                                      lam);
+                                                                      lam, nullptr, nullptr, sp.count_ops);
             // ptile_body ended with every wave's stores (local and remote) retired and a barrier
             if (wave == 0) {
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
@@ -2713,7 +2735,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 hl.dn_begin = by1 * 16 - 16;
             }
             ptile_body<G, true, decltype(wait_ref), true>(S, tile, a.cur[f], ref, H, W, by0, by1, qp_rd, qp_row,
-                                                          nullptr, nullptr, a.out[f], wait_ref, hl);
+                                                          nullptr, nullptr, a.out[f], wait_ref, hl, 0.0, nullptr, nullptr, sp.count_ops);
             // ptile_body ended with every wave's stores (local and remote) retired and a barrier
             if (wave == 0) {
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
@@ -2733,10 +2755,13 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                                                                        qp_row, nullptr, nullptr, a.out[f], wait_ref,
                                                                        PHalo{}, lam, &s_dense,
                                                                        reinterpret_cast<int32_t*>(tilefb) +
-                                                                           (size_t)f * ntiles + tile);
+                                                                           (size_t)f * ntiles + tile,
+                                                                       sp.count_ops);
             SO_RUN_PROF(52, __builtin_amdgcn_s_memtime() - pt0);
             // ptile_body ended with every wave's write-through stores retired and a barrier
-            if (wave == 0)
+            // (sp.lose_task: SO_OPT_TEST_LOSE_FLAG, the wait diagnostics' test -- that task's flag
+            // is never set, so its dependants time out and record themselves)
+            if (wave == 0 && task + 1 != sp.lose_task)
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -2878,6 +2903,8 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
         if (max_wg > 0 && grid > max_wg) grid = max_wg;
         PRunStripe sp = sp0;
         sp.gbase = sp0.gbase + f0;
+        sp.count_ops = option(SO_OPT_COUNT_SAD_OPS);
+        sp.lose_task = f0 == 0 ? option(SO_OPT_TEST_LOSE_FLAG) : 0;
         if (MODE == kRunTwoPass || MODE == kRunFPipe2P) {   // pass 2 of a row about one grid's worth of tasks after its pass 1
             const int tiles_x = (nbx + G::TBX - 1) / G::TBX, ntr = (rows + G::TBY - 1) / G::TBY;
             // about one grid's worth of tile rows (a pass-2 task then rarely waits holding its

@@ -57,6 +57,8 @@ struct PRunStripe {
     const int32_t* roi;
     int qp_lo, qp_hi;
     int p2lag;   // tile rows between a row's pass-1 and pass-2 tasks in the queue (1..ntr)
+    int count_ops;   // count the searches' SAD byte operations (SO_OPT_COUNT_SAD_OPS)
+    int lose_task;   // one GPU: task + 1 whose done flag is never set (SO_OPT_TEST_LOSE_FLAG), 0: none
 };
 
 size_t p_run_workspace_words(int H, int W);

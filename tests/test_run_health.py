@@ -87,8 +87,9 @@ def test_set_option_validates_and_round_trips():
     with _lib.option(_lib.OPT_FASTME_SEGMENT, 8):
         assert lib.so_get_option(_lib.OPT_FASTME_SEGMENT) == 8
     assert lib.so_get_option(_lib.OPT_FASTME_SEGMENT) == 32
+    assert lib.so_get_option(_lib.OPT_COUNT_SAD_OPS) == 0
     for opt, bad in ((_lib.OPT_RUN_2PASS_FUSED, 2), (_lib.OPT_FASTME_SEGMENT, 0), (_lib.OPT_FASTME_WARMUP, -1),
-                     (99, 0), (0, 0)):
+                     (_lib.OPT_COUNT_SAD_OPS, 2), (99, 0), (0, 0)):
         assert lib.so_set_option(opt, bad) == _lib.SO_E_INVALID
         assert b"so_set_option" in lib.so_last_error()
 
