@@ -967,7 +967,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
     // st[2]: SAD byte operations executed for this tile (every v_sad_u8 / v_sad_hi_u8 lane
     // instruction counts 4): the current tile's 4x4 sums, here
     uint32_t& st_ops = L.st[2];
-    if (tid == 0) st_ops = G::NBLK * 16 * 4 * 4;
+    if (tid == 0) st_ops = L.count_ops ? G::NBLK * 16 * 4 * 4 : 0u;
 #ifdef SO_STAMPS
     uint32_t& st_sur = L.st[1];
     if (tid == 0) st_sur = 0;
@@ -2332,26 +2332,7 @@ SO_DEV uint32_t rmw_read(const uint32_t* c) {
 // first, writes the diagnostic record (ws[kRunDiagWord..+31]) and keeps reading the awaited
 // flags for up to 50 ms more to record when they arrive.  Returns the lane's last raw value.
 // (Durations in 32 bits of 100 MHz ticks: the wait state is a handful of SGPRs.)
-SO_DEV uint32_t run_poll_full(const uint32_t* c, bool need, bool sysl, uint32_t* ws, const RunWait& w) {
-#ifdef SO_WAIT_SIMPLE   // TEMP A/B: the round-3 loop
-    {
-        const uint32_t one = (threadIdx.x & 63) == 0 ? 1u : 0u;
-        uint32_t raw = 0;
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        for (;;) {
-            raw = sysl ? __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                       : __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const bool ok = raw == (sysl ? w.sys_want : w.want);
-            if (__builtin_amdgcn_ballot_w64(need && !ok) == 0) break;
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > w.limit) {
-                __hip_atomic_fetch_add(&ws[kRunTimeoutWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-        return raw;
-    }
-#endif
+SO_DEV uint32_t run_poll(const uint32_t* c, bool need, bool sysl, uint32_t* ws, const RunWait& w) {
     const int lane = threadIdx.x & 63;
     const uint32_t one = lane == 0 ? 1u : 0u;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -2442,28 +2423,6 @@ SO_DEV uint32_t run_poll_full(const uint32_t* c, bool need, bool sysl, uint32_t*
     return raw;
 }
 
-#ifdef SO_WAIT_CALL   // TEMP A/B: the long wait out of line
-__device__ __attribute__((noinline)) uint32_t run_poll_slow(const uint32_t* c, bool need, bool sysl, uint32_t* ws,
-                                                            const RunWait& w) {
-    return run_poll_full(c, need, sysl, ws, w);
-}
-#endif
-
-SO_DEV uint32_t run_poll(const uint32_t* c, bool need, bool sysl, uint32_t* ws, const RunWait& w) {
-#ifdef SO_WAIT_CALL
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        const uint32_t raw = sysl ? __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                                  : __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__builtin_amdgcn_ballot_w64(need && raw != (sysl ? w.sys_want : w.want)) == 0) return raw;
-        __builtin_amdgcn_s_sleep(1);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kRunEscalateTicks) break;
-    }
-    return run_poll_slow(c, need, sysl, ws, w);
-#else
-    return run_poll_full(c, need, sysl, ws, w);
-#endif
-}
 
 // VBS: VBSEnable (the block + sub-block dense search, tq16_vbs; ~128 VGPRs, 4 waves per SIMD)
 template <int NW, int MODE, bool VBS = false>
