@@ -367,6 +367,63 @@ def roofline_of(rl: dict, config: str) -> dict:
     return out
 
 
+def rc_roofline(codec, frames_dev, symbols, reps: int, config: str) -> dict:
+    """configs[4] (ROI + two-pass RC): its P-frames run as a per-frame kernel sequence -- pass 1
+    (p_tile_kernel<8, true>: search + forward transform for the token counts), so_qp_map, pass 2
+    (inter_tq_kernel on pass 1's motion vectors, SO_REUSE_ME) -- replayed here with HIP events on
+    the launch stream over the timed GOP's references.  The HBM fraction of a P-frame's
+    algorithmic bytes (as the one-pass roofline) over that sequence's time; the VALU busy
+    fraction of the pass-1 kernel from the committed PMC counters."""
+    eng = codec.engine()
+    qp_sched = codec.row_qp_schedule(eng.nby)
+    qdev = eng.qp_row_tensor(qp_sched)
+    roi = codec.roi_block_offsets()
+    roi_dev = eng.device_const_i32(roi) if roi is not None else None
+    lo, hi = codec.qp_clamp
+    nf = frames_dev.shape[0]
+    qp = codec.const_init_Qp
+    tmp = eng.new_symbols(1)
+    qmap = torch.empty(eng.nb, dtype=torch.int32, device=eng.device)
+    stream = torch.cuda.current_stream(eng.device)
+
+    def seq():
+        for i in range(1, nf):
+            sym = eng.encode_p(frames_dev[i], [symbols[i - 1].recon], qp, qp_sched, out=tmp, qp_row_dev=qdev,
+                               tokens_only=True)
+            eng.qp_map(sym.tokens, qp, qdev, roi_dev, qmap, qp_lo=lo, qp_hi=hi)
+            eng.encode_p(frames_dev[i], [symbols[i - 1].recon], qp, qp_sched, out=tmp, qp_row_dev=qdev,
+                         qp_map_dev=qmap, reuse_me=True)
+    t_end = time.perf_counter() + 0.2
+    while time.perf_counter() < t_end:
+        seq()
+        torch.cuda.synchronize()
+    n_rep = max(2, reps // 10)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(n_rep):
+        seq()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    per_frame = e0.elapsed_time(e1) / 1e3 / n_rep / (nf - 1)
+    frame_bytes = 5 * eng.h * eng.w + 37 * eng.nb
+    gbs = frame_bytes / per_frame / 1e9
+    pm = pmc_record(config, "so::p_tile_kernel<8, true>")
+    valu = None
+    if pm.get("sq_active_inst_valu") and pm.get("grbm_gui_active"):
+        cyc = pm["grbm_gui_active"] / 8
+        valu = {"kernel": "p_tile_kernel<8, true> (pass 1)",
+                "valu_busy_frac": round(4 * pm["sq_active_inst_valu"] / (cyc * N_SIMD), 4),
+                "waves_per_simd": round(4 * pm["sq_wave_cycles"] / (cyc * N_SIMD), 2) if pm.get("sq_wave_cycles") else None,
+                "source": f"profiles/pmc_me_traffic.json [{config}]"}
+    return {"bound": "hbm", "kernel": "two-pass P-frame sequence: p_tile_kernel<8, true> (pass 1) + qp_map_kernel + "
+                                      "inter_tq_kernel<16, false, false> (pass 2, SO_REUSE_ME)",
+            "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5),
+            "traffic": None, "algorithmic_bytes": frame_bytes, "per_frame_us": round(per_frame * 1e6, 2),
+            "binding_limit": "valu", "valu": valu,
+            "note": "algorithmic bytes of one P-frame (5 B/px + 37 B/block) over the measured time of its three "
+                    "launches; pass 1 re-reads the current and reference rows pass 2 reads again"}
+
+
 def gop_roofline(cfg, step_s: float, gops: int = 1) -> dict:
     """Whole-step HBM fraction: every frame's algorithmic bytes (cur +
     ref read, recon + int16 QTC written = 5 B/px, 37 B/block of symbols) over the measured step
@@ -981,6 +1038,9 @@ def main(argv=None):
         # one-GPU GOP supplies the reference reconstructions it replays)
         syms = res["symbols"] if not stripe else codec.encode_device(frames, cfg["intra_dur"])["symbols"]
         rl = kernel_roofline(codec, frames, syms, args.kernel_reps, components=not cfg.get("vbs"))
+    rl_rc = None
+    if rank == 0 and not args.cpu_plumbing and cfg.get("rc", 0) >= 3 and not stripe and codec.engine().pipelined_ok(1):
+        rl_rc = rc_roofline(codec, frames, res["symbols"], args.kernel_reps, name)
 
     # ---- after timing: parity of the timed output ----
     parity = None
@@ -1084,7 +1144,8 @@ def main(argv=None):
                    "parallelism": (mode_note.format(exchange_note) if stripe else f"gop-per-rank x{world}"),
                    "launch": "hip-graph (one GOP per replay)" if args.graph else "host launches"},
         "parity": parity,
-        "roofline": roofline_of(rl, name) if rl else None,
+        "roofline": roofline_of(rl, name) if rl else rl_rc,
+        "roofline_gop": gop_roofline(cfg, elapsed / args.steps) if (world == 1 and not args.cpu_plumbing) else None,
         "cpu_baseline": cpu if (cpu is None or "error" not in cpu) else None,
         "psnr_mean_db": round(psnr_mean, 4) if psnr_mean is not None else None,
         "psnr_delta_db": parity.get("psnr_delta_db") if parity else None,

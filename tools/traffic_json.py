@@ -64,7 +64,8 @@ if not per:   # no counter CSVs for this tag (e.g. the GPU call never ran): keep
     sys.exit(f"no FETCH_SIZE / WRITE_SIZE rows under {base}/{tag}_{cfg}_*: nothing written")
 if not calib:
     sys.exit(f"no calibration rows under {base}/{tag}_calib: nothing written")
-out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_me_traffic.json")
+out = os.environ.get("PMC_JSON") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                 "profiles", "pmc_me_traffic.json")
 doc = json.load(open(out)) if os.path.exists(out) else {}
 doc["_note"] = ("per launch: hbm_bytes = calib_b32 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 from separate rocprofv3 "
                 "--pmc passes over `bench.py --steps 1 --warmup 1 --kernel-reps 5` (tools/gpu_traffic.sh); calib = "
