@@ -610,6 +610,9 @@ int me_fme_launch(const uint8_t* cur, const uint8_t* planes, size_t pstride, int
 #define SO_SEA_CAP_VBS 384   // sub-block bounds leave more survivors (4K VBS P-run 161.5 -> 158.8 us,
                              // dense blocks 8.9 -> 3.8 %; 768: 161.5, profiles/r03/r03n/vbs_ab.log)
 #endif
+#ifndef SO_B4_PD   // byte-sum rows in flight in the SEA bound loop (A/B builds: 3, 4)
+#define SO_B4_PD 2
+#endif
 #ifndef SO_PTILE_WPE16   // waves per SIMD of the 16-wave fused tile kernels (A/B builds only)
 #define SO_PTILE_WPE16 8
 #endif
@@ -1179,7 +1182,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             // byte-sum rows through a ring of PD rows in flight: the row used in step sr_ was
             // loaded PD steps earlier, so LDS latency overlaps PD steps of v_sad_u8 work
             // (one step ahead left every step waiting on its own loads)
-            constexpr int PD = 2;
+            constexpr int PD = SO_B4_PD;
             uint32_t n0[PD], n1[PD];
 #pragma unroll
             for (int k = 0; k < PD; ++k) { n0[k] = p1[k * (B4P / 4)]; n1[k] = p1[k * (B4P / 4) + 1]; }
