@@ -22,11 +22,12 @@ def main():
     for rd in range(a.rounds):
         for v in (a.variants if rd % 2 == 0 else a.variants[::-1]):
             env = dict(os.environ)
-            if "=" in v:
-                k, val = v.split("=", 1)
-                env[k] = val
-            elif v != "default":
-                env["SO_LIB_PATH"] = v
+            for part in v.split(":"):          # lib.so, ENV=VAL, or lib.so:ENV=VAL[:ENV=VAL]
+                if "=" in part:
+                    k, val = part.split("=", 1)
+                    env[k] = val
+                elif part != "default":
+                    env["SO_LIB_PATH"] = part
             r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
             line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
             if not line:
