@@ -1439,6 +1439,14 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
 // FP64 transpose scratch per block of the fused tile: 16 x 17 doubles.  (Two-half transposes,
 // 16 x 9, would let 4 workgroups fit per CU but spill at 64-80 VGPRs: measured slower, DESIGN.md.)
 constexpr int kTqScratch = 16 * 17;
+// SO_FWD_MFMA=1: the fused tiles' forward transform on the matrix cores with an exactness
+// certificate (fwd_mfma).  Bit-exact (the GPU suite passes through it) but measured slower, so
+// off: 73.6 vs 67.0 us per 4K P-frame -- the FP32 MFMA runs at the FP32 vector rate and does not
+// hide behind the other waves' VALU here, and the certificate costs ~19 lane operations per
+// coefficient against ~7 for the FP64 pocketfft forward it replaces.
+#ifndef SO_FWD_MFMA
+#define SO_FWD_MFMA 0
+#endif
 template <class G>
 struct PTileGeo {
     static constexpr int B4 = (G::B4RS * G::B4P + 4) / 4;             // dwords
@@ -1484,7 +1492,8 @@ struct PTileLds {
     uint32_t st[3];
     int32_t mer[NU][4];                    // decoded ME records (dx, dy, ref, sad)
     int32_t msum[G::TBY];                  // two-pass runs: pass-1 token sum of each block row
-    double un[VBS ? PTileGeoVbs<G>::U64 : PTileGeo<G>::U64];   // byte sums + survivor lists | FP64 transposes
+    uint32_t fwd_flags;                    // fwd_mfma: blocks whose levels need the FP64 forward
+    alignas(16) double un[VBS ? PTileGeoVbs<G>::U64 : PTileGeo<G>::U64];   // byte sums + survivor lists | FP64 transposes
     // VBS: the chosen levels of each block (16 lanes x 8 packed int16 pairs) and its split state
     // (0 block, 1 split, 2 none) between tq16_vbs_fwd and tq16_vbs_inv
     uint32_t lev[VBS ? G::NBLK * 16 * 8 : 1];
@@ -1504,10 +1513,12 @@ struct PHalo {
 // The exact transform path of one block: 16 lanes (l = row) run scipy.fftpack's pocketfft
 // DCT-II / DCT-III sequence in FP64 (so_dct.h) -- the arithmetic of inter_tq_kernel<16,
 // false, false>.  `scratch` = 16 x 17 doubles of LDS owned by the calling lanes.
+// `qs` (fwd_mfma): the block's levels, already certified (16 x 16 int16 at the start of
+// `scratch`); null = run the FP64 forward transform here.
 template <class G, bool SC1, bool HALO = false, bool TOK = false>
 SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, int byt0, int nbx, int by0, int by1,
                        int W, int qp_rd, const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map,
-                       const PFrameOut& o, const PHalo& hl = PHalo{}) {
+                       const PFrameOut& o, const PHalo& hl = PHalo{}, bool qs = false) {
     constexpr int SR = G::SR, TBX = G::TBX;
     const int bxl = g % TBX, byl = g / TBX;
     const int gbx = bx0 + bxl, gby = byt0 + byl;
@@ -1519,29 +1530,42 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
         const int prow = byl * 16 + SR + dy + l, pcol = bxl * 16 + SR + dx;   // window coordinates
         const uint32_t* crow = S.curt + (byl * 16 + l) * G::CPD + bxl * 4;
         double* dl = scratch;
-        int res[16];
-        {
-            uint32_t pw[4];
-            win_row16<G::RP>(S.win, prow, pcol, pw);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t cw = crow[k];
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    res[4 * k + e] = (int)((cw >> (8 * e)) & 255) - (int)((pw[k] >> (8 * e)) & 255);
-            }
-        }
-        double tcr[16];
-        xform2d_rows<16, false>(dl, l, res, tcr);
         // np.round to int by the 1.5 * 2^52 shift (|values| < 2^51): x + kRne rounds x to an
         // integer half-to-even, held in the low mantissa dword as two's complement -- one
         // v_add_f64 instead of v_rndne + v_cvt_i32
         constexpr double kRne = 0x1.8p52;
         int q[16];
+        if (qs) {
+            const so_v4u* qr = reinterpret_cast<const so_v4u*>(reinterpret_cast<const int16_t*>(dl) + l * 16);
 #pragma unroll
-        for (int c = 0; c < 16; ++c)
-            q[c] = (int)(uint32_t)__builtin_bit_cast(
-                uint64_t, __builtin_amdgcn_ldexp(__builtin_rint(tcr[c]), -q_exp_fast<16>(l, c, qpr)) + kRne);
+            for (int h = 0; h < 2; ++h) {
+                const so_v4u v = qr[h];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    q[8 * h + 2 * e] = (int)(int16_t)(v[e] & 0xFFFFu);
+                    q[8 * h + 2 * e + 1] = (int)v[e] >> 16;
+                }
+            }
+        } else {
+            int res[16];
+            {
+                uint32_t pw[4];
+                win_row16<G::RP>(S.win, prow, pcol, pw);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t cw = crow[k];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        res[4 * k + e] = (int)((cw >> (8 * e)) & 255) - (int)((pw[k] >> (8 * e)) & 255);
+                }
+            }
+            double tcr[16];
+            xform2d_rows<16, false>(dl, l, res, tcr);
+#pragma unroll
+            for (int c = 0; c < 16; ++c)
+                q[c] = (int)(uint32_t)__builtin_bit_cast(
+                    uint64_t, __builtin_amdgcn_ldexp(__builtin_rint(tcr[c]), -q_exp_fast<16>(l, c, qpr)) + kRne);
+        }
         const int tok = block_tokens<16>(nullptr, l, q);
         if constexpr (TOK) {   // pass 1 of two-pass RC: the token count is all that is used
             if (l == 0) o.tokens[b] = tok;
@@ -1605,6 +1629,95 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
             if (o.sse) o.sse[b] = sse;
         }
     }
+}
+
+// ---- the forward transform on the matrix cores (SO_FWD_MFMA) -------------------------------
+// fwd_mfma: Z = C R C^T of one block on one wave's 64 lanes, 8 v_mfma_f32_16x16x4_f32, then a
+// certificate per coefficient that the FP32 result quantises to the level pocketfft's FP64
+// one does (tq16_exact: the arithmetic of Encoder.py:781-789):
+//  * bound: an MFMA step is a k-ordered chain of single-rounding FP32 FMAs, so a 16-term chain
+//    is within gamma_16 ~ 16u sum|a b| of its exact value (u = 2^-24); the matrix entries
+//    (dct16_f32) are within u relative of C.  The two products together:
+//    |z - Z| <= 34.04 u max|C_ur C_vk| sum|R| <= 2.512e-7 sum|R|  (max|C_ur C_vk| = 0.1238),
+//    and pocketfft's FP64 result is within 1e-11 of Z.
+//  * the level q(Z) = rne(rint(Z) / 2^k) is, for k >= 1, constant in Z except for steps at
+//    mid +- 1/2, mid = (floor(Z / 2^k) + 1/2) 2^k.  When ||z - mid| - 1/2| > delta (both
+//    differences exact where they matter, Sterbenz), no step lies within delta of z and
+//    q(z) == q(pocketfft).  k = 0 (qp 0) steps at every half-integer: such blocks are flagged.
+// A flagged block (some coefficient within delta of mid +- 1/2: ~4 delta / 2^k of them, 3-6 %
+// of the blocks at QP 4) gets the FP64 forward in phase B.
+__constant__ float kDctCos32[17] = {
+    0x1.6a09e6p-2f, 0x1.684b9cp-2f, 0x1.63150cp-2f, 0x1.5a730cp-2f, 0x1.4e7aeap-2f, 0x1.3f4a24p-2f,
+    0x1.2d062ep-2f, 0x1.17dc14p-2f, 0x1.000000p-2f, 0x1.cb598cp-3f, 0x1.92469cp-3f, 0x1.5553e4p-3f,
+    0x1.1517a8p-3f, 0x1.a4608ap-4f, 0x1.1a855ep-4f, 0x1.1be352p-5f, 0.0f};   // fl32(sqrt(1/8) cos(pi j / 32))
+
+// C[u][r] of the orthonormal 16-point DCT-II (scipy.fftpack.dct norm='ortho') in FP32
+SO_DEV float dct16_f32(int u, int r) {
+    if (u == 0) return 0.25f;
+    const int j = ((2 * r + 1) * u) & 63;
+    const int m = j <= 32 ? j : 64 - j;
+    return m <= 16 ? kDctCos32[m] : -kDctCos32[32 - m];
+}
+
+typedef float so_v4f __attribute__((ext_vector_type(4)));
+constexpr float kFwdBound = 2.6e-7f;   // >= 2.512e-7 (above) + the rounding of delta itself
+
+// One block on one wave: lane (c4 = ln >> 4, r = ln & 15) feeds R[r][4 c4 + s] and
+// C[r][4 c4 + s] at MFMA step s (A[i][k] = lane (k, i), B[k][j] = lane (k, j)); the first
+// product's D (lane (c4, v): Y[4 c4 + i][v]) is the second's B operand as it stands.  Writes
+// the 256 levels as int16 rows to the start of the block's scratch and flags the block in
+// S.fwd_flags when the certificate fails.
+template <class G>
+SO_DEV void fwd_mfma(PTileLds<G>& S, int g, int ln, const float (&cs)[4], int bx0, int byt0, int nbx, int by1,
+                     int qp_rd, const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map) {
+    constexpr int SR = G::SR, TBX = G::TBX;
+    const int bxl = g % TBX, byl = g / TBX;
+    const int gbx = bx0 + bxl, gby = byt0 + byl;
+    if (gbx >= nbx || gby >= by1) return;   // uniform over the wave
+    const int qpr = qp_map ? qp_map[(size_t)gby * nbx + gbx] : (qp_row ? qp_row[gby] : qp_rd);
+    const int r = ln & 15, c4 = ln >> 4;
+    const int dx = S.mer[g][0], dy = S.mer[g][1];
+    const uint32_t cw = S.curt[(byl * 16 + r) * G::CPD + bxl * 4 + c4];
+    const uint32_t pw = win_u32<G::RP>(S.win, byl * 16 + SR + dy + r, bxl * 16 + SR + dx + 4 * c4);
+    float a[4];
+    uint32_t sab = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int d = (int)((cw >> (8 * s)) & 255) - (int)((pw >> (8 * s)) & 255);
+        a[s] = (float)d;
+        sab += (uint32_t)(d < 0 ? -d : d);
+    }
+    sab = wave_sum_u32(sab);
+    so_v4f y = {0.f, 0.f, 0.f, 0.f}, z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) y = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], cs[s], y, 0, 0, 0);   // Y = R C^T
+#pragma unroll
+    for (int s = 0; s < 4; ++s) z = __builtin_amdgcn_mfma_f32_16x16x4f32(cs[s], y[s], z, 0, 0, 0);   // Z = C Y
+    const float delta = __builtin_fmaf((float)sab, kFwdBound, 0x1p-20f);
+    bool near = qpr < 1;
+    int16_t* qd = reinterpret_cast<int16_t*>(S.un + g * kTqScratch);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // z[i] = Z[4 c4 + i][r]
+        const int u = 4 * c4 + i, k = q_exp_fast<16>(u, r, qpr);
+        const float zi = z[i];
+        const float mid = __builtin_amdgcn_ldexpf(__builtin_floorf(__builtin_amdgcn_ldexpf(zi, -k)) + 0.5f, k);
+        near |= __builtin_fabsf(__builtin_fabsf(zi - mid) - 0.5f) <= delta;
+        qd[u * 16 + r] = (int16_t)(int)__builtin_rintf(__builtin_amdgcn_ldexpf(__builtin_rintf(zi), -k));
+    }
+#ifdef SO_FWD_FORCE   // A/B timing builds only: 0 = never flagged (wrong levels), 1 = always
+    near = SO_FWD_FORCE;
+#endif
+    if (__builtin_amdgcn_ballot_w64(near) != 0 && ln == 0) atomicOr(&S.fwd_flags, 1u << g);
+}
+
+// Phase-B position p -> block: the flagged blocks first (so their FP64 forwards share waves),
+// then the rest, each in block order.
+template <int NBLK>
+SO_DEV int fwd_order(uint32_t m, int p) {
+    const int nf = __builtin_popcount(m);
+    uint32_t s = p < nf ? m : (~m & ((1u << NBLK) - 1u));
+    for (int t = p < nf ? p : p - nf; t > 0; --t) s &= s - 1u;
+    return __builtin_ctz(s);
 }
 
 // 8 bytes of window row `row` from byte column `col`, as 2 dwords (3 aligned ds_read_b32 +
@@ -1989,13 +2102,33 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
     // the tile's dense-block count (p_run_kernel: the next frame's same tile reads it), stored
     // write-through now so that the drain below covers it
     if (fb_out != nullptr && tid == 0) store_sc1_i32(fb_out, (int)S.st[0]);
+    if (tid == 0) S.fwd_flags = 0u;
     __syncthreads();
     SO_SEA_STAMP(6, __builtin_amdgcn_s_memtime());
+    constexpr bool kFwdMfma = !VBS && SO_FWD_MFMA && SO_PROF_PHASE != 1;
+    if constexpr (kFwdMfma) {   // every wave: blocks w, w + NW on the matrix cores
+        const int ln = tid & 63;
+        float cs[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) cs[s] = dct16_f32(ln & 15, 4 * (ln >> 4) + s);
+        for (int g = tid >> 6; g < G::NBLK; g += G::NW)
+            fwd_mfma<G>(S, g, ln, cs, bx0, byt0, nbx, by1, qp_rd, qp_row, qp_map);
+        __syncthreads();
+#ifdef SO_FWD_COUNT   // A/B builds only: the flagged blocks replace the SAD count (words 66..67)
+        if (tid == 0) S.st[2] = (uint32_t)__builtin_popcount(S.fwd_flags);
+#endif
+    }
     {   // block g = wave * TQ_BPW + (lane >> 4) on lanes [0, 16 * TQ_BPW) of waves 0..NBLK/TQ_BPW-1
         // (the even waves, or every wave with 2 blocks, measured slower: 4K 71.8 / 79.8 vs
-        // 67.2 us per frame, 1088p 30.7 / 31.7 vs 28.7)
+        // 67.2 us per frame, 1088p 30.7 / 31.7 vs 28.7); after fwd_mfma, the flagged blocks first
         const int ln = tid & 63, w = tid >> 6;
-        const int gq = w * G::TQ_BPW + (ln >> 4);
+        int gq = w * G::TQ_BPW + (ln >> 4);
+        bool qs = false;
+        if constexpr (kFwdMfma) {
+            const uint32_t m = S.fwd_flags;
+            if (m != 0u && gq < G::NBLK) gq = fwd_order<G::NBLK>(m, gq);
+            qs = !((m >> gq) & 1u);
+        }
         if (SO_PROF_PHASE == 1 && ln < 16 * G::TQ_BPW && gq < G::NBLK) {
             // no transforms: the current rows stand in for the reconstruction, so the next
             // frame searches realistic content
@@ -2014,7 +2147,7 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
                                            byt0, nbx, by0, by1, W, qp_rd, qp_row, qp_map, lam, o);
             else
                 tq16_exact<G, SC1, HALO, TOK>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by0, by1, W, qp_rd,
-                                              qp_row, qp_map, o, hl);
+                                              qp_row, qp_map, o, hl, qs);
         }
     }
     if constexpr (VBS) {
