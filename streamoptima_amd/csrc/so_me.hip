@@ -236,10 +236,12 @@ SO_DEV uint64_t widen17_fme(uint32_t b32, uint32_t X, int hh, int xi, bool xok, 
 // keys into keys[nblk + 4u + j].  Used by me_wave_kernel.
 // ONE: the window is a single copy (me_sea2_kernel): the lane's 16 bytes at any column are
 // five ds_read_b32 + four v_alignbyte per row instead of four reads of its shifted copy.
+// `c1` (dwords from win): copies 1..3 at win + c1 + (s - 1) CS instead of win + s CS (the
+// fused tile's dense tiles keep copy 0 in the window and stage the others into its scratch).
 template <int BS, bool SUB, int RPD, int CS, bool FME = false, bool ONE = false>
 SO_DEV void wave_dense_block(const uint32_t* win, unsigned long long* keys, int nblk, const uint8_t* __restrict__ cur,
                              int W, int H, int x, int y, int bxl, int byl, int u, int tid, int r,
-                             FmePhase ph = FmePhase{0, 0}) {
+                             FmePhase ph = FmePhase{0, 0}, int c1 = CS) {
     constexpr int SR = 16, NT = 17;
     constexpr int NDW = BS / 4, HALF = 8, NPASS = BS / HALF, NR = NT + HALF - 1;
     // lane identity re-derived per block through an opaque asm: otherwise LICM hoists
@@ -249,7 +251,8 @@ SO_DEV void wave_dense_block(const uint32_t* win, unsigned long long* keys, int 
     const int xi = lane & 31, hh = lane >> 5;
     const uint32_t X = hh ? 0u : 31u;
     // phase-1 lane: window column bxl*BS + xi (dx = xi - 16) in copy xi & 3
-    const int q1 = (ONE ? 0 : (xi & 3) * CS) + (byl * BS + 16 * hh) * RPD + ((bxl * BS + xi) >> 2);
+    const int q1 = (ONE || (xi & 3) == 0 ? 0 : c1 + ((xi & 3) - 1) * CS) + (byl * BS + 16 * hh) * RPD +
+                   ((bxl * BS + xi) >> 2);
     const uint32_t sh1 = (uint32_t)((bxl * BS + xi) & 3);   // ONE: byte shift of the lane's column
     // phase-2 lane: dx = +16 (column bxl*BS + 32, copy 0), dy index = lane (< 33)
     const int d2 = lane < 33 ? lane : 32;
@@ -637,6 +640,7 @@ struct Sea2GeoT {
     static constexpr int NW = NW_, NTHREADS = NW * 64;
     static constexpr int CAP = SO_SEA_CAP, CAPV = SO_SEA_CAP_VBS;
     static constexpr int CAPL = CAP > CAPV ? CAP : CAPV;   // list entries per wave
+    static constexpr int DCS = WR * RP + 8;                // dense tiles: window copy stride (8 mod 32)
     static constexpr int CPD = TPX / 4 + 1;               // current-tile pitch in dwords: 16 rows of
                                                           // one block column land on 16 banks
     static_assert(WD * B4NB <= NTHREADS, "byte-sum threads");
@@ -689,6 +693,8 @@ struct Sea2Lds {
     unsigned long long* keys;  // [NBLK] packed best key per block
     uint32_t* st;              // [3]: dense-fallback blocks, survivors (SO_STAMPS only), SAD byte ops
     int count_ops;             // st[2] is counted (SO_OPT_COUNT_SAD_OPS)
+    int dense4;                // dwords from win to the room for window copies 1..3 of a dense tile
+                               // (DCS apart, 8 mod 32); 0 = none: dense tiles read the single copy
 };
 
 // Exact SEA full search of tile `tile` (16 blocks of 16x16) over nref references.  On
@@ -1073,12 +1079,33 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
         if (r == 0) SO_SEA_STAMP(3, __builtin_amdgcn_s_memtime());
         if (probe == 5) continue;   // phase-attribution builds (SO_PROF_PHASE=2): no search at all
         if (dense_flag && __builtin_amdgcn_readfirstlane(*dense_flag)) {   // uniform: the whole tile dense
+            // the window's byte-shifted copies 1..3 into the free scratch (no byte sums or lists
+            // here): every row the scan reads is then four aligned ds_read_b32 instead of five
+            // plus four v_alignbyte (me_wave_kernel's layout)
+            const int c1 = L.dense4;
+            if (c1 != 0) {
+                uint32_t* const cp = win + c1;
+                for (int i = tid; i < G::WR * RP; i += G::NTHREADS) {
+                    const uint32_t a = win[i], b = win[i + 1];
+                    cp[i] = __builtin_amdgcn_alignbyte(b, a, 1);
+                    cp[G::DCS + i] = __builtin_amdgcn_alignbyte(b, a, 2);
+                    cp[2 * G::DCS + i] = __builtin_amdgcn_alignbyte(b, a, 3);
+                }
+                __syncthreads();
+            }
 #pragma unroll 1
             for (int u = wave; u < G::NBLK; u = next_block(u)) {
                 const int bxl = u % TBX, byl = u / TBX;
                 if (bx0 + bxl >= nbx || byt0 + byl >= by1) continue;   // wave-uniform
                 const int x = x0 + bxl * 16, y = y0 + byl * 16;
-                if (VBS && x != 0 && y != 0)
+                if (c1 != 0) {
+                    if (VBS && x != 0 && y != 0)
+                        wave_dense_block<16, true, RP, G::DCS>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u, tid, r,
+                                                               FmePhase{0, 0}, c1);
+                    else
+                        wave_dense_block<16, false, RP, G::DCS>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u, tid,
+                                                                r, FmePhase{0, 0}, c1);
+                } else if (VBS && x != 0 && y != 0)
                     wave_dense_block<16, true, RP, 0, false, true>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u,
                                                                    tid, r);
                 else
@@ -2077,7 +2104,16 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
     using P = PTileGeo<G>;
     uint32_t* const b4w = reinterpret_cast<uint32_t*>(S.un);
     uint16_t* const list = reinterpret_cast<uint16_t*>(b4w + P::B4);
-    const Sea2Lds L{S.win, b4w, S.curt, S.a4, list, S.lcount, S.keys, S.st, count_ops};
+    // room for a dense tile's three shifted window copies in the scratch, 8 (mod 32) dwords on
+    constexpr int kUnDw = 2 * (VBS ? PTileGeoVbs<G>::U64 : PTileGeo<G>::U64);
+    int dense4 = 0;
+#ifndef SO_DENSE_ONE   // A/B builds: dense tiles read the single window copy
+    if constexpr (3 * G::DCS + 32 <= kUnDw) {
+        const int d = (int)((reinterpret_cast<uintptr_t>(b4w) - reinterpret_cast<uintptr_t>(S.win)) / 4);
+        dense4 = d + ((8 - d) & 31);
+    }
+#endif
+    const Sea2Lds L{S.win, b4w, S.curt, S.a4, list, S.lcount, S.keys, S.st, count_ops, dense4};
     RefSet refs{};
     refs.p[0] = ref;
 #ifndef SO_PROF_PHASE   // phase-attribution A/B builds only (tools/prun_phase.py): 1 = no transforms
