@@ -3,7 +3,7 @@
 # persistent grids).  Exercises the rank launch, the p2p hand-off setup + self-check, the timed
 # strong-scaling loop and the parity check of configs[3]; the numbers are not a scaling result.
 cd "$GRAFT_REPO_ROOT" || exit 1
-export TMPDIR=/tmp
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out
 for n in ${NS:-2 4}; do
   timeout -k 10 400 python -u bench.py --gpus $n --share-gpu --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} \
