@@ -165,6 +165,26 @@ def test_unpack_round_trip_and_decode(gpu):
         assert torch.equal(rec[:288, :352].cpu(), s.recon[:288, :352].cpu()), i
 
 
+@pytest.mark.parametrize("vbs", [False, True])
+def test_pack_unpack_decode_round_trip_4k(gpu, vbs):
+    """The same round trip at the benchmarked size (3840 x 2160, the persistent run's I + 3 P
+    frames): packed stream -> so_unpack_frames -> the decoder's GPU reconstruction equals the
+    encoder's, frame by frame -- a size-independent property of the full-size output."""
+    h, w = 2160, 3840
+    c, syms = _encode(gpu, h, w, 4, 4, vbs, seed=3)
+    eng = c.engine()
+    offs, out = eng.pack_symbols(syms)
+    un = eng.unpack_symbols([s.frame_type for s in syms], list(out), list(offs))
+    for i, (s, u) in enumerate(zip(syms, un)):
+        assert torch.equal(u.qtc, s.qtc) and torch.equal(u.split, s.split), i
+        if s.frame_type == 0:
+            rec = eng.recon_intra(u.split, u.mv, u.qtc, 4)
+        else:
+            rec = eng.recon_inter([syms[i - 1].recon], u.split, u.mv, u.qtc, 4)
+        torch.cuda.synchronize()
+        assert torch.equal(rec[:h, :w], s.recon[:h, :w]), i
+
+
 def test_unpack_rejects_malformed(gpu):
     c, syms = _encode(gpu, 288, 352, 2, 2, False)
     eng = c.engine()
