@@ -106,8 +106,10 @@ def parse(argv=None):
                          "has one (1080p: 10-frame GOPs with oracle fixtures)")
     ap.add_argument("--no-content-records", action="store_true",
                     help="skip the N=1 records on low-texture / noise-only content")
-    ap.add_argument("--graph", action="store_true",
-                    help="replay the GOP as one captured HIP graph (measured slower than host launches here)")
+    ap.add_argument("--no-graph", dest="graph", action="store_false",
+                    help="one GOP per step by host launches instead of the default replay of one captured HIP "
+                         "graph per GOP (N = 1 and --shard gop): the same kernels without the host launch gaps, "
+                         "within noise to 1 %% faster (profiles/r04/bench_graph_ab.log)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal on a one-GPU host: every rank on cuda:0, gloo collectives, each rank's persistent "
                          "grid capped to a 1/(2N) share of the GPU (numbers are not a scaling measurement)")
@@ -1142,7 +1144,8 @@ def main(argv=None):
                    "content": cfg.get("content", "bench"),
                    "transform": "fp64 pocketfft-exact DCT",
                    "parallelism": (mode_note.format(exchange_note) if stripe else f"gop-per-rank x{world}"),
-                   "launch": "hip-graph (one GOP per replay)" if args.graph else "host launches"},
+                   "launch": ("hip-graph (one GOP per replay)" if (args.graph and not stripe and not args.cpu_plumbing)
+                              else "host launches")},
         "parity": parity,
         "roofline": roofline_of(rl, name) if rl else rl_rc,
         "roofline_gop": gop_roofline(cfg, elapsed / args.steps) if (world == 1 and not args.cpu_plumbing) else None,
