@@ -41,7 +41,7 @@ intra_tq_kernel(const uint8_t* __restrict__ cur, int H, int W, int by0, int nrow
     constexpr int G = BS, BPW = 256 / G, SB = BS / 2;
     constexpr int LDS_D = VBS ? 288 : BS * (BS + 1);
     __shared__ double ldsd[BPW * LDS_D];
-    __shared__ uint8_t ldsf[BPW * BS * BS];
+    __shared__ uint8_t ldsf[VBS ? BPW * BS * BS : 1];   // sub_tokens' flags (block_tokens: registers only)
     __shared__ uint8_t ldsl[BPW * BS * SRM];
     const int tid = threadIdx.x, g = tid / G, l = tid % G;
     const int nbx = W / BS, nb = nbx * nrows;
