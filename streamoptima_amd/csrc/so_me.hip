@@ -2546,28 +2546,19 @@ SO_DEV uint32_t run_poll(const uint32_t* c, bool need, bool sysl, uint32_t* ws, 
                 uint32_t hw, xcc;
                 asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
                 asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-                uint32_t v = other;
-                v = lane == 1 ? (uint32_t)w.task : v;
-                v = lane == 2 ? (uint32_t)w.f : v;
-                v = lane == 3 ? (uint32_t)w.dep : v;
-                v = lane == 4 ? (uint32_t)w.tile : v;
-                v = lane == 5 ? w.want : v;
-                v = lane == 6 ? w.sys_want : v;
-                v = lane == 7 ? ((uint32_t)w.mode | (esc ? 1u << 12 : 0u)) : v;
-                v = lane == 8 ? (uint32_t)bneed : v;
-                v = lane == 9 ? (uint32_t)bsys : v;
-                v = lane == 10 ? active : v;
-                v = lane == 11 ? now : v;
-                v = lane == 12 ? susp : v;
-                v = lane == 13 ? 0u : v;
-                v = lane == 14 ? 0xFFFFFFFFu : v;
-                v = lane == 15 ? hw : v;
-                v = lane == 16 ? xcc : v;
-                v = lane == 17 ? (uint32_t)blockIdx.x : v;
-                v = lane == 18 ? (uint32_t)gridDim.x : v;
-                v = lane == 19 ? (uint32_t)brmw : v;
-                if (lane >= 1 && lane < 32)
-                    __hip_atomic_store(&ws[kRunDiagWord + lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // words 1..19 from lane 0 (a per-lane select chain here had its 19 lane masks
+                // hoisted out of the persistent loop into spilled SGPRs), words 20..31: the flags
+                if (lane >= 20 && lane < 32)
+                    __hip_atomic_store(&ws[kRunDiagWord + lane], other, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0) {
+                    const uint32_t rec[19] = {(uint32_t)w.task, (uint32_t)w.f, (uint32_t)w.dep, (uint32_t)w.tile, w.want,
+                                              w.sys_want, (uint32_t)w.mode | (esc ? 1u << 12 : 0u), (uint32_t)bneed,
+                                              (uint32_t)bsys, active, now, susp, 0u, 0xFFFFFFFFu, hw, xcc,
+                                              (uint32_t)blockIdx.x, (uint32_t)gridDim.x, (uint32_t)brmw};
+#pragma unroll
+                    for (int i = 0; i < 19; ++i)
+                        __hip_atomic_store(&ws[kRunDiagWord + 1 + i], rec[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
                 // keep reading the awaited flags (atomically) for up to 50 ms: when -- whether --
                 // they arrive tells a slow holder from a lost or unseen flag
                 const unsigned long long ta = __builtin_amdgcn_s_memrealtime();
