@@ -1,7 +1,8 @@
 """Per-GOP time of the configs[4] workload (4K ROI + two-pass RC) under environment
 variants (SO_P2LAG=..., SO_PIPELINE=0), each in a fresh process:
     python tools/rc2p_ab.py SO_P2LAG=1 SO_P2LAG=68 SO_PIPELINE=0 SO_LIB_PATH=x.so,SO_P2LAG=68
-(comma-joined settings form one variant; an SO_RUN_PROFILE library adds per-phase kcycles)"""
+(comma-joined settings form one variant; an SO_RUN_PROFILE library adds per-phase kcycles;
+AB_FUSED=1 with SO_RUN_2PASS=1 runs the fused two-pass launch)"""
 import json
 import os
 import subprocess
@@ -16,6 +17,9 @@ dev = torch.device("cuda:0")
 import os
 cfg = dict(WORKLOADS[os.environ.get("AB_CFG", "4k_rc2pass")])
 codec = build_codec(cfg, parse([]), dev)
+if os.environ.get("AB_FUSED") == "1":   # both passes in one persistent launch (needs SO_RUN_2PASS=1)
+    from streamoptima_amd import _lib
+    _lib.set_option(_lib.OPT_RUN_2PASS_FUSED, 1)
 fr = make_frames(cfg, dev, cfg["seed"])
 ts, enq = [], []
 for _ in range(6):
