@@ -377,9 +377,17 @@ SO_DEV int block_tokens(uint8_t* flags, int l, const int* q) {
     // M_{l+1}: DPP row_shl:1 (lane i reads lane i+1 of its 16-lane row; the value from
     // the next group at the group's last lane is never used: i = N-1 has no pair)
     const uint32_t mn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x101, 0xF, 0xF, false);
-    const int base = (threadIdx.x & 63) & ~(N - 1);
-    const uint32_t m0 = (uint32_t)__shfl((int)m, base, 64);
-    const uint32_t mlast = (uint32_t)__shfl((int)m, base + N - 1, 64);
+    uint32_t m0, mlast;
+    if constexpr (N == 16) {
+        // M_0 and M_15 of the lane's 16-lane row: DPP row_newbcast (gfx90a+), no LDS round
+        // trip and no lane index (which the persistent run hoisted and spilled)
+        m0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x150, 0xF, 0xF, false);
+        mlast = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x150 + N - 1, 0xF, 0xF, false);
+    } else {
+        const int base = (threadIdx.x & 63) & ~(N - 1);
+        m0 = (uint32_t)__shfl((int)m, base, 64);
+        mlast = (uint32_t)__shfl((int)m, base + N - 1, 64);
+    }
     constexpr uint32_t kInner = ((1u << N) - 1) & ~1u;
     int tr = 0;
     if (l <= N - 2) {

@@ -976,7 +976,12 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
     // st[2]: SAD byte operations executed for this tile (every v_sad_u8 / v_sad_hi_u8 lane
     // instruction counts 4): the current tile's 4x4 sums, here
     uint32_t& st_ops = L.st[2];
-    if (tid == 0) st_ops = L.count_ops ? G::NBLK * 16 * 4 * 4 : 0u;
+    if (tid == 0) {
+        // recomputed per tile: the persistent run hoisted this select and spilled it
+        uint32_t ops0 = L.count_ops ? G::NBLK * 16 * 4 * 4 : 0u;
+        asm volatile("" : "+v"(ops0));
+        st_ops = ops0;
+    }
 #ifdef SO_STAMPS
     uint32_t& st_sur = L.st[1];
     if (tid == 0) st_sur = 0;
@@ -2630,8 +2635,17 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     // this launch's epoch: ws[2] + 1 (ws[2] = the last finished launch's; written by that
     // launch's last workgroup, so every workgroup here reads it before it can change).  Done
     // flags hold the epoch of the launch that set them: nothing is zeroed between launches.
-    const uint32_t ep = __builtin_amdgcn_readfirstlane(
+    const uint32_t ep0 = __builtin_amdgcn_readfirstlane(
         __hip_atomic_load(&ws[kRunEpochWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+#ifndef SO_EP_REG
+    // inside the loop the epoch is re-read from LDS where it is used: a register held across
+    // the persistent loop was spilled to scratch and reloaded per task on wave 0's path
+    __shared__ uint32_t s_ep;
+    if (tid == 0) s_ep = ep0;   // visible after the dequeue barrier below
+#define ep ((uint32_t)__builtin_amdgcn_readfirstlane(*(lds_vu32p)&s_ep))
+#else
+    const uint32_t ep = ep0;
+#endif
     for (;;) {
         if (wave == 0) {
             const int t = (int)__builtin_amdgcn_readfirstlane(
@@ -2689,6 +2703,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 #ifdef SO_STAMPS
             if (lane == 0 && rec) rec[9] = __builtin_amdgcn_s_memrealtime();
 #endif
+            const int lane = opaque_tid() & 63;   // recomputed per task (hoisted, it was spilled)
             const int nx = tx + lane % 3 - 1, ny = ty + lane / 3 - 1;
             const bool need = (FPIPE || dep >= 0) && lane < 9 && nx >= 0 && nx < tiles_x && ny >= 0 && ny < ntr;
             // the timeout count, read once per tile: after one timeout the later tiles of the
@@ -2923,6 +2938,9 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
         }
     }
 }
+#ifndef SO_EP_REG
+#undef ep
+#endif
 
 // [kRunDoneBase, +kRunMax * ntiles64) done flags, then (two-pass runs) kRunMax * ntiles128
 // pass-1 done flags and kRunMax * nb pass-1 token counts
