@@ -167,8 +167,8 @@ SO_DEV void load_row_i16(const int16_t* __restrict__ p, int* v) {
 // Integer rows (T = int, N = 16: residuals forward, dequantised coefficients inverse) go through
 // the scratch as int32 and take dct2_16_i / dct3_16_i on axis 0: half the first transpose's
 // LDS bytes and the exact integer steps on the 2-cycle pipe.
-template <int N, bool INVERSE, class T>
-SO_DEV void xform2d_rows(double* lds, int l, const T* in_row, double* out_row) {
+template <int N, bool INVERSE, class T, class TWt = typename dct::Rfft<N>::TW>
+SO_DEV void xform2d_rows(double* lds, int l, const T* in_row, double* out_row, const TWt& tw = TWt{}) {
     constexpr int P = N + 1;
     double v[N];
     if constexpr (N == 16 && __is_same(T, int)) {
@@ -180,21 +180,21 @@ SO_DEV void xform2d_rows(double* lds, int l, const T* in_row, double* out_row) {
 #pragma unroll
         for (int r = 0; r < N; ++r) x[r] = li[r * P + l];
         wave_sync();   // every lane's int reads before the doubles below overwrite them
-        if constexpr (INVERSE) dct::dct3_16_i(x, v); else dct::dct2_16_i(x, v);   // axis 0 (columns)
+        if constexpr (INVERSE) dct::dct3_16_i(x, v, tw); else dct::dct2_16_i(x, v, tw);   // axis 0 (columns)
     } else {
 #pragma unroll
         for (int c = 0; c < N; ++c) lds[l * P + c] = (double)in_row[c];
         wave_sync();
 #pragma unroll
         for (int r = 0; r < N; ++r) v[r] = lds[r * P + l];
-        if constexpr (INVERSE) dct::dct3<N>(v); else dct::dct2<N>(v);   // axis 0 (columns)
+        if constexpr (INVERSE) dct::dct3<N>(v, tw); else dct::dct2<N>(v, tw);   // axis 0 (columns)
     }
 #pragma unroll
     for (int r = 0; r < N; ++r) lds[r * P + l] = v[r];
     wave_sync();
 #pragma unroll
     for (int c = 0; c < N; ++c) v[c] = lds[l * P + c];
-    if constexpr (INVERSE) dct::dct3<N>(v); else dct::dct2<N>(v);   // axis 1 (rows)
+    if constexpr (INVERSE) dct::dct3<N>(v, tw); else dct::dct2<N>(v, tw);   // axis 1 (rows)
 #pragma unroll
     for (int c = 0; c < N; ++c) out_row[c] = v[c];
     wave_sync();   // lds free for reuse

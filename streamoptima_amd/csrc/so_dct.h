@@ -20,51 +20,95 @@ namespace so {
 namespace dct {
 
 // pocketfft T_dcst23 twiddle[i] ~= cos(pi (i+1) / (2N)) (4N-point sincos table values)
+constexpr double kTw16Dct[15] = {
+    0x1.fd88da3d12526p-1, 0x1.f6297cff75cb0p-1, 0x1.e9f4156c62ddap-1, 0x1.d906bcf328d46p-1,
+    0x1.c38b2f180bdb1p-1, 0x1.a9b66290ea1a3p-1, 0x1.8bc806b151741p-1, 0x1.6a09e667f3bccp-1,
+    0x1.44cf325091dd6p-1, 0x1.1c73b39ae68c8p-1, 0x1.e2b5d3806f639p-2, 0x1.87de2a6aea961p-2,
+    0x1.294062ed59f04p-2, 0x1.8f8b83c69a60ap-3, 0x1.917a6bc29b424p-4};
+// rfftp first-factor twiddles, pocketfft layout wa[i + x*(ido-1)], ido = 4
+constexpr double kTw16Rf[9] = {
+    0x1.d906bcf328d46p-1, 0x1.87de2a6aea963p-2, 0.0,
+    0x1.6a09e667f3bccp-1, 0x1.6a09e667f3bcdp-1, 0.0,
+    0x1.87de2a6aea963p-2, 0x1.d906bcf328d46p-1, 0.0};
+constexpr double kSqrt2 = 0x1.6a09e667f3bcdp+0;
+constexpr double kHsqt2 = 0x1.6a09e667f3bcdp-1;
+
+// Every constant a pass multiplies by goes through these accessors (the halved and doubled
+// twiddles are exact: scaling by a power of two).  TW16 / TW8 fold them into the code as
+// literals; TW16R reads the same values from kTw16Tab through a pointer (below).
 struct TW16 {
-    static SO_DEV double dct(int i) {
-        constexpr double t[15] = {
-            0x1.fd88da3d12526p-1, 0x1.f6297cff75cb0p-1, 0x1.e9f4156c62ddap-1, 0x1.d906bcf328d46p-1,
-            0x1.c38b2f180bdb1p-1, 0x1.a9b66290ea1a3p-1, 0x1.8bc806b151741p-1, 0x1.6a09e667f3bccp-1,
-            0x1.44cf325091dd6p-1, 0x1.1c73b39ae68c8p-1, 0x1.e2b5d3806f639p-2, 0x1.87de2a6aea961p-2,
-            0x1.294062ed59f04p-2, 0x1.8f8b83c69a60ap-3, 0x1.917a6bc29b424p-4};
-        return t[i];
-    }
-    // rfftp first-factor twiddles, pocketfft layout wa[i + x*(ido-1)], ido = 4
-    static SO_DEV double rf(int i) {
-        constexpr double t[9] = {
-            0x1.d906bcf328d46p-1, 0x1.87de2a6aea963p-2, 0.0,
-            0x1.6a09e667f3bccp-1, 0x1.6a09e667f3bcdp-1, 0.0,
-            0x1.87de2a6aea963p-2, 0x1.d906bcf328d46p-1, 0.0};
-        return t[i];
-    }
-    static constexpr double fct = 0x1.6a09e667f3bcdp-3;  // T(1/sqrt(32))
+    SO_DEV double dct(int i) const { return kTw16Dct[i]; }
+    SO_DEV double hdct(int i) const { return 0.5 * kTw16Dct[i]; }
+    SO_DEV double dct2x(int i) const { return 2 * kTw16Dct[i]; }
+    SO_DEV double rf(int i) const { return kTw16Rf[i]; }
+    SO_DEV double fct() const { return 0x1.6a09e667f3bcdp-3; }   // T(1/sqrt(32))
+    SO_DEV double sqrt2() const { return kSqrt2; }
+    SO_DEV double hsqrt2() const { return kSqrt2 * 0.5; }
+    SO_DEV double hsqt2() const { return kHsqt2; }
 };
 struct TW8 {
-    static SO_DEV double dct(int i) {
+    SO_DEV double dct(int i) const {
         constexpr double t[7] = {
             0x1.f6297cff75cb0p-1, 0x1.d906bcf328d46p-1, 0x1.a9b66290ea1a3p-1, 0x1.6a09e667f3bccp-1,
             0x1.1c73b39ae68c8p-1, 0x1.87de2a6aea963p-2, 0x1.8f8b83c69a60ap-3};
         return t[i];
     }
-    static SO_DEV double rf(int i) {
+    SO_DEV double hdct(int i) const { return 0.5 * dct(i); }
+    SO_DEV double dct2x(int i) const { return 2 * dct(i); }
+    SO_DEV double rf(int i) const {
         constexpr double t[2] = {0x1.6a09e667f3bccp-1, 0x1.6a09e667f3bcdp-1};
         return t[i];
     }
-    static constexpr double fct = 0x1.0p-2;  // T(1/sqrt(16))
+    SO_DEV double fct() const { return 0x1.0p-2; }   // T(1/sqrt(16))
+    SO_DEV double sqrt2() const { return kSqrt2; }
+    SO_DEV double hsqrt2() const { return kSqrt2 * 0.5; }
+    SO_DEV double hsqt2() const { return kHsqt2; }
 };
 
-constexpr double kSqrt2 = 0x1.6a09e667f3bcdp+0;
-constexpr double kHsqt2 = 0x1.6a09e667f3bcdp-1;
+// The N = 16 constants as one table in constant memory, read by scalar loads through TW16R.
+// A kernel that runs the transforms inside a persistent loop takes the table's address through
+// an optimisation barrier once per pass (tw16_table()): the loads then stay in the pass, where
+// the values live in SGPRs for its length only.  As literals, the ~45 constants were hoisted
+// out of the loop, held in SGPRs across it and spilled to VGPR lanes (a v_writelane /
+// v_readlane pair per constant and task).
+#define SO_TW_D(i) kTw16Dct[i]
+#define SO_TW_H(i) (0.5 * kTw16Dct[i])
+static __constant__ double kTw16Tab[45] = {
+    SO_TW_D(0), SO_TW_D(1), SO_TW_D(2), SO_TW_D(3), SO_TW_D(4), SO_TW_D(5), SO_TW_D(6), SO_TW_D(7),
+    SO_TW_D(8), SO_TW_D(9), SO_TW_D(10), SO_TW_D(11), SO_TW_D(12), SO_TW_D(13), SO_TW_D(14),
+    SO_TW_H(0), SO_TW_H(1), SO_TW_H(2), SO_TW_H(3), SO_TW_H(4), SO_TW_H(5), SO_TW_H(6), SO_TW_H(7),
+    SO_TW_H(8), SO_TW_H(9), SO_TW_H(10), SO_TW_H(11), SO_TW_H(12), SO_TW_H(13), SO_TW_H(14),
+    kTw16Rf[0], kTw16Rf[1], kTw16Rf[2], kTw16Rf[3], kTw16Rf[4], kTw16Rf[5], kTw16Rf[6], kTw16Rf[7], kTw16Rf[8],
+    0x1.6a09e667f3bcdp-3, kSqrt2, kSqrt2 * 0.5, kHsqt2, 2 * kTw16Dct[7], 0.0};
+#undef SO_TW_D
+#undef SO_TW_H
+typedef const __attribute__((address_space(4))) double* so_cdp;
+struct TW16R {
+    so_cdp p;
+    SO_DEV double dct(int i) const { return p[i]; }
+    SO_DEV double hdct(int i) const { return p[15 + i]; }
+    SO_DEV double dct2x(int i) const { return i == 7 ? p[43] : 2 * p[i]; }   // only i = 7 is used
+    SO_DEV double rf(int i) const { return p[30 + i]; }
+    SO_DEV double fct() const { return p[39]; }
+    SO_DEV double sqrt2() const { return p[40]; }
+    SO_DEV double hsqrt2() const { return p[41]; }
+    SO_DEV double hsqt2() const { return p[42]; }
+};
+SO_DEV TW16R tw16_table() {
+    so_cdp q = (so_cdp)kTw16Tab;
+    asm volatile("" : "+s"(q));
+    return TW16R{q};
+}
 
 #define SO_PM(a, b, c, d) { a = (c) + (d); b = (c) - (d); }
 #define SO_MULPM(a, b, c, d, e, f) { a = (c) * (e) + (d) * (f); b = (c) * (f) - (d) * (e); }
 
 // ---- real-FFT passes (radix 2 / radix 4), compile-time ido / l1 ----------------------
 template <int IDO, int L1, class TW>
-SO_DEV void radf2(const double* cc, double* ch) {
+SO_DEV void radf2(const double* cc, double* ch, const TW& tw) {
 #define CC(a, b, c) cc[(a) + IDO * ((b) + L1 * (c))]
 #define CH(a, b, c) ch[(a) + IDO * ((b) + 2 * (c))]
-#define WA(x, i) TW::rf((i) + (x) * (IDO - 1))
+#define WA(x, i) tw.rf((i) + (x) * (IDO - 1))
 #pragma unroll
     for (int k = 0; k < L1; k++) SO_PM(CH(0, 0, k), CH(IDO - 1, 1, k), CC(0, k, 0), CC(0, k, 1));
     if constexpr ((IDO & 1) == 0) {
@@ -91,7 +135,7 @@ SO_DEV void radf2(const double* cc, double* ch) {
 }
 
 template <int IDO, int L1, class TW>
-SO_DEV void radf4(const double* cc, double* ch) {
+SO_DEV void radf4(const double* cc, double* ch, const TW& tw) {
 #define CC(a, b, c) cc[(a) + IDO * ((b) + L1 * (c))]
 #define CH(a, b, c) ch[(a) + IDO * ((b) + 4 * (c))]
 #pragma unroll
@@ -104,8 +148,8 @@ SO_DEV void radf4(const double* cc, double* ch) {
     if constexpr ((IDO & 1) == 0) {
 #pragma unroll
         for (int k = 0; k < L1; k++) {
-            double ti1 = -kHsqt2 * (CC(IDO - 1, k, 1) + CC(IDO - 1, k, 3));
-            double tr1 = kHsqt2 * (CC(IDO - 1, k, 1) - CC(IDO - 1, k, 3));
+            double ti1 = -tw.hsqt2() * (CC(IDO - 1, k, 1) + CC(IDO - 1, k, 3));
+            double tr1 = tw.hsqt2() * (CC(IDO - 1, k, 1) - CC(IDO - 1, k, 3));
             SO_PM(CH(IDO - 1, 0, k), CH(IDO - 1, 2, k), CC(IDO - 1, k, 0), tr1);
             SO_PM(CH(0, 3, k), CH(0, 1, k), ti1, CC(IDO - 1, k, 2));
         }
@@ -135,7 +179,7 @@ SO_DEV void radf4(const double* cc, double* ch) {
 }
 
 template <int IDO, int L1, class TW>
-SO_DEV void radb2(const double* cc, double* ch) {
+SO_DEV void radb2(const double* cc, double* ch, const TW& tw) {
 #define CC(a, b, c) cc[(a) + IDO * ((b) + 2 * (c))]
 #define CH(a, b, c) ch[(a) + IDO * ((b) + L1 * (c))]
 #pragma unroll
@@ -164,7 +208,7 @@ SO_DEV void radb2(const double* cc, double* ch) {
 }
 
 template <int IDO, int L1, class TW>
-SO_DEV void radb4(const double* cc, double* ch) {
+SO_DEV void radb4(const double* cc, double* ch, const TW& tw) {
 #define CC(a, b, c) cc[(a) + IDO * ((b) + 4 * (c))]
 #define CH(a, b, c) ch[(a) + IDO * ((b) + L1 * (c))]
 #pragma unroll
@@ -186,9 +230,9 @@ SO_DEV void radb4(const double* cc, double* ch) {
             SO_PM(ti1, ti2, CC(0, 3, k), CC(0, 1, k));
             SO_PM(tr2, tr1, CC(IDO - 1, 0, k), CC(IDO - 1, 2, k));
             CH(IDO - 1, k, 0) = tr2 + tr2;
-            CH(IDO - 1, k, 1) = kSqrt2 * (tr1 - ti1);
+            CH(IDO - 1, k, 1) = tw.sqrt2() * (tr1 - ti1);
             CH(IDO - 1, k, 2) = ti2 + ti2;
-            CH(IDO - 1, k, 3) = -kSqrt2 * (tr1 + ti1);
+            CH(IDO - 1, k, 3) = -tw.sqrt2() * (tr1 + ti1);
         }
     }
     if constexpr (IDO > 2) {
@@ -220,43 +264,46 @@ SO_DEV void radb4(const double* cc, double* ch) {
 template <int N> struct Rfft;
 template <> struct Rfft<16> {
     using TW = TW16;
-    static SO_DEV void backward(double* c) {
+    template <class T>
+    static SO_DEV void backward(double* c, const T& tw) {
         double ch[16];
-        radb4<4, 1, TW16>(c, ch);
-        radb4<1, 4, TW16>(ch, c);
+        radb4<4, 1>(c, ch, tw);
+        radb4<1, 4>(ch, c, tw);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) c[i] *= TW16::fct;
+        for (int i = 0; i < 16; ++i) c[i] *= tw.fct();
     }
-    static SO_DEV void forward(double* c) {
+    template <class T>
+    static SO_DEV void forward(double* c, const T& tw) {
         double ch[16];
-        radf4<1, 4, TW16>(c, ch);
-        radf4<4, 1, TW16>(ch, c);
+        radf4<1, 4>(c, ch, tw);
+        radf4<4, 1>(ch, c, tw);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) c[i] *= TW16::fct;
+        for (int i = 0; i < 16; ++i) c[i] *= tw.fct();
     }
 };
 template <> struct Rfft<8> {
     using TW = TW8;
-    static SO_DEV void backward(double* c) {
+    template <class T>
+    static SO_DEV void backward(double* c, const T& tw) {
         double ch[8];
-        radb2<4, 1, TW8>(c, ch);
-        radb4<1, 2, TW8>(ch, c);
+        radb2<4, 1>(c, ch, tw);
+        radb4<1, 2>(ch, c, tw);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) c[i] *= TW8::fct;
+        for (int i = 0; i < 8; ++i) c[i] *= tw.fct();
     }
-    static SO_DEV void forward(double* c) {
+    template <class T>
+    static SO_DEV void forward(double* c, const T& tw) {
         double ch[8];
-        radf4<1, 2, TW8>(c, ch);
-        radf2<4, 1, TW8>(ch, c);
+        radf4<1, 2>(c, ch, tw);
+        radf2<4, 1>(ch, c, tw);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) c[i] *= TW8::fct;
+        for (int i = 0; i < 8; ++i) c[i] *= tw.fct();
     }
 };
 
 // DCT-II, ortho (pocketfft T_dcst23::exec type 2, cosine)
-template <int N>
-SO_DEV void dct2(double* c) {
-    using TW = typename Rfft<N>::TW;
+template <int N, class TW = typename Rfft<N>::TW>
+SO_DEV void dct2(double* c, const TW& tw = TW{}) {
     constexpr int NS2 = (N + 1) / 2;
     c[0] *= 2;
     c[N - 1] *= 2;
@@ -266,38 +313,37 @@ SO_DEV void dct2(double* c) {
         c[k + 1] -= c[k];
         c[k] += t;
     }
-    Rfft<N>::backward(c);
+    Rfft<N>::backward(c, tw);
     // 0.5 (t1 +- t2) with the 0.5 folded into the twiddles: scaling by a power of two
     // commutes with every rounding (no under/overflow at these magnitudes), so
     // (0.5 w) a + (0.5 v) b == 0.5 (w a + v b) bit for bit
 #pragma unroll
     for (int k = 1; k < NS2; ++k) {
         const int kc = N - k;
-        const double ha = 0.5 * TW::dct(k - 1), hb = 0.5 * TW::dct(kc - 1);
+        const double ha = tw.hdct(k - 1), hb = tw.hdct(kc - 1);
         double t1 = ha * c[kc] + hb * c[k];
         double t2 = ha * c[k] - hb * c[kc];
         c[k] = t1 + t2;
         c[kc] = t1 - t2;
     }
-    c[NS2] *= TW::dct(NS2 - 1);
-    c[0] *= kSqrt2 * 0.5;
+    c[NS2] *= tw.dct(NS2 - 1);
+    c[0] *= tw.hsqrt2();
 }
 
 // DCT-III, ortho (pocketfft T_dcst23::exec type 3, cosine)
-template <int N>
-SO_DEV void dct3(double* c) {
-    using TW = typename Rfft<N>::TW;
+template <int N, class TW = typename Rfft<N>::TW>
+SO_DEV void dct3(double* c, const TW& tw = TW{}) {
     constexpr int NS2 = (N + 1) / 2;
-    c[0] *= kSqrt2;
+    c[0] *= tw.sqrt2();
 #pragma unroll
     for (int k = 1; k < NS2; ++k) {
         const int kc = N - k;
         double t1 = c[k] + c[kc], t2 = c[k] - c[kc];
-        c[k] = TW::dct(k - 1) * t2 + TW::dct(kc - 1) * t1;
-        c[kc] = TW::dct(k - 1) * t1 - TW::dct(kc - 1) * t2;
+        c[k] = tw.dct(k - 1) * t2 + tw.dct(kc - 1) * t1;
+        c[kc] = tw.dct(k - 1) * t1 - tw.dct(kc - 1) * t2;
     }
-    c[NS2] *= 2 * TW::dct(NS2 - 1);
-    Rfft<N>::forward(c);
+    c[NS2] *= tw.dct2x(NS2 - 1);
+    Rfft<N>::forward(c, tw);
 #pragma unroll
     for (int k = 1; k < N - 1; k += 2) {
         double t = c[k];
@@ -313,8 +359,8 @@ SO_DEV void dct3(double* c) {
 // converted where it first meets a twiddle: the same doubles bit for bit, with as many
 // conversions as loading the 16 inputs as doubles took.  54 of dct2's FP64 ops and 14 of
 // dct3's move to the integer pipe.
-SO_DEV void dct2_16_i(const int (&x)[16], double (&c)[16]) {
-    using TW = TW16;
+template <class TW = TW16>
+SO_DEV void dct2_16_i(const int (&x)[16], double (&c)[16], const TW& tw = TW{}) {
     int y[16];   // T_dcst23 type-2 prelude
     y[0] = 2 * x[0];
     y[15] = 2 * x[15];
@@ -337,9 +383,9 @@ SO_DEV void dct2_16_i(const int (&x)[16], double (&c)[16]) {
         const int ti1 = y[12] + y[4], ti2 = y[12] - y[4];
         const int tr2 = y[3] + y[11], tr1 = y[3] - y[11];
         ih3 = tr2 + tr2;
-        h7 = kSqrt2 * (double)(tr1 - ti1);
+        h7 = tw.sqrt2() * (double)(tr1 - ti1);
         ih11 = ti2 + ti2;
-        h15 = -kSqrt2 * (double)(tr1 + ti1);
+        h15 = -tw.sqrt2() * (double)(tr1 + ti1);
     }
     {
         const int tr2 = y[1] + y[13], tr1 = y[1] - y[13];
@@ -352,12 +398,12 @@ SO_DEV void dct2_16_i(const int (&x)[16], double (&c)[16]) {
         const double ci3 = (double)(ti2 - ti3);
         const double cr4 = (double)(tr1 + tr4), cr2 = (double)(tr1 - tr4);
         const double ci2 = (double)(ti1 + ti4), ci4 = (double)(ti1 - ti4);
-        h6 = TW::rf(0) * ci2 + TW::rf(1) * cr2;
-        h5 = TW::rf(0) * cr2 - TW::rf(1) * ci2;
-        h10 = TW::rf(3) * ci3 + TW::rf(4) * cr3;
-        h9 = TW::rf(3) * cr3 - TW::rf(4) * ci3;
-        h14 = TW::rf(6) * ci4 + TW::rf(7) * cr4;
-        h13 = TW::rf(6) * cr4 - TW::rf(7) * ci4;
+        h6 = tw.rf(0) * ci2 + tw.rf(1) * cr2;
+        h5 = tw.rf(0) * cr2 - tw.rf(1) * ci2;
+        h10 = tw.rf(3) * ci3 + tw.rf(4) * cr3;
+        h9 = tw.rf(3) * cr3 - tw.rf(4) * ci3;
+        h14 = tw.rf(6) * ci4 + tw.rf(7) * cr4;
+        h13 = tw.rf(6) * cr4 - tw.rf(7) * ci4;
     }
     // radb4<1, 4>: CC(0, b, k) = h[b + 4 k], CH(0, k, j) = c[k + 4 j]
     {   // k = 0: all four inputs integers
@@ -389,33 +435,33 @@ SO_DEV void dct2_16_i(const int (&x)[16], double (&c)[16]) {
         c[7] = __builtin_fma(-2.0, h14, tr1);
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) c[i] *= TW::fct;
+    for (int i = 0; i < 16; ++i) c[i] *= tw.fct();
     // dct2's post-twiddles, unchanged
 #pragma unroll
     for (int k = 1; k < 8; ++k) {
         const int kc = 16 - k;
-        const double ha = 0.5 * TW::dct(k - 1), hb = 0.5 * TW::dct(kc - 1);
+        const double ha = tw.hdct(k - 1), hb = tw.hdct(kc - 1);
         double t1 = ha * c[kc] + hb * c[k];
         double t2 = ha * c[k] - hb * c[kc];
         c[k] = t1 + t2;
         c[kc] = t1 - t2;
     }
-    c[8] *= TW::dct(7);
-    c[0] *= kSqrt2 * 0.5;
+    c[8] *= tw.dct(7);
+    c[0] *= tw.hsqrt2();
 }
 
-SO_DEV void dct3_16_i(const int (&x)[16], double (&c)[16]) {
-    using TW = TW16;
-    c[0] = (double)x[0] * kSqrt2;
+template <class TW = TW16>
+SO_DEV void dct3_16_i(const int (&x)[16], double (&c)[16], const TW& tw = TW{}) {
+    c[0] = (double)x[0] * tw.sqrt2();
 #pragma unroll
     for (int k = 1; k < 8; ++k) {
         const int kc = 16 - k;
         const double t1 = (double)(x[k] + x[kc]), t2 = (double)(x[k] - x[kc]);
-        c[k] = TW::dct(k - 1) * t2 + TW::dct(kc - 1) * t1;
-        c[kc] = TW::dct(k - 1) * t1 - TW::dct(kc - 1) * t2;
+        c[k] = tw.dct(k - 1) * t2 + tw.dct(kc - 1) * t1;
+        c[kc] = tw.dct(k - 1) * t1 - tw.dct(kc - 1) * t2;
     }
-    c[8] = (double)x[8] * (2 * TW::dct(7));
-    Rfft<16>::forward(c);
+    c[8] = (double)x[8] * tw.dct2x(7);
+    Rfft<16>::forward(c, tw);
 #pragma unroll
     for (int k = 1; k < 15; k += 2) {
         double t = c[k];
@@ -426,8 +472,8 @@ SO_DEV void dct3_16_i(const int (&x)[16], double (&c)[16]) {
 
 // The same for N = 8 (the VBS sub-blocks): rfftp [2, 4]; 24 of dct2<8>'s FP64 ops and 6 of
 // dct3<8>'s move to int32.
-SO_DEV void dct2_8_i(const int (&x)[8], double (&c)[8]) {
-    using TW = TW8;
+template <class TW = TW8>
+SO_DEV void dct2_8_i(const int (&x)[8], double (&c)[8], const TW& tw = TW{}) {
     int y[8];
     y[0] = 2 * x[0];
     y[7] = 2 * x[7];
@@ -441,8 +487,8 @@ SO_DEV void dct2_8_i(const int (&x)[8], double (&c)[8]) {
     const int ih3 = 2 * y[3], ih7 = -2 * y[4];
     const int ih1 = y[1] + y[5], tr2 = y[1] - y[5];
     const int ti2 = y[2] + y[6], ih2 = y[2] - y[6];
-    const double h6 = TW::rf(0) * (double)ti2 + TW::rf(1) * (double)tr2;
-    const double h5 = TW::rf(0) * (double)tr2 - TW::rf(1) * (double)ti2;
+    const double h6 = tw.rf(0) * (double)ti2 + tw.rf(1) * (double)tr2;
+    const double h5 = tw.rf(0) * (double)tr2 - tw.rf(1) * (double)ti2;
     // radb4<1, 2>: CC(0, b, k) = h[b + 4 k], CH(0, k, j) = c[k + 2 j]
     {   // k = 0: all four inputs integers
         const int t2 = ih0 + ih3, t1 = ih0 - ih3;
@@ -459,32 +505,32 @@ SO_DEV void dct2_8_i(const int (&x)[8], double (&c)[8]) {
         c[3] = __builtin_fma(-2.0, h6, t1);
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) c[i] *= TW::fct;
+    for (int i = 0; i < 8; ++i) c[i] *= tw.fct();
 #pragma unroll
     for (int k = 1; k < 4; ++k) {
         const int kc = 8 - k;
-        const double ha = 0.5 * TW::dct(k - 1), hb = 0.5 * TW::dct(kc - 1);
+        const double ha = tw.hdct(k - 1), hb = tw.hdct(kc - 1);
         double t1 = ha * c[kc] + hb * c[k];
         double t2 = ha * c[k] - hb * c[kc];
         c[k] = t1 + t2;
         c[kc] = t1 - t2;
     }
-    c[4] *= TW::dct(3);
-    c[0] *= kSqrt2 * 0.5;
+    c[4] *= tw.dct(3);
+    c[0] *= tw.hsqrt2();
 }
 
-SO_DEV void dct3_8_i(const int (&x)[8], double (&c)[8]) {
-    using TW = TW8;
-    c[0] = (double)x[0] * kSqrt2;
+template <class TW = TW8>
+SO_DEV void dct3_8_i(const int (&x)[8], double (&c)[8], const TW& tw = TW{}) {
+    c[0] = (double)x[0] * tw.sqrt2();
 #pragma unroll
     for (int k = 1; k < 4; ++k) {
         const int kc = 8 - k;
         const double t1 = (double)(x[k] + x[kc]), t2 = (double)(x[k] - x[kc]);
-        c[k] = TW::dct(k - 1) * t2 + TW::dct(kc - 1) * t1;
-        c[kc] = TW::dct(k - 1) * t1 - TW::dct(kc - 1) * t2;
+        c[k] = tw.dct(k - 1) * t2 + tw.dct(kc - 1) * t1;
+        c[kc] = tw.dct(k - 1) * t1 - tw.dct(kc - 1) * t2;
     }
-    c[4] = (double)x[4] * (2 * TW::dct(3));
-    Rfft<8>::forward(c);
+    c[4] = (double)x[4] * tw.dct2x(3);
+    Rfft<8>::forward(c, tw);
 #pragma unroll
     for (int k = 1; k < 7; k += 2) {
         double t = c[k];

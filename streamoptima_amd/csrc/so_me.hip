@@ -1547,6 +1547,13 @@ struct PHalo {
 // false, false>.  `scratch` = 16 x 17 doubles of LDS owned by the calling lanes.
 // `qs` (fwd_mfma): the block's levels, already certified (16 x 16 int16 at the start of
 // `scratch`); null = run the FP64 forward transform here.
+// The twiddles of tq16_exact's transforms: scalar loads from the constant table, behind one
+// optimisation barrier per 2-D transform (dct::tw16_table); -DSO_TQ_TW_LITERAL: as literals.
+#ifdef SO_TQ_TW_LITERAL
+#define SO_TQ_TW() dct::TW16{}
+#else
+#define SO_TQ_TW() dct::tw16_table()
+#endif
 template <class G, bool SC1, bool HALO = false, bool TOK = false>
 SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, int byt0, int nbx, int by0, int by1,
                        int W, int qp_rd, const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map,
@@ -1592,7 +1599,7 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
                 }
             }
             double tcr[16];
-            xform2d_rows<16, false>(dl, l, res, tcr);
+            xform2d_rows<16, false>(dl, l, res, tcr, SO_TQ_TW());
 #pragma unroll
             for (int c = 0; c < 16; ++c)
                 q[c] = (int)(uint32_t)__builtin_bit_cast(
@@ -1607,7 +1614,7 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
         int dq[16];
         double rd[16];
         dequant_row_int<16>(q, l, qpr, dq);
-        xform2d_rows<16, true>(dl, l, dq, rd);
+        xform2d_rows<16, true>(dl, l, dq, rd, SO_TQ_TW());
         int rec[16];
         {
             uint32_t pw[4];
