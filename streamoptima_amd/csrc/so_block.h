@@ -239,8 +239,8 @@ SO_DEV void xform2d_rows_half(double* lds, int l, const T* in_row, double* out_r
 // (l & 3), (l & 3) + 4 on input and output.  lds: 4 x 8 x 9 doubles.
 // Integer rows (T = int) go through the scratch as int32 and take dct2_8_i / dct3_8_i on the
 // column pass, as xform2d_rows<16> does.
-template <bool INVERSE, class T>
-SO_DEV void xform2d_sub(double* lds, int l, const T (&in)[2][8], double (&out)[2][8]) {
+template <bool INVERSE, class T, class TWt = dct::TW8>
+SO_DEV void xform2d_sub(double* lds, int l, const T (&in)[2][8], double (&out)[2][8], const TWt& tw = TWt{}) {
     const int j = l >> 2, r0 = l & 3;
     double* s = lds + j * 72;
     if constexpr (__is_same(T, int)) {
@@ -259,7 +259,7 @@ SO_DEV void xform2d_sub(double* lds, int l, const T (&in)[2][8], double (&out)[2
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             double v[8];
-            if constexpr (INVERSE) dct::dct3_8_i(x[h], v); else dct::dct2_8_i(x[h], v);
+            if constexpr (INVERSE) dct::dct3_8_i(x[h], v, tw); else dct::dct2_8_i(x[h], v, tw);
 #pragma unroll
             for (int r = 0; r < 8; ++r) s[r * 9 + r0 + 4 * h] = v[r];
         }
@@ -275,7 +275,7 @@ SO_DEV void xform2d_sub(double* lds, int l, const T (&in)[2][8], double (&out)[2
             const int col = r0 + 4 * h;
 #pragma unroll
             for (int r = 0; r < 8; ++r) v[r] = s[r * 9 + col];
-            if constexpr (INVERSE) dct::dct3<8>(v); else dct::dct2<8>(v);
+            if constexpr (INVERSE) dct::dct3<8>(v, tw); else dct::dct2<8>(v, tw);
 #pragma unroll
             for (int r = 0; r < 8; ++r) s[r * 9 + col] = v[r];
         }
@@ -287,7 +287,7 @@ SO_DEV void xform2d_sub(double* lds, int l, const T (&in)[2][8], double (&out)[2
         const int row = r0 + 4 * h;
 #pragma unroll
         for (int c = 0; c < 8; ++c) v[c] = s[row * 9 + c];
-        if constexpr (INVERSE) dct::dct3<8>(v); else dct::dct2<8>(v);
+        if constexpr (INVERSE) dct::dct3<8>(v, tw); else dct::dct2<8>(v, tw);
 #pragma unroll
         for (int c = 0; c < 8; ++c) out[h][c] = v[c];
     }

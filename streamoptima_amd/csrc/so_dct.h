@@ -46,19 +46,15 @@ struct TW16 {
     SO_DEV double hsqrt2() const { return kSqrt2 * 0.5; }
     SO_DEV double hsqt2() const { return kHsqt2; }
 };
+constexpr double kTw8Dct[7] = {
+    0x1.f6297cff75cb0p-1, 0x1.d906bcf328d46p-1, 0x1.a9b66290ea1a3p-1, 0x1.6a09e667f3bccp-1,
+    0x1.1c73b39ae68c8p-1, 0x1.87de2a6aea963p-2, 0x1.8f8b83c69a60ap-3};
+constexpr double kTw8Rf[2] = {0x1.6a09e667f3bccp-1, 0x1.6a09e667f3bcdp-1};
 struct TW8 {
-    SO_DEV double dct(int i) const {
-        constexpr double t[7] = {
-            0x1.f6297cff75cb0p-1, 0x1.d906bcf328d46p-1, 0x1.a9b66290ea1a3p-1, 0x1.6a09e667f3bccp-1,
-            0x1.1c73b39ae68c8p-1, 0x1.87de2a6aea963p-2, 0x1.8f8b83c69a60ap-3};
-        return t[i];
-    }
-    SO_DEV double hdct(int i) const { return 0.5 * dct(i); }
-    SO_DEV double dct2x(int i) const { return 2 * dct(i); }
-    SO_DEV double rf(int i) const {
-        constexpr double t[2] = {0x1.6a09e667f3bccp-1, 0x1.6a09e667f3bcdp-1};
-        return t[i];
-    }
+    SO_DEV double dct(int i) const { return kTw8Dct[i]; }
+    SO_DEV double hdct(int i) const { return 0.5 * kTw8Dct[i]; }
+    SO_DEV double dct2x(int i) const { return 2 * kTw8Dct[i]; }
+    SO_DEV double rf(int i) const { return kTw8Rf[i]; }
     SO_DEV double fct() const { return 0x1.0p-2; }   // T(1/sqrt(16))
     SO_DEV double sqrt2() const { return kSqrt2; }
     SO_DEV double hsqrt2() const { return kSqrt2 * 0.5; }
@@ -98,6 +94,28 @@ SO_DEV TW16R tw16_table() {
     so_cdp q = (so_cdp)kTw16Tab;
     asm volatile("" : "+s"(q));
     return TW16R{q};
+}
+// The same for N = 8 (the VBS sub-blocks).
+static __constant__ double kTw8Tab[21] = {
+    kTw8Dct[0], kTw8Dct[1], kTw8Dct[2], kTw8Dct[3], kTw8Dct[4], kTw8Dct[5], kTw8Dct[6],
+    0.5 * kTw8Dct[0], 0.5 * kTw8Dct[1], 0.5 * kTw8Dct[2], 0.5 * kTw8Dct[3], 0.5 * kTw8Dct[4],
+    0.5 * kTw8Dct[5], 0.5 * kTw8Dct[6],
+    kTw8Rf[0], kTw8Rf[1], 0x1.0p-2, kSqrt2, kSqrt2 * 0.5, kHsqt2, 2 * kTw8Dct[3]};
+struct TW8R {
+    so_cdp p;
+    SO_DEV double dct(int i) const { return p[i]; }
+    SO_DEV double hdct(int i) const { return p[7 + i]; }
+    SO_DEV double dct2x(int i) const { return i == 3 ? p[20] : 2 * p[i]; }   // only i = 3 is used
+    SO_DEV double rf(int i) const { return p[14 + i]; }
+    SO_DEV double fct() const { return 0x1.0p-2; }   // an inline constant
+    SO_DEV double sqrt2() const { return p[17]; }
+    SO_DEV double hsqrt2() const { return p[18]; }
+    SO_DEV double hsqt2() const { return p[19]; }
+};
+SO_DEV TW8R tw8_table() {
+    so_cdp q = (so_cdp)kTw8Tab;
+    asm volatile("" : "+s"(q));
+    return TW8R{q};
 }
 
 #define SO_PM(a, b, c, d) { a = (c) + (d); b = (c) - (d); }

@@ -1551,8 +1551,10 @@ struct PHalo {
 // optimisation barrier per 2-D transform (dct::tw16_table); -DSO_TQ_TW_LITERAL: as literals.
 #ifdef SO_TQ_TW_LITERAL
 #define SO_TQ_TW() dct::TW16{}
+#define SO_TQ_TW8() dct::TW8{}
 #else
 #define SO_TQ_TW() dct::tw16_table()
+#define SO_TQ_TW8() dct::tw8_table()
 #endif
 template <class G, bool SC1, bool HALO = false, bool TOK = false>
 SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, int byt0, int nbx, int by0, int by1,
@@ -1875,7 +1877,7 @@ SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, ui
             for (int e = 0; e < 4; ++e) res[4 * k + e] = (int)((cw >> (8 * e)) & 255) - (int)((pw[k] >> (8 * e)) & 255);
         }
         double tcr[16];
-        xform2d_rows<16, false>(scratch, l, res, tcr);
+        xform2d_rows<16, false>(scratch, l, res, tcr, SO_TQ_TW());
         int tc[16], q[16];
 #pragma unroll
         for (int c = 0; c < 16; ++c) tc[c] = (int)__builtin_rint(tcr[c]);
@@ -1910,7 +1912,7 @@ SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, ui
             }
         }
         double std_[2][8];
-        xform2d_sub<false>(scratch, l, sres, std_);
+        xform2d_sub<false>(scratch, l, sres, std_, SO_TQ_TW8());
         int stc[2][8], qs[2][8];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -2028,7 +2030,7 @@ SO_DEV void tq16_vbs_inv(PTileLds<G, true>& S, int k, int l, double* scratch, in
         unpack_i16<16>(lv, q);
         dequant_row_int<16>(q, l, qpr, dq);
         double rd[16];
-        xform2d_rows<16, true>(scratch, l, dq, rd);
+        xform2d_rows<16, true>(scratch, l, dq, rd, SO_TQ_TW());
         int rec[16];
         {
             uint32_t pw[4];
@@ -2062,7 +2064,7 @@ SO_DEV void tq16_vbs_inv(PTileLds<G, true>& S, int k, int l, double* scratch, in
             dequant_row_int<8>(qs, r0 + 4 * h, qpm1, sdq[h]);
         }
         double srd[2][8];
-        xform2d_sub<true>(scratch, l, sdq, srd);
+        xform2d_sub<true>(scratch, l, sdq, srd, SO_TQ_TW8());
         const int xs = x + (j & 1) * 8, ys = y + (j >> 1) * 8;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -2253,7 +2255,7 @@ SO_DEV void tq16_pass1(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
             }
         }
         double tcr[16];
-        xform2d_rows<16, false>(scratch, l, res, tcr);
+        xform2d_rows<16, false>(scratch, l, res, tcr, SO_TQ_TW());
         constexpr double kRne = 0x1.8p52;
         int q[16];
 #pragma unroll
@@ -2327,7 +2329,7 @@ SO_DEV void tq16_pass2(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
                     res[4 * k + e] = (int)((cw[k] >> (8 * e)) & 255) - (int)((pw[k] >> (8 * e)) & 255);
         }
         double tcr[16];
-        xform2d_rows<16, false>(scratch, l, res, tcr);
+        xform2d_rows<16, false>(scratch, l, res, tcr, SO_TQ_TW());
         constexpr double kRne = 0x1.8p52;
         int q[16];
 #pragma unroll
@@ -2339,7 +2341,7 @@ SO_DEV void tq16_pass2(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
         int dq[16];
         double rd[16];
         dequant_row_int<16>(q, l, qpr, dq);
-        xform2d_rows<16, true>(scratch, l, dq, rd);
+        xform2d_rows<16, true>(scratch, l, dq, rd, SO_TQ_TW());
         int rec[16];
         {
             uint32_t pw[4];
