@@ -2108,12 +2108,14 @@ SO_DEV void store_sc1_i32(int32_t* p, int v) {
     asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 }
 
-template <class G, bool SC1, class Pre = NoPre, bool HALO = false, bool TOK = false, bool VBS = false>
+template <class G, bool SC1, class Pre = NoPre, bool HALO = false, bool TOK = false, bool VBS = false,
+          class Post = NoPre>
 SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict__ cur, const uint8_t* ref, int H, int W,
                        int by0, int by1, int qp_rd, const int32_t* __restrict__ qp_row,
                        const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best, const PFrameOut& o,
                        const Pre& pre = Pre(), const PHalo& hl = PHalo{}, double lam = 0.0,
-                       const int* dense_flag = nullptr, int32_t* fb_out = nullptr, int count_ops = 0) {
+                       const int* dense_flag = nullptr, int32_t* fb_out = nullptr, int count_ops = 0,
+                       const Post& post = Post()) {
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY;
     using P = PTileGeo<G>;
     uint32_t* const b4w = reinterpret_cast<uint32_t*>(S.un);
@@ -2210,6 +2212,7 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
         }
     }
     SO_SEA_STAMP(7, __builtin_amdgcn_s_memtime());
+    post();   // p_run_kernel: the next task's dequeue, in flight with the drain below
     if constexpr (SC1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
     SO_SEA_STAMP(14, __builtin_amdgcn_s_memtime());
     __syncthreads();
@@ -2601,6 +2604,27 @@ SO_DEV uint32_t run_poll(const uint32_t* c, bool need, bool sysl, uint32_t* ws, 
 }
 
 
+// The run's task dequeue, called by a whole wave: ONE returning atomic add of 1 to ws[0] (exec =
+// lane 0 inside the asm), then s_waitcnt vmcnt(0), which also drains the wave's earlier stores.
+// Returns the task index in lane 0.  (Written as `fetch_add(ws, lane == 0 ? 1 : 0)` by every
+// lane, the compiler's atomic optimizer turned it into a 64-iteration readlane / writelane scan
+// over the lanes before the atomic, and waited on the result right after it; a `lane == 0`
+// branch ahead of the loop's barrier was structurised into a hang, tools/ubench_rowdeps.cpp.)
+SO_DEV uint32_t run_dequeue(uint32_t* ws) {
+    uint32_t r;
+    uint64_t sv;
+    asm volatile(
+        "s_mov_b64 %1, exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "global_atomic_add %0, %2, %3, off sc0\n\t"
+        "s_waitcnt vmcnt(0)\n\t"
+        "s_mov_b64 exec, %1"
+        : "=&v"(r), "=&s"(sv)
+        : "v"(ws), "v"(1u)
+        : "memory");
+    return r;
+}
+
 // VBS: VBSEnable (the block + sub-block dense search, tq16_vbs; ~128 VGPRs, 4 waves per SIMD)
 template <int NW, int MODE, bool VBS = false>
 __global__ void __launch_bounds__(NW * 64)
@@ -2655,13 +2679,20 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 #else
     const uint32_t ep = ep0;
 #endif
+    // The plain run dequeues its next task at the end of the current one (ptile_body's `post`,
+    // before the drain of the tile's stores), so the atomic's round trip overlaps the drain
+    // instead of following the done flag.  Still deadlock-free: a workgroup holds at most one
+    // not-yet-started task, and the lowest unfinished task is either running or held by a
+    // workgroup whose current task (dequeued before it) has finished.
+    uint32_t nxt_v = 0;       // wave 0: the atomic's result (VGPR; read at the loop top)
+    bool nxt_taken = false;   // uniform
     for (;;) {
         if (wave == 0) {
-            const int t = (int)__builtin_amdgcn_readfirstlane(
-                __hip_atomic_fetch_add(&ws[0], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            s_task = t;
+            if (!nxt_taken) nxt_v = run_dequeue(ws);
+            s_task = (int)__builtin_amdgcn_readfirstlane(nxt_v);
             s_dense = 0;
         }
+        nxt_taken = false;
         __syncthreads();
         const int task = __builtin_amdgcn_readfirstlane(s_task);
         if (task >= ntasks) break;   // uniform: every wave leaves
@@ -2897,12 +2928,17 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 #ifdef SO_RUN_PROFILE
             const unsigned long long pt0 = __builtin_amdgcn_s_memtime();
 #endif
-            ptile_body<G, true, decltype(wait_ref), false, false, VBS>(S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd,
-                                                                       qp_row, nullptr, nullptr, a.out[f], wait_ref,
-                                                                       PHalo{}, lam, &s_dense,
-                                                                       reinterpret_cast<int32_t*>(tilefb) +
-                                                                           (size_t)f * ntiles + tile,
-                                                                       sp.count_ops);
+#ifndef SO_DEQ_LATE   // A/B builds: dequeue at the loop top, after the done flag
+            const auto take_next = [&]() {
+                if (wave == 0) nxt_v = run_dequeue(ws);   // waits for the tile's stores too
+                nxt_taken = true;
+            };
+#else
+            const NoPre take_next{};
+#endif
+            ptile_body<G, true, decltype(wait_ref), false, false, VBS, decltype(take_next)>(
+                S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd, qp_row, nullptr, nullptr, a.out[f], wait_ref, PHalo{}, lam,
+                &s_dense, reinterpret_cast<int32_t*>(tilefb) + (size_t)f * ntiles + tile, sp.count_ops, take_next);
             SO_RUN_PROF(52, __builtin_amdgcn_s_memtime() - pt0);
             // ptile_body ended with every wave's write-through stores retired and a barrier
             // (sp.lose_task: SO_OPT_TEST_LOSE_FLAG, the wait diagnostics' test -- that task's flag
