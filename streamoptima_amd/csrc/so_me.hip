@@ -2526,7 +2526,7 @@ SO_DEV uint32_t run_poll(const uint32_t* c, bool need, bool sysl, uint32_t* ws, 
     const uint32_t one = lane == 0 ? 1u : 0u;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t last = 0, susp = 0, raw = 0;   // ticks since t0 at the last poll; descheduled ticks
-    bool esc = false;
+    bool esc = false, first = true;
     for (;;) {
         if (sysl)
             raw = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2536,6 +2536,19 @@ SO_DEV uint32_t run_poll(const uint32_t* c, bool need, bool sysl, uint32_t* ws, 
             raw = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const bool ok = raw == (sysl ? w.sys_want : w.want);
         if (__builtin_amdgcn_ballot_w64(need && !ok) == 0) break;
+#if SO_RUN_ABORT_CHECK
+        // the timeout count, read once per wait and only when it has to wait: after one timeout
+        // the later waits of the run return at once (the run is already flagged wrong), so a
+        // lost flag cannot stall the launch for 50 ms per remaining tile.  (Read ahead of every
+        // first poll it put a memory round trip on every tile's path; polled in the loop it put
+        // every waiting workgroup on one word: +70 % per frame.)
+        if (first) {
+            first = false;
+            if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(ws + kRunTimeoutWord, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT)) != 0u)
+                break;
+        }
+#endif
         __builtin_amdgcn_s_sleep(1);
         const uint32_t now = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t0), gap = now - last;
         last = now;
@@ -2746,13 +2759,6 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             const int lane = opaque_tid() & 63;   // recomputed per task (hoisted, it was spilled)
             const int nx = tx + lane % 3 - 1, ny = ty + lane / 3 - 1;
             const bool need = (FPIPE || dep >= 0) && lane < 9 && nx >= 0 && nx < tiles_x && ny >= 0 && ny < ntr;
-            // the timeout count, read once per tile: after one timeout the later tiles of the
-            // run skip their waits (the run is already flagged wrong), so a lost flag cannot
-            // stall the launch for 50 ms per remaining tile.  (Polling it in the loop put
-            // every waiting workgroup on one word: +70 % per frame.)
-#if SO_RUN_ABORT_CHECK
-            if (__hip_atomic_load(ws + kRunTimeoutWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
-#endif
             const uint32_t* c = done + (size_t)(dep > 0 ? dep : 0) * ntiles + (need ? ny * tiles_x + nx : 0);
             bool rneed = false;
             if constexpr (FPIPE) {   // the previous frame's tiles arrive from the previous rank
@@ -2835,16 +2841,10 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             } else {
                 if (wave == 0) {   // every tile of this tile row finished pass 1 (tiles_x <= 64)
                     const uint32_t* c = sp.p1done + (size_t)f * ntiles + ty * tiles_x + (lane < tiles_x ? lane : 0);
-#if SO_RUN_ABORT_CHECK
-                    const bool skip =
-                        __hip_atomic_load(ws + kRunTimeoutWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-#else
-                    const bool skip = false;
-#endif
                     // 50 ms of polling; 2 s in the frame pipeline, whose pass-1 tasks may wait that
                     // long on another rank's reconstruction
                     const RunWait rw{task, f, -2, tile, MODE | (2 << 8), ep, sp.epoch, FPIPE ? 200000000ull : 5000000ull};
-                    if (!skip) run_poll(c, lane < tiles_x, false, ws, rw);
+                    run_poll(c, lane < tiles_x, false, ws, rw);
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     SO_RUN_PROF(50, __builtin_amdgcn_s_memtime() - pt0);
