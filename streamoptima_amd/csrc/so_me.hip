@@ -2809,6 +2809,16 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 if (lane == 0) s_dense = fb >= 8u ? 1 : 0;
             }
         };
+        // ptile_body's `post`: the next task's dequeue, before the tile's drain (one-GPU,
+        // frame-pipeline and stripe runs)
+#ifndef SO_DEQ_LATE   // A/B builds: dequeue at the loop top, after the done flag
+        const auto take_next = [&]() {
+            if (wave == 0) nxt_v = run_dequeue(ws);   // waits for the tile's stores too
+            nxt_taken = true;
+        };
+#else
+        const NoPre take_next{};
+#endif
         const uint8_t* ref = FPIPE ? sp.land0 + (long long)(sp.gbase + f) * sp.stride
                                    : (MODE == kRunSingle || TWOP) ? a.ref[f] : (f ? a.out[f - 1].recon : ref0);
         if constexpr (TWOP) {
@@ -2889,9 +2899,9 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             PHalo hl{};
             hl.dn = code >= 0 ? pbase + (long long)slot * sp.stride : nullptr;   // every row of the tile
             hl.dn_begin = 0;
-            ptile_body<G, true, decltype(wait_ref), true, false, VBS>(S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd,
-                                                                      qp_row, nullptr, nullptr, a.out[f], wait_ref, hl,
-                                                                      lam, nullptr, nullptr, sp.count_ops);
+            ptile_body<G, true, decltype(wait_ref), true, false, VBS, decltype(take_next)>(
+                S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd, qp_row, nullptr, nullptr, a.out[f], wait_ref, hl, lam,
+                nullptr, nullptr, sp.count_ops, take_next);
             // ptile_body ended with every wave's stores (local and remote) retired and a barrier
             if (wave == 0) {
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
@@ -2911,8 +2921,9 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 hl.dn = sp.peer_dn0 + (long long)gf * sp.stride;
                 hl.dn_begin = by1 * 16 - 16;
             }
-            ptile_body<G, true, decltype(wait_ref), true>(S, tile, a.cur[f], ref, H, W, by0, by1, qp_rd, qp_row,
-                                                          nullptr, nullptr, a.out[f], wait_ref, hl, 0.0, nullptr, nullptr, sp.count_ops);
+            ptile_body<G, true, decltype(wait_ref), true, false, false, decltype(take_next)>(
+                S, tile, a.cur[f], ref, H, W, by0, by1, qp_rd, qp_row, nullptr, nullptr, a.out[f], wait_ref, hl, 0.0,
+                nullptr, nullptr, sp.count_ops, take_next);
             // ptile_body ended with every wave's stores (local and remote) retired and a barrier
             if (wave == 0) {
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
@@ -2927,14 +2938,6 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
         } else {
 #ifdef SO_RUN_PROFILE
             const unsigned long long pt0 = __builtin_amdgcn_s_memtime();
-#endif
-#ifndef SO_DEQ_LATE   // A/B builds: dequeue at the loop top, after the done flag
-            const auto take_next = [&]() {
-                if (wave == 0) nxt_v = run_dequeue(ws);   // waits for the tile's stores too
-                nxt_taken = true;
-            };
-#else
-            const NoPre take_next{};
 #endif
             ptile_body<G, true, decltype(wait_ref), false, false, VBS, decltype(take_next)>(
                 S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd, qp_row, nullptr, nullptr, a.out[f], wait_ref, PHalo{}, lam,
