@@ -125,9 +125,10 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
  *                            predictor chain (1) instead of the speculated segments (0, default)
  *   SO_OPT_FASTME_SEGMENT    blocks per speculated segment (default 32, >= 1)
  *   SO_OPT_FASTME_WARMUP     blocks a segment's guess runs ahead of it (default 32, >= 0)
- *   SO_OPT_COUNT_SAD_OPS     the persistent runs count their searches' SAD byte operations into
- *                            workspace words 66..67 (1; default 0: the count's LDS atomics cost
- *                            ~1 % of the run, so only a measurement turns it on)
+ *   SO_OPT_COUNT_SAD_OPS     the one-GPU persistent runs (so_encode_p_run / _runs) count their
+ *                            searches' SAD byte operations into workspace words 66..67 (1; default
+ *                            0: a separate test-hook kernel instantiation runs while it is set,
+ *                            so the product kernels carry no counting code)
  * so_set_option returns SO_E_INVALID for an unknown option or a value out of range.
  */
 #define SO_OPT_RUN_2PASS_FUSED 1
@@ -135,6 +136,14 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
 #define SO_OPT_FASTME_SEGMENT 3
 #define SO_OPT_FASTME_WARMUP 4
 #define SO_OPT_COUNT_SAD_OPS 5
+/* TEST ONLY -- never set it around work whose output is used.  SO_OPT_TEST_LOSE_FLAG = k > 0:
+ * the next one-GPU run never sets the done flag of its task k - 1, so the tiles that wait on it
+ * time out (50 ms each) and record themselves, and that run's symbols are WRONG (the wait
+ * diagnostics' test, tests/test_gpu_waits.py).  It is read when a run is enqueued, so a run
+ * captured into a graph would stay broken on every replay: a one-GPU run enqueued on a
+ * capturing stream while it is set fails with SO_E_INVALID.  Both this option and
+ * SO_OPT_COUNT_SAD_OPS select a separate test-hook instantiation of the one-GPU run kernel; the
+ * product kernels carry neither hook. */
 #define SO_OPT_TEST_LOSE_FLAG 6
 int so_set_option(int option, int value);
 int so_get_option(int option);
@@ -202,6 +211,11 @@ size_t so_p_run_workspace_elems(int H, int W);
  * launch that cannot become resident would leave the others waiting on its tasks (DESIGN.md
  * section 6, "Forward progress").  SO_E_INVALID if the device query fails. */
 int so_p_run_resident_workgroups(int vbs);
+/* The same for ONE run kind: mode 0 the one-GPU run (so_encode_p_run / _runs), 1 the stripe
+ * run, 2 the frame pipeline, 3 the fused two-pass run, 4 the two-pass frame pipeline (vbs: modes
+ * 0 and 2).  so_p_run_resident_workgroups(vbs) is the smallest of these, so a claim sized by it
+ * fits whichever kernel a rank launches.  SO_E_INVALID for another mode or a failed query. */
+int so_p_run_mode_resident_workgroups(int mode, int vbs);
 int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W,
                     int bs, int sr, int qp_rd, const int32_t* qp_row, int vbs, double lam,
                     uint8_t* const* out_split,

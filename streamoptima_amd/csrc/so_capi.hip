@@ -426,6 +426,19 @@ int so_p_run_resident_workgroups(int vbs) {
     return n;
 }
 
+int so_p_run_mode_resident_workgroups(int mode, int vbs) {
+    if (mode < 0 || mode > 4 || (vbs && mode != 0 && mode != 2)) {
+        set_error("so_p_run_mode_resident_workgroups: mode %d%s", mode, vbs ? " with vbs (modes 0, 2)" : " (0..4)");
+        return SO_E_INVALID;
+    }
+    const int n = p_run_capacity(vbs ? 1 : 0, mode);
+    if (n <= 0) {
+        set_error("so_p_run_mode_resident_workgroups: device query failed");
+        return SO_E_INVALID;
+    }
+    return n;
+}
+
 int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int bs, int sr,
                     int qp_rd, const int32_t* qp_row, int vbs, double lam, uint8_t* const* out_split,
                     int16_t* const* out_mv, int16_t* const* out_qtc, int32_t* const* out_tokens,

@@ -2639,7 +2639,11 @@ SO_DEV uint32_t run_dequeue(uint32_t* ws) {
 }
 
 // VBS: VBSEnable (the block + sub-block dense search, tq16_vbs; ~128 VGPRs, 4 waves per SIMD)
-template <int NW, int MODE, bool VBS = false>
+// HOOKS: the measurement / test hooks -- the searches' SAD byte-operation count
+// (SO_OPT_COUNT_SAD_OPS) and the deliberately lost done flag (SO_OPT_TEST_LOSE_FLAG).  Only
+// kRunSingle has a HOOKS instantiation, launched only while one of those options is set, so the
+// timed kernels carry neither (count_ops folds to the constant 0 and its atomics are dead code).
+template <int NW, int MODE, bool VBS = false, bool HOOKS = false>
 __global__ void __launch_bounds__(NW * 64)
 __attribute__((amdgpu_waves_per_eu(VBS ? 4 : (NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE))))
 p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, int H, int W,
@@ -2654,6 +2658,8 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     constexpr bool STRIPE = MODE == kRunStripe, FPIPE = MODE == kRunFPipe || MODE == kRunFPipe2P;
     constexpr bool TWOP = MODE == kRunTwoPass || MODE == kRunFPipe2P;
     static_assert(!(VBS && (TWOP || MODE == kRunStripe)), "VBS runs: one GPU and the frame pipeline");
+    static_assert(!HOOKS || MODE == kRunSingle, "test hooks: the one-GPU run only");
+    const int count_ops = HOOKS ? sp.count_ops : 0;   // a compile-time 0 without HOOKS
     const int by0 = STRIPE ? sp.by0 : 0, by1 = STRIPE ? sp.by1 : H / 16;
     const int tiles_x = (nbx + G::TBX - 1) / G::TBX, ntr = (by1 - by0 + G::TBY - 1) / G::TBY;
     const int ntiles = tiles_x * ntr;
@@ -2832,7 +2838,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 using P = PTileGeo<G>;
                 uint32_t* const b4w = reinterpret_cast<uint32_t*>(S.un);
                 const Sea2Lds L{S.win, b4w, S.curt, S.a4, reinterpret_cast<uint16_t*>(b4w + P::B4), S.lcount, S.keys,
-                                S.st, sp.count_ops};
+                                S.st, count_ops};
                 RefSet refs{};
                 refs.p[0] = ref;
                 sea2_tile<G>(L, tile, a.cur[f], refs, 1, H, W, 0, by1, 0, wait_ref);   // ends with a barrier
@@ -2901,7 +2907,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             hl.dn_begin = 0;
             ptile_body<G, true, decltype(wait_ref), true, false, VBS, decltype(take_next)>(
                 S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd, qp_row, nullptr, nullptr, a.out[f], wait_ref, hl, lam,
-                nullptr, nullptr, sp.count_ops, take_next);
+                nullptr, nullptr, count_ops, take_next);
             // ptile_body ended with every wave's stores (local and remote) retired and a barrier
             if (wave == 0) {
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
@@ -2923,7 +2929,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             }
             ptile_body<G, true, decltype(wait_ref), true, false, false, decltype(take_next)>(
                 S, tile, a.cur[f], ref, H, W, by0, by1, qp_rd, qp_row, nullptr, nullptr, a.out[f], wait_ref, hl, 0.0,
-                nullptr, nullptr, sp.count_ops, take_next);
+                nullptr, nullptr, count_ops, take_next);
             // ptile_body ended with every wave's stores (local and remote) retired and a barrier
             if (wave == 0) {
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
@@ -2941,18 +2947,18 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 #endif
             ptile_body<G, true, decltype(wait_ref), false, false, VBS, decltype(take_next)>(
                 S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd, qp_row, nullptr, nullptr, a.out[f], wait_ref, PHalo{}, lam,
-                &s_dense, reinterpret_cast<int32_t*>(tilefb) + (size_t)f * ntiles + tile, sp.count_ops, take_next);
+                &s_dense, reinterpret_cast<int32_t*>(tilefb) + (size_t)f * ntiles + tile, count_ops, take_next);
             SO_RUN_PROF(52, __builtin_amdgcn_s_memtime() - pt0);
             // ptile_body ended with every wave's write-through stores retired and a barrier
             // (sp.lose_task: SO_OPT_TEST_LOSE_FLAG, the wait diagnostics' test -- that task's flag
             // is never set, so its dependants time out and record themselves)
-            if (wave == 0 && task + 1 != sp.lose_task)
+            if (wave == 0 && !(HOOKS && task + 1 == sp.lose_task))
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
         }
         if (pass == 1 && tid == 0) {   // this tile's dense-searched blocks and SAD byte operations
             s_fbsum += S.st[0];
-            s_ops += S.st[2];
+            if constexpr (HOOKS) s_ops += S.st[2];
         }
 #ifdef SO_STAMPS
         if (tid == 0 && rec) {
@@ -3032,11 +3038,37 @@ static int run_shape(const void* kernel, int* ncu, int* per_cu) {
 
 // Resident workgroups of the persistent run kernel on the current device (so_p_run_resident_
 // workgroups): the grid a launch uses when nothing caps it.
-int p_run_capacity(int vbs) {
-    int ncu = 0, per_cu = 0;
-    const int rc = vbs ? run_shape(reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, kRunSingle, true>), &ncu, &per_cu)
-                       : run_shape(reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, kRunSingle, false>), &ncu, &per_cu);
-    return rc != SO_OK ? -rc : ncu * per_cu;
+// mode < 0: the smallest over every instantiation a run of that VBS setting may launch (the
+// one-GPU run with and without test hooks, the stripe, frame-pipeline and two-pass modes): the
+// ranks sharing one device size their claims by it, whichever kernel each of them launches.
+int p_run_capacity(int vbs, int mode) {
+    constexpr int NW = SO_PTILE_NW;
+    const void* ks[8];
+    int n = 0;
+    const auto add = [&](int m, const void* k) {
+        if (mode < 0 || mode == m) ks[n++] = k;
+    };
+    if (vbs) {
+        add(kRunSingle, reinterpret_cast<const void*>(p_run_kernel<NW, kRunSingle, true>));
+        add(kRunSingle, reinterpret_cast<const void*>(p_run_kernel<NW, kRunSingle, true, true>));
+        add(kRunFPipe, reinterpret_cast<const void*>(p_run_kernel<NW, kRunFPipe, true>));
+    } else {
+        add(kRunSingle, reinterpret_cast<const void*>(p_run_kernel<NW, kRunSingle, false>));
+        add(kRunSingle, reinterpret_cast<const void*>(p_run_kernel<NW, kRunSingle, false, true>));
+        add(kRunStripe, reinterpret_cast<const void*>(p_run_kernel<NW, kRunStripe, false>));
+        add(kRunFPipe, reinterpret_cast<const void*>(p_run_kernel<NW, kRunFPipe, false>));
+        add(kRunTwoPass, reinterpret_cast<const void*>(p_run_kernel<NW, kRunTwoPass, false>));
+        add(kRunFPipe2P, reinterpret_cast<const void*>(p_run_kernel<NW, kRunFPipe2P, false>));
+    }
+    if (n == 0) return -SO_E_INVALID;
+    int best = 0;
+    for (int i = 0; i < n; ++i) {
+        int ncu = 0, per_cu = 0;
+        const int rc = run_shape(ks[i], &ncu, &per_cu);
+        if (rc != SO_OK) return -rc;
+        if (i == 0 || ncu * per_cu < best) best = ncu * per_cu;
+    }
+    return best;
 }
 
 // refs / deps (may be null: one run, frame g predicting from g - 1 and frame 0 from ref0): frame g
@@ -3048,9 +3080,21 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
                           int max_wg, hipStream_t st, const uint8_t* const* refs = nullptr,
                           const int* deps = nullptr, int conc = 1, double lam = 0.0) {
     using G = Sea2GeoT<SO_PTILE_NW>;
+    // the test-hook instantiation (one GPU only) while SO_OPT_COUNT_SAD_OPS / _TEST_LOSE_FLAG is set
+    const bool hooks = MODE == kRunSingle && (option(SO_OPT_COUNT_SAD_OPS) != 0 || option(SO_OPT_TEST_LOSE_FLAG) != 0);
+    const void* const kfn = hooks ? reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, MODE == kRunSingle>)
+                                  : reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, false>);
+    if (hooks && option(SO_OPT_TEST_LOSE_FLAG) != 0) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+            set_error("p_run: SO_OPT_TEST_LOSE_FLAG is set while the stream is capturing (the graph would lose a "
+                      "flag on every replay)");
+            return SO_E_INVALID;
+        }
+    }
     int ncu = 0, per_cu = 0;
     {
-        const int rc = run_shape(reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS>), &ncu, &per_cu);
+        const int rc = run_shape(kfn, &ncu, &per_cu);
         if (rc != SO_OK) return rc;
     }
     const int nbx = W / 16;
@@ -3105,8 +3149,14 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
 #endif
             sp.p2lag = lag < 1 ? 1 : (lag > ntr ? ntr : lag);
         }
-        hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, MODE, VBS>), dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), 0, st, a, n,
-                           f0 ? outs[f0 - 1].recon : ref0, H, W, qp_rd, qp_row, ws, (int)(f0 * ntiles), sp, lam);
+        if (hooks)
+            hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, MODE, VBS, MODE == kRunSingle>), dim3((unsigned)grid),
+                               dim3(SO_PTILE_NW * 64), 0, st, a, n, f0 ? outs[f0 - 1].recon : ref0, H, W, qp_rd, qp_row, ws,
+                               (int)(f0 * ntiles), sp, lam);
+        else
+            hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, MODE, VBS, false>), dim3((unsigned)grid), dim3(SO_PTILE_NW * 64),
+                               0, st, a, n, f0 ? outs[f0 - 1].recon : ref0, H, W, qp_rd, qp_row, ws, (int)(f0 * ntiles),
+                               sp, lam);
         const int rc = check_launch("p_run_kernel");
         if (rc != SO_OK) return rc;
     }

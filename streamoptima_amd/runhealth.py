@@ -3,8 +3,9 @@ SO_P_RUN_TIMEOUT_WORD .. SO_P_RUN_DIAG_WORD; DESIGN.md section 4, "Waits").
 
 Every consumer of a run workspace (Engine, the stripe and frame-pipeline ranks) reads the
 words 32..127 in ONE device-to-host copy, raises with the decoded record of the first wait
-that timed out, and keeps the non-fatal counts (stale reads repaired by an atomic read,
-descheduled poll intervals) for the bench line.
+that timed out, raises as well when a wait found its flag only through an atomic read (a
+stale read: the consumer protocol failed, even though that wait completed), and keeps the
+non-fatal count of descheduled poll intervals for the bench line.
 """
 from __future__ import annotations
 
@@ -108,6 +109,13 @@ def check(ws: torch.Tensor | None, log: HealthLog | None, what: str) -> None:
     if h["timeouts"]:
         raise RuntimeError(f"{what}: {h['timeouts']} dependency wait(s) timed out; the symbols are unreliable. "
                            f"First: {describe(h['record'])}")
+    if h["stale_reads"]:
+        # the consumer protocol (relaxed polls + one agent acquire) kept missing a flag that was
+        # set: the wait completed through atomic reads, but the hand-off rule the run's
+        # correctness argument rests on did not hold, so the run is not trusted either
+        raise RuntimeError(f"{what}: {h['stale_reads']} dependency wait(s) read a done flag only through an atomic "
+                           "read after 1 ms of relaxed polls (a stale cached copy): the hand-off protocol failed, "
+                           "the run is not trusted")
 
 
 def timed_out(ws: torch.Tensor | None) -> bool:

@@ -366,3 +366,18 @@ def test_in_process_ranks_must_fit_one_gpu(gpu):
         FramePipeRank(engines[0], 3, 0, 6, max_wg=1)
     for r in ranks:
         r.close()
+
+
+def test_claim_capacity_fits_every_run_kind(gpu):
+    """The capacity ranks size their claims by (so_p_run_resident_workgroups) is the smallest of
+    every run kernel they may launch: the stripe, frame-pipeline and two-pass kernels carry extra
+    hand-off code and may fit fewer workgroups per CU than the one-GPU run."""
+    from streamoptima_amd import _lib
+    lib = _lib.load()
+    for vbs, modes in ((0, (0, 1, 2, 3, 4)), (1, (0, 2))):
+        cap = lib.so_p_run_resident_workgroups(vbs)
+        per = {m: lib.so_p_run_mode_resident_workgroups(m, vbs) for m in modes}
+        assert cap > 0 and all(v > 0 for v in per.values()), (cap, per)
+        assert cap == min(per.values()), (vbs, cap, per)
+    assert lib.so_p_run_mode_resident_workgroups(1, 1) < 0      # no VBS stripe run
+    assert lib.so_p_run_mode_resident_workgroups(7, 0) < 0

@@ -43,11 +43,15 @@ def test_check_raises_with_the_record_and_clears():
     log = runhealth.HealthLog()
     runhealth.check(ws, log, "p_run_kernel")            # nothing: no raise, nothing logged
     assert log.as_dict()["timeouts"] == 0
-    ws[runhealth.STALE_WORD] = 2
     ws[runhealth.GAP_WORD] = 3
-    runhealth.check(ws, log, "p_run_kernel")            # non-fatal counts only
+    runhealth.check(ws, log, "p_run_kernel")            # a non-fatal count only
+    assert (log.stale_reads, log.descheduled_polls) == (0, 3)
+    assert int(ws[runhealth.GAP_WORD]) == 0
+    ws[runhealth.STALE_WORD] = 2                        # a stale read: counted, cleared, and fatal
+    with pytest.raises(RuntimeError, match=r"2 dependency wait\(s\) read a done flag only through an atomic read"):
+        runhealth.check(ws, log, "p_run_kernel")
     assert (log.stale_reads, log.descheduled_polls) == (2, 3)
-    assert int(ws[runhealth.STALE_WORD]) == 0 and int(ws[runhealth.GAP_WORD]) == 0
+    assert int(ws[runhealth.STALE_WORD]) == 0
     ws[runhealth.TIMEOUT_WORD] = 4
     ws[runhealth.CLAIM_WORD] = 4
     words = _record_words()
