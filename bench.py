@@ -574,10 +574,10 @@ def pcie_inclusive(codec, cfg, frames_dev, reps: int = 6) -> dict:
     dn = torch.empty(host.numel(), dtype=torch.uint8).pin_memory()
     flat = frames_dev.view(-1)[:host.numel()]
 
-    def h2d():
+    def up_only():
         frames_dev.copy_(host, non_blocking=True)
 
-    def d2h():
+    def down_only():
         dn.copy_(flat, non_blocking=True)
 
     def rate(fn):
@@ -589,7 +589,7 @@ def pcie_inclusive(codec, cfg, frames_dev, reps: int = 6) -> dict:
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         return host.numel() / min(ts[1:]) / 1e9
-    h2d_gbs, d2h_gbs = rate(h2d), rate(d2h)
+    h2d_gbs, d2h_gbs = rate(up_only), rate(down_only)
     link = {"h2d_gbs": round(h2d_gbs, 2), "d2h_gbs": round(d2h_gbs, 2), "bytes": int(host.numel()),
             "method": "one pinned copy of the GOP's planes each way alone (copy engine, no kernel), best of "
                       f"{reps} after one warm-up"}

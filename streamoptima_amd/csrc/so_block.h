@@ -350,6 +350,19 @@ SO_DEV void dequant_row_i(const int* q, int row, int qp, double* dq) {
     for (int c = 0; c < N; ++c) dq[c] = __builtin_amdgcn_ldexp((double)q[c], q_exp_fast<N>(row, c, qp));
 }
 
+// quantize_TC on integer TC (Encoder.py:787-789): np.round(TC / 2^k) half to even, branch-free in
+// int32 (2-cycle VALU).  With TC = q0 2^k + r (floor, 0 <= r < 2^k), h = 2^(k-1) and b = q0 & 1,
+// floor((TC + h - 1 + b) / 2^k) = q0 + [r > h or (r == h and b)] for k >= 1; k = 0 is TC.
+SO_DEV int quant_rne_i(int tc, int k) {
+    const int bias = k > 0 ? ((1 << k) >> 1) - 1 + ((tc >> k) & 1) : 0;
+    return (tc + bias) >> k;
+}
+template <int N>
+SO_DEV void quant_row_int(const int* tc, int row, int qp, int* q) {
+#pragma unroll
+    for (int c = 0; c < N; ++c) q[c] = quant_rne_i(tc[c], q_exp_fast<N>(row, c, qp));
+}
+
 // QTC * Q as int32 (xform2d_rows' integer inverse path): |q| 2^k <= |TC| + 2^(k-1)
 template <int N>
 SO_DEV void dequant_row_int(const int* q, int row, int qp, int* dq) {
@@ -420,6 +433,38 @@ SO_DEV int sub_tokens(uint8_t* flags, int l, const int (&q)[2][8]) {
     }
     wave_sync();
     return group_sum<16>(nnz + tr) + 4;
+}
+
+// sub_tokens in registers: the same count from the sub-blocks' row masks, no LDS and no barrier
+// (the VBS run's LDS budget).  Lane l holds rows r0 = l & 3 and r0 + 4 of sub-block l >> 2; the
+// quad of lanes of a sub-block gathers all 8 row masks (byte i of lo / hi = row i / i + 4), then
+// each lane counts the scan-order transitions that start in its two rows (block_tokens' three
+// kinds of consecutive pairs, for N = 8):
+//   inside a diagonal  (i, j) -> (i+1, j-1), j >= 1, i <= 6: bits 1..7 of M_i vs M_{i+1} << 1;
+//   diagonal k <= 6 ends at (k, 0), the next starts at (0, k+1): M_k bit 0 vs M_0 bit k+1;
+//   diagonal k >= 7 ends at (7, k-7), the next starts at (m, 7), m = k-6 in 1..7: M_7 bit m-1
+//   vs M_m bit 7.
+SO_DEV int sub_tokens_reg(int l, const int (&q)[2][8]) {
+    const int r0 = l & 3;
+    uint32_t m0 = 0, m1 = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        m0 |= (q[0][c] != 0 ? 1u : 0u) << c;
+        m1 |= (q[1][c] != 0 ? 1u : 0u) << c;
+    }
+    uint32_t lo = m0 << (8 * r0), hi = m1 << (8 * r0);
+    lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0xB1, 0xF, 0xF, false);
+    lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x4E, 0xF, 0xF, false);
+    const uint32_t n0 = r0 < 3 ? (lo >> (8 * r0 + 8)) & 255u : hi & 255u;    // M_{r0+1}
+    const uint32_t n1 = r0 < 3 ? (hi >> (8 * r0 + 8)) & 255u : 0u;           // M_{r0+5}
+    const uint32_t M0 = lo & 255u, M7 = hi >> 24;
+    int tr = __builtin_popcount((m0 ^ (n0 << 1)) & 0xFEu) + (int)((m0 & 1u) ^ ((M0 >> (r0 + 1)) & 1u)) +
+             (int)(((M7 >> (r0 + 3)) & 1u) ^ (m1 >> 7));
+    if (r0 < 3) tr += __builtin_popcount((m1 ^ (n1 << 1)) & 0xFEu) + (int)((m1 & 1u) ^ ((M0 >> (r0 + 5)) & 1u));
+    if (r0 >= 1) tr += (int)(((M7 >> (r0 - 1)) & 1u) ^ (m0 >> 7));
+    return group_sum<16>(__builtin_popcount(m0) + __builtin_popcount(m1) + tr) + 4;
 }
 
 // calculate_RD_cost (Encoder.py:1133-1158): lam * bits + mae, two roundings (no FMA:

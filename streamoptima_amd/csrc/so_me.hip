@@ -163,20 +163,27 @@ SO_DEV void acc_fence_n(uint32_t (&a)[N]) {
 // `ex16`: drop t = 16 of the lower half (the duplicate dy = 0 row) -- the FME row phase
 // a = 1 maps it to dy = +1 half-pel, which the upper half's t = 0 already covers, and
 // keeping it would break the lane's |dy| order (|-1| == |+1| at t = 15 and t = 16).
+// HALF: the SAD is the whole accumulator (0), its low 16 bits (1) or its high 16 bits (2) --
+// the VBS dense search keeps a lane's left / right quadrant SADs packed in one register.
+template <int HALF = 0>
+SO_DEV uint32_t half16(uint32_t v) {
+    return HALF == 0 ? v : HALF == 1 ? (v & 0xFFFFu) : (v >> 16);
+}
+template <int HALF = 0>
 SO_DEV uint32_t lane_best17(const uint32_t (&a)[17], uint32_t X, int hh, int dlo, int dhi, bool edge,
                             bool ex16 = false) {
     uint32_t best = 0xFFFFFFFFu;
     if (!edge) {
 #pragma unroll
         for (int t = 0; t < 17; ++t) {
-            const uint32_t k = ((a[t] << 5) | (uint32_t)t) ^ X;
+            const uint32_t k = ((half16<HALF>(a[t]) << 5) | (uint32_t)t) ^ X;
             best = k < best ? k : best;
         }
     } else {
 #pragma unroll
         for (int t = 0; t < 17; ++t) {
             const int di = 16 * hh + t;
-            uint32_t k = ((a[t] << 5) | (uint32_t)t) ^ X;
+            uint32_t k = ((half16<HALF>(a[t]) << 5) | (uint32_t)t) ^ X;
             k = (di < dlo || di > dhi || (t == 16 && ex16 && hh == 0)) ? 0xFFFFFFFFu : k;
             best = k < best ? k : best;
         }
@@ -257,7 +264,10 @@ SO_DEV void wave_dense_block(const uint32_t* win, unsigned long long* keys, int 
     // phase-2 lane: dx = +16 (column bxl*BS + 32, copy 0), dy index = lane (< 33)
     const int d2 = lane < 33 ? lane : 32;
     const int q2 = (byl * BS + d2) * RPD + ((bxl * BS + 32) >> 2);
-    uint32_t accL[NT], accR[NT], S[NT];
+    // VBS (SUB): acc[t] = left-quadrant SAD | right-quadrant SAD << 16 (v_sad_u8 / v_sad_hi_u8;
+    // an 8 x 8 SAD is < 2^14) and S[t] the packed sum over both passes (< 2^15 per half): 34
+    // accumulators instead of 51 live through the scan
+    uint32_t accL[NT], S[NT];
     uint32_t a2L[NPASS], a2R[NPASS];
 #pragma unroll
     for (int t = 0; t < NT; ++t) S[t] = 0;
@@ -274,7 +284,7 @@ SO_DEV void wave_dense_block(const uint32_t* win, unsigned long long* keys, int 
         load_cur_sgpr<HALF, NDW>(cur, W, x, ycur, cr);
         if (SUB || pass == 0) {   // without VBS accL accumulates the whole block
 #pragma unroll
-            for (int t = 0; t < NT; ++t) { accL[t] = 0; accR[t] = 0; }
+            for (int t = 0; t < NT; ++t) accL[t] = 0;
         }
         // phase 1: rows pass*8 + jj of the lane's 24-row strip
         // volatile: the four dwords stay four ds_read_b32 -- merged into one b128 they
@@ -313,7 +323,7 @@ SO_DEV void wave_dense_block(const uint32_t* win, unsigned long long* keys, int 
                 if (rr >= 0 && rr < HALF) {
 #pragma unroll
                     for (int k = 0; k < NDW; ++k) {
-                        if (SUB && k >= NDW / 2) accR[t] = __builtin_amdgcn_sad_u8(cr[rr][k], wc[k], accR[t]);
+                        if (SUB && k >= NDW / 2) accL[t] = __builtin_amdgcn_sad_hi_u8(cr[rr][k], wc[k], accL[t]);
                         else accL[t] = __builtin_amdgcn_sad_u8(cr[rr][k], wc[k], accL[t]);
                     }
                 }
@@ -321,7 +331,6 @@ SO_DEV void wave_dense_block(const uint32_t* win, unsigned long long* keys, int 
 #pragma unroll
             for (int k = 0; k < NDW; ++k) wc[k] = wn[k];
             acc_fence_n<NT>(accL);
-            if constexpr (SUB) acc_fence_n<NT>(accR);
         }
         // phase 2: the dx = +16 candidate of dy index d2, rows pass*8 .. +8
         uint32_t l2 = 0, r2 = 0;
@@ -352,17 +361,20 @@ SO_DEV void wave_dense_block(const uint32_t* win, unsigned long long* keys, int 
                 dhi = H - 8 - ys + SR - 1; dhi = dhi > 32 ? 32 : dhi;
             }
             const bool edge = FME || dlo > 0 || dhi < 32;
-            subb[2 * pass] = lane_best17(accL, X, hh, dlo, dhi, edge, FME && ph.a);
-            subb[2 * pass + 1] = lane_best17(accR, X, hh, dlo, dhi, edge, FME && ph.a);
+            subb[2 * pass] = lane_best17<1>(accL, X, hh, dlo, dhi, edge, FME && ph.a);
+            subb[2 * pass + 1] = lane_best17<2>(accL, X, hh, dlo, dhi, edge, FME && ph.a);
             sub2[2 * pass] = l2;
             sub2[2 * pass + 1] = r2;
 #pragma unroll
-            for (int t = 0; t < NT; ++t) S[t] += accL[t] + accR[t];
+            for (int t = 0; t < NT; ++t) S[t] += accL[t];
         }
     }
     if constexpr (!SUB) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) S[t] = accL[t];
+    } else {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) S[t] = (S[t] & 0xFFFFu) + (S[t] >> 16);
     }
     // block keys: phase 1 (lane's 17 candidates) and phase 2 (dx = +16)
     int dlo, dhi;
@@ -673,6 +685,47 @@ extern "C" int so_debug_set_run_stamps(void* p) {
 #define SO_SEA_STAMP(i, v) do { } while (0)
 #endif
 
+// ISA census builds (-DSO_MARKS, tools/isa_census.py): a comment line in the assembly at each
+// phase boundary of the persistent loop; nothing is emitted otherwise.
+// -DSO_MARKS_COUNT (tools/valu_census.py): every marker a wave passes adds 1 to its LDS counter
+// (the lowest active lane's ds_add_u32; no VALU beyond the two operand moves), and each
+// workgroup adds its counters to g_mark_counts at exit: executions per phase per launch, which
+// weight the static census into a dynamic VALU table.
+#define SO_MARK_NAMES(X) X(loop_top) X(stage_cur) X(stage_cur_int) X(stage_cur_edge) X(cur_sums) X(wait) \
+    X(poll_iter) X(stage_win) X(stage_win_int) X(stage_win_edge) X(dense_tile) X(dense_tile_block) X(byte_sums) \
+    X(block_top) X(bound) X(umin) X(ballots) X(dense_fallback) X(survivors) X(sur_one) X(sur_le4) X(sur_pass) \
+    X(search_end) X(decode_keys) X(tq_residual) X(tq_fwd) X(tq_quant) X(tq_tokens) X(tq_qtc_store) X(tq_inv) \
+    X(tq_recon) X(tq_sse_records) X(post) X(done_flag) X(task_end)
+#define SO_MARK_ENUM(n) kMark_##n,
+enum SoMarkId { SO_MARK_NAMES(SO_MARK_ENUM) kMarkCount };
+#undef SO_MARK_ENUM
+#if defined(SO_MARKS_COUNT)
+__device__ unsigned* g_mark_counts = nullptr;
+__shared__ unsigned s_mark_cnt[64];
+extern "C" int so_debug_set_mark_counts(void* p) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_mark_counts), &p, sizeof(p));
+}
+SO_DEV void so_mark_hit(int id) {
+    uint64_t sv, m;
+    uint32_t f;
+    asm volatile(   // exec = the lowest active lane (none: s_ff1 gives -1, bit 63 & 0 = 0)
+        "s_mov_b64 %0, exec\n\t"
+        "s_ff1_i32_b64 %2, exec\n\t"
+        "s_lshl_b64 %1, 1, %2\n\t"
+        "s_and_b64 exec, exec, %1\n\t"
+        "ds_add_u32 %3, %4\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(sv), "=&s"(m), "=&s"(f)
+        : "v"((uint32_t)(uintptr_t)&s_mark_cnt[id]), "v"(1u)
+        : "memory", "scc");
+}
+#define SO_MARK(name) so_mark_hit(kMark_##name)
+#elif defined(SO_MARKS)
+#define SO_MARK(name) asm volatile(";SO_MARK " #name)
+#else
+#define SO_MARK(name) do { } while (0)
+#endif
+
 // threadIdx.x behind an optimisation barrier: inside p_run_kernel's persistent loop the
 // tid-derived addresses are then recomputed per task instead of being hoisted out of the
 // loop and held in (spilled) registers across it.
@@ -706,6 +759,19 @@ struct NoPre {
 // `pre` runs (on every wave) after the current tile is staged and before the first
 // reference's window is read: p_run_kernel waits there for the reference's tiles, so the
 // current-tile staging overlaps that wait.
+// Waves per SIMD the VBS run kernel is compiled for: 6 (three 8-wave workgroups per CU: 80
+// VGPRs, 53.2 KB of LDS) -- 4K VBS P-frame 120.4 vs 136.3 us at 4 waves / SIMD (128 VGPRs),
+// VALU busy 0.868 vs 0.735, 1.03x the VALU instructions (profiles/r05/vbs_ab4.log, pmc_vbs4)
+#ifndef SO_VBS_WPE
+#define SO_VBS_WPE 6
+#endif
+// SO_VBS_LEAN: the VBS search / transforms hold fewer values in VGPRs (block bounds recomputed
+// where used, current rows re-read per survivor pass, levels requantised from the coefficients)
+// at the price of ~3 % more VALU -- what the 80-VGPR (6 waves / SIMD) build needs; at 128 VGPRs
+// (4 waves / SIMD) the plain forms are faster
+#ifndef SO_VBS_LEAN
+#define SO_VBS_LEAN (SO_VBS_WPE >= 6)
+#endif
 // ---- VBSEnable: exact SEA for a block and its four 8x8 sub-blocks (sea_vbs_block) ----------
 // The block search of find_best_match plus the sub-block searches of inter_prediction
 // (Encoder.py:512-544: find_best_match of each 8x8 sub-block over its own +-16 window), for a
@@ -730,11 +796,15 @@ SO_DEV void vbs_eval_list(const Sea2Lds& L, const uint16_t* list, uint32_t n, in
     constexpr int RP = G::RP, CPD = G::CPD;
     const int sidx = lane >> 2, q = lane & 3;
     const int crow0 = byl * 16 * CPD + bxl * 4;
+    // SO_VBS_LEAN: the current rows are re-read from LDS per pass (a list is mostly one pass of
+    // 16): held across the loop they take 16 VGPRs while the 34 packed sub-bounds are live
     uint32_t cr[4][4];
+    if constexpr (!SO_VBS_LEAN) {
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr)
+        for (int rr = 0; rr < 4; ++rr)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) cr[rr][k] = L.curt[crow0 + (4 * q + rr) * CPD + k];
+            for (int k = 0; k < 4; ++k) cr[rr][k] = L.curt[crow0 + (4 * q + rr) * CPD + k];
+    }
 #pragma unroll 1
     for (uint32_t s0 = 0; s0 < n; s0 += 16) {
         const bool act = s0 + (uint32_t)sidx < n;
@@ -748,11 +818,14 @@ SO_DEV void vbs_eval_list(const Sea2Lds& L, const uint16_t* list, uint32_t n, in
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
             lds_vu32p p = (lds_vu32p)(L.win + wo + rr * RP);
+            lds_vu32p c = (lds_vu32p)(L.curt + crow0 + (4 * q + rr) * CPD);
             const uint32_t q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4];
-            sl = __builtin_amdgcn_sad_u8(cr[rr][0], __builtin_amdgcn_alignbyte(q1, q0, sh), sl);
-            sl = __builtin_amdgcn_sad_u8(cr[rr][1], __builtin_amdgcn_alignbyte(q2, q1, sh), sl);
-            srr = __builtin_amdgcn_sad_u8(cr[rr][2], __builtin_amdgcn_alignbyte(q3, q2, sh), srr);
-            srr = __builtin_amdgcn_sad_u8(cr[rr][3], __builtin_amdgcn_alignbyte(q4, q3, sh), srr);
+            const uint32_t c0 = SO_VBS_LEAN ? c[0] : cr[rr][0], c1 = SO_VBS_LEAN ? c[1] : cr[rr][1];
+            const uint32_t c2 = SO_VBS_LEAN ? c[2] : cr[rr][2], c3 = SO_VBS_LEAN ? c[3] : cr[rr][3];
+            sl = __builtin_amdgcn_sad_u8(c0, __builtin_amdgcn_alignbyte(q1, q0, sh), sl);
+            sl = __builtin_amdgcn_sad_u8(c1, __builtin_amdgcn_alignbyte(q2, q1, sh), sl);
+            srr = __builtin_amdgcn_sad_u8(c2, __builtin_amdgcn_alignbyte(q3, q2, sh), srr);
+            srr = __builtin_amdgcn_sad_u8(c3, __builtin_amdgcn_alignbyte(q4, q3, sh), srr);
         }
         // quad lanes q = 0, 1 hold rows 0-7 (top sub-blocks), 2, 3 rows 8-15: pair them up
         uint32_t v = sl | (srr << 16);
@@ -834,17 +907,24 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
             acc = __builtin_amdgcn_sad_hi_u8(AR[j], qv & 0xFFFF0000u, __builtin_amdgcn_sad_u8(AL[j], qv & 0xFFFFu, acc));
         }
     }
-    // block bound keys (LBq << 16) | t: the four sub-block bounds summed
-    uint32_t lb[NT];
+    // block bounds LBq(t): the four sub-block bounds summed (SO_VBS_LEAN: recomputed where used,
+    // the list-A test, instead of held in 17 more VGPRs through the lists)
+    const auto blb0 = [&](int t) { return __builtin_amdgcn_sad_u16(T[t], 0u, __builtin_amdgcn_sad_u16(Bt[t], 0u, 0u)); };
+    uint32_t lbs[SO_VBS_LEAN ? 1 : NT];
+    if constexpr (!SO_VBS_LEAN) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
-        lb[t] = (__builtin_amdgcn_sad_u16(T[t], 0u, __builtin_amdgcn_sad_u16(Bt[t], 0u, 0u)) << 16) | (uint32_t)t;
+        for (int t = 0; t < NT; ++t) lbs[t] = blb0(t);
+    }
+    const auto blb = [&](int t) { return SO_VBS_LEAN ? blb0(t) : lbs[SO_VBS_LEAN ? 0 : t]; };
     const uint32_t lb2 = __builtin_amdgcn_sad_u16(l2T, 0u, __builtin_amdgcn_sad_u16(l2B, 0u, 0u));
     const bool ok2 = lane < 33;
     // ---- 2. U and the block survivors (A) -------------------------------------------------------
-    uint32_t kt = lb[0];
+    uint32_t kt = 0xFFFFFFFFu;
 #pragma unroll
-    for (int t = 1; t < NT; ++t) kt = lb[t] < kt ? lb[t] : kt;
+    for (int t = 0; t < NT; ++t) {
+        const uint32_t k = (blb(t) << 16) | (uint32_t)t;
+        kt = k < kt ? k : kt;
+    }
     uint32_t kl = ((kt >> 16) << 11) | (uint32_t)(xi * 33 + 16 * hh + (kt & 31));
     {
         const uint32_t k2 = (lb2 << 11) | (uint32_t)(32 * 33 + d2);
@@ -862,14 +942,16 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
         U = wave_sum_u32(__builtin_amdgcn_sad_u8(L.curt[crow0 + row * CPD + kk], w, 0u));
     }
     const uint32_t qU = (U + 240) >> 4;
-    int thr = (int)((qU << 16) | 0xFFFFu);
-    asm volatile("" : "+v"(thr));
+    // list-A membership of the lane's 17 candidates as a bit mask (the list-B test reads it)
+    uint32_t amask = 0;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) amask |= (blb(t) <= qU ? 1u : 0u) << t;
     uint16_t* const mylist = L.list + wave * G::CAPL;
     const int cbase = xi * 33 + 16 * hh;
     uint32_t nA = 0;
 #pragma unroll
     for (int t = 0; t <= NT; ++t) {
-        const bool pass = t < NT ? (int)lb[t] <= thr : (ok2 && lb2 <= qU);
+        const bool pass = t < NT ? ((amask >> t) & 1u) != 0u : (ok2 && lb2 <= qU);
         const uint64_t bal = __builtin_amdgcn_ballot_w64(pass);
         if (bal) {
             const uint32_t pos = nA + lane_prefix(bal);
@@ -906,7 +988,7 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
     uint32_t nB = 0;
 #pragma unroll
     for (int t = 0; t <= NT; ++t) {
-        const bool pass = t < NT ? (any_sub(T[t], Bt[t]) && !((int)lb[t] <= thr))
+        const bool pass = t < NT ? (any_sub(T[t], Bt[t]) && ((amask >> t) & 1u) == 0u)
                                  : (ok2 && any_sub(l2T, l2B) && !(lb2 <= qU));
         const uint64_t bal = __builtin_amdgcn_ballot_w64(pass);
         if (bal) {
@@ -989,6 +1071,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
     SO_SEA_STAMP(1, __builtin_amdgcn_s_memtime());
 #endif
 
+    SO_MARK(stage_cur);
     for (int i = tid; i < G::NBLK * (VBS ? 5 : 1); i += G::NTHREADS) keys[i] = kNoKey;
     // interior window (uniform): thread = (row, column phase) with immediate per-dword offsets
     constexpr int WTPR = G::NTHREADS / G::WR, WNPT = (RP + WTPR - 1) / WTPR;
@@ -1000,6 +1083,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
         // per-dword offsets are immediates, so staging costs a few VALU per thread
         constexpr int TPR = G::NTHREADS / G::TPY, NPT = (CP / 4) / TPR;   // threads per row, dwords per thread
         static_assert(G::NTHREADS % G::TPY == 0 && (CP / 4) % TPR == 0, "current-tile staging");
+        SO_MARK(stage_cur_int);
         const int rr = tid / TPR, c0 = tid - rr * TPR;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(cur + (size_t)(y0 + rr) * W + x0) + c0;
         uint32_t v[NPT];
@@ -1008,6 +1092,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
 #pragma unroll
         for (int k = 0; k < NPT; ++k) curt[rr * G::CPD + c0 + k * TPR] = v[k];
     } else {   // current tile (zero outside the frame / stripe)
+        SO_MARK(stage_cur_edge);
         constexpr int N = G::TPY * CP / 4, IT = (N + G::NTHREADS - 1) / G::NTHREADS;
         uint32_t v[IT];
 #pragma unroll
@@ -1026,6 +1111,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             }
     }
     __syncthreads();
+    SO_MARK(cur_sums);
     for (int i = tid; i < G::NBLK * 16; i += G::NTHREADS) {   // (block, j, ii) -> byte ii of a4[blk*4 + j]
         const int blk = i >> 4, j = (i >> 2) & 3, ii = i & 3;
         const int rr = (blk / TBX) * 16 + 4 * j, m = (blk % TBX) * 4 + ii;
@@ -1051,11 +1137,14 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
     };
     for (int r = 0; r < nref; ++r) {
         const uint8_t* ref = refs.p[r];
+        SO_MARK(wait);
         if (r == 0) pre();
+        SO_MARK(stage_win);
         if (tid == 0) *grab = (uint32_t)G::NW;   // read after the barrier below
         __syncthreads();
         if (r == 0) SO_SEA_STAMP(2, __builtin_amdgcn_s_memtime());
         if (win_int) {   // all loads first, then the LDS stores
+            SO_MARK(stage_win_int);
             uint32_t wv0[WNPT];
             const uint32_t* src = reinterpret_cast<const uint32_t*>(ref + (size_t)(y0 - SR + wwr) * W + (x0 - SR)) + wc0;
 #pragma unroll
@@ -1065,6 +1154,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             for (int k = 0; k < WNPT; ++k)
                 if (wc0 + k * WTPR < RP) win[wwr * RP + wc0 + k * WTPR] = wv0[k];
         } else {   // window: all loads first, then the LDS stores (zero outside the frame)
+            SO_MARK(stage_win_edge);
             constexpr int N = G::WR * RP, IT = (N + G::NTHREADS - 1) / G::NTHREADS;
             uint32_t v[IT];
 #pragma unroll
@@ -1084,6 +1174,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
         if (r == 0) SO_SEA_STAMP(3, __builtin_amdgcn_s_memtime());
         if (probe == 5) continue;   // phase-attribution builds (SO_PROF_PHASE=2): no search at all
         if (dense_flag && __builtin_amdgcn_readfirstlane(*dense_flag)) {   // uniform: the whole tile dense
+            SO_MARK(dense_tile);
             // the window's byte-shifted copies 1..3 into the free scratch (no byte sums or lists
             // here): every row the scan reads is then four aligned ds_read_b32 instead of five
             // plus four v_alignbyte (me_wave_kernel's layout)
@@ -1100,6 +1191,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             }
 #pragma unroll 1
             for (int u = wave; u < G::NBLK; u = next_block(u)) {
+                SO_MARK(dense_tile_block);
                 const int bxl = u % TBX, byl = u / TBX;
                 if (bx0 + bxl >= nbx || byt0 + byl >= by1) continue;   // wave-uniform
                 const int x = x0 + bxl * 16, y = y0 + byl * 16;
@@ -1127,6 +1219,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
         // b4[row * B4P + (c & 3) * WD + (c >> 2)] (a candidate's four sums of one 4x4 row --
         // columns c, c+4, c+8, c+12 -- are then consecutive bytes).  Thread = (dword column m:
         // columns 4m..4m+3, band of B4BAND output rows).
+        SO_MARK(byte_sums);
         if (tid == 0) SO_OPS_ADD(&st_ops, (uint32_t)(G::WD * G::B4NB * (G::B4BAND + 3) * 4 * 4));
         if (tid < G::WD * G::B4NB) {
             const int m = tid % G::WD, band = tid / G::WD;
@@ -1167,6 +1260,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
         if (probe == 1) continue;   // timing probe (tools/me_ab2.py): staging + byte sums only
 #pragma unroll 1
         for (int u = wave; u < G::NBLK; u = next_block(u)) {
+            SO_MARK(block_top);
             const int bxl = u % TBX, byl = u / TBX;
             if (bx0 + bxl >= nbx || byt0 + byl >= by1) continue;   // wave-uniform
             const int x = x0 + bxl * 16, y = y0 + byl * 16;
@@ -1190,6 +1284,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             asm volatile("" : "+v"(lane));
             const int xi = lane & 31, hh = lane >> 5;
             const int d2 = lane < 33 ? lane : 32;
+            SO_MARK(bound);
             uint32_t A[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) A[j] = a4[u * 4 + j];
@@ -1245,6 +1340,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
 #pragma unroll
                 for (int j = 0; j < 4; ++j) lb2 = __builtin_amdgcn_sad_u8(A[j], p2[4 * j * (B4P / 4)], lb2);
             }
+            SO_MARK(umin);
             constexpr uint32_t kBig = 0x7FFFFFFFu;   // a masked row: above every (LBq << 16) | t
             int dlo = SR - y;              dlo = dlo < 0 ? 0 : dlo;
             int dhi = H - 16 - y + SR - 1; dhi = dhi > 32 ? 32 : dhi;
@@ -1283,6 +1379,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
                 continue;
             }
             // ---- 3. survivors: 16 LBq - 240 <= U, i.e. LBq <= qU = (U + 240) >> 4 ------------
+            SO_MARK(ballots);
             const uint32_t qU = (U + 240) >> 4;
             // per-lane threshold (dx-invalid lanes: -1, nothing passes), opaque so that the
             // compare stays a plain v_cmp whose mask IS the ballot (folded back into
@@ -1316,16 +1413,19 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
                     SO_OPS_ADD(&st_ops, kDenseSadOps);
                 }
                 if (probe == 3) continue;
+                SO_MARK(dense_fallback);
                 // fallback: the dense wave search on the single-copy window
                 wave_dense_block<16, false, RP, 0, false, true>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u, tid,
                                                                 r);
                 continue;
             }
             if (probe == 4) continue;
+            SO_MARK(survivors);
             if (nsur == 1) {
                 // the smallest-bound candidate cs always survives (16 LBq(cs) - 240 <= SAD(cs) = U),
                 // so a lone survivor IS cs and its SAD is U: no second evaluation (the median
                 // block on textured content)
+                SO_MARK(sur_one);
                 const int dx = cdx - 16, dy = cdi - 16;
                 const uint64_t key = me_key(U, (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy)), (uint32_t)r,
                                             (uint32_t)cs);
@@ -1339,6 +1439,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             uint64_t best = kNoKey;
             if (nsur <= 4) {
                 // one pass: 16 lanes (one DPP row) per survivor, a row per lane
+                SO_MARK(sur_le4);
                 const int sidx = lane >> 4, row = lane & 15;
                 const uint32_t* cr_ = curt + crow0 + row * G::CPD;
                 const uint32_t c0 = cr_[0], c1 = cr_[1], c2 = cr_[2], c3 = cr_[3];
@@ -1372,6 +1473,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
                     for (int k = 0; k < 4; ++k) cr[rr][k] = curt[crow0 + (4 * q + rr) * G::CPD + k];
 #pragma unroll 1
                 for (uint32_t s0 = 0; s0 < nsur; s0 += 16) {
+                    SO_MARK(sur_pass);
                     const bool act = s0 + (uint32_t)sidx < nsur;
                     const int cand = act ? (int)mylist[s0 + sidx] : cs;
                     const int dxi = cand / 33, di = cand - dxi * 33;
@@ -1400,6 +1502,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             if (lane == 0 && best < keys[u]) keys[u] = best;
         }
     }
+    SO_MARK(search_end);
     __syncthreads();
 }
 
@@ -1487,11 +1590,13 @@ struct PTileGeo {
     static constexpr int U64 = ((B4 + LIST + 1) / 2 > TQD) ? (B4 + LIST + 1) / 2 : TQD;
 };
 // VBSEnable (tq16_vbs): 16 x 18 doubles per block (the 16 x 17 transpose of the block, or the
-// four 8 x 9 of its sub-blocks) + 256 bytes of sub-block token flags
+// four 8 x 9 of its sub-blocks); between tq16_vbs_fwd and tq16_vbs_inv the same scratch holds the
+// block's chosen levels (16 lanes x 8 packed int16 pairs).  Sub-block tokens: registers
+// (sub_tokens_reg).  LDS per tile 53.9 KB: three workgroups per CU (160 KB).
 constexpr int kTqScratchVbs = 288;
 template <class G>
 struct PTileGeoVbs {
-    static constexpr int TQD = G::NBLK * kTqScratchVbs + G::NBLK * 256 / 8;
+    static constexpr int TQD = G::NBLK * kTqScratchVbs;
     static constexpr int U64 = ((PTileGeo<G>::B4 + PTileGeo<G>::LIST + 1) / 2 > TQD)
                                    ? (PTileGeo<G>::B4 + PTileGeo<G>::LIST + 1) / 2 : TQD;
 };
@@ -1511,6 +1616,20 @@ SO_DEV void win_row16(const uint32_t* win, int row, int col, uint32_t (&w)[4]) {
 
 typedef uint32_t so_v4u __attribute__((ext_vector_type(4)));
 
+// A decoded ME record in LDS: dx, dy, ref as int16 and the SAD as uint16 (a 16 x 16 SAD is at
+// most 65,280; 0xFFFF = no valid candidate, decode_key's -1).  Half the bytes of four int32:
+// the VBS tile's 80 records then leave its LDS at 53.2 KB, under the 53,760 B at which a CU
+// still holds three workgroups (tools/ubench_lds_occ.cpp: 53,880 B gives two, although the
+// occupancy API reports three).
+struct MeRec {
+    uint16_t v[4];
+    SO_DEV int operator[](int k) const { return k < 3 ? (int)(int16_t)v[k] : (v[3] == 0xFFFFu ? -1 : (int)v[3]); }
+    SO_DEV void set(const int32_t (&r)[4]) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = (uint16_t)r[k];
+    }
+};
+
 // The LDS of one fused tile.
 // VBS: keys / mer hold the 16 blocks' records, then the 4 sub-blocks of each (NBLK + 4 g + j).
 template <class G, bool VBS = false>
@@ -1522,13 +1641,12 @@ struct PTileLds {
     uint32_t lcount[G::NW];
     unsigned long long keys[NU];
     uint32_t st[3];
-    int32_t mer[NU][4];                    // decoded ME records (dx, dy, ref, sad)
+    MeRec mer[NU];                         // decoded ME records (dx, dy, ref, sad)
     int32_t msum[G::TBY];                  // two-pass runs: pass-1 token sum of each block row
     uint32_t fwd_flags;                    // fwd_mfma: blocks whose levels need the FP64 forward
     alignas(16) double un[VBS ? PTileGeoVbs<G>::U64 : PTileGeo<G>::U64];   // byte sums + survivor lists | FP64 transposes
-    // VBS: the chosen levels of each block (16 lanes x 8 packed int16 pairs) and its split state
-    // (0 block, 1 split, 2 none) between tq16_vbs_fwd and tq16_vbs_inv
-    uint32_t lev[VBS ? G::NBLK * 16 * 8 : 1];
+    // VBS: each block's split state (0 block, 1 split, 2 none) between tq16_vbs_fwd and
+    // tq16_vbs_inv (its levels wait in its transpose scratch)
     uint8_t vsp[VBS ? G::NBLK : 1];
 };
 
@@ -1588,6 +1706,7 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
                 }
             }
         } else {
+            SO_MARK(tq_residual);
             int res[16];
             {
                 uint32_t pw[4];
@@ -1601,22 +1720,28 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
                 }
             }
             double tcr[16];
+            SO_MARK(tq_fwd);
             xform2d_rows<16, false>(dl, l, res, tcr, SO_TQ_TW());
+            SO_MARK(tq_quant);
 #pragma unroll
             for (int c = 0; c < 16; ++c)
                 q[c] = (int)(uint32_t)__builtin_bit_cast(
                     uint64_t, __builtin_amdgcn_ldexp(__builtin_rint(tcr[c]), -q_exp_fast<16>(l, c, qpr)) + kRne);
         }
+        SO_MARK(tq_tokens);
         const int tok = block_tokens<16>(nullptr, l, q);
         if constexpr (TOK) {   // pass 1 of two-pass RC: the token count is all that is used
             if (l == 0) o.tokens[b] = tok;
             return;
         }
+        SO_MARK(tq_qtc_store);
         store_row_i16<16>(o.qtc + b * 256 + l * 16, q);
         int dq[16];
         double rd[16];
         dequant_row_int<16>(q, l, qpr, dq);
+        SO_MARK(tq_inv);
         xform2d_rows<16, true>(dl, l, dq, rd, SO_TQ_TW());
+        SO_MARK(tq_recon);
         int rec[16];
         {
             uint32_t pw[4];
@@ -1649,6 +1774,7 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
         } else {
             store_row_u8<16>(o.recon, W, x, y + l, rec);
         }
+        SO_MARK(tq_sse_records);
         int sse = 0;
         if (o.sse) {
 #pragma unroll
@@ -1848,7 +1974,7 @@ SO_DEV void unpack_i16(const uint32_t* p, int* v) {
 }
 
 template <class G, bool SC1, bool HALO = false>
-SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, uint8_t* flags, int bx0, int byt0, int nbx,
+SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, int bx0, int byt0, int nbx,
                      int by0, int by1, int W, int qp_rd, const int32_t* __restrict__ qp_row,
                          const int32_t* __restrict__ qp_map, double lam, const PFrameOut& o) {
     constexpr int SR = G::SR, TBX = G::TBX;
@@ -1864,7 +1990,12 @@ SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, ui
     const int dx = S.mer[g][0], dy = S.mer[g][1], rf = S.mer[g][2], sad = S.mer[g][3];
     const int prow = byl * 16 + SR + dy + l, pcol = bxl * 16 + SR + dx;   // window coordinates
     const uint32_t* crow = S.curt + (byl * 16 + l) * G::CPD + bxl * 4;
-    uint32_t tcp[8], qp8[8];   // the block's coefficients and its levels at the RD QP, packed
+    // the coefficients survive the RD decision (packed int16 pairs: |TC| <= 4080), and without
+    // SO_VBS_LEAN also the levels at the RD QP (qp8 / qsp: reused when the final QP is the RD QP,
+    // otherwise requantised from the coefficients in int32); SO_VBS_LEAN always requantises --
+    // the levels would keep 16 more VGPRs live across the sub-block transforms
+    constexpr int NQ = SO_VBS_LEAN ? 1 : 8;
+    uint32_t tcp[8], qp8[NQ], qsp[NQ];
     int tok_b = 0;
     {
         int res[16];
@@ -1878,23 +2009,26 @@ SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, ui
         }
         double tcr[16];
         xform2d_rows<16, false>(scratch, l, res, tcr, SO_TQ_TW());
-        int tc[16], q[16];
+        int tc[16];
 #pragma unroll
         for (int c = 0; c < 16; ++c) tc[c] = (int)__builtin_rint(tcr[c]);
-        quant_row_i<16>(tc, l, qp_rd, q);
-        if (x != 0 && y != 0) tok_b = block_tokens<16>(nullptr, l, q);   // uniform
+        if (!SO_VBS_LEAN || (x != 0 && y != 0)) {   // uniform
+            int q[16];
+            quant_row_int<16>(tc, l, qp_rd, q);
+            if (x != 0 && y != 0) tok_b = block_tokens<16>(nullptr, l, q);
+            if constexpr (!SO_VBS_LEAN) pack_i16<16>(q, qp8);
+        }
         pack_i16<16>(tc, tcp);
-        pack_i16<16>(q, qp8);
     }
     bool split = false;
     int mae_num = sad;
     const int j = l >> 2, r0 = l & 3;
     int sdx = 0, sdy = 0, sref = 0;
-    uint32_t stcp[8], qsp[8];   // the sub-blocks' coefficients and levels at max(QP_rd - 1, 0), packed
+    uint32_t stcp[8];   // the sub-blocks' coefficients, packed
     const int sxl = bxl * 16 + (j & 1) * 8, syl = byl * 16 + (j >> 1) * 8;   // sub-block in the tile (px)
     const int qpm1_rd = qp_rd > 0 ? qp_rd - 1 : qp_rd;
     if (x != 0 && y != 0) {   // uniform
-        const int32_t* sm = S.mer[G::NBLK + 4 * g + j];
+        const MeRec& sm = S.mer[G::NBLK + 4 * g + j];
         sdx = sm[0]; sdy = sm[1]; sref = sm[2];
         int sres[2][8];
 #pragma unroll
@@ -1918,13 +2052,13 @@ SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, ui
         for (int h = 0; h < 2; ++h) {
 #pragma unroll
             for (int c = 0; c < 8; ++c) stc[h][c] = (int)__builtin_rint(std_[h][c]);
-            quant_row_i<8>(stc[h], r0 + 4 * h, qpm1_rd, qs[h]);
+            quant_row_int<8>(stc[h], r0 + 4 * h, qpm1_rd, qs[h]);
         }
-        const int tok_v = sub_tokens(flags, l, qs);
+        const int tok_v = sub_tokens_reg(l, qs);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             pack_i16<8>(stc[h], stcp + 4 * h);
-            pack_i16<8>(qs[h], qsp + 4 * h);
+            if constexpr (!SO_VBS_LEAN) pack_i16<8>(qs[h], qsp + 4 * h);
         }
         int ssum = 0;
         bool vinf = false;
@@ -1942,15 +2076,16 @@ SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, ui
         mae_num = vinf ? -1 : ssum;
     }
     // the chosen levels at the block's final QP: QTC, tokens and the block records now; the
-    // levels to LDS for tq16_vbs_inv (after the tile's barrier, in split-sorted order)
-    uint32_t* const lv = S.lev + (g * 16 + l) * 8;
+    // levels into the block's (now free) transpose scratch for tq16_vbs_inv (after the tile's
+    // barrier, in split-sorted order)
+    uint32_t* const lv = reinterpret_cast<uint32_t*>(scratch) + l * 8;
     int tok;
     if (!split) {
         int q[16];
-        if (qpr != qp_rd) {
+        if (SO_VBS_LEAN || qpr != qp_rd) {
             int tc[16];
             unpack_i16<16>(tcp, tc);
-            quant_row_i<16>(tc, l, qpr, q);
+            quant_row_int<16>(tc, l, qpr, q);
         } else {
             unpack_i16<16>(qp8, q);
         }
@@ -1961,18 +2096,18 @@ SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, ui
     } else {
         const int qpm1 = qpr > 0 ? qpr - 1 : qpr;
         int qs[2][8];
-        if (qpm1 != qpm1_rd) {
+        if (SO_VBS_LEAN || qpm1 != qpm1_rd) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 int stc[8];
                 unpack_i16<8>(stcp + 4 * h, stc);
-                quant_row_i<8>(stc, r0 + 4 * h, qpm1, qs[h]);
+                quant_row_int<8>(stc, r0 + 4 * h, qpm1, qs[h]);
             }
         } else {
 #pragma unroll
             for (int h = 0; h < 2; ++h) unpack_i16<8>(qsp + 4 * h, qs[h]);
         }
-        tok = sub_tokens(flags, l, qs);
+        tok = sub_tokens_reg(l, qs);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             store_row_i16<8>(o.qtc + b * 256 + j * 64 + (r0 + 4 * h) * 8, qs[h]);
@@ -1992,9 +2127,12 @@ SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, ui
 // order (unsplit blocks first, then split ones, then none): the four blocks of a wave then
 // take one of the two inverse paths -- a wave with both ran both (about two waves in three on
 // the bench content, split ~50 %), now at most one wave per tile does.  Reads the levels
-// tq16_vbs_fwd left in LDS; dequantisation, IDCT, reconstruction and SSE.
+// tq16_vbs_fwd left in the block's scratch (`un`: the tile's transpose scratch; block g's is
+// un + g * kTqScratchVbs, and the slot's lanes use it for the transposes too, once the levels are
+// in registers: the slot -> block map is a permutation, so no other lanes touch it);
+// dequantisation, IDCT, reconstruction and SSE.
 template <class G, bool SC1, bool HALO = false>
-SO_DEV void tq16_vbs_inv(PTileLds<G, true>& S, int k, int l, double* scratch, int bx0, int byt0, int nbx,
+SO_DEV void tq16_vbs_inv(PTileLds<G, true>& S, int k, int l, double* un, int bx0, int byt0, int nbx,
                          int by0, int by1, int W, int qp_rd, const int32_t* __restrict__ qp_row,
                          const int32_t* __restrict__ qp_map, const PFrameOut& o, const PHalo& hl = PHalo{}) {
     constexpr int SR = G::SR, TBX = G::TBX;
@@ -2019,7 +2157,15 @@ SO_DEV void tq16_vbs_inv(PTileLds<G, true>& S, int k, int l, double* scratch, in
     const size_t b = (size_t)(gby - by0) * nbx + gbx;
     const int x = gbx * 16, y = gby * 16;
     const int qpr = qp_map ? qp_map[(size_t)gby * nbx + gbx] : (qp_row ? qp_row[gby] : qp_rd);
-    const uint32_t* const lv = S.lev + (g * 16 + l) * 8;
+    double* const scratch = un + g * kTqScratchVbs;
+    uint32_t lv[8];
+    {
+        const so_v4u* lp = reinterpret_cast<const so_v4u*>(reinterpret_cast<const uint32_t*>(scratch) + l * 8);
+        const so_v4u a = lp[0], b = lp[1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { lv[e] = a[e]; lv[4 + e] = b[e]; }
+    }
+    wave_sync();   // every lane's levels read before the transposes below overwrite them
     const uint32_t* crow = S.curt + (byl * 16 + l) * G::CPD + bxl * 4;
     const int j = l >> 2, r0 = l & 3;
     int sse = 0;
@@ -2053,7 +2199,7 @@ SO_DEV void tq16_vbs_inv(PTileLds<G, true>& S, int k, int l, double* scratch, in
         }
     } else {
         const int qpm1 = qpr > 0 ? qpr - 1 : qpr;
-        const int32_t* sm = S.mer[G::NBLK + 4 * g + j];
+        const MeRec& sm = S.mer[G::NBLK + 4 * g + j];
         const int sdx = sm[0], sdy = sm[1];
         const int sxl = bxl * 16 + (j & 1) * 8, syl = byl * 16 + (j >> 1) * 8;   // sub-block in the tile (px)
         int sdq[2][8];
@@ -2139,12 +2285,15 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
                            dense_flag);   // ends with a barrier
 
     const int tid = opaque_tid();
+    SO_MARK(decode_keys);
     SO_SEA_STAMP(5, __builtin_amdgcn_s_memtime());
     const int nbx = W / 16;
     const int tiles_x = (nbx + TBX - 1) / TBX;
     const int bx0 = (tile % tiles_x) * TBX, byt0 = by0 + (tile / tiles_x) * TBY;
     for (int i = tid; i < PTileLds<G, VBS>::NU; i += G::NTHREADS) {
-        decode_key(S.keys[i], SR, S.mer[i]);
+        int32_t rec4[4];
+        decode_key(S.keys[i], SR, rec4);
+        S.mer[i].set(rec4);
         const int gbx = bx0 + i % TBX, gby = byt0 + i / TBX;
         if (out_best && i < G::NBLK && gbx < nbx && gby < by1) {
             int32_t* ob = out_best + ((size_t)(gby - by0) * nbx + gbx) * 4;
@@ -2194,9 +2343,8 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
             }
         } else if (ln < 16 * G::TQ_BPW && gq < G::NBLK) {
             if constexpr (VBS)
-                tq16_vbs_fwd<G, SC1, HALO>(S, gq, ln & 15, S.un + gq * kTqScratchVbs,
-                                           reinterpret_cast<uint8_t*>(S.un + G::NBLK * kTqScratchVbs) + gq * 256, bx0,
-                                           byt0, nbx, by0, by1, W, qp_rd, qp_row, qp_map, lam, o);
+                tq16_vbs_fwd<G, SC1, HALO>(S, gq, ln & 15, S.un + gq * kTqScratchVbs, bx0, byt0, nbx, by0, by1, W, qp_rd,
+                                           qp_row, qp_map, lam, o);
             else
                 tq16_exact<G, SC1, HALO, TOK>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by0, by1, W, qp_rd,
                                               qp_row, qp_map, o, hl, qs);
@@ -2207,11 +2355,12 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
             __syncthreads();   // every block's levels and split state in LDS
             const int ln = tid & 63, gq = (tid >> 6) * G::TQ_BPW + (ln >> 4);
             if (ln < 16 * G::TQ_BPW && gq < G::NBLK)
-                tq16_vbs_inv<G, SC1, HALO>(S, gq, ln & 15, S.un + gq * kTqScratchVbs, bx0, byt0, nbx, by0, by1, W, qp_rd,
+                tq16_vbs_inv<G, SC1, HALO>(S, gq, ln & 15, S.un, bx0, byt0, nbx, by0, by1, W, qp_rd,
                                            qp_row, qp_map, o, hl);
         }
     }
     SO_SEA_STAMP(7, __builtin_amdgcn_s_memtime());
+    SO_MARK(post);
     post();   // p_run_kernel: the next task's dequeue, in flight with the drain below
     if constexpr (SC1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
     SO_SEA_STAMP(14, __builtin_amdgcn_s_memtime());
@@ -2535,6 +2684,7 @@ SO_DEV uint32_t run_poll(const uint32_t* c, bool need, bool sysl, uint32_t* ws, 
         else
             raw = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const bool ok = raw == (sysl ? w.sys_want : w.want);
+        SO_MARK(poll_iter);
         if (__builtin_amdgcn_ballot_w64(need && !ok) == 0) break;
 #if SO_RUN_ABORT_CHECK
         // the timeout count, read once per wait and only when it has to wait: after one timeout
@@ -2638,14 +2788,14 @@ SO_DEV uint32_t run_dequeue(uint32_t* ws) {
     return r;
 }
 
-// VBS: VBSEnable (the block + sub-block dense search, tq16_vbs; ~128 VGPRs, 4 waves per SIMD)
+// VBS: VBSEnable (the block + sub-block SEA and the RD split, tq16_vbs_fwd / _inv; 80 VGPRs, 6 waves per SIMD)
 // HOOKS: the measurement / test hooks -- the searches' SAD byte-operation count
 // (SO_OPT_COUNT_SAD_OPS) and the deliberately lost done flag (SO_OPT_TEST_LOSE_FLAG).  Only
 // kRunSingle has a HOOKS instantiation, launched only while one of those options is set, so the
 // timed kernels carry neither (count_ops folds to the constant 0 and its atomics are dead code).
 template <int NW, int MODE, bool VBS = false, bool HOOKS = false>
 __global__ void __launch_bounds__(NW * 64)
-__attribute__((amdgpu_waves_per_eu(VBS ? 4 : (NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE))))
+__attribute__((amdgpu_waves_per_eu(VBS ? SO_VBS_WPE : (NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE))))
 p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, int H, int W,
              int qp_rd, const int32_t* __restrict__ qp_row, uint32_t* __restrict__ ws, int ws_stamp_base,
              const PRunStripe sp, double lam) {
@@ -2684,6 +2834,9 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
         s_fbsum = 0;
         s_ops = 0;
     }
+#ifdef SO_MARKS_COUNT
+    if (tid < 64) s_mark_cnt[tid] = 0u;   // visible after the loop's first barrier
+#endif
     // this launch's epoch: ws[2] + 1 (ws[2] = the last finished launch's; written by that
     // launch's last workgroup, so every workgroup here reads it before it can change).  Done
     // flags hold the epoch of the launch that set them: nothing is zeroed between launches.
@@ -2706,6 +2859,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     uint32_t nxt_v = 0;       // wave 0: the atomic's result (VGPR; read at the loop top)
     bool nxt_taken = false;   // uniform
     for (;;) {
+        SO_MARK(loop_top);
         if (wave == 0) {
             if (!nxt_taken) nxt_v = run_dequeue(ws);
             s_task = (int)__builtin_amdgcn_readfirstlane(nxt_v);
@@ -2842,7 +2996,11 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 RefSet refs{};
                 refs.p[0] = ref;
                 sea2_tile<G>(L, tile, a.cur[f], refs, 1, H, W, 0, by1, 0, wait_ref);   // ends with a barrier
-                for (int i = tid; i < G::NBLK; i += G::NTHREADS) decode_key(S.keys[i], G::SR, S.mer[i]);
+                for (int i = tid; i < G::NBLK; i += G::NTHREADS) {
+                    int32_t rec4[4];
+                    decode_key(S.keys[i], G::SR, rec4);
+                    S.mer[i].set(rec4);
+                }
                 __syncthreads();
                 const int t2 = opaque_tid(), ln = t2 & 63, gq = (t2 >> 6) * G::TQ_BPW + (ln >> 4);
                 if (ln < 16 * G::TQ_BPW && gq < G::NBLK)
@@ -2949,6 +3107,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd, qp_row, nullptr, nullptr, a.out[f], wait_ref, PHalo{}, lam,
                 &s_dense, reinterpret_cast<int32_t*>(tilefb) + (size_t)f * ntiles + tile, count_ops, take_next);
             SO_RUN_PROF(52, __builtin_amdgcn_s_memtime() - pt0);
+            SO_MARK(done_flag);
             // ptile_body ended with every wave's write-through stores retired and a barrier
             // (sp.lose_task: SO_OPT_TEST_LOSE_FLAG, the wait diagnostics' test -- that task's flag
             // is never set, so its dependants time out and record themselves)
@@ -2956,6 +3115,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
         }
+        SO_MARK(task_end);
         if (pass == 1 && tid == 0) {   // this tile's dense-searched blocks and SAD byte operations
             s_fbsum += S.st[0];
             if constexpr (HOOKS) s_ops += S.st[2];
@@ -2971,6 +3131,10 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
         }
 #endif
     }
+#ifdef SO_MARKS_COUNT
+    __syncthreads();
+    if (tid < kMarkCount && g_mark_counts) atomicAdd(&g_mark_counts[tid], s_mark_cnt[tid]);
+#endif
     // the last workgroup out resets the task and exit counters and publishes the epoch
     if (wave == 0) {
         const uint32_t fbsum = __builtin_amdgcn_readfirstlane(s_fbsum);
@@ -3013,6 +3177,7 @@ size_t p_run_workspace_words(int H, int W) {
 // (the occupancy API), cached per (device, kernel) under a mutex -- a process may drive several
 // devices from several host threads.  (The grid only sizes the run: a workgroup that is not
 // resident holds no task, so an over-estimate costs speed, never progress.)
+constexpr size_t kLdsPerCuObserved = 161280;   // 3 x 53,760 B resident at once (ubench_lds_occ)
 static int run_shape(const void* kernel, int* ncu, int* per_cu) {
     static std::mutex mu;
     static std::map<std::pair<int, const void*>, std::pair<int, int>> cache;
@@ -3029,6 +3194,16 @@ static int run_shape(const void* kernel, int* ncu, int* per_cu) {
         int n = 0, p = 0;
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&p, kernel, SO_PTILE_NW * 64, 0) != hipSuccess || p <= 0) p = 1;
+        // The occupancy API over-counts near the LDS limit on gfx950: it reports three
+        // 512-thread workgroups per CU for 53,880 B of LDS, but a CU runs only two of them at
+        // once (three up to 53,760 B; tools/ubench_lds_occ.cpp, profiles/r05/ubench_lds_occ.log).
+        // Count 512-B granules against the 161,280 B three such workgroups were seen to share.
+        hipFuncAttributes fa{};
+        if (hipFuncGetAttributes(&fa, kernel) == hipSuccess && fa.sharedSizeBytes > 0) {
+            const size_t g = (fa.sharedSizeBytes + 511) & ~(size_t)511;
+            const int by_lds = (int)(kLdsPerCuObserved / g);
+            if (by_lds >= 1 && by_lds < p) p = by_lds;
+        }
         it = cache.emplace(key, std::make_pair(n, p)).first;
     }
     *ncu = it->second.first;
