@@ -92,6 +92,7 @@ def parse(argv=None):
     ap.add_argument("--gops-in-flight", type=lambda v: [int(x) for x in v.split(",") if x], default=[2],
                     help="N=1 records of a GOP stream: k GOPs per step with interleaved P-runs (comma list; '' = none)")
     ap.add_argument("--no-pcie", action="store_true")
+    ap.add_argument("--pcie-last", action="store_true", help="measure the section-4 region after the records (A/B)")
     ap.add_argument("--kernel-reps", type=int, default=20)
     ap.add_argument("--exchange", choices=("p2p", "allgather"), default="p2p",
                     help="stripe hand-off: inside the persistent launch over xGMI (p2p, self-checked against "
@@ -1172,6 +1173,11 @@ def main(argv=None):
     headline_health = None
     if codec is not None and not stripe:
         headline_health = codec.engine().wait_health.as_dict()
+    # BASELINE.md section 4's region first, right after the headline (a run of records ahead of it
+    # left the region 1.6x slower on one box: profiles/r05/pcie_order.log)
+    pcie = None
+    if rank == 0 and world == 1 and not args.cpu_plumbing and not args.no_pcie and plain_cfg and not args.pcie_last:
+        pcie = guarded("pcie_inclusive", lambda: pcie_inclusive(codec, cfg, frames))
     records = None
     if rank == 0 and world == 1 and not args.cpu_plumbing and not args.no_records and name == "4k":
         records = {"1080p": guarded("records.1080p", lambda: record_single("1080p", args, dev))}
@@ -1186,12 +1192,11 @@ def main(argv=None):
         # ROI + two-pass rate-control GOP, each measured and parity-checked like the headline
         for nm in ("4k_vbs", "4k_rc2pass"):
             records[nm] = guarded(f"records.{nm}", lambda nm=nm: record_single(nm, args, dev))
+    if rank == 0 and world == 1 and not args.cpu_plumbing and not args.no_pcie and plain_cfg and args.pcie_last:
+        pcie = guarded("pcie_inclusive", lambda: pcie_inclusive(codec, cfg, frames))
     if rank == 0 and args.cpu_plumbing and args.inject_failure and not any(
             d["what"] == args.inject_failure for d in degraded):   # the mechanism, on a CPU-only host
         records = {args.inject_failure: guarded(args.inject_failure, lambda: {"plumbing": True})}
-    pcie = None
-    if rank == 0 and world == 1 and not args.cpu_plumbing and not args.no_pcie and plain_cfg:
-        pcie = guarded("pcie_inclusive", lambda: pcie_inclusive(codec, cfg, frames))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.cpu_plumbing:
         cpu = guarded("cpu_baseline", lambda: cpu_baseline(cfg, args.cpu_rows, args.cpu_pool_rows))

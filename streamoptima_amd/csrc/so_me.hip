@@ -693,7 +693,7 @@ extern "C" int so_debug_set_run_stamps(void* p) {
 // weight the static census into a dynamic VALU table.
 #define SO_MARK_NAMES(X) X(loop_top) X(stage_cur) X(stage_cur_int) X(stage_cur_edge) X(cur_sums) X(wait) \
     X(poll_iter) X(stage_win) X(stage_win_int) X(stage_win_edge) X(dense_tile) X(dense_tile_block) X(byte_sums) \
-    X(block_top) X(bound) X(umin) X(ballots) X(dense_fallback) X(survivors) X(sur_one) X(sur_le4) X(sur_pass) \
+    X(block_top) X(bound) X(umin) X(umin_edge) X(ballots) X(bal_row) X(dense_fallback) X(survivors) X(sur_one) X(sur_le4) X(sur_pass) \
     X(search_end) X(decode_keys) X(tq_residual) X(tq_fwd) X(tq_quant) X(tq_tokens) X(tq_qtc_store) X(tq_inv) \
     X(tq_recon) X(tq_sse_records) X(post) X(done_flag) X(task_end)
 #define SO_MARK_ENUM(n) kMark_##n,
@@ -1030,12 +1030,20 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
 // directly (p_run_kernel sets it when the same tile of the previous frame had most of its
 // blocks overflow the SEA bound: flat or noise-like content, where computing the bound only to
 // fall back costs more than it saves).
+// prev_mv (optional): the motion records (int16 [nb][12], dx and dy first; rows relative to by0)
+// of the frame before `cur` against the same kind of reference -- the co-located block's vector
+// there is a second candidate for U (below).  Only a hint: any VALID candidate's SAD bounds the
+// minimum from above, so a stale or garbage record (it is read unordered, and is range-checked)
+// can cost survivors, never exactness.
 template <class G, class Pre = NoPre, bool VBS = false>
 SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cur, const RefSet& refs, int nref,
                       int H, int W, int by0, int by1, int probe, const Pre& pre = Pre(),
-                      const int* dense_flag = nullptr) {
+                      const int* dense_flag = nullptr, const int16_t* prev_mv = nullptr) {
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY, RP = G::RP, NT = G::NT;
     constexpr int B4P = G::B4P, CAP = G::CAP, CP = G::TPX;
+#ifdef SO_NO_MV_HINT   // A/B builds: U from the smallest-bound candidate only
+    prev_mv = nullptr;
+#endif
     uint32_t* const win = L.win;
     uint32_t* const b4w = L.b4w;
     uint8_t* const b4 = reinterpret_cast<uint8_t*>(b4w);
@@ -1264,6 +1272,11 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             const int bxl = u % TBX, byl = u / TBX;
             if (bx0 + bxl >= nbx || byt0 + byl >= by1) continue;   // wave-uniform
             const int x = x0 + bxl * 16, y = y0 + byl * 16;
+            // the co-located block's vector in the previous frame (issued now, used after the bounds)
+            uint32_t pmv = 0x80008000u;   // (-32768, -32768): no hint
+            if (!VBS && prev_mv != nullptr && r == 0)
+                pmv = __builtin_amdgcn_readfirstlane(
+                    *reinterpret_cast<const uint32_t*>(prev_mv + ((size_t)(byt0 + byl - by0) * nbx + bx0 + bxl) * 12));
             if constexpr (VBS) {
                 if (x != 0 && y != 0) {   // uniform: block + sub-block search
 #ifndef SO_VBS_DENSE_ONLY   // A/B builds: every sub-searched block dense
@@ -1348,6 +1361,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             const bool x2ok = x + 16 < W - 16;
             const bool ok2 = lane < 33 && x2ok && d2 >= dlo && d2 <= dhi;
             if (dlo > 0 || dhi < 32) {
+                SO_MARK(umin_edge);
                 const int tlo = dlo - 16 * hh, thi = dhi - 16 * hh;
 #pragma unroll
                 for (int t = 0; t < NT; ++t) lb[t] = (t < tlo || t > thi) ? kBig : lb[t];
@@ -1363,16 +1377,33 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
                 kl = (ok2 && k2 < kl) ? k2 : kl;
             }
             const uint32_t kmin = wave_min_u32(kl);
-            // the bound pass: 68 + 4 SAD lane instructions, the U evaluation: 1
+            // the bound pass: 68 + 4 SAD lane instructions, the U evaluation: 1 (2 with a valid hint)
             if (lane == 0) SO_OPS_ADD(&st_ops, kmin == 0xFFFFFFFFu ? 72u * 256u : 73u * 256u);
             if (kmin == 0xFFFFFFFFu) continue;                 // no valid candidate: key stays none
             const int cs = (int)(kmin & 2047), cdx = cs / 33, cdi = cs - cdx * 33;
             const int crow0 = byl * 16 * G::CPD + bxl * 4;   // current block in curt (dwords)
+            // U = min(SAD of the smallest-bound candidate, SAD at the previous frame's vector of
+            // this block when that is a valid candidate): both SADs in one wave sum, packed in the
+            // 16-bit halves (each <= 65,280).  The previous frame's vector is close to the minimum
+            // for most blocks; with it a 4K bench P-frame leaves 9.5 instead of 15.9 survivors per
+            // block, 0.18 % instead of 1.4 % past the cap (tests/analysis/sea_u_sources.py)
+            const int pdx = (int)(int16_t)(pmv & 0xFFFFu), pdy = (int)pmv >> 16;
+            const bool pv = pdx >= -SR && pdx <= SR && pdy >= -SR && pdy <= SR && x + pdx >= 0 && x + pdx < W - 16 &&
+                            y + pdy >= 0 && y + pdy < H - 16;   // uniform
             uint32_t U;
             {
                 const int row = lane >> 2, kk = lane & 3;
+                const uint32_t c = curt[crow0 + row * G::CPD + kk];
                 const uint32_t w = win_u32<RP>(win, byl * 16 + cdi + row, bxl * 16 + cdx + 4 * kk);
-                U = wave_sum_u32(__builtin_amdgcn_sad_u8(curt[crow0 + row * G::CPD + kk], w, 0u));
+                uint32_t sp = __builtin_amdgcn_sad_u8(c, w, 0u);
+                if (pv) {
+                    const uint32_t wp = win_u32<RP>(win, byl * 16 + SR + pdy + row, bxl * 16 + SR + pdx + 4 * kk);
+                    sp = __builtin_amdgcn_sad_hi_u8(c, wp, sp);
+                }
+                const uint32_t both = wave_sum_u32(sp);
+                U = both & 0xFFFFu;
+                if (pv && (both >> 16) < U) U = both >> 16;
+                if (pv && lane == 0) SO_OPS_ADD(&st_ops, 256u);
             }
             if (probe == 2) {
                 if (lane == 0 && U < keys[u]) keys[u] = U;
@@ -1399,6 +1430,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
                 const bool pass = t < NT ? (int)lb[t] <= thr : (ok2 && lb2 <= qU);
                 const uint64_t bal = __builtin_amdgcn_ballot_w64(pass);
                 if (bal) {   // uniform
+                    SO_MARK(bal_row);
                     const uint32_t pos = nsur + lane_prefix(bal);
                     if (pass && pos < (uint32_t)CAP) mylist[pos] = (uint16_t)(t < NT ? cbase + t : 32 * 33 + d2);
                     nsur += (uint32_t)__builtin_popcountll(bal);
@@ -2261,7 +2293,7 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
                        const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best, const PFrameOut& o,
                        const Pre& pre = Pre(), const PHalo& hl = PHalo{}, double lam = 0.0,
                        const int* dense_flag = nullptr, int32_t* fb_out = nullptr, int count_ops = 0,
-                       const Post& post = Post()) {
+                       const Post& post = Post(), const int16_t* prev_mv = nullptr) {
     constexpr int SR = G::SR, TBX = G::TBX, TBY = G::TBY;
     using P = PTileGeo<G>;
     uint32_t* const b4w = reinterpret_cast<uint32_t*>(S.un);
@@ -2282,7 +2314,7 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
 #define SO_PROF_PHASE 0  // (the tile's current rows stored as its reconstruction), 2 = no search
 #endif                   // (window staged, every block at mv (0, 0))
     sea2_tile<G, Pre, VBS>(L, tile, cur, refs, 1, H, W, by0, by1, SO_PROF_PHASE == 2 ? 5 : 0, pre,
-                           dense_flag);   // ends with a barrier
+                           dense_flag, prev_mv);   // ends with a barrier
 
     const int tid = opaque_tid();
     SO_MARK(decode_keys);
@@ -2995,7 +3027,8 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                                 S.st, count_ops};
                 RefSet refs{};
                 refs.p[0] = ref;
-                sea2_tile<G>(L, tile, a.cur[f], refs, 1, H, W, 0, by1, 0, wait_ref);   // ends with a barrier
+                sea2_tile<G>(L, tile, a.cur[f], refs, 1, H, W, 0, by1, 0, wait_ref, nullptr,
+                             MODE == kRunTwoPass && dep >= 0 ? a.out[dep].mv : nullptr);   // ends with a barrier
                 for (int i = tid; i < G::NBLK; i += G::NTHREADS) {
                     int32_t rec4[4];
                     decode_key(S.keys[i], G::SR, rec4);
@@ -3087,7 +3120,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             }
             ptile_body<G, true, decltype(wait_ref), true, false, false, decltype(take_next)>(
                 S, tile, a.cur[f], ref, H, W, by0, by1, qp_rd, qp_row, nullptr, nullptr, a.out[f], wait_ref, hl, 0.0,
-                nullptr, nullptr, count_ops, take_next);
+                nullptr, nullptr, count_ops, take_next, f > 0 ? a.out[f - 1].mv : nullptr);
             // ptile_body ended with every wave's stores (local and remote) retired and a barrier
             if (wave == 0) {
                 __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
@@ -3105,7 +3138,10 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 #endif
             ptile_body<G, true, decltype(wait_ref), false, false, VBS, decltype(take_next)>(
                 S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd, qp_row, nullptr, nullptr, a.out[f], wait_ref, PHalo{}, lam,
-                &s_dense, reinterpret_cast<int32_t*>(tilefb) + (size_t)f * ntiles + tile, count_ops, take_next);
+                &s_dense, reinterpret_cast<int32_t*>(tilefb) + (size_t)f * ntiles + tile, count_ops, take_next,
+                // VBS: the same hint for the block's U measured slower (4K VBS P-frame 123.1 vs
+                // 121.3 us: 8 more VGPR spills; profiles/r05/hint_ab_vbs.log)
+                !VBS && dep >= 0 ? a.out[dep].mv : nullptr);
             SO_RUN_PROF(52, __builtin_amdgcn_s_memtime() - pt0);
             SO_MARK(done_flag);
             // ptile_body ended with every wave's write-through stores retired and a barrier

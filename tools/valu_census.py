@@ -20,7 +20,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 NAMES = ("loop_top stage_cur stage_cur_int stage_cur_edge cur_sums wait poll_iter stage_win stage_win_int "
-         "stage_win_edge dense_tile dense_tile_block byte_sums block_top bound umin ballots dense_fallback survivors "
+         "stage_win_edge dense_tile dense_tile_block byte_sums block_top bound umin umin_edge ballots bal_row dense_fallback survivors "
          "sur_one sur_le4 sur_pass search_end decode_keys tq_residual tq_fwd tq_quant tq_tokens tq_qtc_store tq_inv "
          "tq_recon tq_sse_records post done_flag task_end").split()
 
