@@ -406,12 +406,14 @@ class Y_Video_codec(BlockAPI):
         # (engine.encode_p_run): same symbols, frames overlapped on the device
         run_ok = not rc_switch and self.nRefFrames == 1 and eng.pipelined_ok(1) and os.environ.get("SO_PIPELINE", "1") != "0"
         pipelined = run_ok and not two_pass and roi_dev is None
-        # two-pass RC (with or without ROI): opt-in (SO_RUN_2PASS=1), a P-run in one
-        # so_encode_p_run_2pass call -- the per-frame kernel sequence enqueued by the library
-        # (same GPU time as this loop, a third of its host time, but a synchronous GOP measured
-        # 0.6 ms slower) or, with SO_RUN_2PASS_FUSED=1, both passes in one persistent launch
+        # two-pass RC (with or without ROI): a P-run in one so_encode_p_run_2pass call -- the
+        # per-frame kernel sequence enqueued by the library (the same kernels as the per-frame
+        # loop below, a third of its host time, and pass 1 gets the previous frame's motion
+        # records as its search hint, which the per-call C-ABI of the loop has no argument for;
+        # SO_RUN_2PASS=0: the loop) or, with SO_OPT_RUN_2PASS_FUSED, both passes in one
+        # persistent launch
         pipelined2 = (run_ok and two_pass and eng.pipelined_ok(1, vbs_ok=False)
-                      and os.environ.get("SO_RUN_2PASS", "0") == "1")
+                      and os.environ.get("SO_RUN_2PASS", "1") == "1")
         if pipelined and chunk is None and intra_dur < nframes - 1 and wait_input_default and on_output_default:
             # several P-runs between I-frames: independent chains, interleaved in one launch
             return self.encode_gops_device([frames_dev], intra_dur, symbols=[symbols] if symbols else None,

@@ -46,7 +46,7 @@ constexpr size_t kFastSegWords = 2 * 4096 * 6;   // so_fastme.hip: the speculate
 int p_tile_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int by0, int by1, int qp_rd,
                   const int32_t* qp_row, const int32_t* qp_map, int32_t* out_best, uint8_t* out_split,
                   int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon,
-                  int32_t* out_sse, hipStream_t st, bool tokens_only = false);
+                  int32_t* out_sse, hipStream_t st, bool tokens_only = false, const int16_t* prev_mv = nullptr);
 
 struct PackFrame {
     const uint8_t* split;
@@ -71,6 +71,12 @@ int stripe_halo_push_launch(const uint8_t* plane, int W, int by0, int by1, uint8
                             uint32_t* up_flags, uint32_t* dn_flags, int gf, uint32_t epoch, hipStream_t st);
 int frame_push_launch(const uint8_t* plane, int H, int W, uint8_t* dst, uint32_t* flags, uint32_t epoch,
                       hipStream_t st);
+
+#ifdef SO_AB
+// A/B builds only (not in the header): tools that set the SO_AB environment knobs
+// (tools/ab_guard.py) check for this symbol, so a knob can never silently measure the default path
+extern "C" int so_debug_ab_build(void) { return 1; }
+#endif
 
 // The fused search + transform tile kernel (so_me.hip p_tile_kernel) covers the headline
 // configuration: bs 16, sr 16, full search, no VBS / FME, one reference.  SO_FUSED=0 or an
@@ -564,8 +570,9 @@ int so_encode_p_run_2pass(const uint8_t* const* curs, int nframes, const uint8_t
         RefSet rs{};
         rs.p[0] = i ? out_recon[i - 1] : ref0;
         const PFrameOut& o = outs[(size_t)i];
+        // pass 1 with the previous frame's (final) motion records as the search's U hint
         SO_TRY(p_tile_launch(curs[i], rs, H, W, 0, nby, qp_rd, qp_row, nullptr, best, o.split, o.mv, o.qtc, o.tokens,
-                             o.mae, o.recon, o.sse, st, true));
+                             o.mae, o.recon, o.sse, st, true, i ? out_mv[i - 1] : nullptr));
         hipLaunchKernelGGL(qp_map_kernel, dim3(nby), dim3(256), 0, st, o.tokens, nbx, 0, qp_rd, qp_row, roi, qp_lo,
                            qp_hi, o.qpmap);
         SO_TRY(check_launch("qp_map_kernel"));

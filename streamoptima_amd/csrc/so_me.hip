@@ -695,7 +695,9 @@ extern "C" int so_debug_set_run_stamps(void* p) {
     X(poll_iter) X(stage_win) X(stage_win_int) X(stage_win_edge) X(dense_tile) X(dense_tile_block) X(byte_sums) \
     X(block_top) X(bound) X(umin) X(umin_edge) X(ballots) X(bal_row) X(dense_fallback) X(survivors) X(sur_one) X(sur_le4) X(sur_pass) \
     X(search_end) X(decode_keys) X(tq_residual) X(tq_fwd) X(tq_quant) X(tq_tokens) X(tq_qtc_store) X(tq_inv) \
-    X(tq_recon) X(tq_sse_records) X(post) X(done_flag) X(task_end)
+    X(tq_recon) X(tq_sse_records) X(post) X(done_flag) X(task_end) X(vbs_block) X(vbs_umin) X(vbs_list_a) \
+    X(vbs_pass) X(vbs_list_b) X(vbs_final) X(vbs_dense) X(vbs_fwd) X(vbs_fwd_sub) X(vbs_final_q) X(vbs_inv) \
+    X(vbs_inv_split) X(vbs_inv_end)
 #define SO_MARK_ENUM(n) kMark_##n,
 enum SoMarkId { SO_MARK_NAMES(SO_MARK_ENUM) kMarkCount };
 #undef SO_MARK_ENUM
@@ -807,6 +809,7 @@ SO_DEV void vbs_eval_list(const Sea2Lds& L, const uint16_t* list, uint32_t n, in
     }
 #pragma unroll 1
     for (uint32_t s0 = 0; s0 < n; s0 += 16) {
+        SO_MARK(vbs_pass);
         const bool act = s0 + (uint32_t)sidx < n;
         const int cand = act ? (int)list[s0 + sidx] : cs;
         const int dxi = cand / 33, di = cand - dxi * 33;
@@ -848,6 +851,7 @@ SO_DEV void vbs_eval_list(const Sea2Lds& L, const uint16_t* list, uint32_t n, in
 template <class G>
 SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
     constexpr int NT = G::NT, B4P = G::B4P, CAP = G::CAPV, RP = G::RP, CPD = G::CPD;
+    SO_MARK(vbs_block);
     int lane = tid & 63;
     asm volatile("" : "+v"(lane));
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -909,6 +913,7 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
     }
     // block bounds LBq(t): the four sub-block bounds summed (SO_VBS_LEAN: recomputed where used,
     // the list-A test, instead of held in 17 more VGPRs through the lists)
+    SO_MARK(vbs_umin);
     const auto blb0 = [&](int t) { return __builtin_amdgcn_sad_u16(T[t], 0u, __builtin_amdgcn_sad_u16(Bt[t], 0u, 0u)); };
     uint32_t lbs[SO_VBS_LEAN ? 1 : NT];
     if constexpr (!SO_VBS_LEAN) {
@@ -942,6 +947,7 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
         U = wave_sum_u32(__builtin_amdgcn_sad_u8(L.curt[crow0 + row * CPD + kk], w, 0u));
     }
     const uint32_t qU = (U + 240) >> 4;
+    SO_MARK(vbs_list_a);
     // list-A membership of the lane's 17 candidates as a bit mask (the list-B test reads it)
     uint32_t amask = 0;
 #pragma unroll
@@ -974,6 +980,7 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
     const uint32_t uBL = wave_min_u32(top ? ~0u : best0) >> 17;
     const uint32_t uBR = wave_min_u32(top ? ~0u : best1) >> 17;
     // ---- 3. the sub-block survivors (B): some sub-block bound <= its U_j, not evaluated in A ----
+    SO_MARK(vbs_list_b);
     typedef short so_v2i16 __attribute__((ext_vector_type(2)));
     const uint32_t thT = (((uTL + 60) >> 4) + 1) | ((((uTR + 60) >> 4) + 1) << 16);
     const uint32_t thB = (((uBL + 60) >> 4) + 1) | ((((uBR + 60) >> 4) + 1) << 16);
@@ -1003,6 +1010,7 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     vbs_eval_list<G>(L, mylist, nB, cs, bxl, byl, lane, bestB, best0, best1);
+    SO_MARK(vbs_final);
     const uint64_t kb = wave_min_u64_dpp(bestB);
     // the 32-bit sub-block keys widened to the 64-bit key layout (SAD << 32 | md << 24 | cand)
     const auto widen = [](uint32_t k) {
@@ -1287,6 +1295,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
                         SO_OPS_ADD(&st_ops, kDenseSadOps);
                     }
 #ifndef SO_TEST_NODENSE
+                    SO_MARK(vbs_dense);
                     wave_dense_block<16, true, RP, 0, false, true>(win, keys, G::NBLK, cur, W, H, x, y, bxl, byl, u,
                                                                    tid, r);
 #endif
@@ -2007,7 +2016,7 @@ SO_DEV void unpack_i16(const uint32_t* p, int* v) {
 
 template <class G, bool SC1, bool HALO = false>
 SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, int bx0, int byt0, int nbx,
-                     int by0, int by1, int W, int qp_rd, const int32_t* __restrict__ qp_row,
+                         int by0, int by1, int W, int qp_rd, const int32_t* __restrict__ qp_row,
                          const int32_t* __restrict__ qp_map, double lam, const PFrameOut& o) {
     constexpr int SR = G::SR, TBX = G::TBX;
     const int bxl = g % TBX, byl = g / TBX;
@@ -2022,13 +2031,16 @@ SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, in
     const int dx = S.mer[g][0], dy = S.mer[g][1], rf = S.mer[g][2], sad = S.mer[g][3];
     const int prow = byl * 16 + SR + dy + l, pcol = bxl * 16 + SR + dx;   // window coordinates
     const uint32_t* crow = S.curt + (byl * 16 + l) * G::CPD + bxl * 4;
-    // the coefficients survive the RD decision (packed int16 pairs: |TC| <= 4080), and without
-    // SO_VBS_LEAN also the levels at the RD QP (qp8 / qsp: reused when the final QP is the RD QP,
-    // otherwise requantised from the coefficients in int32); SO_VBS_LEAN always requantises --
-    // the levels would keep 16 more VGPRs live across the sub-block transforms
-    constexpr int NQ = SO_VBS_LEAN ? 1 : 8;
-    uint32_t tcp[8], qp8[NQ], qsp[NQ];
+    // The chosen levels go to the block's QTC rows.  The block's levels at the RD QP are stored
+    // there as soon as they exist: when the block is not split and its QP is the RD QP (no
+    // per-row / per-block QP: always), that store is final, neither the levels nor their tokens
+    // are recomputed, and tq16_vbs_inv reads them back from there (after the tile's barrier; the
+    // same workgroup, so the same L1).  A split block's levels also wait in its scratch for the
+    // inverse.  Only the block's coefficients stay in registers through the sub-block
+    // transforms (packed int16 pairs, |TC| <= 4080), to requantise at another QP.
+    uint32_t tcp[8];
     int tok_b = 0;
+    SO_MARK(vbs_fwd);
     {
         int res[16];
         uint32_t pw[4];
@@ -2041,27 +2053,23 @@ SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, in
         }
         double tcr[16];
         xform2d_rows<16, false>(scratch, l, res, tcr, SO_TQ_TW());
-        int tc[16];
+        int tc[16], q[16];
 #pragma unroll
         for (int c = 0; c < 16; ++c) tc[c] = (int)__builtin_rint(tcr[c]);
-        if (!SO_VBS_LEAN || (x != 0 && y != 0)) {   // uniform
-            int q[16];
-            quant_row_int<16>(tc, l, qp_rd, q);
-            if (x != 0 && y != 0) tok_b = block_tokens<16>(nullptr, l, q);
-            if constexpr (!SO_VBS_LEAN) pack_i16<16>(q, qp8);
-        }
+        quant_row_int<16>(tc, l, qp_rd, q);
+        tok_b = block_tokens<16>(nullptr, l, q);
+        store_row_i16<16>(o.qtc + b * 256 + l * 16, q);
         pack_i16<16>(tc, tcp);
     }
     bool split = false;
-    int mae_num = sad;
+    int mae_num = sad, tok = tok_b;
     const int j = l >> 2, r0 = l & 3;
-    int sdx = 0, sdy = 0, sref = 0;
-    uint32_t stcp[8];   // the sub-blocks' coefficients, packed
-    const int sxl = bxl * 16 + (j & 1) * 8, syl = byl * 16 + (j >> 1) * 8;   // sub-block in the tile (px)
     const int qpm1_rd = qp_rd > 0 ? qp_rd - 1 : qp_rd;
     if (x != 0 && y != 0) {   // uniform
+        SO_MARK(vbs_fwd_sub);
         const MeRec& sm = S.mer[G::NBLK + 4 * g + j];
-        sdx = sm[0]; sdy = sm[1]; sref = sm[2];
+        const int sdx = sm[0], sdy = sm[1], sref = sm[2];
+        const int sxl = bxl * 16 + (j & 1) * 8, syl = byl * 16 + (j >> 1) * 8;   // sub-block in the tile (px)
         int sres[2][8];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -2087,10 +2095,23 @@ SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, in
             quant_row_int<8>(stc[h], r0 + 4 * h, qpm1_rd, qs[h]);
         }
         const int tok_v = sub_tokens_reg(l, qs);
+        // the sub-blocks' levels and coefficients wait in the (now free) transpose scratch, packed:
+        // [l * 8, +8) the levels (an int16 row pair per lane, as the QTC rows hold them), [128 + l
+        // * 8, +8) the coefficients -- through the decision the lanes hold only the block's tcp
+        uint32_t* const sl = reinterpret_cast<uint32_t*>(scratch);
+        {
+            uint32_t pq[8], pc[8];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            pack_i16<8>(stc[h], stcp + 4 * h);
-            if constexpr (!SO_VBS_LEAN) pack_i16<8>(qs[h], qsp + 4 * h);
+            for (int h = 0; h < 2; ++h) {
+                pack_i16<8>(qs[h], pq + 4 * h);
+                pack_i16<8>(stc[h], pc + 4 * h);
+            }
+            so_v4u* const d = reinterpret_cast<so_v4u*>(sl + l * 8);
+            d[0] = so_v4u{pq[0], pq[1], pq[2], pq[3]};
+            d[1] = so_v4u{pq[4], pq[5], pq[6], pq[7]};
+            so_v4u* const e = reinterpret_cast<so_v4u*>(sl + 128 + l * 8);
+            e[0] = so_v4u{pc[0], pc[1], pc[2], pc[3]};
+            e[1] = so_v4u{pc[4], pc[5], pc[6], pc[7]};
         }
         int ssum = 0;
         bool vinf = false;
@@ -2105,47 +2126,53 @@ SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, in
         const double c_v = rd_cost(lam, 64 + 8 * tok_v, mae_v);
         const double c_b = rd_cost(lam, 16 + 8 * tok_b, mae_b);
         split = !(c_b < c_v);
-        mae_num = vinf ? -1 : ssum;
-    }
-    // the chosen levels at the block's final QP: QTC, tokens and the block records now; the
-    // levels into the block's (now free) transpose scratch for tq16_vbs_inv (after the tile's
-    // barrier, in split-sorted order)
-    uint32_t* const lv = reinterpret_cast<uint32_t*>(scratch) + l * 8;
-    int tok;
-    if (!split) {
-        int q[16];
-        if (SO_VBS_LEAN || qpr != qp_rd) {
-            int tc[16];
-            unpack_i16<16>(tcp, tc);
-            quant_row_int<16>(tc, l, qpr, q);
-        } else {
-            unpack_i16<16>(qp8, q);
-        }
-        tok = block_tokens<16>(nullptr, l, q);
-        store_row_i16<16>(o.qtc + b * 256 + l * 16, q);
-        pack_i16<16>(q, lv);
-        if (l < 12) o.mv[b * 12 + l] = (int16_t)(l == 0 ? dx : l == 1 ? dy : l == 2 ? rf : 0);
-    } else {
-        const int qpm1 = qpr > 0 ? qpr - 1 : qpr;
-        int qs[2][8];
-        if (SO_VBS_LEAN || qpm1 != qpm1_rd) {
+        SO_MARK(vbs_final_q);
+        if (split) {   // uniform: the sub-blocks' levels at the block's final QP - 1
+            mae_num = vinf ? -1 : ssum;
+            const int qpm1 = qpr > 0 ? qpr - 1 : qpr;
+            so_v4u* const d = reinterpret_cast<so_v4u*>(sl + l * 8);
+            if (qpm1 != qpm1_rd) {   // uniform: requantise the coefficients at the block's QP - 1
+                const so_v4u* const e = reinterpret_cast<const so_v4u*>(sl + 128 + l * 8);
+                int qf[2][8];
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                int stc[8];
-                unpack_i16<8>(stcp + 4 * h, stc);
-                quant_row_int<8>(stc, r0 + 4 * h, qpm1, qs[h]);
+                for (int h = 0; h < 2; ++h) {
+                    const so_v4u v = e[h];
+                    const uint32_t pc[4] = {v[0], v[1], v[2], v[3]};
+                    int t8[8];
+                    unpack_i16<8>(pc, t8);
+                    int rq = r0 + 4 * h;
+                    asm volatile("" : "+v"(rq));   // (as lq below)
+                    quant_row_int<8>(t8, rq, qpm1, qf[h]);
+                }
+                tok = sub_tokens_reg(l, qf);
+                uint32_t pq[8];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) pack_i16<8>(qf[h], pq + 4 * h);
+                d[0] = so_v4u{pq[0], pq[1], pq[2], pq[3]};
+                d[1] = so_v4u{pq[4], pq[5], pq[6], pq[7]};
+            } else {
+                tok = tok_v;
             }
-        } else {
+            // the packed pairs are the QTC rows' int16 layout: 16-byte stores as they stand
 #pragma unroll
-            for (int h = 0; h < 2; ++h) unpack_i16<8>(qsp + 4 * h, qs[h]);
+            for (int h = 0; h < 2; ++h)
+                *reinterpret_cast<so_v4u*>(o.qtc + b * 256 + j * 64 + (r0 + 4 * h) * 8) = d[h];
+            if (r0 < 3) o.mv[b * 12 + 3 * j + r0] = (int16_t)(r0 == 0 ? sdx : r0 == 1 ? sdy : sref);
         }
-        tok = sub_tokens_reg(l, qs);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            store_row_i16<8>(o.qtc + b * 256 + j * 64 + (r0 + 4 * h) * 8, qs[h]);
-            pack_i16<8>(qs[h], lv + 4 * h);
+    }
+    // the row index behind an optimisation barrier for the requantisations below: otherwise the
+    // per-coefficient exponents of the RD-QP quantisation are kept (spilled) to be reused here
+    int lq = l;
+    asm volatile("" : "+v"(lq));
+    if (!split) {
+        if (qpr != qp_rd) {   // uniform: requantise at the block's own QP
+            int tc[16], q[16];
+            unpack_i16<16>(tcp, tc);
+            quant_row_int<16>(tc, lq, qpr, q);
+            tok = block_tokens<16>(nullptr, l, q);
+            store_row_i16<16>(o.qtc + b * 256 + l * 16, q);
         }
-        if (r0 < 3) o.mv[b * 12 + 3 * j + r0] = (int16_t)(r0 == 0 ? sdx : r0 == 1 ? sdy : sref);
+        if (l < 12) o.mv[b * 12 + l] = (int16_t)(l == 0 ? dx : l == 1 ? dy : l == 2 ? rf : 0);
     }
     if (l == 0) {
         S.vsp[g] = (uint8_t)split;
@@ -2159,10 +2186,9 @@ SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, in
 // order (unsplit blocks first, then split ones, then none): the four blocks of a wave then
 // take one of the two inverse paths -- a wave with both ran both (about two waves in three on
 // the bench content, split ~50 %), now at most one wave per tile does.  Reads the levels
-// tq16_vbs_fwd left in the block's scratch (`un`: the tile's transpose scratch; block g's is
-// un + g * kTqScratchVbs, and the slot's lanes use it for the transposes too, once the levels are
-// in registers: the slot -> block map is a permutation, so no other lanes touch it);
-// dequantisation, IDCT, reconstruction and SSE.
+// tq16_vbs_fwd left -- an unsplit block's in its QTC rows (this workgroup's stores, before the
+// barrier), a split one's packed in its scratch; dequantisation, IDCT, reconstruction and SSE.  `un`: the tile's transpose scratch (slot k's
+// lanes use block g's part, un + g * kTqScratchVbs: the slot -> block map is a permutation).
 template <class G, bool SC1, bool HALO = false>
 SO_DEV void tq16_vbs_inv(PTileLds<G, true>& S, int k, int l, double* un, int bx0, int byt0, int nbx,
                          int by0, int by1, int W, int qp_rd, const int32_t* __restrict__ qp_row,
@@ -2189,15 +2215,8 @@ SO_DEV void tq16_vbs_inv(PTileLds<G, true>& S, int k, int l, double* un, int bx0
     const size_t b = (size_t)(gby - by0) * nbx + gbx;
     const int x = gbx * 16, y = gby * 16;
     const int qpr = qp_map ? qp_map[(size_t)gby * nbx + gbx] : (qp_row ? qp_row[gby] : qp_rd);
+    SO_MARK(vbs_inv);
     double* const scratch = un + g * kTqScratchVbs;
-    uint32_t lv[8];
-    {
-        const so_v4u* lp = reinterpret_cast<const so_v4u*>(reinterpret_cast<const uint32_t*>(scratch) + l * 8);
-        const so_v4u a = lp[0], b = lp[1];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { lv[e] = a[e]; lv[4 + e] = b[e]; }
-    }
-    wave_sync();   // every lane's levels read before the transposes below overwrite them
     const uint32_t* crow = S.curt + (byl * 16 + l) * G::CPD + bxl * 4;
     const int j = l >> 2, r0 = l & 3;
     int sse = 0;
@@ -2205,7 +2224,7 @@ SO_DEV void tq16_vbs_inv(PTileLds<G, true>& S, int k, int l, double* un, int bx0
         const int dx = S.mer[g][0], dy = S.mer[g][1];
         const int prow = byl * 16 + SR + dy + l, pcol = bxl * 16 + SR + dx;   // window coordinates
         int q[16], dq[16];
-        unpack_i16<16>(lv, q);
+        load_row_i16<16>(o.qtc + b * 256 + l * 16, q);
         dequant_row_int<16>(q, l, qpr, dq);
         double rd[16];
         xform2d_rows<16, true>(scratch, l, dq, rd, SO_TQ_TW());
@@ -2230,16 +2249,23 @@ SO_DEV void tq16_vbs_inv(PTileLds<G, true>& S, int k, int l, double* un, int bx0
             }
         }
     } else {
+        SO_MARK(vbs_inv_split);
         const int qpm1 = qpr > 0 ? qpr - 1 : qpr;
         const MeRec& sm = S.mer[G::NBLK + 4 * g + j];
         const int sdx = sm[0], sdy = sm[1];
         const int sxl = bxl * 16 + (j & 1) * 8, syl = byl * 16 + (j >> 1) * 8;   // sub-block in the tile (px)
         int sdq[2][8];
+        {   // the levels tq16_vbs_fwd left packed in the block's scratch (read before the transposes)
+            const so_v4u* const d = reinterpret_cast<const so_v4u*>(reinterpret_cast<const uint32_t*>(scratch) + l * 8);
+            const so_v4u v0 = d[0], v1 = d[1];
+            wave_sync();
+            const uint32_t pq[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            int qs[8];
-            unpack_i16<8>(lv + 4 * h, qs);
-            dequant_row_int<8>(qs, r0 + 4 * h, qpm1, sdq[h]);
+            for (int h = 0; h < 2; ++h) {
+                int qs[8];
+                unpack_i16<8>(pq + 4 * h, qs);
+                dequant_row_int<8>(qs, r0 + 4 * h, qpm1, sdq[h]);
+            }
         }
         double srd[2][8];
         xform2d_sub<true>(scratch, l, sdq, srd, SO_TQ_TW8());
@@ -2268,6 +2294,7 @@ SO_DEV void tq16_vbs_inv(PTileLds<G, true>& S, int k, int l, double* un, int bx0
             }
         }
     }
+    SO_MARK(vbs_inv_end);
     if (o.sse) {
         sse = group_sum<16>(sse);
         if (l == 0) o.sse[b] = sse;
@@ -2574,12 +2601,12 @@ template <int NW, bool TOK = false>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE)))
 p_tile_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W, int by0, int by1, int qp_rd,
               const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best,
-              PFrameOut o) {
+              PFrameOut o, const int16_t* prev_mv) {
     using G = Sea2GeoT<NW>;
     __shared__ PTileLds<G> S;
     SO_STAMP_REC_SET(g_sea_stamps ? g_sea_stamps + (size_t)blockIdx.x * 12 : nullptr);
     ptile_body<G, false, NoPre, false, TOK>(S, blockIdx.x, cur, refs.p[0], H, W, by0, by1, qp_rd, qp_row, qp_map,
-                                            out_best, o);
+                                            out_best, o, NoPre(), PHalo{}, 0.0, nullptr, nullptr, 0, NoPre(), prev_mv);
 #ifdef SO_STAMPS
     const int tid = threadIdx.x;
     if (tid == 0) {   // tools/sea_stamps.py (STAMP_FUSED=1): epilogue = records + transforms
@@ -2594,20 +2621,21 @@ p_tile_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W, int by
 #endif
 }
 
+// prev_mv (may be null): the previous frame's motion records, the search's U hint (sea2_tile)
 int p_tile_launch(const uint8_t* cur, const RefSet& refs, int H, int W, int by0, int by1, int qp_rd,
                   const int32_t* qp_row, const int32_t* qp_map, int32_t* out_best, uint8_t* out_split,
                   int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon,
-                  int32_t* out_sse, hipStream_t st, bool tokens_only) {
+                  int32_t* out_sse, hipStream_t st, bool tokens_only, const int16_t* prev_mv) {
     const int nbx = W / 16, nrows = by1 - by0;
     if (nrows <= 0) return SO_OK;
     const dim3 grid(((nbx + Sea2Geo::TBX - 1) / Sea2Geo::TBX) * ((nrows + Sea2Geo::TBY - 1) / Sea2Geo::TBY));
     const PFrameOut o{out_split, out_mv, out_qtc, out_tokens, out_mae, out_recon, out_sse, nullptr};
     if (tokens_only)
         hipLaunchKernelGGL((p_tile_kernel<SO_PTILE_NW, true>), grid, dim3(SO_PTILE_NW * 64), 0, st, cur, refs, H, W,
-                           by0, by1, qp_rd, qp_row, qp_map, out_best, o);
+                           by0, by1, qp_rd, qp_row, qp_map, out_best, o, prev_mv);
     else
         hipLaunchKernelGGL((p_tile_kernel<SO_PTILE_NW, false>), grid, dim3(SO_PTILE_NW * 64), 0, st, cur, refs, H, W,
-                           by0, by1, qp_rd, qp_row, qp_map, out_best, o);
+                           by0, by1, qp_rd, qp_row, qp_map, out_best, o, prev_mv);
     return check_launch("p_tile_kernel");
 }
 

@@ -9,6 +9,7 @@ these tensors only when asked.
 from __future__ import annotations
 
 import collections
+import contextlib
 from dataclasses import dataclass, field
 
 import ctypes
@@ -75,6 +76,7 @@ class Engine:
         self._fme_ws = None
         self._consts: collections.OrderedDict = collections.OrderedDict()   # device_const_i32 (LRU)
         self._pinned_consts: set = set()                                    # ... held by captured graphs
+        self._pin_depth = 0   # > 0 inside pinned_consts()
         self.wait_health = runhealth.HealthLog()   # non-fatal wait counts of the persistent runs
 
     MAX_CONSTS = 4096
@@ -84,10 +86,12 @@ class Engine:
         a GOP replayed from a captured HIP graph issues no host->device copy.
 
         The cache is LRU-bounded at MAX_CONSTS entries, except that an entry looked up while
-        a HIP graph is being captured on this device is pinned: the graph holds its raw
-        device pointer, so evicting it would make a later replay read freed memory.  Pinned
-        entries are dropped only by release_consts(), which the owner of such a graph calls
-        once the graph is gone."""
+        a HIP graph is being captured on this device, or inside `with engine.pinned_consts():`,
+        is pinned: a graph holds its raw device pointer, so evicting it would make a later replay
+        read freed memory.  A constant fetched BEFORE a capture and only used inside it must be
+        fetched again inside the capture or under pinned_consts() (the facade looks its constants
+        up on every call, so a captured encode re-fetches them).  Pinned entries are dropped only
+        by release_consts(), which the owner of such a graph calls once the graph is gone."""
         host = torch.as_tensor(values, dtype=torch.int32).contiguous()
         key = (tuple(host.shape), host.numpy().tobytes())
         t = self._consts.get(key)
@@ -100,9 +104,19 @@ class Engine:
                         break
         else:
             self._consts.move_to_end(key)
-        if self.device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+        if self._pin_depth > 0 or (self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()):
             self._pinned_consts.add(key)
         return t
+
+    @contextlib.contextmanager
+    def pinned_consts(self):
+        """Every device constant looked up inside the block is pinned (never LRU-evicted): for
+        constants fetched ahead of a graph capture that the graph will use."""
+        self._pin_depth += 1
+        try:
+            yield self
+        finally:
+            self._pin_depth -= 1
 
     def release_consts(self) -> None:
         """Drop the cached device constants (ROI offsets, row-QP schedules), pinned ones too.

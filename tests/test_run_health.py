@@ -106,6 +106,7 @@ class _ConstHost:
         self.device = torch.device("cpu")
         self._consts = collections.OrderedDict()
         self._pinned_consts = set()
+        self._pin_depth = 0
 
 
 def test_device_consts_are_lru_bounded_not_fatal():
@@ -123,3 +124,8 @@ def test_device_consts_are_lru_bounded_not_fatal():
     assert ((1,), torch.tensor([9], dtype=torch.int32).numpy().tobytes()) in h._consts   # pinned: kept
     Engine.release_consts(h)
     assert not h._consts and not h._pinned_consts
+    with Engine.pinned_consts(h):                   # fetched ahead of a capture: pinned explicitly
+        get([77])
+    for k in range(40, 50):
+        get([k])
+    assert ((1,), torch.tensor([77], dtype=torch.int32).numpy().tobytes()) in h._consts and h._pin_depth == 0

@@ -11,6 +11,9 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from ab_runs import CHILD  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from ab_guard import require_ab_build  # noqa: E402
+require_ab_build()
 
 
 def main():

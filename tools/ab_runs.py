@@ -11,6 +11,9 @@ import json, os, sys, time, torch
 sys.path.insert(0, ".")
 from streamoptima_amd.engine import Engine, alloc_planes
 from streamoptima_amd.synth import synth_sequence_torch
+sys.path.insert(0, "tools")
+from ab_guard import require_ab_build  # noqa: E402  (the child runs from the repo root)
+require_ab_build()
 dev = torch.device("cuda:0")
 out = {}
 for h, w in ((2160, 3840), (1088, 1920), (272, 3840)):

@@ -18,6 +18,9 @@ h, w = 2160, 3840
 fr = alloc_planes(3, h, w, dev)
 fr.copy_(synth_sequence_torch(3, h, w, seed=0, device=dev))
 import os
+sys.path.insert(0, "tools")
+from ab_guard import require_ab_build  # noqa: E402  (the child runs from the repo root)
+require_ab_build()
 eng = Engine(h, w, 16, 16, os.environ.get("PROBE_VBS") == "1", 0.015, dev, me_mode=_lib.ME_FAST)
 i0 = eng.encode_i(fr[0], 4)
 p1 = eng.encode_p(fr[1], [i0.recon], 4)

@@ -6,19 +6,19 @@
 # come back (the raw per-dispatch CSVs exceed gpurun's 64 MiB).
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-mkdir -p gpurun_out/traffic gpurun_out/pmc_r04
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
+mkdir -p gpurun_out/traffic gpurun_out/pmc_${TAG}
 export PMC_JSON=gpurun_out/pmc_me_traffic.json
 cp profiles/pmc_me_traffic.json $PMC_JSON
 for cfg in ${CFGS:-4k 1080p 4k_vbs 4k_rc2pass 4k_lowtex 4k_noise}; do
   bash tools/gpu_traffic.sh $TAG $cfg || exit $?
-  python tools/traffic_json.py gpurun_out/traffic $TAG $cfg > gpurun_out/pmc_r04/traffic_${cfg}.txt 2>&1 || exit $?
+  python tools/traffic_json.py gpurun_out/traffic $TAG $cfg > gpurun_out/pmc_${TAG}/traffic_${cfg}.txt 2>&1 || exit $?
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/traffic/${TAG}_${cfg}_trace -o run -- \
       python3 bench.py --config $cfg --steps 3 --warmup 1 --kernel-reps 5 --no-cpu-baseline --no-records --no-pcie \
-      --no-parity > gpurun_out/pmc_r04/trace_${cfg}.log 2>&1
+      --no-parity > gpurun_out/pmc_${TAG}/trace_${cfg}.log 2>&1
   rc=$?; echo "trace $cfg rc=$rc"; [ $rc -ne 0 ] && exit $rc
   f=$(find gpurun_out/traffic/${TAG}_${cfg}_trace -name "*kernel_stats.csv" | head -1)
-  [ -n "$f" ] && cp "$f" gpurun_out/pmc_r04/kernel_stats_${cfg}.csv
+  [ -n "$f" ] && cp "$f" gpurun_out/pmc_${TAG}/kernel_stats_${cfg}.csv
   rm -rf gpurun_out/traffic/${TAG}_${cfg}_*
 done
 rm -rf gpurun_out/traffic

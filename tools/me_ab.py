@@ -9,6 +9,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from streamoptima_amd import _lib
 from streamoptima_amd.engine import alloc_planes
 from streamoptima_amd.synth import synth_sequence_torch
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from ab_guard import require_ab_build  # noqa: E402
+require_ab_build()
 
 VARIANTS = {"sea": {}, "dense": {"SO_ME_IMPL": "dense"}}
 

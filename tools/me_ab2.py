@@ -11,6 +11,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from streamoptima_amd import _lib  # noqa: E402
 from streamoptima_amd.engine import Engine, alloc_planes  # noqa: E402
 from streamoptima_amd.synth import synth_sequence_torch  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from ab_guard import require_ab_build  # noqa: E402
+require_ab_build()
 
 VARIANTS = {"sea": {}, "dense": {"SO_ME_IMPL": "dense"}, "probe_stage": {"SO_SEA_PROBE": "1"},
             "probe_bounds": {"SO_SEA_PROBE": "2"}, "probe_nofallback": {"SO_SEA_PROBE": "3"},

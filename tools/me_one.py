@@ -6,6 +6,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from streamoptima_amd import _lib
 from streamoptima_amd.engine import Engine, alloc_planes
 from streamoptima_amd.synth import synth_sequence_torch
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from ab_guard import require_ab_build  # noqa: E402
+require_ab_build()
 h, w, n = 2160, 3840, int(os.environ.get("ME_N", 10))
 vbs = os.environ.get("ME_VBS", "0") == "1"
 dev = torch.device("cuda:0")

@@ -15,6 +15,9 @@ from bench import build_codec, make_frames, parse
 from streamoptima_amd.workloads import WORKLOADS
 dev = torch.device("cuda:0")
 import os
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from ab_guard import require_ab_build  # noqa: E402
+require_ab_build()
 cfg = dict(WORKLOADS[os.environ.get("AB_CFG", "4k_rc2pass")])
 codec = build_codec(cfg, parse([]), dev)
 if os.environ.get("AB_FUSED") == "1":   # both passes in one persistent launch (needs SO_RUN_2PASS=1)

@@ -22,7 +22,8 @@ sys.path.insert(0, ROOT)
 NAMES = ("loop_top stage_cur stage_cur_int stage_cur_edge cur_sums wait poll_iter stage_win stage_win_int "
          "stage_win_edge dense_tile dense_tile_block byte_sums block_top bound umin umin_edge ballots bal_row dense_fallback survivors "
          "sur_one sur_le4 sur_pass search_end decode_keys tq_residual tq_fwd tq_quant tq_tokens tq_qtc_store tq_inv "
-         "tq_recon tq_sse_records post done_flag task_end").split()
+         "tq_recon tq_sse_records post done_flag task_end vbs_block vbs_umin vbs_list_a vbs_pass vbs_list_b vbs_final "
+         "vbs_dense vbs_fwd vbs_fwd_sub vbs_final_q vbs_inv vbs_inv_split vbs_inv_end").split()
 
 
 def count():
@@ -55,9 +56,10 @@ def count():
 
 
 def table(path, pmc_valu=None):
-    cen = json.loads(subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_census.py"), "--json"],
-                                    capture_output=True, text=True, check=True).stdout)
     d = json.load(open(path))
+    kernel = f"p_run_kernel<8, 0, {'true' if d.get('vbs') else 'false'}, false>"
+    cen = json.loads(subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_census.py"), "--json",
+                                     "--kernel", kernel], capture_output=True, text=True, check=True).stdout)
     per_launch = {k: v / d["launches"] for k, v in d["counts"].items()}
     blocks = d["frames_per_launch"] * d["blocks_per_frame"]
     rows, tot = [], 0.0
