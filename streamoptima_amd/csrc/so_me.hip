@@ -2126,9 +2126,9 @@ SO_DEV void tq16_vbs_fwd(PTileLds<G, true>& S, int g, int l, double* scratch, in
         const double c_v = rd_cost(lam, 64 + 8 * tok_v, mae_v);
         const double c_b = rd_cost(lam, 16 + 8 * tok_b, mae_b);
         split = !(c_b < c_v);
+        mae_num = vinf ? -1 : ssum;   // the sub-blocks' SAD sum, split or not (as inter_tq_kernel)
         SO_MARK(vbs_final_q);
         if (split) {   // uniform: the sub-blocks' levels at the block's final QP - 1
-            mae_num = vinf ? -1 : ssum;
             const int qpm1 = qpr > 0 ? qpr - 1 : qpr;
             so_v4u* const d = reinterpret_cast<so_v4u*>(sl + l * 8);
             if (qpm1 != qpm1_rd) {   // uniform: requantise the coefficients at the block's QP - 1
