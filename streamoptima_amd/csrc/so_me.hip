@@ -697,7 +697,7 @@ extern "C" int so_debug_set_run_stamps(void* p) {
     X(search_end) X(decode_keys) X(tq_residual) X(tq_fwd) X(tq_quant) X(tq_tokens) X(tq_qtc_store) X(tq_inv) \
     X(tq_recon) X(tq_sse_records) X(post) X(done_flag) X(task_end) X(vbs_block) X(vbs_umin) X(vbs_list_a) \
     X(vbs_pass) X(vbs_list_b) X(vbs_final) X(vbs_dense) X(vbs_fwd) X(vbs_fwd_sub) X(vbs_final_q) X(vbs_inv) \
-    X(vbs_inv_split) X(vbs_inv_end)
+    X(vbs_inv_split) X(vbs_inv_end) X(wait_w0) X(keys_tail)
 #define SO_MARK_ENUM(n) kMark_##n,
 enum SoMarkId { SO_MARK_NAMES(SO_MARK_ENUM) kMarkCount };
 #undef SO_MARK_ENUM
@@ -2344,12 +2344,12 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
                            dense_flag, prev_mv);   // ends with a barrier
 
     const int tid = opaque_tid();
-    SO_MARK(decode_keys);
     SO_SEA_STAMP(5, __builtin_amdgcn_s_memtime());
     const int nbx = W / 16;
     const int tiles_x = (nbx + TBX - 1) / TBX;
     const int bx0 = (tile % tiles_x) * TBX, byt0 = by0 + (tile / tiles_x) * TBY;
     for (int i = tid; i < PTileLds<G, VBS>::NU; i += G::NTHREADS) {
+        SO_MARK(decode_keys);
         int32_t rec4[4];
         decode_key(S.keys[i], SR, rec4);
         S.mer[i].set(rec4);
@@ -2359,6 +2359,7 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
             ob[0] = S.mer[i][0]; ob[1] = S.mer[i][1]; ob[2] = S.mer[i][2]; ob[3] = S.mer[i][3];
         }
     }
+    SO_MARK(keys_tail);
     // the tile's dense-block count (p_run_kernel: the next frame's same tile reads it), stored
     // write-through now so that the drain below covers it
     if (fb_out != nullptr && tid == 0) store_sc1_i32(fb_out, (int)S.st[0]);
@@ -2973,6 +2974,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             const bool remote = STRIPE && (first_row ? sp.my_up_flags != nullptr : false);
             const bool remote_dn = STRIPE && (last_row ? sp.my_dn_flags != nullptr : false);
             if (!FPIPE && dep < 0 && !remote && !remote_dn) return;
+            SO_MARK(wait_w0);
 #ifdef SO_STAMPS
             if (lane == 0 && rec) rec[9] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -3168,7 +3170,9 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd, qp_row, nullptr, nullptr, a.out[f], wait_ref, PHalo{}, lam,
                 &s_dense, reinterpret_cast<int32_t*>(tilefb) + (size_t)f * ntiles + tile, count_ops, take_next,
                 // VBS: the same hint for the block's U measured slower (4K VBS P-frame 123.1 vs
-                // 121.3 us: 8 more VGPR spills; profiles/r05/hint_ab_vbs.log)
+                // 121.3 us: 8 more VGPR spills; profiles/r05/hint_ab_vbs.log), appended to list A
+                // (its quadrant SADs bounding the sub-block U_j) 117.8 vs 115.9 us (6 more spills;
+                // profiles/r05/vbs_ab6_lista_hint.log)
                 !VBS && dep >= 0 ? a.out[dep].mv : nullptr);
             SO_RUN_PROF(52, __builtin_amdgcn_s_memtime() - pt0);
             SO_MARK(done_flag);

@@ -40,6 +40,7 @@ def census(asm: str, fn: str) -> dict:
         m = re.search(r";SO_MARK (\w+)", l)
         if m:
             cur = m.group(1)
+            out.setdefault(cur, collections.Counter())["copies"] += 1   # unrolled / duplicated markers
             continue
         ins = l.strip().split(" ")[0] if l.startswith("\t") or l.startswith(" ") else ""
         if not ins or ins.startswith((";", ".")):
@@ -84,7 +85,7 @@ def main():
     if a.json:
         print(json.dumps({k: dict(v) for k, v in res.items()}))
         return
-    cols = ("valu", "fp64", "sad", "lane_rw", "readfirstlane", "scratch", "lds", "vmem", "salu_smem")
+    cols = ("copies", "valu", "fp64", "sad", "lane_rw", "readfirstlane", "scratch", "lds", "vmem", "salu_smem")
     print(f"{a.kernel}  (static instructions per phase, layout order)")
     print(f"{'phase':16s}" + "".join(f"{c:>14s}" for c in cols))
     tot = collections.Counter()

@@ -23,7 +23,7 @@ NAMES = ("loop_top stage_cur stage_cur_int stage_cur_edge cur_sums wait poll_ite
          "stage_win_edge dense_tile dense_tile_block byte_sums block_top bound umin umin_edge ballots bal_row dense_fallback survivors "
          "sur_one sur_le4 sur_pass search_end decode_keys tq_residual tq_fwd tq_quant tq_tokens tq_qtc_store tq_inv "
          "tq_recon tq_sse_records post done_flag task_end vbs_block vbs_umin vbs_list_a vbs_pass vbs_list_b vbs_final "
-         "vbs_dense vbs_fwd vbs_fwd_sub vbs_final_q vbs_inv vbs_inv_split vbs_inv_end").split()
+         "vbs_dense vbs_fwd vbs_fwd_sub vbs_final_q vbs_inv vbs_inv_split vbs_inv_end wait_w0 keys_tail").split()
 
 
 def count():
@@ -64,18 +64,20 @@ def table(path, pmc_valu=None):
     blocks = d["frames_per_launch"] * d["blocks_per_frame"]
     rows, tot = [], 0.0
     for n in NAMES:
-        st = cen.get(n, {}).get("valu", 0)
+        c = cen.get(n, {})
+        k = max(1, c.get("copies", 1))   # a marker the compiler unrolled / duplicated: per copy
+        st = c.get("valu", 0) / k
         ex = per_launch.get(n, 0.0)
         dyn = st * ex
         tot += dyn
-        rows.append((n, st, ex / blocks, dyn / blocks, cen.get(n, {}).get("fp64", 0) * ex / blocks,
-                     cen.get(n, {}).get("sad", 0) * ex / blocks, cen.get(n, {}).get("lane_rw", 0) * ex / blocks))
+        rows.append((n, round(st, 1), ex / blocks, dyn / blocks, c.get("fp64", 0) / k * ex / blocks,
+                     c.get("sad", 0) / k * ex / blocks, c.get("lane_rw", 0) / k * ex / blocks))
     pro = cen.get("prologue", {}).get("valu", 0)
     print(f"{'phase':18s}{'static VALU':>12s}{'runs/block':>12s}{'VALU/block':>12s}{'FP64/block':>12s}"
           f"{'SAD/block':>12s}{'lane r/w':>10s}")
     for r in rows:
         if r[2] > 0:
-            print(f"{r[0]:18s}{r[1]:12d}{r[2]:12.4f}{r[3]:12.1f}{r[4]:12.1f}{r[5]:12.1f}{r[6]:10.2f}")
+            print(f"{r[0]:18s}{r[1]:12.1f}{r[2]:12.4f}{r[3]:12.1f}{r[4]:12.1f}{r[5]:12.1f}{r[6]:10.2f}")
     print(f"{'TOTAL':18s}{'':12s}{'':12s}{tot / blocks:12.1f}   (+ prologue {pro} static per wave, once per launch)")
     if pmc_valu:
         print(f"PMC SQ_INSTS_VALU per launch {pmc_valu:.4g} = {pmc_valu / blocks:.1f} per block; census / PMC = "
