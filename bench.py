@@ -382,12 +382,16 @@ def roofline_of(rl: dict, config: str) -> dict:
 
 
 def rc_roofline(codec, frames_dev, symbols, reps: int, config: str) -> dict:
-    """configs[4] (ROI + two-pass RC): its P-frames run as a per-frame kernel sequence -- pass 1
-    (p_tile_kernel<8, true>: search + forward transform for the token counts), so_qp_map, pass 2
-    (inter_tq_kernel on pass 1's motion vectors, SO_REUSE_ME) -- replayed here with HIP events on
-    the launch stream over the timed GOP's references.  The HBM fraction of a P-frame's
-    algorithmic bytes (as the one-pass roofline) over that sequence's time; the VALU busy
-    fraction of the pass-1 kernel from the committed PMC counters."""
+    """configs[4] (ROI + two-pass RC): its P-run as the timed GOP enqueues it
+    (so_encode_p_run_2pass) -- by default both passes in one persistent launch
+    (p_run_kernel<8, 3>: each task the pass 2 of one tile, then the pass 1 of another), with
+    SO_OPT_RUN_2PASS_FUSED = 0 the per-frame sequence (p_tile_kernel<8, true> pass 1,
+    inter_tq_kernel<16, false, false, true> pass 2) -- replayed here with HIP events on the launch
+    stream from the timed GOP's I-frame.  The HBM fraction of a P-frame's algorithmic bytes (as
+    the one-pass roofline) over that run's time; the VALU busy fraction of the run kernel (the
+    sequence: of its pass-1 kernel) from the committed PMC counters."""
+    from streamoptima_amd import _lib
+    fused = _lib.load().so_get_option(_lib.OPT_RUN_2PASS_FUSED) == 1 and codec.engine().nby >= 5
     eng = codec.engine()
     qp_sched = codec.row_qp_schedule(eng.nby)
     qdev = eng.qp_row_tensor(qp_sched)
@@ -396,17 +400,13 @@ def rc_roofline(codec, frames_dev, symbols, reps: int, config: str) -> dict:
     lo, hi = codec.qp_clamp
     nf = frames_dev.shape[0]
     qp = codec.const_init_Qp
-    tmp = eng.new_symbols(1)
-    qmap = torch.empty(eng.nb, dtype=torch.int32, device=eng.device)
+    outs = [eng.new_symbols(1) for _ in range(nf - 1)]
+    maps = [torch.empty(eng.nb, dtype=torch.int32, device=eng.device) for _ in range(nf - 1)]
     stream = torch.cuda.current_stream(eng.device)
 
     def seq():
-        for i in range(1, nf):
-            sym = eng.encode_p(frames_dev[i], [symbols[i - 1].recon], qp, qp_sched, out=tmp, qp_row_dev=qdev,
-                               tokens_only=True)
-            eng.qp_map(sym.tokens, qp, qdev, roi_dev, qmap, qp_lo=lo, qp_hi=hi)
-            eng.encode_p(frames_dev[i], [symbols[i - 1].recon], qp, qp_sched, out=tmp, qp_row_dev=qdev,
-                         qp_map_dev=qmap, reuse_me=True)
+        eng.encode_p_run_2pass([frames_dev[i] for i in range(1, nf)], symbols[0].recon, qp, outs, maps,
+                               qp_row=qp_sched, qp_row_dev=qdev, roi_dev=roi_dev, qp_lo=lo, qp_hi=hi)
     t_end = time.perf_counter() + 0.2
     while time.perf_counter() < t_end:
         seq()
@@ -419,23 +419,27 @@ def rc_roofline(codec, frames_dev, symbols, reps: int, config: str) -> dict:
     e1.record(stream)
     torch.cuda.synchronize()
     per_frame = e0.elapsed_time(e1) / 1e3 / n_rep / (nf - 1)
+    eng.check_run()
     frame_bytes = alg_frame_bytes(eng.h, eng.w)
     gbs = frame_bytes / per_frame / 1e9
-    pm = pmc_record(config, "so::p_tile_kernel<8, true>")
+    kname = "so::p_run_kernel<8, 3, false, false>" if fused else "so::p_tile_kernel<8, true>"
+    pm = pmc_record(config, kname)
     valu = None
     if pm.get("sq_active_inst_valu") and pm.get("grbm_gui_active"):
         cyc = pm["grbm_gui_active"] / 8
-        valu = {"kernel": "p_tile_kernel<8, true> (pass 1)",
+        valu = {"kernel": kname[4:] + ("" if fused else " (pass 1)"),
                 "valu_busy_frac": round(4 * pm["sq_active_inst_valu"] / (cyc * N_SIMD), 4),
                 "waves_per_simd": round(4 * pm["sq_wave_cycles"] / (cyc * N_SIMD), 2) if pm.get("sq_wave_cycles") else None,
                 "source": f"profiles/pmc_me_traffic.json [{config}]"}
-    return {"bound": "hbm", "kernel": "two-pass P-frame sequence: p_tile_kernel<8, true> (pass 1) + qp_map_kernel + "
-                                      "inter_tq_kernel<16, false, false> (pass 2, SO_REUSE_ME)",
+    kdesc = ("two-pass P-run in one persistent launch (so_encode_p_run_2pass): p_run_kernel<8, 3, false, false>"
+             if fused else "two-pass P-frame sequence (so_encode_p_run_2pass): p_tile_kernel<8, true> (pass 1) + "
+             "inter_tq_kernel<16, false, false, true> (pass 2: QP map + transforms)")
+    return {"bound": "hbm", "kernel": kdesc,
             "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5),
             "traffic": None, "algorithmic_bytes": frame_bytes, "per_frame_us": round(per_frame * 1e6, 2),
             "binding_limit": "valu", "valu": valu,
             "algorithmic_bytes_def": ALG_BYTES_DEF,
-            "note": "algorithmic bytes of one P-frame over the measured time of its three launches; pass 1 re-reads "
+            "note": "algorithmic bytes of one P-frame over the measured time per P-frame of the run; pass 1 re-reads "
                     "the current and reference rows pass 2 reads again"}
 
 

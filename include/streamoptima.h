@@ -119,8 +119,9 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
  * knobs of the development tools exist only in -DSO_AB builds).  Set them before enqueueing
  * the work they affect; they are read on the host when a call enqueues its launches.
  *   SO_OPT_RUN_2PASS_FUSED   so_encode_p_run_2pass runs both passes of every frame in ONE
- *                            persistent launch (1) instead of the per-frame kernel sequence
- *                            (0, default; measured faster)
+ *                            persistent launch (1, default: measured faster, DESIGN.md section 5;
+ *                            frames of three or more 32-row tile rows) or as the per-frame kernel
+ *                            sequence (0)
  *   SO_OPT_FASTME_SERIAL     fast_me under ParallelMode 0: the one-wavefront serial walk of the
  *                            predictor chain (1) instead of the speculated segments (0, default)
  *   SO_OPT_FASTME_SEGMENT    blocks per speculated segment (default 32, >= 1)
@@ -232,10 +233,11 @@ int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0
  * transforms at those QPs on pass 1's motion vectors.  Identical to the per-frame sequence
  * so_encode_p_rows_ex (pass 1) + so_qp_map + so_encode_p_rows_ex(SO_REUSE_ME) (pass 2);
  * out_qp_map[i] (int32 [nb]) receives frame i's QPs.  roi: int32 [nb] offsets or NULL.  By
- * default the library enqueues that per-frame kernel sequence itself (pass 1 tokens-only, the
- * QP map, pass 2; the ME records kept in the workspace); with so_set_option(
- * SO_OPT_RUN_2PASS_FUSED, 1) both passes run in ONE persistent launch instead (each tile two tasks, a pass-2
- * task waiting for its tile row's pass 1; measured slower).  Frame i predicts from frame i-1's
+ * default both passes run in ONE persistent launch (each task the pass 2 of one tile, then the
+ * pass 1 of the tile tiles_x + 1 positions later; a pass 2 waits for its tile row's pass 1);
+ * with so_set_option(SO_OPT_RUN_2PASS_FUSED, 0), or for frames of fewer than three 32-row tile
+ * rows, the library enqueues the per-frame kernel sequence itself instead (pass 1 tokens-only,
+ * pass 2 with the QP map; the ME records kept in the workspace).  Frame i predicts from frame i-1's
  * pass-2 reconstruction, frame 0 from ref0.  Same coverage and workspace as so_encode_p_run
  * (W <= 8192).
  */

@@ -406,12 +406,11 @@ class Y_Video_codec(BlockAPI):
         # (engine.encode_p_run): same symbols, frames overlapped on the device
         run_ok = not rc_switch and self.nRefFrames == 1 and eng.pipelined_ok(1) and os.environ.get("SO_PIPELINE", "1") != "0"
         pipelined = run_ok and not two_pass and roi_dev is None
-        # two-pass RC (with or without ROI): a P-run in one so_encode_p_run_2pass call -- the
-        # per-frame kernel sequence enqueued by the library (the same kernels as the per-frame
-        # loop below, a third of its host time, and pass 1 gets the previous frame's motion
-        # records as its search hint, which the per-call C-ABI of the loop has no argument for;
-        # SO_RUN_2PASS=0: the loop) or, with SO_OPT_RUN_2PASS_FUSED, both passes in one
-        # persistent launch
+        # two-pass RC (with or without ROI): a P-run in one so_encode_p_run_2pass call -- both
+        # passes of every frame in one persistent launch (default; SO_OPT_RUN_2PASS_FUSED = 0: the
+        # per-frame kernel sequence enqueued by the library), pass 1 with the previous frame's
+        # motion records as its search hint, which the per-call C-ABI of the loop below has no
+        # argument for (SO_RUN_2PASS=0: the loop)
         pipelined2 = (run_ok and two_pass and eng.pipelined_ok(1, vbs_ok=False)
                       and os.environ.get("SO_RUN_2PASS", "1") == "1")
         if pipelined and chunk is None and intra_dur < nframes - 1 and wait_input_default and on_output_default:

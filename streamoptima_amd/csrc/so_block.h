@@ -200,6 +200,40 @@ SO_DEV void xform2d_rows(double* lds, int l, const T* in_row, double* out_row, c
     wave_sync();   // lds free for reuse
 }
 
+// The forward xform2d_rows<16, false> of integer rows through half its LDS (16 x 9 doubles): the
+// int32 transpose fits the scratch whole (16 x 17 words), the FP64 one goes back to rows in two
+// halves (as xform2d_rows_half).  The same operations as xform2d_rows bit for bit (the column
+// pass dct2_16_i on the int32 columns, the row pass dct2 on the doubles).
+template <class TWt>
+SO_DEV void xform2d_fwd_i_half(double* lds, int l, const int* in_row, double* out_row, const TWt& tw) {
+    constexpr int N = 16, PI = N + 1, P = 9;
+    const int hl = l >> 3, cl = l & 7;
+    double v[N];
+    {
+        int* const li = reinterpret_cast<int*>(lds);
+#pragma unroll
+        for (int c = 0; c < N; ++c) li[l * PI + c] = in_row[c];
+        wave_sync();
+        int x[N];
+#pragma unroll
+        for (int r = 0; r < N; ++r) x[r] = li[r * PI + l];
+        wave_sync();   // every lane's int reads before the doubles below overwrite them
+        dct::dct2_16_i(x, v, tw);   // axis 0 (columns)
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {   // columns -> rows
+        if (hl == h) {
+#pragma unroll
+            for (int r = 0; r < N; ++r) lds[r * P + cl] = v[r];
+        }
+        wave_sync();
+#pragma unroll
+        for (int c = 0; c < 8; ++c) out_row[8 * h + c] = lds[l * P + c];
+        wave_sync();
+    }
+    dct::dct2<N>(out_row, tw);   // axis 1 (rows)
+}
+
 // xform2d_rows<16> with half the LDS (16 x 9 doubles): each transpose goes through the buffer in
 // two halves -- rows' columns 0-7 then 8-15 (lanes l < 8 take their column from the first, the
 // others from the second), and back.  The same arithmetic bit for bit; 50 % more LDS

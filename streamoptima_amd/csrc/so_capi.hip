@@ -26,7 +26,7 @@ void set_error(const char* fmt, ...) {
 }
 
 // so_set_option / so_get_option (SO_OPT_*): index = option id
-static std::atomic<int> g_opt[7] = {0, 0, 0, 32, 32, 0, 0};
+static std::atomic<int> g_opt[7] = {0, 1, 0, 32, 32, 0, 0};   // SO_OPT_RUN_2PASS_FUSED on by default
 
 int option(int id) {
     return (id > 0 && id < 7) ? g_opt[id].load(std::memory_order_relaxed) : 0;
@@ -97,6 +97,11 @@ int inter_tq_launch(const uint8_t* cur, const RefSet& refs, const uint8_t* plane
                     int bs, int by0, int by1, const int32_t* best, const int32_t* sub, int qp_rd, const int32_t* qp_row,
                     const int32_t* qp_map, int vbs, double lam, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc, int32_t* out_tokens,
                     int32_t* out_mae, uint8_t* out_recon, int32_t* out_sse, hipStream_t st);
+int inter_tq_2pass_launch(const uint8_t* cur, const RefSet& refs, int H, int W, const int32_t* best, const int32_t* t1,
+                          int qp_rd, const int32_t* qp_row, const int32_t* roi, int qp_lo, int qp_hi,
+                          int32_t* out_qpmap, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc,
+                          int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon, int32_t* out_sse,
+                          hipStream_t st);
 int inter_recon_launch(const RefSet& refs, const uint8_t* planes, size_t pstride, int H, int W, int bs, int qp,
                        const int32_t* qp_row, const int32_t* qp_map, const uint8_t* split, const int16_t* mv, const int16_t* qtc,
                        uint8_t* out_recon, hipStream_t st);
@@ -558,26 +563,32 @@ int so_encode_p_run_2pass(const uint8_t* const* curs, int nframes, const uint8_t
                                     out_sse ? out_sse[i] : nullptr, out_qp_map[i]};
     }
     hipStream_t st = (hipStream_t)stream;
-    if (option(SO_OPT_RUN_2PASS_FUSED) == 1)   // opt-in: both passes in one persistent launch
+    // default: both passes of every frame in one persistent launch (each task the pass 2 of one
+    // tile and the pass 1 of another), for frames of three tile rows or
+    // more; otherwise, or with SO_OPT_RUN_2PASS_FUSED = 0, the per-frame sequence below
+    if (option(SO_OPT_RUN_2PASS_FUSED) == 1 && p_run_2pass_fused_ok(H, W))
         return p_run_2pass_launch(curs, nframes, ref0, H, W, qp_rd, qp_row, roi, qp_lo, qp_hi, outs.data(), workspace,
                                   st);
-    // default (faster): per frame, pass 1 (fused search + tokens only),
-    // the QP map, pass 2 (transforms on pass 1's ME records, kept in the workspace), enqueued
-    // from here with no host round trip per frame
+    // per frame, pass 1 (fused search + tokens only) and pass 2 (the QP map from pass 1's token
+    // counts, then the transforms on pass 1's ME records, kept in the workspace), enqueued from
+    // here with no host round trip per frame
+    // the workspace's pass-1 region (kRunMax >= 5 blocks' words per block): the ME records
+    // (4 words per block), then the pass-1 token counts (1 word per block)
     int32_t* best = p_run_t1_region(workspace, H, W);
     const int nbx = W / 16, nby = H / 16;
+    int32_t* t1 = best + (size_t)4 * nbx * nby;
+    static_assert(kRunMax >= 5, "the pass-1 region holds 4 + 1 words per block");
     for (int i = 0; i < nframes; ++i) {
         RefSet rs{};
         rs.p[0] = i ? out_recon[i - 1] : ref0;
         const PFrameOut& o = outs[(size_t)i];
         // pass 1 with the previous frame's (final) motion records as the search's U hint
-        SO_TRY(p_tile_launch(curs[i], rs, H, W, 0, nby, qp_rd, qp_row, nullptr, best, o.split, o.mv, o.qtc, o.tokens,
+        SO_TRY(p_tile_launch(curs[i], rs, H, W, 0, nby, qp_rd, qp_row, nullptr, best, o.split, o.mv, o.qtc, t1,
                              o.mae, o.recon, o.sse, st, true, i ? out_mv[i - 1] : nullptr));
-        hipLaunchKernelGGL(qp_map_kernel, dim3(nby), dim3(256), 0, st, o.tokens, nbx, 0, qp_rd, qp_row, roi, qp_lo,
-                           qp_hi, o.qpmap);
-        SO_TRY(check_launch("qp_map_kernel"));
-        SO_TRY(inter_tq_launch(curs[i], rs, nullptr, so_fme_plane_stride(H, W), H, W, 16, 0, nby, best, nullptr, qp_rd,
-                               qp_row, o.qpmap, 0, 0.0, o.split, o.mv, o.qtc, o.tokens, o.mae, o.recon, o.sse, st));
+        // pass 2 derives the QP map from the pass-1 tokens itself (qp_map_kernel's rule) and
+        // stores it: no separate QP-map launch per frame
+        SO_TRY(inter_tq_2pass_launch(curs[i], rs, H, W, best, t1, qp_rd, qp_row, roi, qp_lo, qp_hi, o.qpmap, o.split,
+                                     o.mv, o.qtc, o.tokens, o.mae, o.recon, o.sse, st));
     }
     return SO_OK;
 }

@@ -1615,6 +1615,12 @@ me_sea2_kernel(const uint8_t* __restrict__ cur, RefSet refs, int nref, int H, in
 // FP64 transpose scratch per block of the fused tile: 16 x 17 doubles.  (Two-half transposes,
 // 16 x 9, would let 4 workgroups fit per CU but spill at 64-80 VGPRs: measured slower, DESIGN.md.)
 constexpr int kTqScratch = 16 * 17;
+// The tokens-only pass-1 tile (p_tile_kernel<8, true>) transforms through half of it (16 x 9,
+// xform2d_fwd_i_half): 33.7 KB of LDS per workgroup, four workgroups per CU instead of three
+#ifndef SO_PTILE_TOK_HALF
+#define SO_PTILE_TOK_HALF 1
+#endif
+constexpr int kTqScratchHalf = 16 * 9;
 // SO_FWD_MFMA=1: the fused tiles' forward transform on the matrix cores with an exactness
 // certificate (fwd_mfma).  Bit-exact (the GPU suite passes through it) but measured slower, so
 // off: 73.6 vs 67.0 us per 4K P-frame -- the FP32 MFMA runs at the FP32 vector rate and does not
@@ -1623,11 +1629,11 @@ constexpr int kTqScratch = 16 * 17;
 #ifndef SO_FWD_MFMA
 #define SO_FWD_MFMA 0
 #endif
-template <class G>
+template <class G, bool HALFTQ = false>
 struct PTileGeo {
     static constexpr int B4 = (G::B4RS * G::B4P + 4) / 4;             // dwords
     static constexpr int LIST = G::NW * G::CAPL / 2;                  // dwords
-    static constexpr int TQD = G::NBLK * kTqScratch;                  // doubles
+    static constexpr int TQD = G::NBLK * (HALFTQ ? kTqScratchHalf : kTqScratch);   // doubles
     static constexpr int U64 = ((B4 + LIST + 1) / 2 > TQD) ? (B4 + LIST + 1) / 2 : TQD;
 };
 // VBSEnable (tq16_vbs): 16 x 18 doubles per block (the 16 x 17 transpose of the block, or the
@@ -1673,7 +1679,7 @@ struct MeRec {
 
 // The LDS of one fused tile.
 // VBS: keys / mer hold the 16 blocks' records, then the 4 sub-blocks of each (NBLK + 4 g + j).
-template <class G, bool VBS = false>
+template <class G, bool VBS = false, bool HALFTQ = false>
 struct PTileLds {
     static constexpr int NU = G::NBLK * (VBS ? 5 : 1);
     uint32_t win[G::WR * G::RP + 4];
@@ -1685,7 +1691,7 @@ struct PTileLds {
     MeRec mer[NU];                         // decoded ME records (dx, dy, ref, sad)
     int32_t msum[G::TBY];                  // two-pass runs: pass-1 token sum of each block row
     uint32_t fwd_flags;                    // fwd_mfma: blocks whose levels need the FP64 forward
-    alignas(16) double un[VBS ? PTileGeoVbs<G>::U64 : PTileGeo<G>::U64];   // byte sums + survivor lists | FP64 transposes
+    alignas(16) double un[VBS ? PTileGeoVbs<G>::U64 : PTileGeo<G, HALFTQ>::U64];   // byte sums + survivor lists | FP64 transposes
     // VBS: each block's split state (0 block, 1 split, 2 none) between tq16_vbs_fwd and
     // tq16_vbs_inv (its levels wait in its transpose scratch)
     uint8_t vsp[VBS ? G::NBLK : 1];
@@ -1715,8 +1721,8 @@ struct PHalo {
 #define SO_TQ_TW() dct::tw16_table()
 #define SO_TQ_TW8() dct::tw8_table()
 #endif
-template <class G, bool SC1, bool HALO = false, bool TOK = false>
-SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, int byt0, int nbx, int by0, int by1,
+template <class G, bool SC1, bool HALO = false, bool TOK = false, bool HALFTQ = false>
+SO_DEV void tq16_exact(PTileLds<G, false, HALFTQ>& S, int g, int l, double* scratch, int bx0, int byt0, int nbx, int by0, int by1,
                        int W, int qp_rd, const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map,
                        const PFrameOut& o, const PHalo& hl = PHalo{}, bool qs = false) {
     constexpr int SR = G::SR, TBX = G::TBX;
@@ -1762,7 +1768,11 @@ SO_DEV void tq16_exact(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
             }
             double tcr[16];
             SO_MARK(tq_fwd);
-            xform2d_rows<16, false>(dl, l, res, tcr, SO_TQ_TW());
+            static_assert(!HALFTQ || TOK, "the half scratch carries the forward transform only");
+            if constexpr (HALFTQ)
+                xform2d_fwd_i_half(dl, l, res, tcr, SO_TQ_TW());
+            else
+                xform2d_rows<16, false>(dl, l, res, tcr, SO_TQ_TW());
             SO_MARK(tq_quant);
 #pragma unroll
             for (int c = 0; c < 16; ++c)
@@ -2314,8 +2324,8 @@ SO_DEV void store_sc1_i32(int32_t* p, int v) {
 }
 
 template <class G, bool SC1, class Pre = NoPre, bool HALO = false, bool TOK = false, bool VBS = false,
-          class Post = NoPre>
-SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict__ cur, const uint8_t* ref, int H, int W,
+          class Post = NoPre, bool HALFTQ = false>
+SO_DEV void ptile_body(PTileLds<G, VBS, HALFTQ>& S, int tile, const uint8_t* __restrict__ cur, const uint8_t* ref, int H, int W,
                        int by0, int by1, int qp_rd, const int32_t* __restrict__ qp_row,
                        const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best, const PFrameOut& o,
                        const Pre& pre = Pre(), const PHalo& hl = PHalo{}, double lam = 0.0,
@@ -2326,7 +2336,7 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
     uint32_t* const b4w = reinterpret_cast<uint32_t*>(S.un);
     uint16_t* const list = reinterpret_cast<uint16_t*>(b4w + P::B4);
     // room for a dense tile's three shifted window copies in the scratch, 8 (mod 32) dwords on
-    constexpr int kUnDw = 2 * (VBS ? PTileGeoVbs<G>::U64 : PTileGeo<G>::U64);
+    constexpr int kUnDw = 2 * (VBS ? PTileGeoVbs<G>::U64 : PTileGeo<G, HALFTQ>::U64);
     int dense4 = 0;
 #ifndef SO_DENSE_ONE   // A/B builds: dense tiles read the single window copy
     if constexpr (3 * G::DCS + 32 <= kUnDw) {
@@ -2406,7 +2416,8 @@ SO_DEV void ptile_body(PTileLds<G, VBS>& S, int tile, const uint8_t* __restrict_
                 tq16_vbs_fwd<G, SC1, HALO>(S, gq, ln & 15, S.un + gq * kTqScratchVbs, bx0, byt0, nbx, by0, by1, W, qp_rd,
                                            qp_row, qp_map, lam, o);
             else
-                tq16_exact<G, SC1, HALO, TOK>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by0, by1, W, qp_rd,
+                tq16_exact<G, SC1, HALO, TOK>(S, gq, ln & 15, S.un + gq * (HALFTQ ? kTqScratchHalf : kTqScratch), bx0,
+                                              byt0, nbx, by0, by1, W, qp_rd,
                                               qp_row, qp_map, o, hl, qs);
         }
     }
@@ -2599,12 +2610,13 @@ SO_DEV void tq16_pass2(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
 #define SO_PTILE_NW 8
 #endif
 template <int NW, bool TOK = false>
-__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE)))
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(
+    NW >= 16 ? SO_PTILE_WPE16 : (TOK && SO_PTILE_TOK_HALF ? 8 : SO_SEA2_WPE))))
 p_tile_kernel(const uint8_t* __restrict__ cur, RefSet refs, int H, int W, int by0, int by1, int qp_rd,
               const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best,
               PFrameOut o, const int16_t* prev_mv) {
     using G = Sea2GeoT<NW>;
-    __shared__ PTileLds<G> S;
+    __shared__ PTileLds<G, false, TOK && SO_PTILE_TOK_HALF> S;
     SO_STAMP_REC_SET(g_sea_stamps ? g_sea_stamps + (size_t)blockIdx.x * 12 : nullptr);
     ptile_body<G, false, NoPre, false, TOK>(S, blockIdx.x, cur, refs.p[0], H, W, by0, by1, qp_rd, qp_row, qp_map,
                                             out_best, o, NoPre(), PHalo{}, 0.0, nullptr, nullptr, 0, NoPre(), prev_mv);
@@ -2877,7 +2889,12 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
     // two-pass: 2 tasks per tile; per frame the pass-1 tasks of tile row r + 1 are queued ahead
     // of the pass-2 tasks of row r (which wait for all of row r's pass 1), so every wait is
     // on tasks earlier in the queue
-    const int per_frame = TWOP ? 2 * ntiles : ntiles, ntasks = per_frame * nframes;
+    // kRunTwoPass (one GPU): each task runs a pass-2 unit, then a pass-1 unit (MERGE2P, below):
+    // nframes * ntiles units of each, the pass-2 units lag2 = ntiles - (tiles_x + 1) tasks behind
+    constexpr bool MERGE2P = MODE == kRunTwoPass;
+    const int lag2 = ntiles - (tiles_x + 1);
+    const int per_frame = TWOP && !MERGE2P ? 2 * ntiles : ntiles;
+    const int ntasks = per_frame * nframes + (MERGE2P ? lag2 : 0);
     uint32_t* const done = ws + kRunDoneBase;
     // kRunSingle: per (frame, tile) the count of blocks that searched dense (after the done
     // flags, the pass-1 flags and token counts: p_run_workspace_words)
@@ -2935,9 +2952,14 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
         SO_STAMP_REC_SET(rec);
         if (tid == 0 && rec) rec[8] = __builtin_amdgcn_s_memrealtime();
 #endif
-        const int f = task / per_frame;
-        int tile = task - f * per_frame, pass = 1;
-        if constexpr (TWOP) {
+        // MERGE2P: the task's pass-1 unit (frame-major (f, tile); none in the trailing lag2 tasks,
+        // which then name their pass-2 unit here) and its pass-2 unit u2 (none while < 0)
+        const int u2 = MERGE2P ? task - lag2 : -1;
+        const bool has1 = !MERGE2P || task < nframes * ntiles;
+        const int u = has1 ? task : u2;
+        const int f = u / per_frame;
+        int tile = u - f * per_frame, pass = has1 ? 1 : 2;
+        if constexpr (TWOP && !MERGE2P) {
             // [P1 rows 0..L-1] [P1 row L][P2 row 0] [P1 row L+1][P2 row 1] ... [P2 rows ntr-L..]:
             // a pass-2 task is queued L tile rows after its row's pass 1 (L = sp.p2lag, about
             // one grid's worth of tasks), so it rarely waits holding its slot
@@ -3045,12 +3067,14 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                                    : (MODE == kRunSingle || TWOP) ? a.ref[f] : (f ? a.out[f - 1].recon : ref0);
         if constexpr (TWOP) {
             const int nb = nbx * (H / 16);
-            int32_t* const t1 = sp.t1 + (size_t)f * nb;
-            const int bx0 = tx * G::TBX, byt0 = ty * G::TBY;
 #ifdef SO_RUN_PROFILE
             const unsigned long long pt0 = __builtin_amdgcn_s_memtime();
 #endif
-            if (pass == 1) {
+            // pass 1 of (f, tile): the search (after the 3x3 reference tiles' done flags) and the
+            // forward transform for the token counts; stores the ME records and tokens, then p1done
+            const auto pass1_unit = [&]() {
+                int32_t* const t1 = sp.t1 + (size_t)f * nb;
+                const int bx0 = tx * G::TBX, byt0 = ty * G::TBY;
                 using P = PTileGeo<G>;
                 uint32_t* const b4w = reinterpret_cast<uint32_t*>(S.un);
                 const Sea2Lds L{S.win, b4w, S.curt, S.a4, reinterpret_cast<uint16_t*>(b4w + P::B4), S.lcount, S.keys,
@@ -3075,12 +3099,20 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                     __hip_atomic_store(sp.p1done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                 SO_RUN_PROF(48, __builtin_amdgcn_s_memtime() - pt0);
-            } else {
+            };
+            // pass 2 of (f2, tile2): after its tile row's p1done flags, the row's token sums, the
+            // block QPs and the transforms on pass 1's records; stores the symbols and the
+            // reconstruction, then the done flag
+            const auto pass2_unit = [&](int f2, int tile2) {
+                int32_t* const t1 = sp.t1 + (size_t)f2 * nb;
+                const int ty2 = tile2 / tiles_x;
+                const int bx0 = (tile2 - ty2 * tiles_x) * G::TBX, byt0 = ty2 * G::TBY;
+                const uint8_t* const ref2 = FPIPE ? sp.land0 + (long long)(sp.gbase + f2) * sp.stride : a.ref[f2];
                 if (wave == 0) {   // every tile of this tile row finished pass 1 (tiles_x <= 64)
-                    const uint32_t* c = sp.p1done + (size_t)f * ntiles + ty * tiles_x + (lane < tiles_x ? lane : 0);
+                    const uint32_t* c = sp.p1done + (size_t)f2 * ntiles + ty2 * tiles_x + (lane < tiles_x ? lane : 0);
                     // 50 ms of polling; 2 s in the frame pipeline, whose pass-1 tasks may wait that
                     // long on another rank's reconstruction
-                    const RunWait rw{task, f, -2, tile, MODE | (2 << 8), ep, sp.epoch, FPIPE ? 200000000ull : 5000000ull};
+                    const RunWait rw{task, f2, -2, tile2, MODE | (2 << 8), ep, sp.epoch, FPIPE ? 200000000ull : 5000000ull};
                     run_poll(c, lane < tiles_x, false, ws, rw);
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3097,23 +3129,40 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 }
                 __syncthreads();
                 // frame pipeline: where the final reconstruction goes (kRunFPipe's push code)
-                const int code = FPIPE ? a.dep[f] : -1;
+                const int code = FPIPE ? a.dep[f2] : -1;
                 uint8_t* const push = code >= 0 ? ((code & 1) ? sp.peer_up0 : sp.peer_dn0) +
                                                       (long long)(code >> 1) * sp.stride : nullptr;
                 const int t2 = opaque_tid(), ln = t2 & 63, gq = (t2 >> 6) * G::TQ_BPW + (ln >> 4);
                 if (ln < 16 * G::TQ_BPW && gq < G::NBLK)
                     tq16_pass2<G>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by1, W, qp_rd, qp_row, sp.roi,
-                                  sp.qp_lo, sp.qp_hi, a.cur[f], ref, a.out[f], t1, push);
+                                  sp.qp_lo, sp.qp_hi, a.cur[f2], ref2, a.out[f2], t1, push);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // local and remote stores retired
                 __syncthreads();
                 if (wave == 0) {
-                    __hip_atomic_store(done + (size_t)f * ntiles + tile, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(done + (size_t)f2 * ntiles + tile2, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (lane == 0 && code >= 0)
                         __hip_atomic_store(((code & 1) ? sp.peer_up_flags : sp.peer_dn_flags) +
-                                               (size_t)(code >> 1) * ntiles + tile,
+                                               (size_t)(code >> 1) * ntiles + tile2,
                                            sp.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 }
                 SO_RUN_PROF(49, __builtin_amdgcn_s_memtime() - pt0);
+            };
+            if constexpr (MERGE2P) {
+                // task k: pass 2 of unit k - lag2, then pass 1 of unit k.  Pass 1 of (f, t) needs
+                // frame f-1's tiles up to t + tiles_x + 1, whose pass-2 units run in tasks up to
+                // k (this one: unit k - lag2 = (f-1, t + tiles_x + 1)); pass 2 of unit j needs the
+                // pass 1 of its tile row, units up to j + tiles_x - 1, in tasks before j + lag2
+                // when 2 tiles_x < ntiles (the launcher checks).  So every wait is on this task's
+                // own first part or on earlier tasks: deadlock-free as the one-pass run.
+                if (u2 >= 0) {
+                    const int f2 = u2 / ntiles;
+                    pass2_unit(f2, u2 - f2 * ntiles);
+                }
+                if (has1) pass1_unit();
+            } else if (pass == 1) {
+                pass1_unit();
+            } else {
+                pass2_unit(f, tile);
             }
         } else if constexpr (FPIPE) {
             // where frame f's reconstruction goes (the ring direction alternates per block of N
@@ -3441,11 +3490,21 @@ int32_t* p_run_t1_region(uint32_t* ws, int H, int W) {
     return reinterpret_cast<int32_t*>(ws + kRunDoneBase + 2 * (size_t)kRunMax * run_tiles(H, W, Sea2Geo::TBX, Sea2Geo::TBY));
 }
 
+// The merged two-pass schedule's deadlock-freedom needs 2 tiles_x < ntiles: three tile rows or more
+bool p_run_2pass_fused_ok(int H, int W) {
+    const int tiles_x = (W / 16 + Sea2Geo::TBX - 1) / Sea2Geo::TBX;
+    return 2 * tiles_x < run_tiles(H, W, Sea2Geo::TBX, Sea2Geo::TBY);
+}
+
 // Two-pass rate control over a run (so_encode_p_run_2pass): one run as p_run_launch, each tile
 // as a pass-1 and a pass-2 task (kRunTwoPass).
 int p_run_2pass_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,
                        const int32_t* qp_row, const int32_t* roi, int qp_lo, int qp_hi, const PFrameOut* outs,
                        uint32_t* ws, hipStream_t st) {
+    if (!p_run_2pass_fused_ok(H, W)) {
+        set_error("so_encode_p_run_2pass (fused): needs three tile rows (H > %d)", 2 * 16 * Sea2Geo::TBY);
+        return SO_E_UNSUPPORTED;
+    }
     PRunStripe sp{};
     sp.by0 = 0;
     sp.by1 = H / 16;

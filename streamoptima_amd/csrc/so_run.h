@@ -63,6 +63,7 @@ struct PRunStripe {
 
 size_t p_run_workspace_words(int H, int W);
 int p_run_capacity(int vbs, int mode = -1);
+bool p_run_2pass_fused_ok(int H, int W);
 int32_t* p_run_t1_region(uint32_t* ws, int H, int W);
 // vbs / lam: VBSEnable (the block + sub-block search and the RD split inside the run)
 int p_run_launch(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W, int qp_rd,

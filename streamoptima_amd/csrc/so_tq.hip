@@ -14,7 +14,17 @@
 
 namespace so {
 
-template <int BS, bool VBS, bool FME>
+// Two-pass pass 2 with the QP map derived in the kernel (QPM; so_encode_p_run_2pass): the
+// pass-1 token counts t1 (stripe-local, one per block), the ROI offsets and the clamp of
+// qp_map_kernel (so_capi.hip), whose per-block QP this reproduces; the map is also written out.
+struct QpmArgs {
+    const int32_t* t1;
+    const int32_t* roi;
+    int qp_lo, qp_hi;
+    int32_t* out_qpmap;
+};
+
+template <int BS, bool VBS, bool FME, bool QPM = false>
 __global__ void __launch_bounds__(256)
 inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, const uint8_t* __restrict__ planes, size_t pstride,
                 int H, int W, int by0, int nrows,
@@ -23,7 +33,7 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, const uint8_t* __r
                 uint8_t* __restrict__ out_split,
                 int16_t* __restrict__ out_mv, int16_t* __restrict__ out_qtc,
                 int32_t* __restrict__ out_tokens, int32_t* __restrict__ out_mae,
-                uint8_t* __restrict__ out_recon, int32_t* __restrict__ out_sse) {
+                uint8_t* __restrict__ out_recon, int32_t* __restrict__ out_sse, const QpmArgs qa) {
     constexpr int G = BS, BPW = 256 / G, SB = BS / 2;
     constexpr int LDS_D = VBS ? 288 : BS * (BS + 1);
     __shared__ double ldsd[BPW * LDS_D];
@@ -31,12 +41,43 @@ inter_tq_kernel(const uint8_t* __restrict__ cur, RefSet refs, const uint8_t* __r
     const int tid = threadIdx.x, g = tid / G, l = tid % G;
     const int nbx = W / BS, nb = nbx * nrows;
     const int b = blockIdx.x * BPW + g;   // block index inside the stripe [by0, by0 + nrows)
+    // QPM: the pass-1 token sum m of each block row this workgroup's blocks lie in (at most 3:
+    // nbx >= 8), by the whole workgroup before any lane group leaves -- measured faster than
+    // each block's 16 lanes summing its row themselves (configs[4] per-frame sequence 2.797 vs
+    // 2.856 ms per GOP, and 2.937 with those loads unrolled)
+    long long m_row = 0;
+    if constexpr (QPM) {
+        __shared__ long long s_m[3][4];
+        const int b0 = blockIdx.x * BPW, bl = (b0 + BPW < nb ? b0 + BPW : nb) - 1;
+        const int rA = b0 / nbx, nr = bl / nbx - rA + 1;
+        for (int k = 0; k < nr; ++k) {   // uniform
+            const int32_t* t = qa.t1 + (size_t)(rA + k) * nbx;
+            long long m = 0;
+            for (int i = tid; i < nbx; i += 256) m += t[i];
+#pragma unroll
+            for (int s = 32; s >= 1; s >>= 1) m += __shfl_xor(m, s, 64);
+            if ((tid & 63) == 0) s_m[k][tid >> 6] = m;
+        }
+        __syncthreads();
+        if (b < nb) {
+            const int k = b / nbx - rA;
+            m_row = s_m[k][0] + s_m[k][1] + s_m[k][2] + s_m[k][3];
+        }
+    }
     if (b >= nb) return;  // whole lane group leaves; only wave-scope exchange below
     double* dl = ldsd + g * LDS_D;
     uint8_t* fl = ldsf + g * BS * BS;
     const int bx = b % nbx, by = by0 + b / nbx, x = bx * BS, y = by * BS;
     // per-block QP map (ROI / two-pass RC) > per-row RC QP > the frame QP
-    const int qpr = qp_map ? qp_map[(size_t)by * nbx + bx] : (qp_row ? qp_row[by] : qp_rd);
+    int qpr = qp_map ? qp_map[(size_t)by * nbx + bx] : (qp_row ? qp_row[by] : qp_rd);
+    if constexpr (QPM) {   // qp_map_kernel's rule (delta from t n against 2m, 4m, m/2, m/4)
+        const long long tn = (long long)qa.t1[b] * nbx;
+        const int d = (tn >= 2 * m_row) + (tn >= 4 * m_row) - (2 * tn < m_row) - (4 * tn < m_row);
+        int q = (qp_row ? qp_row[by] : qp_rd) + d + (qa.roi ? qa.roi[(size_t)by * nbx + bx] : 0);
+        q = q < qa.qp_lo ? qa.qp_lo : (q > qa.qp_hi ? qa.qp_hi : q);
+        qpr = q;
+        if (l == 0) qa.out_qpmap[(size_t)by * nbx + bx] = q;
+    }
 
     const int32_t* bb = best + (size_t)b * 4;
     const int dx = bb[0], dy = bb[1], rf = bb[2], sad = bb[3];
@@ -270,12 +311,32 @@ int inter_tq_launch(const uint8_t* cur, const RefSet& refs, const uint8_t* plane
 #define SO_TQ(B, V, F)                                                                                             \
     hipLaunchKernelGGL((inter_tq_kernel<B, V, F>), grid, blk, 0, st, cur, refs, planes, pstride, H, W, by0, nrows,   \
                        best, sub, qp_rd, qp_row, qp_map, lam, out_split, out_mv, out_qtc, out_tokens, out_mae,       \
-                       out_recon, out_sse)
+                       out_recon, out_sse, QpmArgs{})
     const bool fme = planes != nullptr;
     if (bs == 16 && vbs) { if (fme) SO_TQ(16, true, true); else SO_TQ(16, true, false); }
     else if (bs == 16) { if (fme) SO_TQ(16, false, true); else SO_TQ(16, false, false); }
     else { if (fme) SO_TQ(8, false, true); else SO_TQ(8, false, false); }
 #undef SO_TQ
+    return check_launch("inter_tq_kernel");
+}
+
+// Two-pass pass 2 (so_encode_p_run_2pass): inter_tq_kernel<16, false, false> with the QP map
+// of the pass-1 token counts t1 computed in the kernel (one launch less per frame than
+// qp_map_kernel + inter_tq_kernel; the same QPs, which it also stores into out_qpmap)
+int inter_tq_2pass_launch(const uint8_t* cur, const RefSet& refs, int H, int W, const int32_t* best, const int32_t* t1,
+                          int qp_rd, const int32_t* qp_row, const int32_t* roi, int qp_lo, int qp_hi,
+                          int32_t* out_qpmap, uint8_t* out_split, int16_t* out_mv, int16_t* out_qtc,
+                          int32_t* out_tokens, int32_t* out_mae, uint8_t* out_recon, int32_t* out_sse,
+                          hipStream_t st) {
+    const int nbx = W / 16, nrows = H / 16, nb = nbx * nrows;
+    if (nbx < 8) {   // a workgroup's 16 blocks then span at most 3 block rows
+        set_error("inter_tq_2pass_launch: W %d below 128", W);
+        return SO_E_UNSUPPORTED;
+    }
+    hipLaunchKernelGGL((inter_tq_kernel<16, false, false, true>), dim3((nb + 15) / 16), dim3(256), 0, st, cur, refs,
+                       nullptr, (size_t)0, H, W, 0, nrows, best, nullptr, qp_rd, qp_row, nullptr, 0.0, out_split,
+                       out_mv, out_qtc, out_tokens, out_mae, out_recon, out_sse,
+                       QpmArgs{t1, roi, qp_lo, qp_hi, out_qpmap});
     return check_launch("inter_tq_kernel");
 }
 

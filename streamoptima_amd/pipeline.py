@@ -487,6 +487,22 @@ class FramePipeRank:
         self._planes, self._flags = ctypes.c_void_p(), ctypes.c_void_p()
         _release_slots(self)
 
+    def prepare(self, nf: int, qp_row=None, two_pass: bool = False):
+        """Allocate what encode() of an nf-frame GOP needs (this rank's symbol buffers, the QP
+        maps, the row-QP constant) without launching anything; encode() calls it too.  Ranks
+        sharing one GPU in one process (the tests) prepare every rank before any rank encodes,
+        so that no host-side allocation runs while another rank's persistent grid is waiting.
+        Returns (the symbols by global frame index, the row-QP tensor or None)."""
+        e = self.eng
+        mine = self.frames_of(nf)
+        if self._syms is None or len(self._syms) != len(mine):
+            self._syms = {k: e.new_symbols(0 if k == 0 else 1) for k in mine}
+        if two_pass:
+            for s in self._syms.values():
+                if "qp_map" not in s.extra:
+                    s.extra["qp_map"] = torch.empty(e.nb, dtype=torch.int32, device=e.device)
+        return self._syms, (e.qp_row_tensor(qp_row) if qp_row is not None else None)
+
     def encode(self, frames: torch.Tensor, intra_dur: int, qp: int, qp_row=None, roi_dev=None,
                two_pass: bool = False, qp_clamp=(0, 12)) -> dict:
         """This rank's frames of the GOP {global index: FrameSymbols} (whole-frame symbols,
@@ -511,14 +527,7 @@ class FramePipeRank:
         self.epoch += 1
         ep, st = self.epoch, self._st()
         mine = self.frames_of(nf)
-        if self._syms is None or len(self._syms) != len(mine):
-            self._syms = {k: e.new_symbols(0 if k == 0 else 1) for k in mine}
-        syms = self._syms
-        qrd = e.qp_row_tensor(qp_row) if qp_row is not None else None
-        if two_pass:
-            for s in syms.values():
-                if "qp_map" not in s.extra:
-                    s.extra["qp_map"] = torch.empty(e.nb, dtype=torch.int32, device=e.device)
+        syms, qrd = self.prepare(nf, qp_row, two_pass)
         pplanes, pflags = self.peer
         ks = mine
         if self.rank == 0:

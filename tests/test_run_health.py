@@ -87,7 +87,7 @@ def test_header_words_match_the_host_constants():
 def test_set_option_validates_and_round_trips():
     lib = _lib.load()
     assert lib.so_get_option(_lib.OPT_FASTME_SEGMENT) == 32 and lib.so_get_option(_lib.OPT_FASTME_WARMUP) == 32
-    assert lib.so_get_option(_lib.OPT_RUN_2PASS_FUSED) == 0 and lib.so_get_option(_lib.OPT_FASTME_SERIAL) == 0
+    assert lib.so_get_option(_lib.OPT_RUN_2PASS_FUSED) == 1 and lib.so_get_option(_lib.OPT_FASTME_SERIAL) == 0
     with _lib.option(_lib.OPT_FASTME_SEGMENT, 8):
         assert lib.so_get_option(_lib.OPT_FASTME_SEGMENT) == 8
     assert lib.so_get_option(_lib.OPT_FASTME_SEGMENT) == 32
