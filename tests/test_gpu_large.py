@@ -148,6 +148,31 @@ def test_two_pass_run_matches_per_frame(gpu, monkeypatch, roi, fused):
     assert torch.equal(got["sse"], exp["sse"])
 
 
+@pytest.mark.parametrize("h", [96, 64])
+def test_two_pass_run_edge_shapes(gpu, monkeypatch, h):
+    """The default two-pass run at the edge of the merged schedule's coverage: 96 rows (three
+    tile rows, the fewest it takes: 2 tiles_x < ntiles) runs both passes in one launch, 64 rows
+    (two tile rows) falls back to the per-frame sequence -- both against the Python-driven
+    per-frame loop, frame by frame with the QP maps."""
+    from streamoptima_amd.Encoder import Y_Video_codec
+    from streamoptima_amd.digest import symbols_digest
+    from streamoptima_amd.engine import alloc_planes
+    from streamoptima_amd.synth import synth_sequence_torch
+    from streamoptima_amd.workloads import RC_TABLES
+    w, f = 640, 7
+    codec = Y_Video_codec(h, w, f, 16, 16, 4, f, 0, 0.015, False, RCFlag=3, targetBR="2 mbps",
+                          qp_rate_tables=RC_TABLES, roi=[(100, 16, 400, 60, -2)], device=gpu)
+    fr = alloc_planes(f, h, w, gpu)
+    fr.copy_(synth_sequence_torch(f, h, w, seed=5, device=gpu))
+    monkeypatch.setenv("SO_PIPELINE", "0")
+    exp = [symbols_digest(s) for s in codec.encode_device(fr, f)["symbols"]]
+    monkeypatch.delenv("SO_PIPELINE")
+    assert _lib.load().so_get_option(_lib.OPT_RUN_2PASS_FUSED) == 1
+    got = codec.encode_device(fr, f)
+    torch.cuda.synchronize()
+    assert [symbols_digest(s) for s in got["symbols"]] == exp
+
+
 @pytest.mark.parametrize("roi", [None, [(100, 40, 400, 200, -2)]])
 def test_two_pass_gop_replayed_as_hip_graph(gpu, roi):
     """bench.py --graph: a ROI / two-pass GOP captured once as a HIP graph (no host->device
