@@ -118,6 +118,8 @@ def parse(argv=None):
                     help="test mode: make the named secondary measurement (e.g. records.1080p, cpu_baseline; with "
                          "--cpu-plumbing any name) raise, to check that the headline line still prints and the exit "
                          "status is nonzero")
+    ap.add_argument("--detail-out", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                    help="write the uncompacted line (every note and per-field source) here; '' = nowhere")
     ap.add_argument("--cpu-plumbing", action="store_true",
                     help="test mode: gloo + a trivial CPU stand-in engine (no encode, no GPU) to exercise the "
                          "rank launch, sharding, timing and JSON line on a CPU-only host")
@@ -368,10 +370,10 @@ def roofline_of(rl: dict, config: str) -> dict:
            "frames_per_launch": round(rl["run_frames"] / n_launch, 2),
            "per_frame_us": round(rl["run_s"] / rl["run_frames"] * 1e6, 2),
            "binding_limit": "valu",
-           "valu": valu, "sad": sad,
+           "valu_profile": valu, "sad": sad,
            "note": "frac is the required HBM fraction (algorithmic bytes / launch time / 8 TB/s); the kernel is "
                    "bound by VALU issue (SEA search + FP64 pocketfft-exact DCT), whose measured busy fraction is "
-                   "valu.valu_busy_frac"}
+                   "valu_profile.valu_busy_frac (committed PMC counters of the same workload, not this run)"}
     if rl.get("me_s") and rl.get("tq_s"):
         out["components"] = {
             "me_search": {"kernel": "me_sea2_kernel", "launch_us": round(rl["me_s"] * 1e6, 2),
@@ -425,6 +427,9 @@ def rc_roofline(codec, frames_dev, symbols, reps: int, config: str) -> dict:
     frame_bytes = alg_frame_bytes(eng.h, eng.w)
     gbs = frame_bytes / per_frame / 1e9
     kname = "so::p_run_kernel<8, 3, false, false>" if fused else "so::p_tile_kernel<8, true>"
+    # one persistent launch per <= 32 P-frames (fused); the sequence launches per frame
+    n_launch = -(-(nf - 1) // 32) if fused else nf - 1
+    launch_frames = (nf - 1) / n_launch
     pm = pmc_record(config, kname)
     valu = None
     if pm.get("sq_active_inst_valu") and pm.get("grbm_gui_active"):
@@ -438,10 +443,13 @@ def rc_roofline(codec, frames_dev, symbols, reps: int, config: str) -> dict:
              "inter_tq_kernel<16, false, false, true> (pass 2: QP map + transforms)")
     return {"bound": "hbm", "kernel": kdesc,
             "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5),
-            "traffic": None, "algorithmic_bytes": frame_bytes, "per_frame_us": round(per_frame * 1e6, 2),
-            "binding_limit": "valu", "valu": valu,
+            "traffic": round(pm["hbm_bytes"]) if (fused and pm.get("hbm_bytes")) else None,
+            "algorithmic_bytes": round(frame_bytes * launch_frames),
+            "launch_us": round(per_frame * launch_frames * 1e6, 2), "frames_per_launch": round(launch_frames, 2),
+            "per_frame_us": round(per_frame * 1e6, 2),
+            "binding_limit": "valu", "valu_profile": valu,
             "algorithmic_bytes_def": ALG_BYTES_DEF,
-            "note": "algorithmic bytes of one P-frame over the measured time per P-frame of the run; pass 1 re-reads "
+            "note": "algorithmic bytes of the launch's P-frames over the measured time per launch; pass 1 re-reads "
                     "the current and reference rows pass 2 reads again"}
 
 
@@ -963,6 +971,163 @@ class _PlumbingEngine:
         return self._rows(cur, by0, by1, out)
 
 
+# ---- the printed line: compact, definitions stated once ------------------------------------------------
+# the driver's parse failed on a 22.9 KB line (round 5; a 15.9 KB one parsed); its stdout tail keeps
+# ~8 KB, so a line below that is whole even in the tail
+LINE_MAX_BYTES = 7800
+DEFS = {
+    "algorithmic_bytes": ALG_BYTES_DEF,
+    "frac": "required HBM fraction: algorithmic bytes per launch / average launch time (HIP events on the launch "
+            "stream, this run) / 8 TB/s",
+    "traffic": "HBM bytes per launch from separate rocprofv3 --pmc FETCH_SIZE (x2, tools/ubench_fetch.cpp) and "
+               "WRITE_SIZE passes on the same workload: profiles/pmc_me_traffic.json, not this run",
+    "valu_profile": "VALU busy fraction and waves/SIMD of the same kernel from the committed rocprofv3 --pmc "
+                    "counters (profiles/pmc_me_traffic.json), not this run",
+    "binding_limit": "the run kernel is bound by VALU issue (exact SEA search + FP64 pocketfft-exact DCT), not HBM",
+    "sad_exec_frac": "executed v_sad_u8/v_sad_hi_u8 byte ops (counted in-kernel, one untimed replay) / run time / "
+                     "measured v_sad peak 1.434e14 per s (tools/ubench_sad.cpp)",
+    "parity": "per-frame sha256 of every symbol array + recon vs the C oracle's digests (tests/golden/large_gops.json); "
+              "poisoned = one more step into 0xA5-filled outputs, compared again",
+    "records": "other benchmarked configs at 1 GPU, each timed like the headline (median of --record-repeats runs)",
+    "detail": "the uncompacted line (notes, per-field sources) is written to --detail-out",
+}
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if isinstance(d, dict) and k in d}
+
+
+def _compact_valu(v):
+    if not v:
+        return None
+    return _pick(v, ("kernel", "valu_busy_frac", "waves_per_simd"))
+
+
+def _compact_roofline(r, record=False):
+    if not r or "error" in r:
+        return r
+    keys = (("kernel", "achieved", "frac", "traffic", "algorithmic_bytes", "per_frame_us") if record else
+            ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "algorithmic_bytes", "launch_us",
+             "frames_per_launch", "per_frame_us", "binding_limit"))
+    out = _pick(r, keys)
+    if "kernel" in out and out["kernel"].startswith("two-pass"):
+        out["kernel"] = out["kernel"].split(": ", 1)[-1]
+    vp = r.get("valu_profile") or r.get("valu")
+    if vp:
+        out["valu_profile"] = _compact_valu(vp)
+    sad = r.get("sad") or {}
+    if sad.get("executed_frac_of_measured_peak") is not None:
+        out["sad_exec_frac"] = sad["executed_frac_of_measured_peak"]
+    if not record and r.get("components"):
+        out["components_us"] = {k: c.get("launch_us") for k, c in r["components"].items()}
+    return out
+
+
+def _compact_parity(p):
+    if not p or "error" in p:
+        return p
+    out = _pick(p, ("bit_exact", "frames", "gops_checked", "psnr_delta_db", "poisoned_rerun_bit_exact"))
+    if p.get("mismatched_frames"):
+        out["mismatched_frames"] = p["mismatched_frames"]
+    if p.get("note"):
+        out["note"] = p["note"]
+    return out
+
+
+def _compact_health(h):
+    if not h:
+        return h
+    out = _pick(h, ("timeouts", "stale_reads_repaired", "descheduled_polls"))
+    if h.get("records"):
+        out["first_record"] = h["records"][0]
+    return out
+
+
+def _compact_record(r):
+    if not r or "error" in r:
+        return r
+    out = _pick(r, ("value", "ms_per_step", "ms_per_gop", "gops_per_step"))
+    out["workload"] = r.get("workload", "")[:90]
+    if r.get("roofline"):
+        out["roofline"] = _compact_roofline(r["roofline"], record=True)
+    if r.get("roofline_gop"):
+        out["gop_frac"] = r["roofline_gop"].get("frac")
+    if r.get("sea_dense_fallback"):
+        out["dense_frac"] = r["sea_dense_fallback"].get("frac")
+    if r.get("parity"):
+        out["parity"] = _compact_parity(r["parity"])
+    if r.get("wait_health"):
+        out["wait_health"] = _compact_health(r["wait_health"])
+    for k in r:
+        if k not in out and k not in ("workload", "roofline", "roofline_gop", "sea_dense_fallback", "parity",
+                                      "wait_health", "unit", "ms_per_step_runs", "width", "height", "encoded_height",
+                                      "frames", "content", "vbs", "rate_control"):
+            out[k] = r[k]
+    return out
+
+
+def compact_line(full: dict) -> dict:
+    """The printed line: the full line with each shared definition stated once (`defs`) and
+    every secondary entry cut to its numbers (the driver parses one line of bounded size;
+    LINE_MAX_BYTES, tests/test_bench_line.py).  The full line goes to --detail-out."""
+    line = {k: full[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data") if k in full}
+    cfg = dict(full.get("config") or {})
+    line["config"] = _pick(cfg, ("workload", "name", "width", "height", "frames", "intra_dur", "block_size",
+                                 "search_range", "qp", "seed", "vbs", "me", "content", "parallelism", "launch"))
+    line["value_region"] = full.get("value_region")
+    line["roofline"] = _compact_roofline(full.get("roofline"))
+    cpu = full.get("cpu_baseline")
+    if cpu:
+        c = _pick(cpu, ("value", "unit", "cores", "kind", "sample", "host"))
+        if "sample" in c:
+            c["sample"] = c["sample"].split(", numpy port")[0] + ", numpy port of the reference loops (oracle/ref_numpy.py)"
+        if cpu.get("pool"):
+            c["pool"] = _pick(cpu["pool"], ("value", "cores"))
+        if cpu.get("calibration"):
+            c["port_over_reference_time"] = cpu["calibration"].get("port_over_reference_time")
+        line["cpu_baseline"] = c
+    else:
+        line["cpu_baseline"] = cpu
+    line["parity"] = _compact_parity(full.get("parity"))
+    for k in ("psnr_mean_db", "psnr_delta_db", "gpu_over_cpu", "timeouts", "cpu_baseline_error", "degraded", "failed"):
+        if k in full:
+            line[k] = full[k]
+    if full.get("roofline_gop"):
+        line["gop_frac"] = full["roofline_gop"].get("frac")
+    if full.get("sea_dense_fallback"):
+        line["dense_frac"] = full["sea_dense_fallback"].get("frac")
+    if "wait_health" in full:
+        line["wait_health"] = _compact_health(full["wait_health"])
+    s4 = full.get("section4_region")
+    if s4:
+        pc = full.get("pcie_inclusive") or {}
+        rl = s4.get("roofline") or {}
+        line["section4_region"] = {
+            "value": s4.get("value"), "unit": s4.get("unit"), "ms_per_gop": s4.get("ms_per_gop"),
+            "ms_per_gop_median": s4.get("ms_per_gop_median"),
+            "roofline": {"bound": "pcie", "h2d_frac": rl.get("frac"), "achieved": rl.get("achieved"),
+                         "peak": rl.get("peak"), "unit": "GB/s"},
+            "packed_equals_resident_symbols": pc.get("packed_equals_resident_symbols"),
+            "dense_ms_per_gop": (pc.get("dense") or {}).get("ms_per_gop")}
+        for k in ("order_check",):
+            if k in s4:
+                line["section4_region"][k] = s4[k]
+    elif full.get("pcie_inclusive") and "error" in full["pcie_inclusive"]:
+        line["section4_region"] = full["pcie_inclusive"]
+    if full.get("records"):
+        line["records"] = {k: _compact_record(v) for k, v in full["records"].items()}
+    line["defs"] = DEFS
+    # never above the bound: shed the prose first, then the records' workload names
+    if len(json.dumps(line)) > LINE_MAX_BYTES:
+        line["defs"] = {"see": "bench.py DEFS"}
+    if len(json.dumps(line)) > LINE_MAX_BYTES:
+        for r in (line.get("records") or {}).values():
+            if isinstance(r, dict):
+                r.pop("workload", None)
+    return line
+
+
 # ---- main ----------------------------------------------------------------------------------------------
 def main(argv=None):
     args = parse(argv)
@@ -1267,7 +1432,14 @@ def main(argv=None):
         failures.extend(d["what"] for d in degraded)
     if failures:
         line["failed"] = failures
-    print(json.dumps(line), flush=True)
+    if args.detail_out:
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(args.detail_out)), exist_ok=True)
+            with open(args.detail_out, "w") as fh:
+                json.dump(line, fh, indent=1)
+        except OSError as e:
+            print(f"bench.py: --detail-out {args.detail_out}: {e}", file=sys.stderr, flush=True)
+    print(json.dumps(compact_line(line)), flush=True)
     barrier(world)
     if failures:
         sys.exit(f"bench.py: {len(failures)} measurement(s) failed or degraded: {', '.join(failures)} "
