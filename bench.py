@@ -394,8 +394,7 @@ def rc_roofline(codec, frames_dev, symbols, reps: int, config: str) -> dict:
     sequence: of its pass-1 kernel) from the committed PMC counters."""
     from streamoptima_amd import _lib
     e0 = codec.engine()
-    tiles_x, ntr = -(-e0.nbx // 8), -(-e0.nby // 2)   # 128 x 32 px tiles (so_me.hip p_run_2pass_fused_ok)
-    fused = _lib.load().so_get_option(_lib.OPT_RUN_2PASS_FUSED) == 1 and 2 * tiles_x < tiles_x * ntr
+    fused = _lib.load().so_p_run_2pass_fused(e0.h, e0.w) == 1   # the library's own choice
     eng = codec.engine()
     qp_sched = codec.row_qp_schedule(eng.nby)
     qdev = eng.qp_row_tensor(qp_sched)

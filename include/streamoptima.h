@@ -241,6 +241,13 @@ int so_encode_p_run(const uint8_t* const* curs, int nframes, const uint8_t* ref0
  * pass-2 reconstruction, frame 0 from ref0.  Same coverage and workspace as so_encode_p_run
  * (W <= 8192).
  */
+/*
+ * 1 when so_encode_p_run_2pass runs an H x W frame (bs 16) in the one persistent launch (the
+ * option SO_OPT_RUN_2PASS_FUSED is on and the frame has three 32-row tile rows or more, which
+ * the merged schedule's deadlock-freedom needs), 0 when it enqueues the per-frame sequence.
+ */
+int so_p_run_2pass_fused(int H, int W);
+
 int so_encode_p_run_2pass(const uint8_t* const* curs, int nframes, const uint8_t* ref0, int H, int W,
                           int bs, int sr, int qp_rd, const int32_t* qp_row, const int32_t* roi,
                           int qp_lo, int qp_hi, uint8_t* const* out_split, int16_t* const* out_mv,

@@ -41,6 +41,7 @@ _SIGS = {
     "so_p_run_workspace_elems": ([_i, _i], _sz),
     "so_p_run_resident_workgroups": ([_i], _i),
     "so_p_run_mode_resident_workgroups": ([_i, _i], _i),
+    "so_p_run_2pass_fused": ([_i, _i], _i),
     "so_encode_p_run": ([_vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _i, _d, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
                         _i),
     "so_encode_p_run_2pass": ([_vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp,

@@ -437,6 +437,10 @@ int so_p_run_resident_workgroups(int vbs) {
     return n;
 }
 
+int so_p_run_2pass_fused(int H, int W) {
+    return H > 0 && W > 0 && option(SO_OPT_RUN_2PASS_FUSED) == 1 && p_run_2pass_fused_ok(H, W) ? 1 : 0;
+}
+
 int so_p_run_mode_resident_workgroups(int mode, int vbs) {
     if (mode < 0 || mode > 4 || (vbs && mode != 0 && mode != 2)) {
         set_error("so_p_run_mode_resident_workgroups: mode %d%s", mode, vbs ? " with vbs (modes 0, 2)" : " (0..4)");
@@ -566,7 +570,7 @@ int so_encode_p_run_2pass(const uint8_t* const* curs, int nframes, const uint8_t
     // default: both passes of every frame in one persistent launch (each task the pass 2 of one
     // tile and the pass 1 of another), for frames of three tile rows or
     // more; otherwise, or with SO_OPT_RUN_2PASS_FUSED = 0, the per-frame sequence below
-    if (option(SO_OPT_RUN_2PASS_FUSED) == 1 && p_run_2pass_fused_ok(H, W))
+    if (so_p_run_2pass_fused(H, W))
         return p_run_2pass_launch(curs, nframes, ref0, H, W, qp_rd, qp_row, roi, qp_lo, qp_hi, outs.data(), workspace,
                                   st);
     // per frame, pass 1 (fused search + tokens only) and pass 2 (the QP map from pass 1's token

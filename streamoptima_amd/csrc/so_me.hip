@@ -19,6 +19,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -2530,7 +2531,16 @@ SO_DEV void tq16_pass2(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
     if (gbx < nbx && gby < by1) {
         const size_t b = (size_t)gby * nbx + gbx;
         const int x = gbx * 16, y = gby * 16;
-        const int dx = o.mv[b * 12], dy = o.mv[b * 12 + 1];
+        // pass 1's motion vector, clamped to the plane.  Pass 1 keeps every vector inside the
+        // reference's strict candidate bounds (0 <= x + dx < W - 16), so the clamp never moves a
+        // vector pass 1 wrote; it bounds the read when pass 1 did NOT write it: after a timed-out
+        // wait the run's later waits return at once (SO_RUN_ABORT_CHECK), so a pass-2 unit can
+        // run before its row's pass 1 and read whatever the record held -- unclamped, that was
+        // the frame pipeline's hipErrorIllegalAddress after a lost hand-off
+        const int Hp = by1 * 16;
+        int dx = o.mv[b * 12], dy = o.mv[b * 12 + 1];
+        dx = x + dx < 0 ? -x : (x + dx > W - 16 ? W - 16 - x : dx);
+        dy = y + dy < 0 ? -y : (y + dy > Hp - 16 ? Hp - 16 - y : dy);
         int qpr;
         {   // qp_map_kernel (so_capi.hip), per block
             const long long tn = (long long)t1[b] * nbx, m = S.msum[byl];
@@ -2782,8 +2792,14 @@ SO_DEV uint32_t run_poll(const uint32_t* c, bool need, bool sysl, uint32_t* ws, 
         const uint32_t active = now - susp;
         if (!esc && active > (uint32_t)kRunEscalateTicks) {
             esc = true;
+            // a stale copy, not a late arrival: the RMW (served by L2) finds the flag set AND a
+            // relaxed load issued after it still misses it.  Comparing the RMW with `raw`, the
+            // load from before the s_sleep, counted a flag set inside that window as stale
+            // (ADVICE r05); flags only grow (launch epochs), so a coherent load after the RMW
+            // must see at least what the RMW saw.
             const uint32_t v2 = (need && !sysl) ? rmw_read(c) : raw;
-            if (__builtin_amdgcn_ballot_w64(need && !sysl && !ok && v2 == w.want) != 0)
+            const uint32_t v3 = (need && !sysl) ? __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : raw;
+            if (__builtin_amdgcn_ballot_w64(need && !sysl && !ok && v2 == w.want && v3 != w.want) != 0)
                 __hip_atomic_fetch_add(&ws[kRunStaleWord], one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (active > (uint32_t)w.limit) {
@@ -3294,7 +3310,11 @@ size_t p_run_workspace_words(int H, int W) {
 // (the occupancy API), cached per (device, kernel) under a mutex -- a process may drive several
 // devices from several host threads.  (The grid only sizes the run: a workgroup that is not
 // resident holds no task, so an over-estimate costs speed, never progress.)
-constexpr size_t kLdsPerCuObserved = 161280;   // 3 x 53,760 B resident at once (ubench_lds_occ)
+constexpr size_t kLdsPerCuObserved = 161280;   // gfx950: 3 x 53,760 B resident at once (ubench_lds_occ)
+// the VBS run holds three workgroups per CU only while its LDS (PTileLds + the kernel's few
+// scalars) stays within 53,760 B: a later LDS increase must not silently drop it to two
+static_assert(sizeof(PTileLds<Sea2GeoT<SO_PTILE_NW>, true>) + 64 <= kLdsPerCuObserved / 3,
+              "the VBS run's LDS no longer fits three workgroups per gfx950 CU");
 static int run_shape(const void* kernel, int* ncu, int* per_cu) {
     static std::mutex mu;
     static std::map<std::pair<int, const void*>, std::pair<int, int>> cache;
@@ -3315,8 +3335,12 @@ static int run_shape(const void* kernel, int* ncu, int* per_cu) {
         // 512-thread workgroups per CU for 53,880 B of LDS, but a CU runs only two of them at
         // once (three up to 53,760 B; tools/ubench_lds_occ.cpp, profiles/r05/ubench_lds_occ.log).
         // Count 512-B granules against the 161,280 B three such workgroups were seen to share.
+        // (an observation on gfx950 only: other devices keep the occupancy API's count)
+        hipDeviceProp_t prop{};
+        const bool gfx950 = hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+                            std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
         hipFuncAttributes fa{};
-        if (hipFuncGetAttributes(&fa, kernel) == hipSuccess && fa.sharedSizeBytes > 0) {
+        if (gfx950 && hipFuncGetAttributes(&fa, kernel) == hipSuccess && fa.sharedSizeBytes > 0) {
             const size_t g = (fa.sharedSizeBytes + 511) & ~(size_t)511;
             const int by_lds = (int)(kLdsPerCuObserved / g);
             if (by_lds >= 1 && by_lds < p) p = by_lds;
@@ -3373,7 +3397,13 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
                           const int* deps = nullptr, int conc = 1, double lam = 0.0) {
     using G = Sea2GeoT<SO_PTILE_NW>;
     // the test-hook instantiation (one GPU only) while SO_OPT_COUNT_SAD_OPS / _TEST_LOSE_FLAG is set
-    const bool hooks = MODE == kRunSingle && (option(SO_OPT_COUNT_SAD_OPS) != 0 || option(SO_OPT_TEST_LOSE_FLAG) != 0);
+    const bool hook_set = option(SO_OPT_COUNT_SAD_OPS) != 0 || option(SO_OPT_TEST_LOSE_FLAG) != 0;
+    if (hook_set && MODE != kRunSingle) {   // no hook instantiation here: refuse rather than ignore
+        set_error("p_run: SO_OPT_COUNT_SAD_OPS / SO_OPT_TEST_LOSE_FLAG apply to the one-GPU run only (so_encode_p_run, "
+                  "so_encode_p_runs); this run kind has no hook instantiation");
+        return SO_E_INVALID;
+    }
+    const bool hooks = MODE == kRunSingle && hook_set;
     const void* const kfn = hooks ? reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, MODE == kRunSingle>)
                                   : reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, false>);
     if (hooks && option(SO_OPT_TEST_LOSE_FLAG) != 0) {

@@ -173,6 +173,33 @@ def test_two_pass_run_edge_shapes(gpu, monkeypatch, h):
     assert [symbols_digest(s) for s in got["symbols"]] == exp
 
 
+def test_two_pass_run_longer_than_one_launch(gpu, monkeypatch):
+    """The merged two-pass schedule over more P-frames than one launch holds (kRunMax = 32): 39
+    P-frames at 96 rows (three tile rows, the fewest the merged schedule takes) run as two
+    chunked launches, each with its own lag2 tail, and must equal the Python-driven per-frame
+    sequence frame by frame with the QP maps."""
+    from streamoptima_amd.Encoder import Y_Video_codec
+    from streamoptima_amd.digest import symbols_digest
+    from streamoptima_amd.engine import alloc_planes
+    from streamoptima_amd.synth import synth_sequence_torch
+    from streamoptima_amd.workloads import RC_TABLES
+    h, w, f = 96, 640, 40
+    codec = Y_Video_codec(h, w, f, 16, 16, 4, f, 0, 0.015, False, RCFlag=3, targetBR="2 mbps",
+                          qp_rate_tables=RC_TABLES, roi=[(100, 16, 400, 60, -2)], device=gpu)
+    fr = alloc_planes(f, h, w, gpu)
+    fr.copy_(synth_sequence_torch(f, h, w, seed=9, device=gpu))
+    monkeypatch.setenv("SO_PIPELINE", "0")
+    exp = codec.encode_device(fr, f)
+    exp_d = [symbols_digest(s) for s in exp["symbols"]]
+    monkeypatch.delenv("SO_PIPELINE")
+    assert _lib.load().so_p_run_2pass_fused(h, w) == 1
+    got = codec.encode_device(fr, f)
+    torch.cuda.synchronize()
+    codec.engine().check_run()
+    assert [symbols_digest(s) for s in got["symbols"]] == exp_d
+    assert torch.equal(got["sse"], exp["sse"])
+
+
 @pytest.mark.parametrize("roi", [None, [(100, 40, 400, 200, -2)]])
 def test_two_pass_gop_replayed_as_hip_graph(gpu, roi):
     """bench.py --graph: a ROI / two-pass GOP captured once as a HIP graph (no host->device

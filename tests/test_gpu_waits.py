@@ -74,3 +74,45 @@ def test_sad_op_count_is_deterministic_and_output_neutral(gpu):
     assert counts[0] == counts[1]
     blocks = eng.nb * len(curs)
     assert 73 * 256 * blocks < counts[0] < 1152 * 256 * blocks
+
+
+def test_frame_pipeline_two_pass_lost_handoff_reports_and_does_not_fault(gpu):
+    """The frame-pipeline two-pass run (kRunFPipe2P) whose reference never arrives: rank 1 of two
+    is launched alone, so the I-frame push from rank 0 into its landing slot 0 never happens.
+    Its first pass-1 wait times out after 2 s and records itself (frame 0 on dep -1, the landing
+    flags never arrived); every later wait then returns at once, so pass-2 units can run before
+    their row's pass 1 and read motion records nobody wrote.  Those records are poisoned here
+    (dx = dy = 0x7F7F): read unclamped they addressed ~125 MB past the reference plane -- the
+    round-5 hipErrorIllegalAddress.  The run must end without a device fault, check() must
+    raise with the record, and a one-GPU encode on the same device afterwards must be exact."""
+    from streamoptima_amd.digest import symbols_digest
+    from streamoptima_amd.engine import Engine
+    from streamoptima_amd.pipeline import FramePipeRank
+    eng0, fr, i0, outs = _run_setup(gpu, seed=7)
+    curs = [fr[i] for i in range(1, fr.shape[0])]
+    eng0.encode_p_run(curs, i0.recon, 4, outs)
+    eng0.check_run()
+    exp = [symbols_digest(s) for s in outs]
+    h, w, nf = fr.shape[1], fr.shape[2], fr.shape[0]
+    engines = [Engine(h, w, 16, 16, False, 0.015, gpu) for _ in range(2)]
+    ranks = [FramePipeRank(engines[r], 2, r, nf, max_wg=96) for r in range(2)]
+    torch.cuda.synchronize()
+    for r in range(2):
+        ranks[r].connect(ranks[(r + 1) % 2].info(), ranks[(r - 1) % 2].info())
+    qp_row = [4] * (h // 16)
+    syms, _ = ranks[1].prepare(nf, qp_row, True)
+    for s in syms.values():
+        s.mv.view(torch.uint8).fill_(0x7F)
+    torch.cuda.synchronize()
+    ranks[1].encode(fr, nf, 4, qp_row=qp_row, two_pass=True, qp_clamp=(0, 12))
+    torch.cuda.synchronize()                        # a device fault would raise here
+    with pytest.raises(RuntimeError, match=r"frame pipeline, two-pass wait \(pass 1\).*frame 0 on dep -1.*never arrived"):
+        ranks[1].check()
+    rec = ranks[1].wait_health.records[-1]
+    assert rec["mode"] == "frame pipeline, two-pass" and rec["pass"] == 1 and rec["frame"] == 0
+    assert rec["poll_us"] >= 2e6 and rec["lanes_remote"] != 0
+    for r in ranks:
+        r.close()
+    eng0.encode_p_run(curs, i0.recon, 4, outs)      # the device is healthy: same symbols as before
+    eng0.check_run()
+    assert [symbols_digest(s) for s in outs] == exp
