@@ -1431,7 +1431,7 @@ def main(argv=None):
         failures.extend(d["what"] for d in degraded)
     if failures:
         line["failed"] = failures
-    if args.detail_out:
+    if args.detail_out:   # '' = nowhere
         try:
             os.makedirs(os.path.dirname(os.path.abspath(args.detail_out)), exist_ok=True)
             with open(args.detail_out, "w") as fh:

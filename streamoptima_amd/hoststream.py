@@ -27,6 +27,7 @@ import time
 import torch
 
 from .engine import alloc_planes
+from .hwqueue import dedicated_stream
 
 
 class _Buffers:
@@ -49,8 +50,11 @@ class HostStreamEncoder:
         eng = codec.engine()
         self.codec, self.eng, self.nframes, self.chunk = codec, eng, int(nframes), int(chunk)
         self.dev = codec.device
-        self.h2d = torch.cuda.Stream(self.dev)
-        self.d2h = torch.cuda.Stream(self.dev)
+        # the three engines' streams each on a hardware queue of its own (hwqueue.py): on a
+        # shared queue a stream's event wait stalls the others and the region runs serially
+        self.h2d = dedicated_stream(self.dev, "hoststream.h2d")
+        self.d2h = dedicated_stream(self.dev, "hoststream.d2h")
+        self.comp = dedicated_stream(self.dev, "hoststream.compute")
         self.syms = None
         self.bufs = [_Buffers(eng, self.nframes, self.dev) for _ in range(max(1, int(nbuf)))]
 
@@ -94,7 +98,13 @@ class HostStreamEncoder:
         during GOP k's encode."""
         for g in gops:
             self._check(g)
-        eng, comp, nb = self.eng, torch.cuda.current_stream(self.dev), len(self.bufs)
+        caller = torch.cuda.current_stream(self.dev)
+        self.comp.wait_stream(caller)       # the caller's earlier work on the inputs / buffers
+        with torch.cuda.stream(self.comp):
+            self._encode_stream(gops, intra_dur, consume, trace)
+
+    def _encode_stream(self, gops: list, intra_dur: int, consume, trace) -> None:
+        eng, comp, nb = self.eng, self.comp, len(self.bufs)
         if self.syms is None:
             self.syms = [eng.new_symbols(0 if i % intra_dur == 0 else 1) for i in range(self.nframes)]
         pending, waiting = [], []      # chunks whose byte counts are on their way; finished GOPs
