@@ -536,11 +536,13 @@ def pcie_inclusive(codec, cfg, frames_dev, reps: int = 6) -> dict:
     """BASELINE.md §4's timed region: pinned host Y planes -> HBM, the GOP encode, and the
     symbols back to pinned host memory -- as the dense arrays (split, mv, qtc, tokens), and as
     the packed stream (so_pack_frames: varint MVs + RLE token lists, plus per-frame SSE)."""
+    from streamoptima_amd.hostmem import pinned_empty
     f = frames_dev.shape[0]
-    host = frames_dev.cpu().pin_memory()
+    host = pinned_empty(tuple(frames_dev.shape))     # page-locked by registration (hostmem.py)
+    host.copy_(frames_dev.cpu())
     eng = codec.engine()
     pre = [eng.new_symbols(0 if i % cfg["intra_dur"] == 0 else 1) for i in range(f)]
-    outs = [{k: torch.empty(getattr(p, k).shape, dtype=getattr(p, k).dtype).pin_memory()
+    outs = [{k: pinned_empty(tuple(getattr(p, k).shape), getattr(p, k).dtype)
              for k in ("split", "mv", "qtc", "tokens")} for p in pre]
     d2h = sum(t.numel() * t.element_size() for o in outs for t in o.values())
 
@@ -559,7 +561,7 @@ def pcie_inclusive(codec, cfg, frames_dev, reps: int = 6) -> dict:
         got.update(hs.encode(host, cfg["intra_dur"]))
         return sum(got["bytes"]) + 8 * f
 
-    med = {}
+    med, reps_ms = {}, {}
 
     def timed(fn):
         ts, nbytes = [], None
@@ -570,6 +572,7 @@ def pcie_inclusive(codec, cfg, frames_dev, reps: int = 6) -> dict:
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         med[fn.__name__] = float(np.median(ts[1:]))
+        reps_ms[fn.__name__] = [round(t * 1e3, 3) for t in ts]
         return min(ts[1:]), nbytes
 
     def dense_timed():
@@ -585,7 +588,7 @@ def pcie_inclusive(codec, cfg, frames_dev, reps: int = 6) -> dict:
     px = f * cfg["h"] * cfg["w"]
     # the link's own rates on this box: the GOP's pinned Y planes up alone, and as many bytes down
     # alone (copy engines, no kernel) -- the peaks the region's PCIe roofline is measured against
-    dn = torch.empty(host.numel(), dtype=torch.uint8).pin_memory()
+    dn = pinned_empty((host.numel(),))
     flat = frames_dev.view(-1)[:host.numel()]
 
     def up_only():
@@ -612,6 +615,7 @@ def pcie_inclusive(codec, cfg, frames_dev, reps: int = 6) -> dict:
     return {"region": "BASELINE.md §4 (pinned host Y planes in, symbols back in pinned host memory)",
             "mpx_s": round(px / best_p / 1e6, 2), "ms_per_gop": round(best_p * 1e3, 3),
             "ms_per_gop_median": round(med["packed_run"] * 1e3, 3), "reps": reps,
+            "rep_ms": reps_ms.get("packed_run"),
             "h2d_bytes": int(host.numel()), "d2h_bytes": int(d2h_p), "packed_equals_resident_symbols": bool(same),
             "link": link,
             "roofline": {"bound": "pcie", "achieved": round(up_gbs, 2), "peak": link["h2d_gbs"], "unit": "GB/s",

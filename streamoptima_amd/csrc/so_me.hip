@@ -2480,13 +2480,27 @@ SO_DEV void tq16_pass1(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
         }
         double tcr[16];
         xform2d_rows<16, false>(scratch, l, res, tcr, SO_TQ_TW());
+        // TC = np.round(DCT) as int32 (the 1.5 * 2^52 shift rounds half to even, as rint), the
+        // pass-1 levels at the row QP by the exact integer round-half-even shift
         constexpr double kRne = 0x1.8p52;
-        int q[16];
+        int tc[16], q[16];
 #pragma unroll
-        for (int c = 0; c < 16; ++c)
-            q[c] = (int)(uint32_t)__builtin_bit_cast(
-                uint64_t, __builtin_amdgcn_ldexp(__builtin_rint(tcr[c]), -q_exp_fast<16>(l, c, qpr)) + kRne);
+        for (int c = 0; c < 16; ++c) tc[c] = (int)(uint32_t)__builtin_bit_cast(uint64_t, tcr[c] + kRne);
+        quant_row_int<16>(tc, l, qpr, q);
         const int tok = block_tokens<16>(nullptr, l, q);
+        // the coefficients wait for pass 2 in the block's QTC rows (|TC| <= 4080: int16), stored
+        // write-through like the ME records: pass 2 requantises them at the block's QP instead
+        // of forming the residual and running the forward transform again (same MV, same
+        // planes, so the same TC)
+        {
+            uint32_t w[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) w[k] = (uint32_t)(uint16_t)tc[2 * k] | ((uint32_t)tc[2 * k + 1] << 16);
+            const so_v4u v0{w[0], w[1], w[2], w[3]}, v1{w[4], w[5], w[6], w[7]};
+            int16_t* const qp_ = o.qtc + b * 256 + l * 16;
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(qp_), "v"(v0) : "memory");
+            asm volatile("global_store_dwordx4 %0, %1, off offset:16 sc1" ::"v"(qp_), "v"(v1) : "memory");
+        }
         if (l < 12) store_sc1_i16(o.mv + b * 12 + l, l == 0 ? dx : l == 1 ? dy : l == 2 ? rf : 0);
         if (l == 0) {
             o.split[b] = 0;
@@ -2550,25 +2564,12 @@ SO_DEV void tq16_pass2(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
         }
         const uint8_t* crow = cur + (size_t)(y + l) * W + x;
         const uint8_t* prow = ref + (size_t)(y + dy + l) * W + (x + dx);
-        int res[16];
-        {
-            uint32_t cw[4], pw[4];
-            row16_aligned(crow, cw);
-            row16_any(prow, pw);
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    res[4 * k + e] = (int)((cw[k] >> (8 * e)) & 255) - (int)((pw[k] >> (8 * e)) & 255);
-        }
-        double tcr[16];
-        xform2d_rows<16, false>(scratch, l, res, tcr, SO_TQ_TW());
         constexpr double kRne = 0x1.8p52;
-        int q[16];
-#pragma unroll
-        for (int c = 0; c < 16; ++c)
-            q[c] = (int)(uint32_t)__builtin_bit_cast(
-                uint64_t, __builtin_amdgcn_ldexp(__builtin_rint(tcr[c]), -q_exp_fast<16>(l, c, qpr)) + kRne);
+        // the coefficients pass 1 left in the QTC rows (after the wait's acquire), requantised
+        // at the block's QP: q = np.round(TC / 2^k), the exact integer round-half-even shift
+        int tc[16], q[16];
+        load_row_i16<16>(o.qtc + b * 256 + l * 16, tc);
+        quant_row_int<16>(tc, l, qpr, q);
         const int tok = block_tokens<16>(nullptr, l, q);
         store_row_i16<16>(o.qtc + b * 256 + l * 16, q);
         int dq[16];

@@ -27,6 +27,7 @@ import time
 import torch
 
 from .engine import alloc_planes
+from .hostmem import pinned_empty
 from .hwqueue import dedicated_stream
 
 
@@ -37,9 +38,9 @@ class _Buffers:
         self.frames_dev = alloc_planes(nframes, eng.h, eng.w, dev)
         self.offs = torch.empty((nframes, eng.nb + 1), dtype=torch.int32, device=dev)
         self.packed = torch.empty((nframes, eng.pack_bound()), dtype=torch.uint8, device=dev)
-        self.tot_h = torch.empty(nframes, dtype=torch.int32).pin_memory()
-        self.packed_h = torch.empty(self.packed.shape, dtype=torch.uint8).pin_memory()
-        self.sse_h = torch.empty(nframes, dtype=torch.int64).pin_memory()
+        self.tot_h = pinned_empty((nframes,), torch.int32)
+        self.packed_h = pinned_empty(tuple(self.packed.shape))
+        self.sse_h = pinned_empty((nframes,), torch.int64)
         self.enc_done = None      # compute-stream event: this set's frames are no longer read
         self.d2h_done = None      # D2H-stream event: this set's packed streams are downloaded
         self.gop = None           # (index, frame types) of the GOP it holds
