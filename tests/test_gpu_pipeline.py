@@ -408,3 +408,43 @@ def test_claim_capacity_fits_every_run_kind(gpu):
         assert cap == min(per.values()), (vbs, cap, per)
     assert lib.so_p_run_mode_resident_workgroups(1, 1) < 0      # no VBS stripe run
     assert lib.so_p_run_mode_resident_workgroups(7, 0) < 0
+
+
+def test_frame_pipeline_late_rank_is_not_a_stale_read(gpu):
+    """A hand-off that arrives after its waits escalated to atomic reads (1 ms of polling) is a
+    late flag, not a stale one: rank 1's grid is launched 20 ms before rank 0's, so its first
+    waits poll through the escalation point and then see the flags arrive.  check() must report
+    neither a timeout nor a stale read (the detector counts a flag only when a load issued after
+    the RMW still misses what the RMW found), and the GOP must equal the one-GPU
+    encode."""
+    import time
+    from streamoptima_amd.digest import symbols_digest
+    from streamoptima_amd.engine import Engine
+    from streamoptima_amd.pipeline import FramePipeRank
+    name, world, nframes = "1080p", 2, 6
+    cfg, fr = _frames(name, gpu, nframes)
+    h, w = fr.shape[1:]
+    engines = [Engine(h, w, 16, 16, False, 0.015, gpu) for _ in range(world)]
+    streams = _streams(gpu)[:world]
+    ranks = [FramePipeRank(engines[r], world, r, nframes, stream=streams[r], max_wg=768 // (2 * world))
+             for r in range(world)]
+    torch.cuda.synchronize()
+    for r in range(world):
+        ranks[r].connect(ranks[(r + 1) % world].info(), ranks[(r - 1) % world].info())
+    for r in range(world):
+        ranks[r].prepare(nframes)
+    torch.cuda.synchronize()
+    syms = {}
+    for r in (1, 0):
+        with torch.cuda.stream(streams[r]):
+            syms.update(ranks[r].encode(fr, nframes, cfg["qp"]))
+        if r == 1:
+            time.sleep(0.02)
+    torch.cuda.synchronize()
+    for r in ranks:
+        r.check()                                   # raises on a timeout or a stale read
+        assert r.wait_health.stale_reads == 0
+    got = [symbols_digest(syms[k]) for k in range(nframes)]
+    assert got == FIX[name]["frame_sha256"][:nframes]
+    for r in ranks:
+        r.close()
