@@ -532,7 +532,7 @@ def cpu_baseline(cfg, rows: int, pool_rows: int) -> dict:
 
 
 # ---- PCIe-inclusive --------------------------------------------------------------------------------
-def pcie_inclusive(codec, cfg, frames_dev, reps: int = 6) -> dict:
+def pcie_inclusive(codec, cfg, frames_dev, reps: int = 10) -> dict:
     """BASELINE.md §4's timed region: pinned host Y planes -> HBM, the GOP encode, and the
     symbols back to pinned host memory -- as the dense arrays (split, mv, qtc, tokens), and as
     the packed stream (so_pack_frames: varint MVs + RLE token lists, plus per-frame SSE)."""
@@ -565,15 +565,15 @@ def pcie_inclusive(codec, cfg, frames_dev, reps: int = 6) -> dict:
 
     def timed(fn):
         ts, nbytes = [], None
-        for _ in range(reps + 1):      # the first call warms the path (allocations, first copies)
+        for _ in range(reps + 2):      # the first two calls warm the path (allocations, first copies)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             nbytes = fn()
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
-        med[fn.__name__] = float(np.median(ts[1:]))
+        med[fn.__name__] = float(np.median(ts[2:]))
         reps_ms[fn.__name__] = [round(t * 1e3, 3) for t in ts]
-        return min(ts[1:]), nbytes
+        return min(ts[2:]), nbytes
 
     def dense_timed():
         frames_dev.copy_(host, non_blocking=True)
