@@ -314,11 +314,17 @@ def pmc_record(config: str, kernel: str):
         ks = json.load(open(p)).get(config, {}).get("kernels", {})
     except (ValueError, OSError):
         return {}
-    # a kernel name from before the run kernel's test-hook template argument (", false>") matches too
-    alt = kernel[:-len(", false>")] + ">" if kernel.endswith(", false>") else None
+    # exact name first; else a name from before the run kernel's later template arguments (the
+    # test hooks, round 5; the uniform QP, round 6) when those were false
     for k, v in ks.items():
-        if k.startswith(kernel) or (alt and k.startswith(alt)):
+        if k.startswith(kernel):
             return v
+    alt = kernel
+    while alt.endswith(", false>"):
+        alt = alt[:-len(", false>")] + ">"
+        for k, v in ks.items():
+            if k.startswith(alt):
+                return v
     return {}
 
 
@@ -328,7 +334,8 @@ def roofline_of(rl: dict, config: str) -> dict:
     fraction of its algorithmic bytes, the VALU busy fraction and HBM traffic from the
     committed PMC counters of the same workload, and the SAD fraction of the searches'
     EXECUTED v_sad byte operations (kernel-side count, SO_P_RUN_SAD_OPS_WORD)."""
-    kname = f"so::p_run_kernel<8, 0, {'true' if rl['vbs'] else 'false'}, false>"
+    # the VBS workloads carry no row-QP schedule: the uniform-QP instantiation (so_me.hip UQP)
+    kname = ("so::p_run_kernel<8, 0, true, false, true>" if rl["vbs"] else "so::p_run_kernel<8, 0, false, false, false>")
     n_launch = -(-rl["run_frames"] // 32)       # so_encode_p_run: <= 32 frames per launch
     launch_s = rl["run_s"] / n_launch
     alg = rl["run_frames"] * rl["frame_bytes"] / n_launch
@@ -425,7 +432,7 @@ def rc_roofline(codec, frames_dev, symbols, reps: int, config: str) -> dict:
     eng.check_run()
     frame_bytes = alg_frame_bytes(eng.h, eng.w)
     gbs = frame_bytes / per_frame / 1e9
-    kname = "so::p_run_kernel<8, 3, false, false>" if fused else "so::p_tile_kernel<8, true>"
+    kname = "so::p_run_kernel<8, 3, false, false, false>" if fused else "so::p_tile_kernel<8, true>"
     # one persistent launch per <= 32 P-frames (fused); the sequence launches per frame
     n_launch = -(-(nf - 1) // 32) if fused else nf - 1
     launch_frames = (nf - 1) / n_launch
@@ -437,7 +444,7 @@ def rc_roofline(codec, frames_dev, symbols, reps: int, config: str) -> dict:
                 "valu_busy_frac": round(4 * pm["sq_active_inst_valu"] / (cyc * N_SIMD), 4),
                 "waves_per_simd": round(4 * pm["sq_wave_cycles"] / (cyc * N_SIMD), 2) if pm.get("sq_wave_cycles") else None,
                 "source": f"profiles/pmc_me_traffic.json [{config}]"}
-    kdesc = ("two-pass P-run in one persistent launch (so_encode_p_run_2pass): p_run_kernel<8, 3, false, false>"
+    kdesc = ("two-pass P-run in one persistent launch (so_encode_p_run_2pass): p_run_kernel<8, 3, false, false, false>"
              if fused else "two-pass P-frame sequence (so_encode_p_run_2pass): p_tile_kernel<8, true> (pass 1) + "
              "inter_tq_kernel<16, false, false, true> (pass 2: QP map + transforms)")
     return {"bound": "hbm", "kernel": kdesc,

@@ -2883,12 +2883,18 @@ SO_DEV uint32_t run_dequeue(uint32_t* ws) {
 // (SO_OPT_COUNT_SAD_OPS) and the deliberately lost done flag (SO_OPT_TEST_LOSE_FLAG).  Only
 // kRunSingle has a HOOKS instantiation, launched only while one of those options is set, so the
 // timed kernels carry neither (count_ops folds to the constant 0 and its atomics are dead code).
-template <int NW, int MODE, bool VBS = false, bool HOOKS = false>
+// UQP (VBS runs without a row-QP schedule): every block at the RD QP, known at compile time --
+// the block coefficients tq16_vbs_fwd would hold through the sub-block transforms for a
+// requantisation at another QP are then dead (VBS run spills 30 -> 23; 4K VBS GOP 3.311 ->
+// 3.265 ms, profiles/r06/ab_vbs_uqp.log).
+template <int NW, int MODE, bool VBS = false, bool HOOKS = false, bool UQP = false>
 __global__ void __launch_bounds__(NW * 64)
 __attribute__((amdgpu_waves_per_eu(VBS ? SO_VBS_WPE : (NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE))))
 p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, int H, int W,
-             int qp_rd, const int32_t* __restrict__ qp_row, uint32_t* __restrict__ ws, int ws_stamp_base,
+             int qp_rd, const int32_t* __restrict__ qp_row_arg, uint32_t* __restrict__ ws, int ws_stamp_base,
              const PRunStripe sp, double lam) {
+    static_assert(!UQP || VBS, "the uniform-QP instantiation is the VBS run's");
+    const int32_t* __restrict__ const qp_row = UQP ? nullptr : qp_row_arg;
     using G = Sea2GeoT<NW>;
     __shared__ PTileLds<G, VBS> S;
     __shared__ int s_task;
@@ -3360,7 +3366,7 @@ static int run_shape(const void* kernel, int* ncu, int* per_cu) {
 // ranks sharing one device size their claims by it, whichever kernel each of them launches.
 int p_run_capacity(int vbs, int mode) {
     constexpr int NW = SO_PTILE_NW;
-    const void* ks[8];
+    const void* ks[12];
     int n = 0;
     const auto add = [&](int m, const void* k) {
         if (mode < 0 || mode == m) ks[n++] = k;
@@ -3368,7 +3374,10 @@ int p_run_capacity(int vbs, int mode) {
     if (vbs) {
         add(kRunSingle, reinterpret_cast<const void*>(p_run_kernel<NW, kRunSingle, true>));
         add(kRunSingle, reinterpret_cast<const void*>(p_run_kernel<NW, kRunSingle, true, true>));
+        add(kRunSingle, reinterpret_cast<const void*>(p_run_kernel<NW, kRunSingle, true, false, true>));
+        add(kRunSingle, reinterpret_cast<const void*>(p_run_kernel<NW, kRunSingle, true, true, true>));
         add(kRunFPipe, reinterpret_cast<const void*>(p_run_kernel<NW, kRunFPipe, true>));
+        add(kRunFPipe, reinterpret_cast<const void*>(p_run_kernel<NW, kRunFPipe, true, false, true>));
     } else {
         add(kRunSingle, reinterpret_cast<const void*>(p_run_kernel<NW, kRunSingle, false>));
         add(kRunSingle, reinterpret_cast<const void*>(p_run_kernel<NW, kRunSingle, false, true>));
@@ -3405,8 +3414,13 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
         return SO_E_INVALID;
     }
     const bool hooks = MODE == kRunSingle && hook_set;
-    const void* const kfn = hooks ? reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, MODE == kRunSingle>)
-                                  : reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, false>);
+    // VBS without a row-QP schedule: the uniform-QP instantiation (p_run_kernel's UQP)
+    const bool uqp = VBS && qp_row == nullptr;
+    const void* const kfn =
+        hooks ? (uqp ? reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, MODE == kRunSingle, VBS>)
+                     : reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, MODE == kRunSingle>))
+              : (uqp ? reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, false, VBS>)
+                     : reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, false>));
     if (hooks && option(SO_OPT_TEST_LOSE_FLAG) != 0) {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
@@ -3472,14 +3486,19 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
 #endif
             sp.p2lag = lag < 1 ? 1 : (lag > ntr ? ntr : lag);
         }
-        if (hooks)
-            hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, MODE, VBS, MODE == kRunSingle>), dim3((unsigned)grid),
-                               dim3(SO_PTILE_NW * 64), 0, st, a, n, f0 ? outs[f0 - 1].recon : ref0, H, W, qp_rd, qp_row, ws,
-                               (int)(f0 * ntiles), sp, lam);
+        const uint8_t* const r0 = f0 ? outs[f0 - 1].recon : ref0;
+#define SO_P_RUN_GO(HK, UQ)                                                                                        \
+    hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, MODE, VBS, HK, UQ>), dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), \
+                       0, st, a, n, r0, H, W, qp_rd, qp_row, ws, (int)(f0 * ntiles), sp, lam)
+        if (hooks && uqp)
+            SO_P_RUN_GO(MODE == kRunSingle, VBS);
+        else if (hooks)
+            SO_P_RUN_GO(MODE == kRunSingle, false);
+        else if (uqp)
+            SO_P_RUN_GO(false, VBS);
         else
-            hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, MODE, VBS, false>), dim3((unsigned)grid), dim3(SO_PTILE_NW * 64),
-                               0, st, a, n, f0 ? outs[f0 - 1].recon : ref0, H, W, qp_rd, qp_row, ws, (int)(f0 * ntiles),
-                               sp, lam);
+            SO_P_RUN_GO(false, false);
+#undef SO_P_RUN_GO
         const int rc = check_launch("p_run_kernel");
         if (rc != SO_OK) return rc;
     }

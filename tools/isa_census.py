@@ -69,7 +69,7 @@ def census(asm: str, fn: str) -> dict:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernel", default="p_run_kernel<8, 0, false, false>")
+    ap.add_argument("--kernel", default="p_run_kernel<8, 0, false, false, false>")
     ap.add_argument("-D", dest="defines", action="append", default=[])
     ap.add_argument("--json", action="store_true")
     a = ap.parse_args()
