@@ -270,15 +270,27 @@ def kernel_roofline(codec, frames_dev, symbols, reps: int, components: bool = Tr
         while time.perf_counter() < t_end:
             fn()
             torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
-        e0.record(stream)
-        n_rep = max(2, reps // 10) if name == "run" else reps
-        for _ in range(n_rep):
-            fn()
-        e1.record(stream)
-        torch.cuda.synchronize()
-        out[name] = e0.elapsed_time(e1) / n_rep / 1e3  # seconds per call
+        if name == "run":
+            # each launch between its own pair of events on the launch stream; the median of
+            # max(6, reps / 2) launches (one slow launch after the parity pass's idle stretch
+            # set the mean of two)
+            evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(max(6, reps // 2))]
+            for a, b in evs:
+                a.record(stream)
+                fn()
+                b.record(stream)
+            torch.cuda.synchronize()
+            out[name] = float(np.median([a.elapsed_time(b) for a, b in evs])) / 1e3
+        else:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                fn()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            out[name] = e0.elapsed_time(e1) / reps / 1e3  # seconds per call
         if name == "run":
             # the executed SAD operations of the same work: one more (untimed) replay with the
             # kernel-side count on (SO_OPT_COUNT_SAD_OPS, words 66..67; off in timed runs)
@@ -421,14 +433,13 @@ def rc_roofline(codec, frames_dev, symbols, reps: int, config: str) -> dict:
     while time.perf_counter() < t_end:
         seq()
         torch.cuda.synchronize()
-    n_rep = max(2, reps // 10)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(n_rep):
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(max(6, reps // 2))]
+    for a, b in evs:              # each run between its own events; the median (kernel_roofline)
+        a.record(stream)
         seq()
-    e1.record(stream)
+        b.record(stream)
     torch.cuda.synchronize()
-    per_frame = e0.elapsed_time(e1) / 1e3 / n_rep / (nf - 1)
+    per_frame = float(np.median([a.elapsed_time(b) for a, b in evs])) / 1e3 / (nf - 1)
     eng.check_run()
     frame_bytes = alg_frame_bytes(eng.h, eng.w)
     gbs = frame_bytes / per_frame / 1e9
