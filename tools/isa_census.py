@@ -23,11 +23,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def mangled(kernel: str) -> str:
-    m = re.match(r"p_run_kernel<(\d+), (\d+), (true|false), (true|false)>", kernel)
+    m = re.match(r"p_run_kernel<(\d+), (\d+), (true|false), (true|false)(?:, (true|false))?>", kernel)
     if not m:
-        raise SystemExit(f"kernel {kernel!r}: expected p_run_kernel<NW, MODE, VBS, HOOKS>")
+        raise SystemExit(f"kernel {kernel!r}: expected p_run_kernel<NW, MODE, VBS, HOOKS, UQP>")
     b = lambda v: "1" if v == "true" else "0"   # noqa: E731
-    return (f"_ZN2so12p_run_kernelILi{m.group(1)}ELi{m.group(2)}ELb{b(m.group(3))}ELb{b(m.group(4))}EEEvNS_8PRunArgsEiPKhiiiPKiPjiNS_10PRunStripeEd")
+    return (f"_ZN2so12p_run_kernelILi{m.group(1)}ELi{m.group(2)}ELb{b(m.group(3))}ELb{b(m.group(4))}"
+            f"ELb{b(m.group(5) or 'false')}EEEvNS_8PRunArgsEiPKhiiiPKiPjiNS_10PRunStripeEd")
 
 
 def census(asm: str, fn: str) -> dict:

@@ -23,7 +23,8 @@ NAMES = ("loop_top stage_cur stage_cur_int stage_cur_edge cur_sums wait poll_ite
          "stage_win_edge dense_tile dense_tile_block byte_sums block_top bound umin umin_edge ballots bal_row dense_fallback survivors "
          "sur_one sur_le4 sur_pass search_end decode_keys tq_residual tq_fwd tq_quant tq_tokens tq_qtc_store tq_inv "
          "tq_recon tq_sse_records post done_flag task_end vbs_block vbs_umin vbs_list_a vbs_pass vbs_list_b vbs_final "
-         "vbs_dense vbs_fwd vbs_fwd_sub vbs_final_q vbs_inv vbs_inv_split vbs_inv_end wait_w0 keys_tail").split()
+         "vbs_dense vbs_fwd vbs_fwd_sub vbs_final_q vbs_inv vbs_inv_split vbs_inv_end wait_w0 keys_tail p1_tq p1_flag "
+         "p2_wait p2_sums p2_tq p2_flag").split()
 
 
 def count():
@@ -42,22 +43,46 @@ def count():
     fr.copy_(synth_sequence_torch(f, h, w, seed=0, device=dev, content=os.environ.get("SO_AB_CONTENT", "bench")))
     i0 = eng.encode_i(fr[0], 4)
     outs = [eng.new_symbols(1) for _ in range(f - 1)]
-    eng.encode_p_run([fr[i] for i in range(1, f)], i0.recon, 4, outs)   # warm (uncounted)
+    two = os.environ.get("SO_AB_2PASS") == "1"
+    if two:   # configs[4]'s two-pass run: its workload's row-QP schedule, ROI and clamp (bench.py)
+        sys.path.insert(0, ROOT)
+        import bench
+        from streamoptima_amd.workloads import WORKLOADS
+        cfg = dict(WORKLOADS["4k_rc2pass"])
+        codec = bench.build_codec(cfg, None, dev)
+        eng = codec.engine()
+        i0 = eng.encode_i(fr[0], 4)
+        qs = codec.row_qp_schedule(eng.nby)
+        roi = codec.roi_block_offsets()
+        kw = dict(qp_row=qs, qp_row_dev=eng.qp_row_tensor(qs),
+                  roi_dev=eng.device_const_i32(roi) if roi is not None else None,
+                  qp_lo=codec.qp_clamp[0], qp_hi=codec.qp_clamp[1])
+        maps = [torch.empty(eng.nb, dtype=torch.int32, device=dev) for _ in range(f - 1)]
+        outs = [eng.new_symbols(1) for _ in range(f - 1)]
+
+    def run():
+        if two:
+            eng.encode_p_run_2pass([fr[i] for i in range(1, f)], i0.recon, codec.const_init_Qp, outs, maps, **kw)
+        else:
+            eng.encode_p_run([fr[i] for i in range(1, f)], i0.recon, 4, outs)
+    run()   # warm (uncounted)
     torch.cuda.synchronize()
     assert lib.so_debug_set_mark_counts(ctypes.c_void_p(buf.data_ptr())) == 0
     for _ in range(reps):
-        eng.encode_p_run([fr[i] for i in range(1, f)], i0.recon, 4, outs)
+        run()
     torch.cuda.synchronize()
     eng.check_run()
     c = [int(x) & 0xFFFFFFFF for x in buf.cpu().tolist()]
     print(json.dumps({"launches": reps, "frames_per_launch": f - 1, "blocks_per_frame": (h // 16) * (w // 16),
-                      "size": f"{w}x{h}", "vbs": eng.vbs, "content": os.environ.get("SO_AB_CONTENT", "bench"),
+                      "size": f"{w}x{h}", "vbs": eng.vbs, "two_pass": two,
+                      "content": os.environ.get("SO_AB_CONTENT", "bench"),
                       "counts": {n: c[i] for i, n in enumerate(NAMES)}}))
 
 
 def table(path, pmc_valu=None):
     d = json.load(open(path))
-    kernel = ("p_run_kernel<8, 0, true, false, true>" if d.get('vbs') else "p_run_kernel<8, 0, false, false, false>")
+    kernel = ("p_run_kernel<8, 3, false, false, false>" if d.get("two_pass") else
+              "p_run_kernel<8, 0, true, false, true>" if d.get('vbs') else "p_run_kernel<8, 0, false, false, false>")
     cen = json.loads(subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_census.py"), "--json",
                                      "--kernel", kernel], capture_output=True, text=True, check=True).stdout)
     per_launch = {k: v / d["launches"] for k, v in d["counts"].items()}
