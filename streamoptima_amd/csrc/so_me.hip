@@ -698,7 +698,8 @@ extern "C" int so_debug_set_run_stamps(void* p) {
     X(search_end) X(decode_keys) X(tq_residual) X(tq_fwd) X(tq_quant) X(tq_tokens) X(tq_qtc_store) X(tq_inv) \
     X(tq_recon) X(tq_sse_records) X(post) X(done_flag) X(task_end) X(vbs_block) X(vbs_umin) X(vbs_list_a) \
     X(vbs_pass) X(vbs_list_b) X(vbs_final) X(vbs_dense) X(vbs_fwd) X(vbs_fwd_sub) X(vbs_final_q) X(vbs_inv) \
-    X(vbs_inv_split) X(vbs_inv_end) X(wait_w0) X(keys_tail)
+    X(vbs_inv_split) X(vbs_inv_end) X(wait_w0) X(keys_tail) X(p1_tq) X(p1_flag) X(p2_wait) X(p2_sums) X(p2_tq) \
+    X(p2_flag)
 #define SO_MARK_ENUM(n) kMark_##n,
 enum SoMarkId { SO_MARK_NAMES(SO_MARK_ENUM) kMarkCount };
 #undef SO_MARK_ENUM
@@ -3112,10 +3113,12 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                     S.mer[i].set(rec4);
                 }
                 __syncthreads();
+                SO_MARK(p1_tq);
                 const int t2 = opaque_tid(), ln = t2 & 63, gq = (t2 >> 6) * G::TQ_BPW + (ln >> 4);
                 if (ln < 16 * G::TQ_BPW && gq < G::NBLK)
                     tq16_pass1<G>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by1, qp_rd, qp_row, a.out[f],
                                   t1);
+                SO_MARK(p1_flag);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
                 if (wave == 0)
@@ -3131,6 +3134,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 const int ty2 = tile2 / tiles_x;
                 const int bx0 = (tile2 - ty2 * tiles_x) * G::TBX, byt0 = ty2 * G::TBY;
                 const uint8_t* const ref2 = FPIPE ? sp.land0 + (long long)(sp.gbase + f2) * sp.stride : a.ref[f2];
+                SO_MARK(p2_wait);
                 if (wave == 0) {   // every tile of this tile row finished pass 1 (tiles_x <= 64)
                     const uint32_t* c = sp.p1done + (size_t)f2 * ntiles + ty2 * tiles_x + (lane < tiles_x ? lane : 0);
                     // 50 ms of polling; 2 s in the frame pipeline, whose pass-1 tasks may wait that
@@ -3142,6 +3146,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                     SO_RUN_PROF(50, __builtin_amdgcn_s_memtime() - pt0);
                 }
                 __syncthreads();
+                SO_MARK(p2_sums);
                 if (wave < G::TBY) {   // pass-1 token sum of block row byt0 + wave
                     const int row = byt0 + wave;
                     uint32_t sum = 0;
@@ -3155,10 +3160,12 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
                 const int code = FPIPE ? a.dep[f2] : -1;
                 uint8_t* const push = code >= 0 ? ((code & 1) ? sp.peer_up0 : sp.peer_dn0) +
                                                       (long long)(code >> 1) * sp.stride : nullptr;
+                SO_MARK(p2_tq);
                 const int t2 = opaque_tid(), ln = t2 & 63, gq = (t2 >> 6) * G::TQ_BPW + (ln >> 4);
                 if (ln < 16 * G::TQ_BPW && gq < G::NBLK)
                     tq16_pass2<G>(S, gq, ln & 15, S.un + gq * kTqScratch, bx0, byt0, nbx, by1, W, qp_rd, qp_row, sp.roi,
                                   sp.qp_lo, sp.qp_hi, a.cur[f2], ref2, a.out[f2], t1, push);
+                SO_MARK(p2_flag);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // local and remote stores retired
                 __syncthreads();
                 if (wave == 0) {
