@@ -2478,6 +2478,13 @@ SO_DEV void tq16_pass1(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
                 for (int e = 0; e < 4; ++e)
                     res[4 * k + e] = (int)((cw >> (8 * e)) & 255) - (int)((pw[k] >> (8 * e)) & 255);
             }
+            // the prediction row waits for pass 2 in the block's reconstruction rows (write-
+            // through; pass 2 overwrites them with the reconstruction before the tile's done
+            // flag, which every reader of the plane waits for): pass 2 then needs neither the
+            // vector nor a load that depends on it
+            const so_v4u pv{pw[0], pw[1], pw[2], pw[3]};
+            uint8_t* const rp = o.recon + (size_t)(gby * 16 + l) * (nbx * 16) + gbx * 16;
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(rp), "v"(pv) : "memory");
         }
         double tcr[16];
         xform2d_rows<16, false>(scratch, l, res, tcr, SO_TQ_TW());
@@ -2538,7 +2545,7 @@ SO_DEV void row16_aligned(const uint8_t* p, uint32_t (&w)[4]) {
 template <class G>
 SO_DEV void tq16_pass2(PTileLds<G>& S, int g, int l, double* scratch, int bx0, int byt0, int nbx, int by1, int W,
                        int qp_rd, const int32_t* __restrict__ qp_row, const int32_t* __restrict__ roi, int qp_lo,
-                       int qp_hi, const uint8_t* __restrict__ cur, const uint8_t* ref, const PFrameOut& o,
+                       int qp_hi, const uint8_t* __restrict__ cur, const uint8_t* /*ref*/, const PFrameOut& o,
                        const int32_t* __restrict__ t1, uint8_t* push = nullptr) {
     constexpr int TBX = G::TBX;
     const int bxl = g % TBX, byl = g / TBX;
@@ -2546,16 +2553,12 @@ SO_DEV void tq16_pass2(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
     if (gbx < nbx && gby < by1) {
         const size_t b = (size_t)gby * nbx + gbx;
         const int x = gbx * 16, y = gby * 16;
-        // pass 1's motion vector, clamped to the plane.  Pass 1 keeps every vector inside the
-        // reference's strict candidate bounds (0 <= x + dx < W - 16), so the clamp never moves a
-        // vector pass 1 wrote; it bounds the read when pass 1 did NOT write it: after a timed-out
-        // wait the run's later waits return at once (SO_RUN_ABORT_CHECK), so a pass-2 unit can
-        // run before its row's pass 1 and read whatever the record held -- unclamped, that was
-        // the frame pipeline's hipErrorIllegalAddress after a lost hand-off
-        const int Hp = by1 * 16;
-        int dx = o.mv[b * 12], dy = o.mv[b * 12 + 1];
-        dx = x + dx < 0 ? -x : (x + dx > W - 16 ? W - 16 - x : dx);
-        dy = y + dy < 0 ? -y : (y + dy > Hp - 16 ? Hp - 16 - y : dy);
+        // No address here derives from another task's output: pass 1 left the prediction rows
+        // in the block's reconstruction rows and the coefficients in its QTC rows.  (Round 5
+        // read pass 1's motion vector and loaded the prediction at it: after a timed-out wait,
+        // when the run's later waits return at once (SO_RUN_ABORT_CHECK), a pass-2 unit could
+        // run before its row's pass 1 and address ~125 MB past the plane with an unwritten
+        // record -- the frame pipeline's hipErrorIllegalAddress)
         int qpr;
         {   // qp_map_kernel (so_capi.hip), per block
             const long long tn = (long long)t1[b] * nbx, m = S.msum[byl];
@@ -2564,7 +2567,7 @@ SO_DEV void tq16_pass2(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
             qpr = qpr < qp_lo ? qp_lo : (qpr > qp_hi ? qp_hi : qpr);
         }
         const uint8_t* crow = cur + (size_t)(y + l) * W + x;
-        const uint8_t* prow = ref + (size_t)(y + dy + l) * W + (x + dx);
+        const uint8_t* prow = o.recon + (size_t)(y + l) * W + x;   // pass 1's prediction row
         constexpr double kRne = 0x1.8p52;
         // the coefficients pass 1 left in the QTC rows (after the wait's acquire), requantised
         // at the block's QP: q = np.round(TC / 2^k), the exact integer round-half-even shift
@@ -2580,7 +2583,7 @@ SO_DEV void tq16_pass2(PTileLds<G>& S, int g, int l, double* scratch, int bx0, i
         int rec[16];
         {
             uint32_t pw[4];
-            row16_any(prow, pw);
+            row16_aligned(prow, pw);
 #pragma unroll
             for (int c = 0; c < 16; ++c)
                 rec[c] = (int)((pw[c >> 2] >> (8 * (c & 3))) & 255) +
