@@ -313,7 +313,8 @@ def kernel_roofline(codec, frames_dev, symbols, reps: int, components: bool = Tr
     frame_bytes = alg_frame_bytes(h, w)
     return {"me_s": out.get("me"), "tq_s": out.get("tq"), "run_s": out["run"], "run_frames": nf - 1,
             "frame_bytes": frame_bytes, "me_bytes": 2 * h * w + 16 * nb, "tq_bytes": 5 * h * w + 8 * nb,
-            "sad_ops": cands * bs * bs, "cands": cands, "executed_sad_ops": sad_ops, "vbs": eng.vbs}
+            "sad_ops": cands * bs * bs, "cands": cands, "executed_sad_ops": sad_ops, "vbs": eng.vbs,
+            "zero_skip": bool(getattr(eng, "zero_skip", False))}
 
 
 def pmc_record(config: str, kernel: str):
@@ -347,7 +348,9 @@ def roofline_of(rl: dict, config: str) -> dict:
     committed PMC counters of the same workload, and the SAD fraction of the searches'
     EXECUTED v_sad byte operations (kernel-side count, SO_P_RUN_SAD_OPS_WORD)."""
     # the VBS workloads carry no row-QP schedule: the uniform-QP instantiation (so_me.hip UQP)
-    kname = ("so::p_run_kernel<8, 0, true, false, true>" if rl["vbs"] else "so::p_run_kernel<8, 0, false, false, false>")
+    kname = ("so::p_run_kernel<8, 0, true, false, true, false>" if rl["vbs"] else
+             ("so::p_run_kernel<8, 0, false, false, false, true>" if rl.get("zero_skip") else
+              "so::p_run_kernel<8, 0, false, false, false, false>"))
     n_launch = -(-rl["run_frames"] // 32)       # so_encode_p_run: <= 32 frames per launch
     launch_s = rl["run_s"] / n_launch
     alg = rl["run_frames"] * rl["frame_bytes"] / n_launch
@@ -443,7 +446,7 @@ def rc_roofline(codec, frames_dev, symbols, reps: int, config: str) -> dict:
     eng.check_run()
     frame_bytes = alg_frame_bytes(eng.h, eng.w)
     gbs = frame_bytes / per_frame / 1e9
-    kname = "so::p_run_kernel<8, 3, false, false, false>" if fused else "so::p_tile_kernel<8, true>"
+    kname = "so::p_run_kernel<8, 3, false, false, false, false>" if fused else "so::p_tile_kernel<8, true>"
     # one persistent launch per <= 32 P-frames (fused); the sequence launches per frame
     n_launch = -(-(nf - 1) // 32) if fused else nf - 1
     launch_frames = (nf - 1) / n_launch
@@ -455,7 +458,7 @@ def rc_roofline(codec, frames_dev, symbols, reps: int, config: str) -> dict:
                 "valu_busy_frac": round(4 * pm["sq_active_inst_valu"] / (cyc * N_SIMD), 4),
                 "waves_per_simd": round(4 * pm["sq_wave_cycles"] / (cyc * N_SIMD), 2) if pm.get("sq_wave_cycles") else None,
                 "source": f"profiles/pmc_me_traffic.json [{config}]"}
-    kdesc = ("two-pass P-run in one persistent launch (so_encode_p_run_2pass): p_run_kernel<8, 3, false, false, false>"
+    kdesc = ("two-pass P-run in one persistent launch (so_encode_p_run_2pass): p_run_kernel<8, 3, false, false, false, false>"
              if fused else "two-pass P-frame sequence (so_encode_p_run_2pass): p_tile_kernel<8, true> (pass 1) + "
              "inter_tq_kernel<16, false, false, true> (pass 2: QP map + transforms)")
     return {"bound": "hbm", "kernel": kdesc,
@@ -698,9 +701,13 @@ def run_single(cfg, args, dev, parity: bool):
     def step():
         return codec.encode_device(frames, cfg["intra_dur"], symbols=pre, check=False)
     graph = args.graph
+    # one eager GOP first, and its wait-health check: the check also picks the plain run's kernel
+    # for this content (Engine.zero_skip: the all-zero-wave IDCT skip where most blocks quantise
+    # to zero), which the captured graph then replays
+    step()
+    torch.cuda.synchronize()
+    eng.check_run()
     if graph:
-        step()
-        torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         cap = torch.cuda.Stream(dev)
         cap.wait_stream(torch.cuda.current_stream(dev))

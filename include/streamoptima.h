@@ -130,6 +130,12 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
  *                            searches' SAD byte operations into workspace words 66..67 (1; default
  *                            0: a separate test-hook kernel instantiation runs while it is set,
  *                            so the product kernels carry no counting code)
+ *   SO_OPT_RUN_ZERO_SKIP     the one-GPU plain run (so_encode_p_run / _runs, VBS off) launches the
+ *                            instantiation whose waves skip the IDCT when all their blocks
+ *                            quantised to zero (1; exact either way: an all-zero block's inverse
+ *                            is zero).  Faster where most blocks are zero (flat content), a
+ *                            little slower elsewhere; default 0.  The Python engine sets it per
+ *                            run from the previous run's share of all-zero blocks.
  * so_set_option returns SO_E_INVALID for an unknown option or a value out of range.
  */
 #define SO_OPT_RUN_2PASS_FUSED 1
@@ -146,6 +152,7 @@ int so_encode_p_rows(const uint8_t* cur, const uint8_t* const* refs, int nref, i
  * SO_OPT_COUNT_SAD_OPS select a separate test-hook instantiation of the one-GPU run kernel; the
  * product kernels carry neither hook. */
 #define SO_OPT_TEST_LOSE_FLAG 6
+#define SO_OPT_RUN_ZERO_SKIP 7
 int so_set_option(int option, int value);
 int so_get_option(int option);
 

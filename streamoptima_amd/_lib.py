@@ -101,6 +101,7 @@ REUSE_ME = 1   # so_encode_p_rows_ex flags
 TOKENS_ONLY = 2
 # so_set_option (include/streamoptima.h SO_OPT_*)
 OPT_RUN_2PASS_FUSED, OPT_FASTME_SERIAL, OPT_FASTME_SEGMENT, OPT_FASTME_WARMUP, OPT_COUNT_SAD_OPS = 1, 2, 3, 4, 5
+OPT_RUN_ZERO_SKIP = 7
 OPT_TEST_LOSE_FLAG = 6
 
 EXPORTED = tuple(_SIGS)

@@ -26,10 +26,10 @@ void set_error(const char* fmt, ...) {
 }
 
 // so_set_option / so_get_option (SO_OPT_*): index = option id
-static std::atomic<int> g_opt[7] = {0, 1, 0, 32, 32, 0, 0};   // SO_OPT_RUN_2PASS_FUSED on by default
+static std::atomic<int> g_opt[8] = {0, 1, 0, 32, 32, 0, 0, 0};   // SO_OPT_RUN_2PASS_FUSED on by default
 
 int option(int id) {
-    return (id > 0 && id < 7) ? g_opt[id].load(std::memory_order_relaxed) : 0;
+    return (id > 0 && id < 8) ? g_opt[id].load(std::memory_order_relaxed) : 0;
 }
 
 int me_launch(const uint8_t* cur, const RefSet& refs, int nref, int H, int W, int bs, int sr, int by0, int by1,
@@ -323,7 +323,8 @@ extern "C" {
 int so_abi_version(void) { return SO_ABI_VERSION; }
 
 int so_set_option(int opt, int value) {
-    const bool ok = (opt == SO_OPT_RUN_2PASS_FUSED || opt == SO_OPT_FASTME_SERIAL || opt == SO_OPT_COUNT_SAD_OPS)
+    const bool ok = (opt == SO_OPT_RUN_2PASS_FUSED || opt == SO_OPT_FASTME_SERIAL || opt == SO_OPT_COUNT_SAD_OPS ||
+                     opt == SO_OPT_RUN_ZERO_SKIP)
                         ? (value == 0 || value == 1)
                     : opt == SO_OPT_FASTME_SEGMENT                               ? value >= 1
                     : opt == SO_OPT_FASTME_WARMUP || opt == SO_OPT_TEST_LOSE_FLAG ? value >= 0

@@ -1723,7 +1723,8 @@ struct PHalo {
 #define SO_TQ_TW() dct::tw16_table()
 #define SO_TQ_TW8() dct::tw8_table()
 #endif
-template <class G, bool SC1, bool HALO = false, bool TOK = false, bool HALFTQ = false>
+// ZSKIP (SO_OPT_RUN_ZERO_SKIP): a wave whose four blocks all quantised to zero skips the IDCT
+template <class G, bool SC1, bool HALO = false, bool TOK = false, bool HALFTQ = false, bool ZSKIP = false>
 SO_DEV void tq16_exact(PTileLds<G, false, HALFTQ>& S, int g, int l, double* scratch, int bx0, int byt0, int nbx, int by0, int by1,
                        int W, int qp_rd, const int32_t* __restrict__ qp_row, const int32_t* __restrict__ qp_map,
                        const PFrameOut& o, const PHalo& hl = PHalo{}, bool qs = false) {
@@ -1789,57 +1790,86 @@ SO_DEV void tq16_exact(PTileLds<G, false, HALFTQ>& S, int g, int l, double* scra
         }
         SO_MARK(tq_qtc_store);
         store_row_i16<16>(o.qtc + b * 256 + l * 16, q);
-        int dq[16];
-        double rd[16];
-        dequant_row_int<16>(q, l, qpr, dq);
-        SO_MARK(tq_inv);
-        xform2d_rows<16, true>(dl, l, dq, rd, SO_TQ_TW());
-        SO_MARK(tq_recon);
-        int rec[16];
-        {
-            uint32_t pw[4];
-            win_row16<G::RP>(S.win, prow, pcol, pw);
+        // the reconstruction row's store (write-through, plus the neighbours' halo rows) and
+        // its SSE: the tail of both paths below
+        const auto finish = [&](const int (&rec)[16]) -> int {
+            if constexpr (SC1) {
+                so_v4u v;
 #pragma unroll
-            for (int c = 0; c < 16; ++c)
-                rec[c] = (int)((pw[c >> 2] >> (8 * (c & 3))) & 255) +
-                         (int)(uint32_t)__builtin_bit_cast(uint64_t, rd[c] + kRne);
-        }
-        if constexpr (SC1) {
-            so_v4u v;
+                for (int k = 0; k < 4; ++k)
+                    v[k] = (uint32_t)(rec[4 * k] & 255) | ((uint32_t)(rec[4 * k + 1] & 255) << 8) |
+                           ((uint32_t)(rec[4 * k + 2] & 255) << 16) | ((uint32_t)(rec[4 * k + 3] & 255) << 24);
+                uint8_t* rp = o.recon + (size_t)(y + l) * W + x;
+                asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(rp), "v"(v) : "memory");
+                if constexpr (HALO) {
+                    // the rows a neighbouring rank's window reads: system-scope write-through
+                    // stores into its uncached landing plane (peer memory over xGMI)
+                    if (hl.up && y + l < hl.up_end) {
+                        uint8_t* q2 = hl.up + (size_t)(y + l) * W + x;
+                        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(q2), "v"(v) : "memory");
+                    }
+                    if (hl.dn && y + l >= hl.dn_begin) {
+                        uint8_t* q2 = hl.dn + (size_t)(y + l) * W + x;
+                        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(q2), "v"(v) : "memory");
+                    }
+                }
+            } else {
+                store_row_u8<16>(o.recon, W, x, y + l, rec);
+            }
+            SO_MARK(tq_sse_records);
+            int e2 = 0;
+            if (o.sse) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                v[k] = (uint32_t)(rec[4 * k] & 255) | ((uint32_t)(rec[4 * k + 1] & 255) << 8) |
-                       ((uint32_t)(rec[4 * k + 2] & 255) << 16) | ((uint32_t)(rec[4 * k + 3] & 255) << 24);
-            uint8_t* rp = o.recon + (size_t)(y + l) * W + x;
-            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(rp), "v"(v) : "memory");
-            if constexpr (HALO) {
-                // the rows a neighbouring rank's window reads: system-scope write-through
-                // stores into its uncached landing plane (peer memory over xGMI)
-                if (hl.up && y + l < hl.up_end) {
-                    uint8_t* q = hl.up + (size_t)(y + l) * W + x;
-                    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(q), "v"(v) : "memory");
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t cw = crow[k];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int d = (int)((cw >> (8 * e)) & 255) - (rec[4 * k + e] & 255);
+                        e2 += d * d;
+                    }
                 }
-                if (hl.dn && y + l >= hl.dn_begin) {
-                    uint8_t* q = hl.dn + (size_t)(y + l) * W + x;
-                    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(q), "v"(v) : "memory");
-                }
+                e2 = group_sum<16>(e2);
+            }
+            return e2;
+        };
+        const auto full = [&]() -> int {   // dequantisation, IDCT, prediction + inverse
+            int dq[16];
+            double rd[16];
+            dequant_row_int<16>(q, l, qpr, dq);
+            SO_MARK(tq_inv);
+            xform2d_rows<16, true>(dl, l, dq, rd, SO_TQ_TW());
+            SO_MARK(tq_recon);
+            int rec[16];
+            {
+                uint32_t pw[4];
+                win_row16<G::RP>(S.win, prow, pcol, pw);
+#pragma unroll
+                for (int c = 0; c < 16; ++c)
+                    rec[c] = (int)((pw[c >> 2] >> (8 * (c & 3))) & 255) +
+                             (int)(uint32_t)__builtin_bit_cast(uint64_t, rd[c] + kRne);
+            }
+            return finish(rec);
+        };
+        int sse;
+        if constexpr (ZSKIP) {
+            // a block whose levels are all zero (tok == 1: no non-zero, one zero run) has an
+            // exactly zero inverse (every step of pocketfft's sequence on zeros gives +-0,
+            // rounded to 0): a wave whose blocks are all such reconstructs its prediction rows
+            // as they stand.  Its own instantiation (SO_OPT_RUN_ZERO_SKIP), chosen by the host
+            // for content where most blocks quantise to zero: in the default kernel the branch
+            // cost two spills and +0.3-0.5 % on textured content
+            if (__builtin_amdgcn_ballot_w64(tok != 1) == 0) {
+                int rec[16];
+                uint32_t pw[4];
+                win_row16<G::RP>(S.win, prow, pcol, pw);
+#pragma unroll
+                for (int c = 0; c < 16; ++c) rec[c] = (int)((pw[c >> 2] >> (8 * (c & 3))) & 255);
+                sse = finish(rec);
+            } else {
+                sse = full();
             }
         } else {
-            store_row_u8<16>(o.recon, W, x, y + l, rec);
-        }
-        SO_MARK(tq_sse_records);
-        int sse = 0;
-        if (o.sse) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t cw = crow[k];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int d = (int)((cw >> (8 * e)) & 255) - (rec[4 * k + e] & 255);
-                    sse += d * d;
-                }
-            }
-            sse = group_sum<16>(sse);
+            sse = full();
         }
         if (l < 12) o.mv[b * 12 + l] = (int16_t)(l == 0 ? dx : l == 1 ? dy : l == 2 ? rf : 0);
         if (l == 0) {
@@ -2326,7 +2356,7 @@ SO_DEV void store_sc1_i32(int32_t* p, int v) {
 }
 
 template <class G, bool SC1, class Pre = NoPre, bool HALO = false, bool TOK = false, bool VBS = false,
-          class Post = NoPre, bool HALFTQ = false>
+          class Post = NoPre, bool HALFTQ = false, bool ZSKIP = false>
 SO_DEV void ptile_body(PTileLds<G, VBS, HALFTQ>& S, int tile, const uint8_t* __restrict__ cur, const uint8_t* ref, int H, int W,
                        int by0, int by1, int qp_rd, const int32_t* __restrict__ qp_row,
                        const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best, const PFrameOut& o,
@@ -2418,7 +2448,7 @@ SO_DEV void ptile_body(PTileLds<G, VBS, HALFTQ>& S, int tile, const uint8_t* __r
                 tq16_vbs_fwd<G, SC1, HALO>(S, gq, ln & 15, S.un + gq * kTqScratchVbs, bx0, byt0, nbx, by0, by1, W, qp_rd,
                                            qp_row, qp_map, lam, o);
             else
-                tq16_exact<G, SC1, HALO, TOK>(S, gq, ln & 15, S.un + gq * (HALFTQ ? kTqScratchHalf : kTqScratch), bx0,
+                tq16_exact<G, SC1, HALO, TOK, HALFTQ, ZSKIP>(S, gq, ln & 15, S.un + gq * (HALFTQ ? kTqScratchHalf : kTqScratch), bx0,
                                               byt0, nbx, by0, by1, W, qp_rd,
                                               qp_row, qp_map, o, hl, qs);
         }
@@ -2891,13 +2921,15 @@ SO_DEV uint32_t run_dequeue(uint32_t* ws) {
 // the block coefficients tq16_vbs_fwd would hold through the sub-block transforms for a
 // requantisation at another QP are then dead (VBS run spills 30 -> 23; 4K VBS GOP 3.311 ->
 // 3.265 ms, profiles/r06/ab_vbs_uqp.log).
-template <int NW, int MODE, bool VBS = false, bool HOOKS = false, bool UQP = false>
+// ZSKIP (one-GPU plain run, SO_OPT_RUN_ZERO_SKIP): tq16_exact's all-zero-wave IDCT skip
+template <int NW, int MODE, bool VBS = false, bool HOOKS = false, bool UQP = false, bool ZSKIP = false>
 __global__ void __launch_bounds__(NW * 64)
 __attribute__((amdgpu_waves_per_eu(VBS ? SO_VBS_WPE : (NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE))))
 p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, int H, int W,
              int qp_rd, const int32_t* __restrict__ qp_row_arg, uint32_t* __restrict__ ws, int ws_stamp_base,
              const PRunStripe sp, double lam) {
     static_assert(!UQP || VBS, "the uniform-QP instantiation is the VBS run's");
+    static_assert(!ZSKIP || (MODE == kRunSingle && !VBS && !HOOKS), "the zero-skip instantiation is the plain one-GPU run's");
     const int32_t* __restrict__ const qp_row = UQP ? nullptr : qp_row_arg;
     using G = Sea2GeoT<NW>;
     __shared__ PTileLds<G, VBS> S;
@@ -3248,7 +3280,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 #ifdef SO_RUN_PROFILE
             const unsigned long long pt0 = __builtin_amdgcn_s_memtime();
 #endif
-            ptile_body<G, true, decltype(wait_ref), false, false, VBS, decltype(take_next)>(
+            ptile_body<G, true, decltype(wait_ref), false, false, VBS, decltype(take_next), false, ZSKIP>(
                 S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd, qp_row, nullptr, nullptr, a.out[f], wait_ref, PHalo{}, lam,
                 &s_dense, reinterpret_cast<int32_t*>(tilefb) + (size_t)f * ntiles + tile, count_ops, take_next,
                 // VBS: the same hint for the block's U measured slower (4K VBS P-frame 123.1 vs
@@ -3391,6 +3423,7 @@ int p_run_capacity(int vbs, int mode) {
     } else {
         add(kRunSingle, reinterpret_cast<const void*>(p_run_kernel<NW, kRunSingle, false>));
         add(kRunSingle, reinterpret_cast<const void*>(p_run_kernel<NW, kRunSingle, false, true>));
+        add(kRunSingle, reinterpret_cast<const void*>(p_run_kernel<NW, kRunSingle, false, false, false, true>));
         add(kRunStripe, reinterpret_cast<const void*>(p_run_kernel<NW, kRunStripe, false>));
         add(kRunFPipe, reinterpret_cast<const void*>(p_run_kernel<NW, kRunFPipe, false>));
         add(kRunTwoPass, reinterpret_cast<const void*>(p_run_kernel<NW, kRunTwoPass, false>));
@@ -3426,11 +3459,15 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
     const bool hooks = MODE == kRunSingle && hook_set;
     // VBS without a row-QP schedule: the uniform-QP instantiation (p_run_kernel's UQP)
     const bool uqp = VBS && qp_row == nullptr;
+    // the plain one-GPU run with the all-zero-wave IDCT skip (SO_OPT_RUN_ZERO_SKIP; not with hooks)
+    constexpr bool ZS_OK = MODE == kRunSingle && !VBS;
+    const bool zskip = ZS_OK && !hooks && option(SO_OPT_RUN_ZERO_SKIP) != 0;
     const void* const kfn =
         hooks ? (uqp ? reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, MODE == kRunSingle, VBS>)
                      : reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, MODE == kRunSingle>))
-              : (uqp ? reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, false, VBS>)
-                     : reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, false>));
+              : (uqp     ? reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, false, VBS>)
+                 : zskip ? reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, false, false, ZS_OK>)
+                         : reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, false>));
     if (hooks && option(SO_OPT_TEST_LOSE_FLAG) != 0) {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
@@ -3497,17 +3534,19 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
             sp.p2lag = lag < 1 ? 1 : (lag > ntr ? ntr : lag);
         }
         const uint8_t* const r0 = f0 ? outs[f0 - 1].recon : ref0;
-#define SO_P_RUN_GO(HK, UQ)                                                                                        \
-    hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, MODE, VBS, HK, UQ>), dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), \
+#define SO_P_RUN_GO(HK, UQ, ZS)                                                                                         \
+    hipLaunchKernelGGL((p_run_kernel<SO_PTILE_NW, MODE, VBS, HK, UQ, ZS>), dim3((unsigned)grid), dim3(SO_PTILE_NW * 64), \
                        0, st, a, n, r0, H, W, qp_rd, qp_row, ws, (int)(f0 * ntiles), sp, lam)
         if (hooks && uqp)
-            SO_P_RUN_GO(MODE == kRunSingle, VBS);
+            SO_P_RUN_GO(MODE == kRunSingle, VBS, false);
         else if (hooks)
-            SO_P_RUN_GO(MODE == kRunSingle, false);
+            SO_P_RUN_GO(MODE == kRunSingle, false, false);
         else if (uqp)
-            SO_P_RUN_GO(false, VBS);
+            SO_P_RUN_GO(false, VBS, false);
+        else if (zskip)
+            SO_P_RUN_GO(false, false, ZS_OK);
         else
-            SO_P_RUN_GO(false, false);
+            SO_P_RUN_GO(false, false, false);
 #undef SO_P_RUN_GO
         const int rc = check_launch("p_run_kernel");
         if (rc != SO_OK) return rc;

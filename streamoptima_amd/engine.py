@@ -269,13 +269,15 @@ class Engine:
 
         def arr(ts):
             return (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
-        rc = self.lib.so_encode_p_run(
-            arr(curs), n, ref0.data_ptr(), self.h, self.w, self.bs, self.sr, int(qp_rd), _lib.ptr(qrd),
-            int(self.vbs), self.lam,
-            arr([o.split for o in outs]), arr([o.mv for o in outs]), arr([o.qtc for o in outs]),
-            arr([o.tokens for o in outs]), arr([o.mae_num for o in outs]), arr([o.recon for o in outs]),
-            arr([o.sse for o in outs]), self._run_ws.data_ptr(), _lib.stream_handle(self.device))
+        with self._zero_skip_option():
+            rc = self.lib.so_encode_p_run(
+                arr(curs), n, ref0.data_ptr(), self.h, self.w, self.bs, self.sr, int(qp_rd), _lib.ptr(qrd),
+                int(self.vbs), self.lam,
+                arr([o.split for o in outs]), arr([o.mv for o in outs]), arr([o.qtc for o in outs]),
+                arr([o.tokens for o in outs]), arr([o.mae_num for o in outs]), arr([o.recon for o in outs]),
+                arr([o.sse for o in outs]), self._run_ws.data_ptr(), _lib.stream_handle(self.device))
         _lib.check(rc, "so_encode_p_run")
+        self._last_run_outs = list(outs)
         for o in outs:
             o.frame_type, o.qp_rd = 1, int(qp_rd)
             o.qp_row = None if qp_row is None else list(qp_row)
@@ -351,12 +353,15 @@ class Engine:
 
         def arr(ts):
             return (ctypes.c_void_p * n)(*[0 if t is None else t.data_ptr() for t in ts])
-        rc = self.lib.so_encode_p_runs(
-            arr(curs), n, arr(refs), (ctypes.c_int32 * n)(*ref_frame), self.h, self.w, self.bs, self.sr, int(qp_rd),
-            _lib.ptr(qrd), int(self.vbs), self.lam, arr([o.split for o in outs]), arr([o.mv for o in outs]), arr([o.qtc for o in outs]),
-            arr([o.tokens for o in outs]), arr([o.mae_num for o in outs]), arr([o.recon for o in outs]),
-            arr([o.sse for o in outs]), self._run_ws.data_ptr(), _lib.stream_handle(self.device))
+        with self._zero_skip_option():
+            rc = self.lib.so_encode_p_runs(
+                arr(curs), n, arr(refs), (ctypes.c_int32 * n)(*ref_frame), self.h, self.w, self.bs, self.sr,
+                int(qp_rd), _lib.ptr(qrd), int(self.vbs), self.lam, arr([o.split for o in outs]),
+                arr([o.mv for o in outs]), arr([o.qtc for o in outs]), arr([o.tokens for o in outs]),
+                arr([o.mae_num for o in outs]), arr([o.recon for o in outs]), arr([o.sse for o in outs]),
+                self._run_ws.data_ptr(), _lib.stream_handle(self.device))
         _lib.check(rc, "so_encode_p_runs")
+        self._last_run_outs = list(outs)
         for o in outs:
             o.frame_type, o.qp_rd = 1, int(qp_rd)
             o.qp_row = None if qp_row is None else list(qp_row)
@@ -367,12 +372,30 @@ class Engine:
         (never expected: the run's symbols would then be unreliable).  Synchronises."""
         return runhealth.timed_out(getattr(self, "_run_ws", None))
 
+    def _zero_skip_option(self):
+        """SO_OPT_RUN_ZERO_SKIP set around a launch when this engine chose the zero-skip kernel
+        (left alone otherwise: the option's default is off)."""
+        return _lib.option(_lib.OPT_RUN_ZERO_SKIP, 1) if self.zero_skip else contextlib.nullcontext()
+
+    # the plain run's kernel choice by content (SO_OPT_RUN_ZERO_SKIP): the instantiation that
+    # skips the IDCT of all-zero waves when at least this share of the last run's blocks
+    # quantised to zero (flat content; exact either way, DESIGN.md section 9)
+    ZERO_SKIP_SHARE = 0.5
+    zero_skip = False
+
     def check_run(self) -> None:
         """Raise if any encode_p_run since the last check timed out -- naming the first such
         wait from the workspace's diagnostic record (runhealth.describe) -- then clear the
         count; the non-fatal wait counts go to self.wait_health.  Encoder.encode() /
-        encode_device(check=True) and bench.py call it once per GOP."""
+        encode_device(check=True) and bench.py call it once per GOP.  It also picks the
+        plain run's kernel for the next runs from the last run's share of all-zero blocks
+        (tokens == 1), read in the same synchronised check."""
         runhealth.check(getattr(self, "_run_ws", None), self.wait_health, "p_run_kernel")
+        outs = getattr(self, "_last_run_outs", None)
+        if outs and not self.vbs:
+            self._last_run_outs = None
+            zero = torch.stack([(o.tokens == 1).sum() for o in outs]).sum().item()
+            self.zero_skip = zero >= self.ZERO_SKIP_SHARE * self.nb * len(outs)
 
     def take_sad_ops(self) -> int:
         """SAD byte operations the persistent runs' searches executed since the last call

@@ -66,6 +66,27 @@ def test_benchmarked_gop_bit_exact(gpu, name):
     _check(name, res["symbols"], psnr)
 
 
+@pytest.mark.parametrize("name", ["4k_lowtex", "4k", "1080p"])
+def test_zero_skip_kernel_bit_exact_and_selected_by_content(gpu, name):
+    """The plain run's zero-skip instantiation (SO_OPT_RUN_ZERO_SKIP: a wave whose blocks all
+    quantised to zero skips the IDCT) gives the oracle's digests on flat and on textured content
+    (forced on), and Engine.check_run selects it from the last run's share of all-zero blocks:
+    on for the low-texture GOP, off for the textured ones."""
+    cfg, codec = _codec(name, gpu)
+    frames = _frames(cfg, gpu)
+    eng = codec.engine()
+    codec.encode_device(frames, cfg["intra_dur"])            # check=True: the content decision
+    assert eng.zero_skip == (name == "4k_lowtex")
+    eng.zero_skip = True
+    res = codec.encode_device(frames, cfg["intra_dur"], check=False)
+    torch.cuda.synchronize()
+    eng.check_run()
+    hp = frames.shape[1]
+    sse = res["sse"].cpu().numpy()
+    psnr = [10 * np.log10(255 ** 2 / (float(s) / (hp * cfg["w"]))) for s in sse]
+    _check(name, res["symbols"], psnr)
+
+
 def test_interleaved_gops_bit_exact(gpu):
     """encode_gops_device: two copies of the 1080p GOP (configs[1]) and a third GOP of the
     same frames reversed, their P-runs interleaved in ONE persistent launch: each copy equals

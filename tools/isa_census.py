@@ -23,12 +23,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def mangled(kernel: str) -> str:
-    m = re.match(r"p_run_kernel<(\d+), (\d+), (true|false), (true|false)(?:, (true|false))?>", kernel)
+    m = re.match(r"p_run_kernel<(\d+), (\d+), (true|false), (true|false)(?:, (true|false))?(?:, (true|false))?>",
+                 kernel)
     if not m:
-        raise SystemExit(f"kernel {kernel!r}: expected p_run_kernel<NW, MODE, VBS, HOOKS, UQP>")
+        raise SystemExit(f"kernel {kernel!r}: expected p_run_kernel<NW, MODE, VBS, HOOKS, UQP, ZSKIP>")
     b = lambda v: "1" if v == "true" else "0"   # noqa: E731
     return (f"_ZN2so12p_run_kernelILi{m.group(1)}ELi{m.group(2)}ELb{b(m.group(3))}ELb{b(m.group(4))}"
-            f"ELb{b(m.group(5) or 'false')}EEEvNS_8PRunArgsEiPKhiiiPKiPjiNS_10PRunStripeEd")
+            f"ELb{b(m.group(5) or 'false')}ELb{b(m.group(6) or 'false')}EEEvNS_8PRunArgsEiPKhiiiPKiPjiNS_10PRunStripeEd")
 
 
 def census(asm: str, fn: str) -> dict:
@@ -70,7 +71,7 @@ def census(asm: str, fn: str) -> dict:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernel", default="p_run_kernel<8, 0, false, false, false>")
+    ap.add_argument("--kernel", default="p_run_kernel<8, 0, false, false, false, false>")
     ap.add_argument("-D", dest="defines", action="append", default=[])
     ap.add_argument("--json", action="store_true")
     a = ap.parse_args()

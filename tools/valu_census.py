@@ -81,8 +81,9 @@ def count():
 
 def table(path, pmc_valu=None):
     d = json.load(open(path))
-    kernel = ("p_run_kernel<8, 3, false, false, false>" if d.get("two_pass") else
-              "p_run_kernel<8, 0, true, false, true>" if d.get('vbs') else "p_run_kernel<8, 0, false, false, false>")
+    kernel = ("p_run_kernel<8, 3, false, false, false, false>" if d.get("two_pass") else
+              "p_run_kernel<8, 0, true, false, true, false>" if d.get('vbs') else
+              "p_run_kernel<8, 0, false, false, false, false>")
     cen = json.loads(subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_census.py"), "--json",
                                      "--kernel", kernel], capture_output=True, text=True, check=True).stdout)
     per_launch = {k: v / d["launches"] for k, v in d["counts"].items()}
