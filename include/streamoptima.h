@@ -570,12 +570,21 @@ int so_sum_i32_rows(const int32_t* const* rows, int n, int len, int64_t* out, vo
  *   the frame's total, and the stream into out[i][0..total).  Blocks that would pass `cap`
  *   bytes are not written: the caller checks offs[i][nb] <= cap before using out[i].
  *   Stream-ordered, no host synchronisation.
+ * so_pack_frames_ex: the same, and totals[i] = offs[i][nb] (totals: nframes uint32, device
+ *   memory or page-locked host memory the device can address -- stored at system scope, so a
+ *   host that has waited for the stream reads them without a copy; NULL = none).  A host
+ *   streaming the packed bytes out learns each frame's length from it without a gather and a
+ *   copy per chunk (hoststream.HostStreamEncoder).
  */
 size_t so_pack_bound(int nb, int block_size);
 int so_pack_frames(int nframes, const int32_t* frame_types, const uint8_t* const* split,
                    const int16_t* const* mv, const int16_t* const* qtc, int nb, int block_size,
                    uint32_t* const* offs, uint8_t* const* out, unsigned long long cap,
                    void* stream);
+int so_pack_frames_ex(int nframes, const int32_t* frame_types, const uint8_t* const* split,
+                      const int16_t* const* mv, const int16_t* const* qtc, int nb, int block_size,
+                      uint32_t* const* offs, uint8_t* const* out, unsigned long long cap,
+                      uint32_t* totals, void* stream);
 
 /*
  * The inverse (the decoder side of the packed stream): frame i's bytes packed[i] with the

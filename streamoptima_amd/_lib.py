@@ -80,6 +80,7 @@ _SIGS = {
                                      ctypes.c_longlong, ctypes.c_uint32, _i, _i, _vp], _i),   # .. max_wg p2lag stream
     "so_frame_push": ([_vp, _i, _i, _vp, _vp, ctypes.c_uint32, _vp], _i),
     "so_pack_frames": ([_i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, ctypes.c_ulonglong, _vp], _i),
+    "so_pack_frames_ex": ([_i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, ctypes.c_ulonglong, _vp, _vp], _i),
     "so_fme_plane_stride": ([_i, _i], _sz),
     "so_fme_workspace_bytes": ([_i, _i, _i], _sz),
     "so_fme_planes": ([_vp, _i, _i, _i, _vp, _vp], _i),

@@ -66,7 +66,8 @@ struct UnpackFrame {
     int frame_type;
 };
 int unpack_frames_launch(const UnpackFrame* frames, int nframes, int nb, int bs, int32_t* err, hipStream_t st);
-int pack_frames_launch(const PackFrame* frames, int nframes, int nb, int bs, unsigned long long cap, hipStream_t st);
+int pack_frames_launch(const PackFrame* frames, int nframes, int nb, int bs, unsigned long long cap, uint32_t* totals,
+                       hipStream_t st);
 int stripe_halo_push_launch(const uint8_t* plane, int W, int by0, int by1, uint8_t* up, uint8_t* dn,
                             uint32_t* up_flags, uint32_t* dn_flags, int gf, uint32_t epoch, hipStream_t st);
 int frame_push_launch(const uint8_t* plane, int H, int W, uint8_t* dst, uint32_t* flags, uint32_t epoch,
@@ -1158,6 +1159,12 @@ size_t so_pack_bound(int nb, int bs) {
 int so_pack_frames(int nframes, const int32_t* frame_types, const uint8_t* const* split, const int16_t* const* mv,
                    const int16_t* const* qtc, int nb, int bs, uint32_t* const* offs, uint8_t* const* out,
                    unsigned long long cap, void* stream) {
+    return so_pack_frames_ex(nframes, frame_types, split, mv, qtc, nb, bs, offs, out, cap, nullptr, stream);
+}
+
+int so_pack_frames_ex(int nframes, const int32_t* frame_types, const uint8_t* const* split, const int16_t* const* mv,
+                      const int16_t* const* qtc, int nb, int bs, uint32_t* const* offs, uint8_t* const* out,
+                      unsigned long long cap, uint32_t* totals, void* stream) {
     const char* fn = "so_pack_frames";
     if (bs != 16 && bs != 8) {
         set_error("%s: block_size %d not built", fn, bs);
@@ -1178,7 +1185,7 @@ int so_pack_frames(int nframes, const int32_t* frame_types, const uint8_t* const
         }
         fr[i] = PackFrame{split[i], mv[i], qtc[i], offs[i], out[i], frame_types[i]};
     }
-    return pack_frames_launch(fr.data(), nframes, nb, bs, cap, (hipStream_t)stream);
+    return pack_frames_launch(fr.data(), nframes, nb, bs, cap, totals, (hipStream_t)stream);
 }
 
 int so_unpack_frames(int nframes, const int32_t* frame_types, const uint8_t* const* packed, const uint32_t* const* offs,

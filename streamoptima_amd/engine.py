@@ -383,19 +383,35 @@ class Engine:
     ZERO_SKIP_SHARE = 0.5
     zero_skip = False
 
-    def check_run(self) -> None:
+    def check_run(self, defer_stats: bool = False) -> None:
         """Raise if any encode_p_run since the last check timed out -- naming the first such
         wait from the workspace's diagnostic record (runhealth.describe) -- then clear the
         count; the non-fatal wait counts go to self.wait_health.  Encoder.encode() /
         encode_device(check=True) and bench.py call it once per GOP.  It also picks the
         plain run's kernel for the next runs from the last run's share of all-zero blocks
-        (tokens == 1), read in the same synchronised check."""
+        (tokens == 1), read in the same synchronised check -- or, with defer_stats, counted
+        on the stream into page-locked memory and read at the next check (one GOP later; the
+        host-stream region, hoststream.py, does not wait for it)."""
         runhealth.check(getattr(self, "_run_ws", None), self.wait_health, "p_run_kernel")
+        pend = getattr(self, "_zero_pending", None)
+        if pend is not None:
+            self._zero_pending = None
+            ev, host, blocks = pend
+            ev.synchronize()
+            self.zero_skip = int(host[0]) >= self.ZERO_SKIP_SHARE * blocks
         outs = getattr(self, "_last_run_outs", None)
         if outs and not self.vbs:
             self._last_run_outs = None
-            zero = torch.stack([(o.tokens == 1).sum() for o in outs]).sum().item()
-            self.zero_skip = zero >= self.ZERO_SKIP_SHARE * self.nb * len(outs)
+            zero = torch.stack([(o.tokens == 1).sum() for o in outs]).sum()
+            if defer_stats:
+                if getattr(self, "_zero_host", None) is None:
+                    self._zero_host = torch.empty(1, dtype=torch.int64, pin_memory=True)
+                self._zero_host.copy_(zero.view(1), non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                self._zero_pending = (ev, self._zero_host, self.nb * len(outs))
+            else:
+                self.zero_skip = zero.item() >= self.ZERO_SKIP_SHARE * self.nb * len(outs)
 
     def take_sad_ops(self) -> int:
         """SAD byte operations the persistent runs' searches executed since the last call
@@ -455,11 +471,14 @@ class Engine:
     def pack_bound(self, nb: int | None = None) -> int:
         return int(self.lib.so_pack_bound(int(self.nb if nb is None else nb), self.bs))
 
-    def pack_symbols(self, syms: list, offs: torch.Tensor | None = None, out: torch.Tensor | None = None):
+    def pack_symbols(self, syms: list, offs: torch.Tensor | None = None, out: torch.Tensor | None = None,
+                     totals_ptr: int | None = None):
         """Each frame's symbols as one packed byte stream on the device (include/streamoptima.h
         so_pack_frames); asynchronous.  Returns (offs int32 [n, nb + 1], out uint8 [n, cap]):
         frame i's stream is out[i, :offs[i, nb]], block b starts at offs[i, b]
-        (bitstream.unpack_frame decodes it).  The default capacity never overflows."""
+        (bitstream.unpack_frame decodes it).  The default capacity never overflows.
+        totals_ptr: a device address of n uint32 (hostmem.device_ptr of a page-locked host
+        array) that also receives offs[i, nb] (so_pack_frames_ex)."""
         n = len(syms)
         if n == 0:
             raise ValueError("pack_symbols: no frames")
@@ -475,9 +494,9 @@ class Engine:
         def arr(ts):
             return (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
         types = (ctypes.c_int32 * n)(*[int(s.frame_type) for s in syms])
-        rc = self.lib.so_pack_frames(n, types, arr([s.split for s in syms]), arr([s.mv for s in syms]),
-                                     arr([s.qtc for s in syms]), nb, self.bs, arr(list(offs)), arr(list(out)),
-                                     int(cap), _lib.stream_handle(self.device))
+        rc = self.lib.so_pack_frames_ex(n, types, arr([s.split for s in syms]), arr([s.mv for s in syms]),
+                                        arr([s.qtc for s in syms]), nb, self.bs, arr(list(offs)), arr(list(out)),
+                                        int(cap), totals_ptr, _lib.stream_handle(self.device))
         _lib.check(rc, "so_pack_frames")
         return offs, out
 

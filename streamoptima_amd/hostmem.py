@@ -6,6 +6,8 @@ and when it was allocated: tools/s4_probe.py, s4_probe2.py, profiles/r06/s4_prob
 anonymous memory mapped and first touched by this process, then registered with
 hipHostRegister, read at 57.5 GB/s.  pinned_empty() returns such a buffer as a CPU tensor
 (is_pinned() is True).  The mapping stays registered for the life of the process.
+device_ptr() is the address a kernel stores to such a buffer through (so_pack_frames_ex's
+totals).
 """
 from __future__ import annotations
 
@@ -44,3 +46,14 @@ def pinned_empty(shape, dtype=torch.uint8) -> torch.Tensor:
         _KEEP.append((m, base + off, size))
     t = torch.from_numpy(flat[:n]).view(dtype)
     return t.view(shape) if len(tuple(shape)) else t
+
+
+def device_ptr(t: torch.Tensor) -> int:
+    """The device address of page-locked host tensor t's first element (hipHostGetDevicePointer)."""
+    if t.device.type != "cpu" or not t.is_pinned():
+        raise ValueError("device_ptr: a page-locked host tensor is required")
+    p = ctypes.c_void_p()
+    rc = _hip().hipHostGetDevicePointer(ctypes.byref(p), ctypes.c_void_p(t.data_ptr()), ctypes.c_uint(0))
+    if rc != 0 or not p.value:
+        raise RuntimeError(f"hipHostGetDevicePointer failed ({rc})")
+    return int(p.value)

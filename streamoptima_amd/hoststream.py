@@ -27,7 +27,7 @@ import time
 import torch
 
 from .engine import alloc_planes
-from .hostmem import pinned_empty
+from .hostmem import device_ptr, pinned_empty
 from .hwqueue import dedicated_stream
 
 
@@ -39,6 +39,7 @@ class _Buffers:
         self.offs = torch.empty((nframes, eng.nb + 1), dtype=torch.int32, device=dev)
         self.packed = torch.empty((nframes, eng.pack_bound()), dtype=torch.uint8, device=dev)
         self.tot_h = pinned_empty((nframes,), torch.int32)
+        self.tot_dptr = device_ptr(self.tot_h)     # the pack's scan stores each frame's length here
         self.packed_h = pinned_empty(tuple(self.packed.shape))
         self.sse_h = pinned_empty((nframes,), torch.int64)
         self.enc_done = None      # compute-stream event: this set's frames are no longer read
@@ -46,10 +47,31 @@ class _Buffers:
         self.gop = None           # (index, frame types) of the GOP it holds
 
 
+class _PackedViews:
+    """Frame i's packed stream as packed_h[i, :bytes[i]], made when asked for."""
+
+    def __init__(self, packed_h, nbytes):
+        self._p, self._n = packed_h, nbytes
+
+    def __len__(self):
+        return len(self._n)
+
+    def __getitem__(self, i):
+        return self._p[i, :self._n[i]]
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self._n)))
+
+
 class HostStreamEncoder:
-    def __init__(self, codec, nframes: int, chunk: int = 2, nbuf: int = 1):
+    def __init__(self, codec, nframes: int, chunk: int = 2, nbuf: int = 1, upload: str = "chunk"):
+        """upload: "chunk" = one H2D copy per encode unit (the I-frame, each P-run chunk), "frame"
+        = one per frame."""
         eng = codec.engine()
         self.codec, self.eng, self.nframes, self.chunk = codec, eng, int(nframes), int(chunk)
+        if upload not in ("chunk", "frame"):
+            raise ValueError("upload must be 'chunk' or 'frame'")
+        self.upload = upload
         self.dev = codec.device
         # the three engines' streams each on a hardware queue of its own (hwqueue.py): on a
         # shared queue a stream's event wait stalls the others and the region runs serially
@@ -67,21 +89,38 @@ class HostStreamEncoder:
         if tuple(frames_host.shape) != tuple(self.bufs[0].frames_dev.shape) or not frames_host.is_pinned():
             raise ValueError("frames_host must be pinned uint8 of the encoder's padded frame shape")
 
-    def _upload(self, b: _Buffers, frames_host) -> list:
-        up = []
+    def _units(self, intra_dur: int) -> list:
+        """The frame ranges encode_device works on in turn: each I-frame, and the P-runs of at
+        most `chunk` frames between them."""
+        r, i = [], 0
+        while i < self.nframes:
+            j = i + 1
+            if i % intra_dur != 0:
+                while j < self.nframes and j % intra_dur != 0 and j - i < self.chunk:
+                    j += 1
+            r.append((i, j))
+            i = j
+        return r
+
+    def _upload(self, b: _Buffers, frames_host, intra_dur: int) -> list:
+        """Queue the GOP's upload; returns per frame the event after the copy that carries it
+        (one copy per encode unit: 16.6 MB copies ran at 52.6 GB/s, 8.3 MB ones at 50.0 on the
+        GPU box, tools/s4_links.py)."""
+        up = [None] * self.nframes
+        units = self._units(intra_dur) if self.upload == "chunk" else [(i, i + 1) for i in range(self.nframes)]
         with torch.cuda.stream(self.h2d):
             if b.enc_done is not None:
                 self.h2d.wait_event(b.enc_done)      # the GOP that last used these frames is encoded
-            for i in range(self.nframes):
-                b.frames_dev[i].copy_(frames_host[i], non_blocking=True)
+            for k0, k1 in units:
+                b.frames_dev[k0:k1].copy_(frames_host[k0:k1], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(self.h2d)
-                up.append(ev)
+                up[k0:k1] = [ev] * (k1 - k0)
         return up
 
     def _result(self, b: _Buffers) -> dict:
         nbytes = b.tot_h.tolist()
-        return {"packed": [b.packed_h[i, :n] for i, n in enumerate(nbytes)], "bytes": nbytes,
+        return {"packed": _PackedViews(b.packed_h, nbytes), "bytes": nbytes,
                 "sse": b.sse_h.clone(), "frame_type": b.gop[1]}
 
     def encode(self, frames_host: torch.Tensor, intra_dur: int) -> dict:
@@ -121,6 +160,7 @@ class HostStreamEncoder:
                 b, k0, k1, ev = pending.pop(0)
                 ev.synchronize()                    # byte counts of frames [k0, k1) are in tot_h
                 self.d2h.wait_event(ev)
+                mark(f"d2h_go {k0}", self.d2h)
                 with torch.cuda.stream(self.d2h):
                     for i in range(k0, k1):
                         n = int(b.tot_h[i])
@@ -147,10 +187,10 @@ class HostStreamEncoder:
             if b.gop is not None:
                 retire(b)                            # GOP k - nb: long finished when nb > 1
             if k == 0 or nb == 1:
-                ups[k] = self._upload(b, g)
+                ups[k] = self._upload(b, g, intra_dur)
                 mark(f"up_end {k}", self.h2d)
             if nb > 1 and k + 1 < len(gops):       # the next GOP's upload, queued before this encode
-                ups[k + 1] = self._upload(self.bufs[(k + 1) % nb], gops[k + 1])
+                ups[k + 1] = self._upload(self.bufs[(k + 1) % nb], gops[k + 1], intra_dur)
                 mark(f"up_end {k + 1}", self.h2d)
             up = ups.pop(k)
             if b.d2h_done is not None:
@@ -160,12 +200,14 @@ class HostStreamEncoder:
 
             def wait_input(k0, k1, up=up):
                 comp.wait_event(up[k1 - 1])
+                mark(f"chunk_go {k0}", comp)
 
             def on_output(k0, k1, syms, b=b):
-                eng.pack_symbols(syms, b.offs[k0:k1], b.packed[k0:k1])
-                b.tot_h[k0:k1].copy_(b.offs[k0:k1, eng.nb], non_blocking=True)
+                # the scan stores the frames' lengths straight into tot_h (so_pack_frames_ex)
+                eng.pack_symbols(syms, b.offs[k0:k1], b.packed[k0:k1], totals_ptr=b.tot_dptr + 4 * k0)
                 ev = torch.cuda.Event()
                 ev.record(comp)
+                mark(f"chunk_end {k0}", comp)
                 pending.append((b, k0, k1, ev))
                 drain(1)                             # the chunk before this one
 
@@ -181,4 +223,4 @@ class HostStreamEncoder:
         for b in list(waiting):
             retire(b)
         comp.synchronize()
-        eng.check_run()
+        eng.check_run(defer_stats=True)

@@ -87,6 +87,26 @@ def test_pack_capacity_guard(gpu):
     assert (o2[cap:] == 0xAB).all()
 
 
+def test_pack_totals_into_mapped_host_memory(gpu):
+    """so_pack_frames_ex: each frame's total stored by the scan straight into page-locked host
+    memory (hostmem.device_ptr) equals offs[i, nb], with the block offsets those of
+    so_pack_frames, at a frame count past one launch's kPackMax (32) and a block count past
+    one scan tile (8192)."""
+    from streamoptima_amd.hostmem import device_ptr, pinned_empty
+    c, syms = _encode(gpu, 2160, 3840, 3, 3, False)
+    eng = c.engine()
+    many = [syms[i % 3] for i in range(35)]
+    assert eng.nb > 8192
+    offs, out = eng.pack_symbols(many)
+    tot = pinned_empty((36,), torch.int32)
+    tot.fill_(-7)
+    offs2, out2 = eng.pack_symbols(many, totals_ptr=device_ptr(tot) + 4)
+    torch.cuda.synchronize()
+    assert torch.equal(offs, offs2)
+    assert tot[0].item() == -7 and tot[1:].tolist() == offs[:, eng.nb].cpu().tolist()
+    assert all(torch.equal(out[i, :int(offs[i, -1])], out2[i, :int(offs[i, -1])]) for i in range(35))
+
+
 @pytest.mark.parametrize("h,w,frames,intra_dur,chunk", [(288, 384, 7, 7, 2), (2160, 3840, 8, 4, 3)])
 def test_host_stream_matches_resident_encode(gpu, h, w, frames, intra_dur, chunk):
     """hoststream.HostStreamEncoder (overlapped H2D / encode+pack / D2H, P-runs in chunks):
