@@ -782,8 +782,8 @@ def dense_fallback_of(eng, cfg, step) -> dict:
     p_blocks = (cfg["frames"] - -(-cfg["frames"] // cfg["intra_dur"])) * eng.nb
     fb = eng.take_fallback_count()
     return {"blocks": fb, "p_blocks": p_blocks, "frac": round(fb / p_blocks, 5),
-            "note": "P-frame blocks searched dense: the 4x4-cell bound left more survivors than the list holds (192; "
-                    "384 for a VBS block and its sub-blocks), or the tile "
+            "note": "P-frame blocks searched dense: the 4x4-cell bound left more survivors than the list holds (384, "
+                    "also for a VBS block and its sub-blocks), or the tile "
                     "searched dense from the start because the same tile of the previous frame mostly overflowed "
                     "(SO_P_RUN_FALLBACK_WORD, one GOP)"}
 

@@ -620,7 +620,10 @@ int me_fme_launch(const uint8_t* cur, const uint8_t* planes, size_t pstride, int
 #define SO_SEA2_WPE 6
 #endif
 #ifndef SO_SEA_CAP   // survivors per block evaluated from the list; more take the dense fallback
-#define SO_SEA_CAP 192
+#define SO_SEA_CAP 384   // round 6, 192 -> 384 (the list shares LDS with the transform scratch: no
+                         // cost in LDS): configs[4] 2.457 -> 2.41, low texture 2.186 -> 2.112, 4K
+                         // 1.568 -> 1.562 ms per GOP, noise unchanged; 512 and 768 slower
+                         // (profiles/r06/ab_sea_cap*.log)
 #endif
 #ifndef SO_SEA_CAP_VBS   // the same for a VBS block's block / sub-block lists (sea_vbs_block): looser
 #define SO_SEA_CAP_VBS 384   // sub-block bounds leave more survivors (4K VBS P-run 161.5 -> 158.8 us,
