@@ -629,6 +629,12 @@ int me_fme_launch(const uint8_t* cur, const uint8_t* planes, size_t pstride, int
 #define SO_SEA_CAP_VBS 384   // sub-block bounds leave more survivors (4K VBS P-run 161.5 -> 158.8 us,
                              // dense blocks 8.9 -> 3.8 %; 768: 161.5, profiles/r03/r03n/vbs_ab.log)
 #endif
+#ifndef SO_DENSE_THR     // a tile searches dense from the start when the same tile of the
+#define SO_DENSE_THR 8   // reference frame had at least this many of its 16 blocks overflow,
+#endif                   // except every SO_DENSE_PROBE-th frame, which probes the bound again
+#ifndef SO_DENSE_PROBE    // round 6, 4 -> 16: a probe frame pays the bound and the lists of every
+#define SO_DENSE_PROBE 16 // block before their dense search -- noise 3.13 -> 2.94 ms per 4K GOP (8:
+#endif                    // 3.01, 32: 2.91), textured content unchanged (ab_dense_probe_period.log)
 #ifndef SO_B4_PD   // byte-sum rows in flight in the SEA bound loop (A/B builds: 3, 4)
 #define SO_B4_PD 2
 #endif
@@ -3108,11 +3114,11 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
             // the same tile of the reference frame had most of its blocks overflow the SEA bound
-            // -> this one searches dense from the start, except every 4th frame, which probes
-            // the bound again
-            if (MODE == kRunSingle && dep >= 0 && (f & 3) != 0) {
+            // -> this one searches dense from the start, except every SO_DENSE_PROBE-th frame,
+            // which probes the bound again
+            if (MODE == kRunSingle && dep >= 0 && (f & (SO_DENSE_PROBE - 1)) != 0) {
                 const uint32_t fb = (uint32_t)__builtin_amdgcn_readlane((int)raw, 9);
-                if (lane == 0) s_dense = fb >= 8u ? 1 : 0;
+                if (lane == 0) s_dense = fb >= (uint32_t)SO_DENSE_THR ? 1 : 0;
             }
         };
         // ptile_body's `post`: the next task's dequeue, before the tile's drain (one-GPU,
