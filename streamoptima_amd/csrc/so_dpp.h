@@ -65,6 +65,18 @@ SO_DEV uint64_t wave_min_u64_dpp(uint64_t v) {
 
 SO_DEV uint64_t wave_min_u64(uint64_t v) { return wave_min_u64_dpp(v); }
 
+// inclusive prefix sum over the wave (lane i: v_0 + ... + v_i): row_shr 1, 2, 4, 8 inside each
+// 16-lane row, then row_bcast15 / row_bcast31 carry the row totals into the rows above
+SO_DEV uint32_t wave_incl_scan_u32(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, kDppBcast15, 0xA, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, kDppBcast31, 0xC, 0xF, false);
+    return v;
+}
+
 SO_DEV uint32_t lane_prefix(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }

@@ -859,6 +859,44 @@ SO_DEV void vbs_eval_list(const Sea2Lds& L, const uint16_t* list, uint32_t n, in
     }
 }
 
+#ifndef SO_VBS_MASKLIST   // A/B: 0 = the lists built one ballot per candidate row (round 5)
+#define SO_VBS_MASKLIST 1
+#endif
+// A VBS survivor list from per-lane candidate masks (bit t < NT: candidate cbase + t; bit NT:
+// c2, the dx = +16 column's): each lane's entries at its offset in the wave's prefix sum of the
+// masks' popcounts, the set bits written in a loop the wave runs max-popcount times (the lists'
+// candidates sit a few to a lane).  Returns the list length (uniform); past `cap` nothing is
+// written.  The order differs from the one-ballot-per-row build, which the lists' minima over
+// keys unique by candidate do not see.
+template <int NT>
+SO_DEV uint32_t vbs_list_from_masks(uint16_t* list, uint32_t m, int cbase, int c2, uint32_t cap) {
+    const uint32_t c = (uint32_t)__builtin_popcount(m);
+    uint32_t pos, tot;
+    if constexpr (SO_VBS_MASKLIST == 2) {
+        // the prefix by bit planes of the counts (c <= 18 < 32): five ballots and their lane
+        // prefixes, independent of each other -- a short dependency chain instead of six DPP steps
+        pos = 0;
+        tot = 0;
+#pragma unroll
+        for (int b = 0; b < 5; ++b) {
+            const uint64_t bal = __builtin_amdgcn_ballot_w64(((c >> b) & 1u) != 0u);
+            pos += lane_prefix(bal) << b;
+            tot += (uint32_t)__builtin_popcountll(bal) << b;
+        }
+    } else {
+        const uint32_t inc = wave_incl_scan_u32(c);
+        tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        pos = inc - c;
+    }
+    if (tot > cap) return tot;
+    while (m) {
+        const int t = __builtin_ctz(m);
+        m &= m - 1u;
+        list[pos++] = (uint16_t)(t < NT ? cbase + t : c2);
+    }
+    return tot;
+}
+
 template <class G>
 SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
     constexpr int NT = G::NT, B4P = G::B4P, CAP = G::CAPV, RP = G::RP, CPD = G::CPD;
@@ -966,14 +1004,19 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
     uint16_t* const mylist = L.list + wave * G::CAPL;
     const int cbase = xi * 33 + 16 * hh;
     uint32_t nA = 0;
+    if constexpr (SO_VBS_MASKLIST) {
+        nA = vbs_list_from_masks<NT>(mylist, amask | ((ok2 && lb2 <= qU) ? 1u << NT : 0u), cbase, 32 * 33 + d2,
+                                     (uint32_t)CAP);
+    } else {
 #pragma unroll
-    for (int t = 0; t <= NT; ++t) {
-        const bool pass = t < NT ? ((amask >> t) & 1u) != 0u : (ok2 && lb2 <= qU);
-        const uint64_t bal = __builtin_amdgcn_ballot_w64(pass);
-        if (bal) {
-            const uint32_t pos = nA + lane_prefix(bal);
-            if (pass && pos < (uint32_t)CAP) mylist[pos] = (uint16_t)(t < NT ? cbase + t : 32 * 33 + d2);
-            nA += (uint32_t)__builtin_popcountll(bal);
+        for (int t = 0; t <= NT; ++t) {
+            const bool pass = t < NT ? ((amask >> t) & 1u) != 0u : (ok2 && lb2 <= qU);
+            const uint64_t bal = __builtin_amdgcn_ballot_w64(pass);
+            if (bal) {
+                const uint32_t pos = nA + lane_prefix(bal);
+                if (pass && pos < (uint32_t)CAP) mylist[pos] = (uint16_t)(t < NT ? cbase + t : 32 * 33 + d2);
+                nA += (uint32_t)__builtin_popcountll(bal);
+            }
         }
     }
     if (nA > (uint32_t)CAP) return false;
@@ -1004,15 +1047,24 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     uint32_t nB = 0;
+    if constexpr (SO_VBS_MASKLIST) {
+        uint32_t mB = 0;
 #pragma unroll
-    for (int t = 0; t <= NT; ++t) {
-        const bool pass = t < NT ? (any_sub(T[t], Bt[t]) && ((amask >> t) & 1u) == 0u)
-                                 : (ok2 && any_sub(l2T, l2B) && !(lb2 <= qU));
-        const uint64_t bal = __builtin_amdgcn_ballot_w64(pass);
-        if (bal) {
-            const uint32_t pos = nB + lane_prefix(bal);
-            if (pass && pos < (uint32_t)CAP) mylist[pos] = (uint16_t)(t < NT ? cbase + t : 32 * 33 + d2);
-            nB += (uint32_t)__builtin_popcountll(bal);
+        for (int t = 0; t < NT; ++t) mB |= (any_sub(T[t], Bt[t]) ? 1u : 0u) << t;
+        mB &= ~amask;
+        mB |= (ok2 && any_sub(l2T, l2B) && !(lb2 <= qU)) ? 1u << NT : 0u;
+        nB = vbs_list_from_masks<NT>(mylist, mB, cbase, 32 * 33 + d2, (uint32_t)CAP);
+    } else {
+#pragma unroll
+        for (int t = 0; t <= NT; ++t) {
+            const bool pass = t < NT ? (any_sub(T[t], Bt[t]) && ((amask >> t) & 1u) == 0u)
+                                     : (ok2 && any_sub(l2T, l2B) && !(lb2 <= qU));
+            const uint64_t bal = __builtin_amdgcn_ballot_w64(pass);
+            if (bal) {
+                const uint32_t pos = nB + lane_prefix(bal);
+                if (pass && pos < (uint32_t)CAP) mylist[pos] = (uint16_t)(t < NT ? cbase + t : 32 * 33 + d2);
+                nB += (uint32_t)__builtin_popcountll(bal);
+            }
         }
     }
     if (nB > (uint32_t)CAP) return false;
