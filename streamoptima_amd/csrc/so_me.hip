@@ -661,7 +661,10 @@ struct Sea2GeoT {
     static constexpr int NBLK = TBX * TBY;
     static constexpr int NW = NW_, NTHREADS = NW * 64;
     static constexpr int CAP = SO_SEA_CAP, CAPV = SO_SEA_CAP_VBS;
-    static constexpr int CAPL = CAP > CAPV ? CAP : CAPV;   // list entries per wave
+    // list entries per wave: a VBS block's sub-block survivors go to two lists of up to CAPV
+    // (its top and bottom halves, sea_vbs_block); in the fused tiles the lists share LDS with the
+    // transform scratch, which is larger either way
+    static constexpr int CAPL = CAP > 2 * CAPV ? CAP : 2 * CAPV;
     static constexpr int DCS = WR * RP + 8;                // dense tiles: window copy stride (8 mod 32)
     static constexpr int CPD = TPX / 4 + 1;               // current-tile pitch in dwords: 16 rows of
                                                           // one block column land on 16 banks
@@ -859,9 +862,61 @@ SO_DEV void vbs_eval_list(const Sea2Lds& L, const uint16_t* list, uint32_t n, in
     }
 }
 
-#ifndef SO_VBS_MASKLIST   // A/B: 0 = the lists built one ballot per candidate row (round 5)
-#define SO_VBS_MASKLIST 1
-#endif
+// List B by halves (SO_VBS_HALVES): a candidate not in list A can only improve sub-block
+// minima, and mostly passes one sub-block bound, so B holds (candidate, half) entries -- the
+// top half's list at listT, the bottom half's at listBo -- and a pass evaluates 16 entries of
+// each: lanes 0-31 the top ones, lanes 32-63 the bottom ones, two lanes per entry (4 of its
+// 8 rows each), paired by one DPP add into the half's left / right quadrant SADs.  32-bit
+// sub-block keys as vbs_eval_list's, into c0 (left quadrant) and c1 (right) of the lane's half.
+template <class G>
+SO_DEV void vbs_eval_halves(const Sea2Lds& L, const uint16_t* listT, uint32_t nT, const uint16_t* listBo,
+                            uint32_t nBo, int cs, int bxl, int byl, int lane, uint32_t& c0, uint32_t& c1) {
+    constexpr int RP = G::RP, CPD = G::CPD;
+    const bool bot = lane >= 32;
+    const int e = (lane & 31) >> 1;
+    const int r0 = (bot ? 8 : 0) + 4 * (lane & 1);
+    const uint16_t* const list = bot ? listBo : listT;
+    const uint32_t n = bot ? nBo : nT, nmax = nT > nBo ? nT : nBo;
+    const int crow0 = byl * 16 * CPD + bxl * 4 + r0 * CPD;
+#pragma unroll 1
+    for (uint32_t s0 = 0; s0 < nmax; s0 += 16) {
+        SO_MARK(vbs_pass);
+        const bool act = s0 + (uint32_t)e < n;
+        const int cand = act ? (int)list[s0 + e] : cs;
+        const int dxi = cand / 33, di = cand - dxi * 33;
+        const int col = bxl * 16 + dxi;
+        const uint32_t sh = (uint32_t)(col & 3);
+        int wo = (byl * 16 + di + r0) * RP + (col >> 2);
+        asm volatile("" : "+v"(wo));
+        uint32_t sl = 0, srr = 0;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            lds_vu32p p = (lds_vu32p)(L.win + wo + rr * RP);
+            lds_vu32p c = (lds_vu32p)(L.curt + crow0 + rr * CPD);
+            const uint32_t q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4];
+            sl = __builtin_amdgcn_sad_u8(c[0], __builtin_amdgcn_alignbyte(q1, q0, sh), sl);
+            sl = __builtin_amdgcn_sad_u8(c[1], __builtin_amdgcn_alignbyte(q2, q1, sh), sl);
+            srr = __builtin_amdgcn_sad_u8(c[2], __builtin_amdgcn_alignbyte(q3, q2, sh), srr);
+            srr = __builtin_amdgcn_sad_u8(c[3], __builtin_amdgcn_alignbyte(q4, q3, sh), srr);
+        }
+        uint32_t v = sl | (srr << 16);
+        v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kDppQuad1032, 0xF, 0xF, false);   // lanes l, l ^ 1
+        const int dx = dxi - 16, dy = di - 16;
+        const uint32_t md = (uint32_t)((dx < 0 ? -dx : dx) + (dy < 0 ? -dy : dy));
+        const uint32_t t32 = (md << 11) | (uint32_t)cand;
+        const uint32_t k0 = ((v & 0xFFFFu) << 17) | t32, k1 = ((v >> 16) << 17) | t32;
+        c0 = (act && k0 < c0) ? k0 : c0;
+        c1 = (act && k1 < c1) ? k1 : c1;
+    }
+}
+
+#ifndef SO_VBS_HALVES   // A/B builds: 1 = list B by halves.  Bit-exact, but 4K VBS GOP 3.198 ->
+#define SO_VBS_HALVES 0  // 3.359 ms (the second mask, list and four more wave minima cost more than
+#endif                   // the passes saved), 1080p 1.437 -> 1.375 (profiles/r06/ab_vbs_halves.log)
+#ifndef SO_VBS_MASKLIST   // bit 0: list A, bit 1: list B built from masks (0: one ballot per
+#define SO_VBS_MASKLIST 3   // candidate row, round 5).  4K VBS GOP 3.271 -> 3.201 ms (B alone 3.212,
+#endif                      // A alone 3.251); 1080p VBS 1.394 -> 1.430, latency-bound there (a wave
+                            // runs its lanes' longest bit loop) -- profiles/r06/ab_vbs_masklist*.log
 // A VBS survivor list from per-lane candidate masks (bit t < NT: candidate cbase + t; bit NT:
 // c2, the dx = +16 column's): each lane's entries at its offset in the wave's prefix sum of the
 // masks' popcounts, the set bits written in a loop the wave runs max-popcount times (the lists'
@@ -871,23 +926,9 @@ SO_DEV void vbs_eval_list(const Sea2Lds& L, const uint16_t* list, uint32_t n, in
 template <int NT>
 SO_DEV uint32_t vbs_list_from_masks(uint16_t* list, uint32_t m, int cbase, int c2, uint32_t cap) {
     const uint32_t c = (uint32_t)__builtin_popcount(m);
-    uint32_t pos, tot;
-    if constexpr (SO_VBS_MASKLIST == 2) {
-        // the prefix by bit planes of the counts (c <= 18 < 32): five ballots and their lane
-        // prefixes, independent of each other -- a short dependency chain instead of six DPP steps
-        pos = 0;
-        tot = 0;
-#pragma unroll
-        for (int b = 0; b < 5; ++b) {
-            const uint64_t bal = __builtin_amdgcn_ballot_w64(((c >> b) & 1u) != 0u);
-            pos += lane_prefix(bal) << b;
-            tot += (uint32_t)__builtin_popcountll(bal) << b;
-        }
-    } else {
-        const uint32_t inc = wave_incl_scan_u32(c);
-        tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-        pos = inc - c;
-    }
+    const uint32_t inc = wave_incl_scan_u32(c);   // (a prefix by bit planes of c, five ballots:
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);   // slower)
+    uint32_t pos = inc - c;
     if (tot > cap) return tot;
     while (m) {
         const int t = __builtin_ctz(m);
@@ -1004,7 +1045,7 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
     uint16_t* const mylist = L.list + wave * G::CAPL;
     const int cbase = xi * 33 + 16 * hh;
     uint32_t nA = 0;
-    if constexpr (SO_VBS_MASKLIST) {
+    if constexpr ((SO_VBS_MASKLIST & 1) != 0) {
         nA = vbs_list_from_masks<NT>(mylist, amask | ((ok2 && lb2 <= qU) ? 1u << NT : 0u), cbase, 32 * 33 + d2,
                                      (uint32_t)CAP);
     } else {
@@ -1029,10 +1070,9 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
     vbs_eval_list<G>(L, mylist, nA, cs, bxl, byl, lane, bestB, best0, best1);
     // U_j: the smallest sub-block SADs among the evaluated candidates (quad lanes 0, 1: top)
     const bool top = (lane & 2) == 0;
-    const uint32_t uTL = wave_min_u32(top ? best0 : ~0u) >> 17;
-    const uint32_t uTR = wave_min_u32(top ? best1 : ~0u) >> 17;
-    const uint32_t uBL = wave_min_u32(top ? ~0u : best0) >> 17;
-    const uint32_t uBR = wave_min_u32(top ? ~0u : best1) >> 17;
+    const uint32_t mTL = wave_min_u32(top ? best0 : ~0u), mTR = wave_min_u32(top ? best1 : ~0u);
+    const uint32_t mBL = wave_min_u32(top ? ~0u : best0), mBR = wave_min_u32(top ? ~0u : best1);
+    const uint32_t uTL = mTL >> 17, uTR = mTR >> 17, uBL = mBL >> 17, uBR = mBR >> 17;
     // ---- 3. the sub-block survivors (B): some sub-block bound <= its U_j, not evaluated in A ----
     SO_MARK(vbs_list_b);
     typedef short so_v2i16 __attribute__((ext_vector_type(2)));
@@ -1046,8 +1086,54 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // list A read before it is overwritten
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if constexpr (SO_VBS_HALVES) {
+        // (candidate, half) entries: the top list at mylist, the bottom one at mylist + CAP
+        const auto pass_half = [](uint32_t v, uint32_t th) {
+            const so_v2i16 d = __builtin_bit_cast(so_v2i16, v) - __builtin_bit_cast(so_v2i16, th);
+            return (__builtin_bit_cast(uint32_t, d) & 0x80008000u) != 0u;
+        };
+        uint32_t mT = 0, mBo = 0;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            mT |= (pass_half(T[t], thT) ? 1u : 0u) << t;
+            mBo |= (pass_half(Bt[t], thB) ? 1u : 0u) << t;
+        }
+        const bool col_b = ok2 && !(lb2 <= qU);
+        mT = (mT & ~amask) | ((col_b && pass_half(l2T, thT)) ? 1u << NT : 0u);
+        mBo = (mBo & ~amask) | ((col_b && pass_half(l2B, thB)) ? 1u << NT : 0u);
+        const uint32_t nT = vbs_list_from_masks<NT>(mylist, mT, cbase, 32 * 33 + d2, (uint32_t)CAP);
+        const uint32_t nBo = vbs_list_from_masks<NT>(mylist + CAP, mBo, cbase, 32 * 33 + d2, (uint32_t)CAP);
+        if (nT > (uint32_t)CAP || nBo > (uint32_t)CAP) return false;
+        const uint32_t nmax = nT > nBo ? nT : nBo;
+        if (lane == 0) SO_OPS_ADD(&L.st[2], 16u * ((nmax + 15) / 16) * 256u);   // 32 half-candidates per pass
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint64_t kb = wave_min_u64_dpp(bestB);
+        uint32_t c0 = ~0u, c1 = ~0u;
+        vbs_eval_halves<G>(L, mylist, nT, mylist + CAP, nBo, cs, bxl, byl, lane, c0, c1);
+        SO_MARK(vbs_final);
+        const auto widen = [](uint32_t k) {
+            return ((uint64_t)(k >> 17) << 32) | ((uint64_t)((k >> 11) & 63u) << 24) | (uint64_t)(k & 2047u);
+        };
+        const bool bot = lane >= 32;
+        const uint32_t hTL = wave_min_u32(bot ? ~0u : c0), hTR = wave_min_u32(bot ? ~0u : c1);
+        const uint32_t hBL = wave_min_u32(bot ? c0 : ~0u), hBR = wave_min_u32(bot ? c1 : ~0u);
+        const uint64_t kTL = widen(hTL < mTL ? hTL : mTL), kTR = widen(hTR < mTR ? hTR : mTR);
+        const uint64_t kBL = widen(hBL < mBL ? hBL : mBL), kBR = widen(hBR < mBR ? hBR : mBR);
+        if (lane == 0) {
+            unsigned long long* const ks = L.keys;
+            if (kb < ks[u]) ks[u] = kb;
+            unsigned long long* const sk = ks + G::NBLK + 4 * u;
+            if (kTL < sk[0]) sk[0] = kTL;
+            if (kTR < sk[1]) sk[1] = kTR;
+            if (kBL < sk[2]) sk[2] = kBL;
+            if (kBR < sk[3]) sk[3] = kBR;
+        }
+        return true;
+    }
     uint32_t nB = 0;
-    if constexpr (SO_VBS_MASKLIST) {
+    if constexpr ((SO_VBS_MASKLIST & 2) != 0) {
         uint32_t mB = 0;
 #pragma unroll
         for (int t = 0; t < NT; ++t) mB |= (any_sub(T[t], Bt[t]) ? 1u : 0u) << t;
