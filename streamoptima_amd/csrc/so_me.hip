@@ -635,6 +635,9 @@ int me_fme_launch(const uint8_t* cur, const uint8_t* planes, size_t pstride, int
 #ifndef SO_DENSE_PROBE    // round 6, 4 -> 16: a probe frame pays the bound and the lists of every
 #define SO_DENSE_PROBE 16 // block before their dense search -- noise 3.13 -> 2.94 ms per 4K GOP (8:
 #endif                    // 3.01, 32: 2.91), textured content unchanged (ab_dense_probe_period.log)
+#ifndef SO_VBS_HALVES   // A/B builds: 1 = list B by halves.  Bit-exact, but 4K VBS GOP 3.198 ->
+#define SO_VBS_HALVES 0  // 3.359 ms (the second mask, list and four more wave minima cost more than
+#endif                   // the passes saved), 1080p 1.437 -> 1.375 (profiles/r06/ab_vbs_halves.log)
 #ifndef SO_B4_PD   // byte-sum rows in flight in the SEA bound loop (A/B builds: 3, 4)
 #define SO_B4_PD 2
 #endif
@@ -661,10 +664,11 @@ struct Sea2GeoT {
     static constexpr int NBLK = TBX * TBY;
     static constexpr int NW = NW_, NTHREADS = NW * 64;
     static constexpr int CAP = SO_SEA_CAP, CAPV = SO_SEA_CAP_VBS;
-    // list entries per wave: a VBS block's sub-block survivors go to two lists of up to CAPV
-    // (its top and bottom halves, sea_vbs_block); in the fused tiles the lists share LDS with the
-    // transform scratch, which is larger either way
-    static constexpr int CAPL = CAP > 2 * CAPV ? CAP : 2 * CAPV;
+    // list entries per wave (SO_VBS_HALVES: a VBS block's sub-block survivors go to two lists of
+    // up to CAPV, its top and bottom halves; in the fused tiles the lists share LDS with the
+    // transform scratch, which is larger either way)
+    static constexpr int CAPLV = SO_VBS_HALVES ? 2 * CAPV : CAPV;
+    static constexpr int CAPL = CAP > CAPLV ? CAP : CAPLV;
     static constexpr int DCS = WR * RP + 8;                // dense tiles: window copy stride (8 mod 32)
     static constexpr int CPD = TPX / 4 + 1;               // current-tile pitch in dwords: 16 rows of
                                                           // one block column land on 16 banks
@@ -910,9 +914,6 @@ SO_DEV void vbs_eval_halves(const Sea2Lds& L, const uint16_t* listT, uint32_t nT
     }
 }
 
-#ifndef SO_VBS_HALVES   // A/B builds: 1 = list B by halves.  Bit-exact, but 4K VBS GOP 3.198 ->
-#define SO_VBS_HALVES 0  // 3.359 ms (the second mask, list and four more wave minima cost more than
-#endif                   // the passes saved), 1080p 1.437 -> 1.375 (profiles/r06/ab_vbs_halves.log)
 #ifndef SO_VBS_MASKLIST   // bit 0: list A, bit 1: list B built from masks (0: one ballot per
 #define SO_VBS_MASKLIST 3   // candidate row, round 5).  4K VBS GOP 3.271 -> 3.201 ms (B alone 3.212,
 #endif                      // A alone 3.251); 1080p VBS 1.394 -> 1.430, latency-bound there (a wave
