@@ -330,21 +330,28 @@ def test_vbs_run_matches_per_frame(gpu, monkeypatch, h, w, intra_dur, content):
         assert [symbols_digest(s) for s in res[g]["symbols"]] == exp[g], g
 
 
-@pytest.mark.parametrize("content", ["noise", "lowtex"])
+@pytest.mark.parametrize("content", ["noise", "lowtex", "noise_then_bench"])
 def test_dense_predicted_tiles_match_per_frame(gpu, monkeypatch, content):
     """Tiles whose 4x4-cell bounds overflowed in the previous frame (p_run_kernel's tile
     predictor) scan every block densely over the window copies staged in the scratch -- against
     the per-frame kernels (SO_PIPELINE=0: me_wave_kernel's dense search), frame by frame, with
-    edge tiles (640 = 5 tiles, 272 rows)."""
+    edge tiles (640 = 5 tiles, 272 rows).  noise_then_bench: a scene change at frame 9 to
+    textured content, the tiles still predicted dense until the probe frame (every 16th,
+    SO_DENSE_PROBE), over 20 frames."""
     from streamoptima_amd.Encoder import Y_Video_codec
     from streamoptima_amd.digest import symbols_digest
     from streamoptima_amd.engine import alloc_planes
     from streamoptima_amd.synth import synth_sequence_torch
-    h, w, f = 272, 640, 9
+    h, w = 272, 640
+    f = 20 if content == "noise_then_bench" else 9
     codec = Y_Video_codec(h, w, f, 16, 16, 4, f, 0, 0.015, False, device=gpu)
     assert codec.engine().pipelined_ok(1)
     fr = alloc_planes(f, h, w, gpu)
-    fr.copy_(synth_sequence_torch(f, h, w, seed=23, device=gpu, content=content))
+    if content == "noise_then_bench":
+        fr[:9].copy_(synth_sequence_torch(f, h, w, seed=23, device=gpu, content="noise")[:9])
+        fr[9:].copy_(synth_sequence_torch(f, h, w, seed=23, device=gpu)[9:])
+    else:
+        fr.copy_(synth_sequence_torch(f, h, w, seed=23, device=gpu, content=content))
     monkeypatch.setenv("SO_PIPELINE", "0")
     exp = [symbols_digest(s) for s in codec.encode_device(fr, f)["symbols"]]
     monkeypatch.delenv("SO_PIPELINE")
