@@ -914,6 +914,9 @@ SO_DEV void vbs_eval_halves(const Sea2Lds& L, const uint16_t* listT, uint32_t nT
     }
 }
 
+#ifndef SO_VBS_BALLOT_LATENCY   // A/B builds: 0 = mask-built lists in latency-bound runs too.
+#define SO_VBS_BALLOT_LATENCY 1  // 1080p VBS GOP 1.433 -> 1.399 ms, 4K 3.198 -> 3.214 (both paths
+#endif                           // in the kernel; profiles/r06/ab_vbs_ballot_latency.log)
 #ifndef SO_VBS_MASKLIST   // bit 0: list A, bit 1: list B built from masks (0: one ballot per
 #define SO_VBS_MASKLIST 3   // candidate row, round 5).  4K VBS GOP 3.271 -> 3.201 ms (B alone 3.212,
 #endif                      // A alone 3.251); 1080p VBS 1.394 -> 1.430, latency-bound there (a wave
@@ -940,7 +943,7 @@ SO_DEV uint32_t vbs_list_from_masks(uint16_t* list, uint32_t m, int cbase, int c
 }
 
 template <class G>
-SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
+SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid, bool ballot_lists = false) {
     constexpr int NT = G::NT, B4P = G::B4P, CAP = G::CAPV, RP = G::RP, CPD = G::CPD;
     SO_MARK(vbs_block);
     int lane = tid & 63;
@@ -1046,7 +1049,7 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
     uint16_t* const mylist = L.list + wave * G::CAPL;
     const int cbase = xi * 33 + 16 * hh;
     uint32_t nA = 0;
-    if constexpr ((SO_VBS_MASKLIST & 1) != 0) {
+    if ((SO_VBS_MASKLIST & 1) != 0 && !ballot_lists) {
         nA = vbs_list_from_masks<NT>(mylist, amask | ((ok2 && lb2 <= qU) ? 1u << NT : 0u), cbase, 32 * 33 + d2,
                                      (uint32_t)CAP);
     } else {
@@ -1134,7 +1137,7 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid) {
         return true;
     }
     uint32_t nB = 0;
-    if constexpr ((SO_VBS_MASKLIST & 2) != 0) {
+    if ((SO_VBS_MASKLIST & 2) != 0 && !ballot_lists) {
         uint32_t mB = 0;
 #pragma unroll
         for (int t = 0; t < NT; ++t) mB |= (any_sub(T[t], Bt[t]) ? 1u : 0u) << t;
@@ -1213,6 +1216,10 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
     const int nbx = W / 16;
     const int tiles_x = (nbx + TBX - 1) / TBX;
     const int tx = tile % tiles_x, ty = tile / tiles_x;
+    // a persistent grid with more slots than a frame has tiles runs latency-bound (the chain
+    // step of one tile position): there the VBS lists are built one ballot per candidate row,
+    // whose cost does not depend on how the survivors cluster in a lane (SO_VBS_MASKLIST)
+    const bool ballot_lists = SO_VBS_BALLOT_LATENCY && VBS && tiles_x * ((H / 16 + TBY - 1) / TBY) < (int)gridDim.x;
     const int bx0 = tx * TBX, byt0 = by0 + ty * TBY;
     const int x0 = bx0 * 16, y0 = byt0 * 16;
     const int tid = opaque_tid();
@@ -1438,7 +1445,7 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
             if constexpr (VBS) {
                 if (x != 0 && y != 0) {   // uniform: block + sub-block search
 #ifndef SO_VBS_DENSE_ONLY   // A/B builds: every sub-searched block dense
-                    if (x + 48 <= W && y + 48 <= H && sea_vbs_block<G>(L, u, bxl, byl, tid)) continue;
+                    if (x + 48 <= W && y + 48 <= H && sea_vbs_block<G>(L, u, bxl, byl, tid, ballot_lists)) continue;
 #endif
                     if ((tid & 63) == 0) {
                         atomicAdd(&st_fb, 1u);   // counted as a dense fallback
