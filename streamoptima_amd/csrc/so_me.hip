@@ -915,8 +915,9 @@ SO_DEV void vbs_eval_halves(const Sea2Lds& L, const uint16_t* listT, uint32_t nT
 }
 
 #ifndef SO_VBS_BALLOT_LATENCY   // A/B builds: 0 = mask-built lists in latency-bound runs too.
-#define SO_VBS_BALLOT_LATENCY 1  // 1080p VBS GOP 1.433 -> 1.399 ms, 4K 3.198 -> 3.214 (both paths
-#endif                           // in the kernel; profiles/r06/ab_vbs_ballot_latency.log)
+#define SO_VBS_BALLOT_LATENCY 1  // 1080p VBS GOP 1.433 -> 1.399 ms (profiles/r06/ab_vbs_ballot_
+#endif                           // latency.log); the uniform-QP run as two instantiations, 4K
+                                 // unchanged (ab_vbs_latency_twin.log)
 #ifndef SO_VBS_MASKLIST   // bit 0: list A, bit 1: list B built from masks (0: one ballot per
 #define SO_VBS_MASKLIST 3   // candidate row, round 5).  4K VBS GOP 3.271 -> 3.201 ms (B alone 3.212,
 #endif                      // A alone 3.251); 1080p VBS 1.394 -> 1.430, latency-bound there (a wave
@@ -1196,7 +1197,9 @@ SO_DEV bool sea_vbs_block(const Sea2Lds& L, int u, int bxl, int byl, int tid, bo
 // there is a second candidate for U (below).  Only a hint: any VALID candidate's SAD bounds the
 // minimum from above, so a stale or garbage record (it is read unordered, and is range-checked)
 // can cost survivors, never exactness.
-template <class G, class Pre = NoPre, bool VBS = false>
+// LISTS (VBS): how sea_vbs_block builds its survivor lists -- 1 from lane masks, 2 one ballot
+// per candidate row, 0 chosen per launch (below)
+template <class G, class Pre = NoPre, bool VBS = false, int LISTS = 0>
 SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cur, const RefSet& refs, int nref,
                       int H, int W, int by0, int by1, int probe, const Pre& pre = Pre(),
                       const int* dense_flag = nullptr, const int16_t* prev_mv = nullptr) {
@@ -1219,7 +1222,8 @@ SO_DEV void sea2_tile(const Sea2Lds& L, int tile, const uint8_t* __restrict__ cu
     // a persistent grid with more slots than a frame has tiles runs latency-bound (the chain
     // step of one tile position): there the VBS lists are built one ballot per candidate row,
     // whose cost does not depend on how the survivors cluster in a lane (SO_VBS_MASKLIST)
-    const bool ballot_lists = SO_VBS_BALLOT_LATENCY && VBS && tiles_x * ((H / 16 + TBY - 1) / TBY) < (int)gridDim.x;
+    const bool ballot_lists = LISTS == 2 || (LISTS == 0 && SO_VBS_BALLOT_LATENCY && VBS &&
+                                             tiles_x * ((H / 16 + TBY - 1) / TBY) < (int)gridDim.x);
     const int bx0 = tx * TBX, byt0 = by0 + ty * TBY;
     const int x0 = bx0 * 16, y0 = byt0 * 16;
     const int tid = opaque_tid();
@@ -2511,7 +2515,7 @@ SO_DEV void store_sc1_i32(int32_t* p, int v) {
 }
 
 template <class G, bool SC1, class Pre = NoPre, bool HALO = false, bool TOK = false, bool VBS = false,
-          class Post = NoPre, bool HALFTQ = false, bool ZSKIP = false>
+          class Post = NoPre, bool HALFTQ = false, bool ZSKIP = false, int LISTS = 0>
 SO_DEV void ptile_body(PTileLds<G, VBS, HALFTQ>& S, int tile, const uint8_t* __restrict__ cur, const uint8_t* ref, int H, int W,
                        int by0, int by1, int qp_rd, const int32_t* __restrict__ qp_row,
                        const int32_t* __restrict__ qp_map, int32_t* __restrict__ out_best, const PFrameOut& o,
@@ -2537,7 +2541,7 @@ SO_DEV void ptile_body(PTileLds<G, VBS, HALFTQ>& S, int tile, const uint8_t* __r
 #ifndef SO_PROF_PHASE   // phase-attribution A/B builds only (tools/prun_phase.py): 1 = no transforms
 #define SO_PROF_PHASE 0  // (the tile's current rows stored as its reconstruction), 2 = no search
 #endif                   // (window staged, every block at mv (0, 0))
-    sea2_tile<G, Pre, VBS>(L, tile, cur, refs, 1, H, W, by0, by1, SO_PROF_PHASE == 2 ? 5 : 0, pre,
+    sea2_tile<G, Pre, VBS, LISTS>(L, tile, cur, refs, 1, H, W, by0, by1, SO_PROF_PHASE == 2 ? 5 : 0, pre,
                            dense_flag, prev_mv);   // ends with a barrier
 
     const int tid = opaque_tid();
@@ -3076,7 +3080,10 @@ SO_DEV uint32_t run_dequeue(uint32_t* ws) {
 // the block coefficients tq16_vbs_fwd would hold through the sub-block transforms for a
 // requantisation at another QP are then dead (VBS run spills 30 -> 23; 4K VBS GOP 3.311 ->
 // 3.265 ms, profiles/r06/ab_vbs_uqp.log).
-// ZSKIP (one-GPU plain run, SO_OPT_RUN_ZERO_SKIP): tq16_exact's all-zero-wave IDCT skip
+// ZSKIP (one-GPU plain run, SO_OPT_RUN_ZERO_SKIP): tq16_exact's all-zero-wave IDCT skip.  On the
+// one-GPU uniform-QP VBS run the same slot selects the latency-bound twin: its VBS survivor lists
+// built one ballot per candidate row (sea2_tile's LISTS = 2; the host launches it when the grid
+// has more slots than a frame has tiles), the other one building them from lane masks (LISTS = 1)
 template <int NW, int MODE, bool VBS = false, bool HOOKS = false, bool UQP = false, bool ZSKIP = false>
 __global__ void __launch_bounds__(NW * 64)
 __attribute__((amdgpu_waves_per_eu(VBS ? SO_VBS_WPE : (NW >= 16 ? SO_PTILE_WPE16 : SO_SEA2_WPE))))
@@ -3084,7 +3091,9 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
              int qp_rd, const int32_t* __restrict__ qp_row_arg, uint32_t* __restrict__ ws, int ws_stamp_base,
              const PRunStripe sp, double lam) {
     static_assert(!UQP || VBS, "the uniform-QP instantiation is the VBS run's");
-    static_assert(!ZSKIP || (MODE == kRunSingle && !VBS && !HOOKS), "the zero-skip instantiation is the plain one-GPU run's");
+    static_assert(!ZSKIP || (MODE == kRunSingle && !HOOKS && (!VBS || UQP)),
+                  "the zero-skip / latency-lists instantiation is the one-GPU run's");
+    constexpr int LISTS = VBS && MODE == kRunSingle && UQP ? (ZSKIP ? 2 : 1) : 0;
     const int32_t* __restrict__ const qp_row = UQP ? nullptr : qp_row_arg;
     using G = Sea2GeoT<NW>;
     __shared__ PTileLds<G, VBS> S;
@@ -3435,7 +3444,7 @@ p_run_kernel(const PRunArgs a, int nframes, const uint8_t* __restrict__ ref0, in
 #ifdef SO_RUN_PROFILE
             const unsigned long long pt0 = __builtin_amdgcn_s_memtime();
 #endif
-            ptile_body<G, true, decltype(wait_ref), false, false, VBS, decltype(take_next), false, ZSKIP>(
+            ptile_body<G, true, decltype(wait_ref), false, false, VBS, decltype(take_next), false, ZSKIP && !VBS, LISTS>(
                 S, tile, a.cur[f], ref, H, W, 0, by1, qp_rd, qp_row, nullptr, nullptr, a.out[f], wait_ref, PHalo{}, lam,
                 &s_dense, reinterpret_cast<int32_t*>(tilefb) + (size_t)f * ntiles + tile, count_ops, take_next,
                 // VBS: the same hint for the block's U measured slower (4K VBS P-frame 123.1 vs
@@ -3563,7 +3572,7 @@ static int run_shape(const void* kernel, int* ncu, int* per_cu) {
 // ranks sharing one device size their claims by it, whichever kernel each of them launches.
 int p_run_capacity(int vbs, int mode) {
     constexpr int NW = SO_PTILE_NW;
-    const void* ks[12];
+    const void* ks[13];
     int n = 0;
     const auto add = [&](int m, const void* k) {
         if (mode < 0 || mode == m) ks[n++] = k;
@@ -3573,6 +3582,7 @@ int p_run_capacity(int vbs, int mode) {
         add(kRunSingle, reinterpret_cast<const void*>(p_run_kernel<NW, kRunSingle, true, true>));
         add(kRunSingle, reinterpret_cast<const void*>(p_run_kernel<NW, kRunSingle, true, false, true>));
         add(kRunSingle, reinterpret_cast<const void*>(p_run_kernel<NW, kRunSingle, true, true, true>));
+        add(kRunSingle, reinterpret_cast<const void*>(p_run_kernel<NW, kRunSingle, true, false, true, true>));
         add(kRunFPipe, reinterpret_cast<const void*>(p_run_kernel<NW, kRunFPipe, true>));
         add(kRunFPipe, reinterpret_cast<const void*>(p_run_kernel<NW, kRunFPipe, true, false, true>));
     } else {
@@ -3617,6 +3627,10 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
     // the plain one-GPU run with the all-zero-wave IDCT skip (SO_OPT_RUN_ZERO_SKIP; not with hooks)
     constexpr bool ZS_OK = MODE == kRunSingle && !VBS;
     const bool zskip = ZS_OK && !hooks && option(SO_OPT_RUN_ZERO_SKIP) != 0;
+    // the uniform-QP VBS run's latency-bound twin (p_run_kernel's ZSKIP slot on VBS): chosen below
+    // when the grid has more slots than a frame has tiles
+    constexpr bool VL_OK = MODE == kRunSingle && VBS;
+    const bool vlat_ok = VL_OK && uqp && !hooks && SO_VBS_BALLOT_LATENCY;
     const void* const kfn =
         hooks ? (uqp ? reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, MODE == kRunSingle, VBS>)
                      : reinterpret_cast<const void*>(p_run_kernel<SO_PTILE_NW, MODE, VBS, MODE == kRunSingle>))
@@ -3696,6 +3710,8 @@ static int p_run_launch_t(const uint8_t* const* curs, int nframes, const uint8_t
             SO_P_RUN_GO(MODE == kRunSingle, VBS, false);
         else if (hooks)
             SO_P_RUN_GO(MODE == kRunSingle, false, false);
+        else if (uqp && vlat_ok && ntiles < grid)
+            SO_P_RUN_GO(false, VBS, VL_OK);
         else if (uqp)
             SO_P_RUN_GO(false, VBS, false);
         else if (zskip)
