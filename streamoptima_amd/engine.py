@@ -13,6 +13,7 @@ import contextlib
 from dataclasses import dataclass, field
 
 import ctypes
+import os
 
 import torch
 
@@ -380,7 +381,7 @@ class Engine:
     # the plain run's kernel choice by content (SO_OPT_RUN_ZERO_SKIP): the instantiation that
     # skips the IDCT of all-zero waves when at least this share of the last run's blocks
     # quantised to zero (flat content; exact either way)
-    ZERO_SKIP_SHARE = 0.5
+    ZERO_SKIP_SHARE = float(os.environ.get("SO_ZERO_SKIP_SHARE", "0.5"))   # A/B: the share that selects it
     zero_skip = False
 
     def check_run(self, defer_stats: bool = False) -> None:
