@@ -8,7 +8,9 @@ T=${TAG:-s4v}
 timeout -k 10 400 python -u -m pytest tests -x -q -m gpu -k "pack or host_stream or zero_skip" --timeout 200 \
     --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_${T}.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_${T}.log; [ $rc -ne 0 ] && exit $rc
-for v in ${VARIANTS:-"2 frame" "2 chunk" "3 chunk" "1 chunk"}; do
+# VARIANTS: comma-separated "chunk upload" pairs
+IFS=, read -ra VS <<< "${VARIANTS:-2 frame,2 chunk,3 chunk,1 chunk}"
+for v in "${VS[@]}"; do
   set -- $v
   timeout -k 10 120 python -u tools/s4_timeline.py --chunk $1 --upload $2 --reps 12 --quiet >> gpurun_out/s4v_${T}.log 2>&1
   rc=$?; [ $rc -ne 0 ] && { echo "variant $v rc=$rc"; tail -5 gpurun_out/s4v_${T}.log; exit $rc; }
